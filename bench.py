@@ -1,0 +1,326 @@
+#!/usr/bin/env python3
+"""bench.py — tg (decode) tokens/s of the TinyLlama-1.1B Q4_K_M matmul chain on MI355X,
+plus the Q4_K x Q8_K GEMV's achieved HBM bandwidth against the roofline.
+
+Metric (BASELINE.json): "tg128 tok/s + Q4_K GEMV achieved-HBM-GB/s, TinyLlama-1.1B
+Q4_K_M @1 GPU". One step = one decoded token = the model's full per-token MUL_MAT
+chain (every layer's attn_q/k/v, attn_output, ffn_gate/up, ffn_down, then the
+output head; 629.8 MB of K-quant weights, the Q4_K_M type mix of llama-quant.cpp
+[U]: attn_v/ffn_down Q6_K in the 10 use_more_bits layers, output Q6_K), each GEMV
+including its bit-exact Q8_K activation quantization. Weights are synthetic
+random blocks of the real shapes (no network for the GGUF); activations are
+synthetic f32 vectors per stage; non-matmul ops (norm, rope, attention, swiglu:
+1.5 % of the reference's CPU time, out.folded:122) are not part of the chain.
+The chain runs through the ggml-backend mirror (mi355x_backend_graph_compute):
+q/k/v and gate/up fuse into one launch each, and the 89 launches of a token are
+replayed from one hipGraph.
+
+Multi-GPU (--gpus N under torch.distributed.run): every rank decodes its own
+token stream with its own copy of the weights ("replicas", weak scaling); value
+is the aggregate tokens/s = N*K / max-over-ranks time. `--mode rowsplit` instead
+splits every weight matrix's rows over the ranks and all-gathers each stage's
+output with RCCL (the north_star's row-split path; see DESIGN.md for when it pays).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+for _p in (ROOT, os.path.join(ROOT, "ggml-neon-opt_amd")):
+    if _p not in sys.path:
+        sys.path.insert(0, _p)
+
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import ggml_mi355x as g  # noqa: E402
+
+MODELS = {
+    "tinyllama-1.1b": dict(E=2048, L=22, KV=256, FF=5632, V=32000),
+    "llama-3-8b": dict(E=4096, L=32, KV=1024, FF=14336, V=128256),
+    "llama-3-70b": dict(E=8192, L=80, KV=1024, FF=28672, V=128256),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def use_more_bits(i, n):
+    return i < n // 8 or i >= 7 * n // 8 or (i - n // 8) % 3 == 2
+
+
+def q4km_chain(model):
+    """Per-token GEMV chain: list of stages; a stage is a list of (name, type, K, N)
+    sharing one input vector (fused into one launch)."""
+    m = MODELS[model]
+    E, L, KV, FF, V = m["E"], m["L"], m["KV"], m["FF"], m["V"]
+    big = model == "llama-3-70b"
+    stages = []
+    for i in range(L):
+        mb = use_more_bits(i, L)
+        v_type = g.TYPE_Q6_K if mb else (g.TYPE_Q5_K if big else g.TYPE_Q4_K)
+        stages.append([(f"blk.{i}.attn_q", g.TYPE_Q4_K, E, E), (f"blk.{i}.attn_k", g.TYPE_Q4_K, E, KV),
+                       (f"blk.{i}.attn_v", v_type, E, KV)])
+        stages.append([(f"blk.{i}.attn_output", g.TYPE_Q4_K, E, E)])
+        stages.append([(f"blk.{i}.ffn_gate", g.TYPE_Q4_K, E, FF), (f"blk.{i}.ffn_up", g.TYPE_Q4_K, E, FF)])
+        stages.append([(f"blk.{i}.ffn_down", g.TYPE_Q6_K if mb else g.TYPE_Q4_K, FF, E)])
+    stages.append([("output", g.TYPE_Q6_K, E, V)])
+    return stages
+
+
+def random_kquant(type_, N, K, gen, dev):
+    """Random valid K-quant rows generated on the device (every qs/scales byte is
+    legal; d/dmin fp16 in [2^-14, 2^-6], never NaN/Inf)."""
+    nb = K // 256
+    B = g.BLOCK_BYTES[type_]
+    w = torch.randint(0, 256, (N, nb, B), dtype=torch.uint8, device=dev, generator=gen)
+
+    def f16():
+        r = torch.rand((N, nb), device=dev, generator=gen) * (2.0 ** -6 - 2.0 ** -14) + 2.0 ** -14
+        return r.to(torch.float16).view(torch.uint8).view(N, nb, 2)
+
+    if type_ in (g.TYPE_Q4_K, g.TYPE_Q5_K):
+        w[..., 0:2] = f16()
+        w[..., 2:4] = f16()
+    else:
+        w[..., 208:210] = f16()
+    return w.view(N, nb * B)
+
+
+class Chain:
+    """Weights, inputs and ggml-style MUL_MAT nodes for one rank's token chain."""
+
+    def __init__(self, model, dev, seed, row_shard=None):
+        self.model = model
+        self.stages = q4km_chain(model)
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed)
+        self.w, self.x, self.y, self.nodes, self.keep = [], [], [], [], []
+        self.bytes_per_token = 0
+        self.row_shard = row_shard
+        for stage in self.stages:
+            K = stage[0][2]
+            x = torch.randn(K, device=dev, generator=gen)
+            xt = g.make_tensor(g.TYPE_F32, K, 1, x.data_ptr())
+            self.x.append(x)
+            self.keep.append(xt)
+            ws, ys = [], []
+            for name, typ, K_, N in stage:
+                r0, r1 = (0, N) if row_shard is None else row_shard(N)
+                w = random_kquant(typ, r1 - r0, K_, gen, dev)
+                y = torch.empty(r1 - r0, device=dev)
+                wt = g.make_tensor(typ, K_, r1 - r0, w.data_ptr())
+                node = g.make_tensor(g.TYPE_F32, r1 - r0, 1, y.data_ptr(), op=g.OP_MUL_MAT, src0=wt, src1=xt)
+                self.keep.append(wt)
+                self.nodes.append(node)
+                ws.append((typ, w))
+                ys.append(y)
+                self.bytes_per_token += w.numel()
+            self.w.append(ws)
+            self.y.append(ys)
+        torch.cuda.synchronize()
+
+    def launches(self):
+        return len(self.stages)
+
+
+def timed_kernel_stats(be, chain, tokens):
+    """Per-launch kernel timing (hipExtLaunchKernelGGL events) over `tokens` eager chains."""
+    g.timing_enable(True)
+    for _ in range(tokens):
+        rc = be.graph_compute(chain.nodes, use_graph=False)
+        assert rc == 0, rc
+    rows = g.timing_read()
+    g.timing_enable(False)
+    per = {}
+    for name, nbytes, ms in rows:
+        d = per.setdefault(name, {"launches": 0, "bytes": 0.0, "ms": 0.0})
+        d["launches"] += 1
+        d["bytes"] += nbytes
+        d["ms"] += ms
+    return per
+
+
+def large_gemv(dev, reps=20):
+    """Q4_K decode GEMV at Llama-3 shapes, weight buffers rotated over > 512 MB so
+    the 256 MB Infinity Cache cannot serve them."""
+    out = {}
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(7)
+    for label, K, N in (("llama3-8b ffn_up 4096x14336", 4096, 14336), ("llama3-70b ffn_down 28672x8192", 28672, 8192)):
+        nbytes = N * (K // 256) * 144
+        nbuf = max(2, int(np.ceil(600e6 / nbytes)))
+        ws = [random_kquant(g.TYPE_Q4_K, N, K, gen, dev) for _ in range(nbuf)]
+        x = torch.randn(1, K, device=dev, generator=gen)
+        y = torch.empty(1, N, device=dev)
+        for w in ws:
+            g.mul_mat(g.TYPE_Q4_K, w, K, x, out=y)
+        g.timing_enable(True)
+        for r in range(reps):
+            g.mul_mat(g.TYPE_Q4_K, ws[r % nbuf], K, x, out=y)
+        rows = g.timing_read()
+        g.timing_enable(False)
+        ms = [r[2] for r in rows]
+        b = rows[0][1]
+        out[label] = {"bytes": b, "us_median": float(np.median(ms) * 1e3),
+                      "GBps_median": b / (np.median(ms) * 1e-3) / 1e9,
+                      "frac_median": b / (np.median(ms) * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        del ws
+        torch.cuda.empty_cache()
+    return out
+
+
+def cpu_baseline(chain, seconds):
+    """The oracle's restated ggml mul_mat (NEON-order scalar C, pthreads) on the same
+    chain, timed on this host's cores for a bounded number of tokens."""
+    from oracle import kq_oracle as O
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncores = os.cpu_count() or 1
+    threads = max(1, min(16, ncores))
+    host = [[(typ, w.cpu().numpy()) for typ, w in ws] for ws in chain.w]
+    xs = [x.cpu().numpy()[None] for x in chain.x]
+    O.lib()
+    tokens, t0 = 0, time.perf_counter()
+    while True:
+        for si, ws in enumerate(host):
+            for typ, w in ws:
+                O.mul_mat(typ, w, xs[si], n_threads=threads)
+        tokens += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or tokens >= 50:
+            break
+    return {"value": tokens / el, "unit": "tok/s", "cores": threads, "kind": "port",
+            "sample": f"{tokens} token(s) of the full {chain.model} Q4_K_M matmul chain "
+                      f"({chain.bytes_per_token / 1e6:.1f} MB/token) through the oracle's restated "
+                      f"ggml_compute_forward_mul_mat (quantize_row_q8_K_ref + NEON-order vec_dot, "
+                      f"{threads} pthreads), {el:.1f} s"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=128)
+    ap.add_argument("--warmup", type=int, default=16)
+    ap.add_argument("--model", default="tinyllama-1.1b", choices=sorted(MODELS))
+    ap.add_argument("--mode", default="replicas", choices=["replicas", "rowsplit"])
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-large", action="store_true")
+    ap.add_argument("--no-graph", action="store_true")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl")
+    dev = torch.device(f"cuda:{local}")
+    torch.cuda.set_device(dev)
+    if not g.device_available():
+        raise SystemExit("bench: no gfx950 device or libggml_mi355x.so not loadable")
+
+    def barrier():
+        if world > 1:
+            import torch.distributed as dist
+            dist.barrier()
+
+    if args.mode == "rowsplit" and world > 1:
+        from ggml_mi355x.rowsplit import RowSplitChain
+        runner = RowSplitChain(args.model, dev, rank, world, make_chain=Chain)
+        chain = runner.chain
+        step = runner.step
+        stream = torch.cuda.current_stream()
+    else:
+        chain = Chain(args.model, dev, seed=0x51A7 + rank)
+        be = g.Backend(local)
+        stream = torch.cuda.ExternalStream(be.stream)
+        use_graph = not args.no_graph
+
+        def step():
+            rc = be.graph_compute(chain.nodes, use_graph=use_graph)
+            if rc != 0:
+                raise RuntimeError(f"graph_compute failed: {rc}")
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if args.mode != "rowsplit" or world == 1:
+        be.synchronize()
+    barrier()
+    torch.cuda.synchronize()
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    ev0.record(stream)
+    for _ in range(args.steps):
+        step()
+    ev1.record(stream)
+    torch.cuda.synchronize()
+    if args.mode != "rowsplit" or world == 1:
+        be.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    gpu_ms = ev0.elapsed_time(ev1)
+    t_max = elapsed
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        t_max = float(t.item())
+    tokens_total = args.steps * (world if args.mode == "replicas" else 1)
+    value = tokens_total / t_max
+
+    result = None
+    if rank == 0:
+        # roofline of the dominant kernel, from per-launch kernel timestamps
+        roof = None
+        per = {}
+        if args.mode != "rowsplit" or world == 1:
+            per = timed_kernel_stats(be, chain, tokens=4)
+            dom = max(per, key=lambda k: per[k]["ms"])
+            d = per[dom]
+            ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
+            roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
+                    "launches": d["launches"], "bytes_per_launch": d["bytes"] / d["launches"],
+                    "us_per_launch": d["ms"] * 1e3 / d["launches"]}
+        kernels = {k: {"launches": v["launches"], "us_per_launch": round(v["ms"] * 1e3 / v["launches"], 2),
+                       "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} for k, v in per.items()}
+        large = None if args.no_large or world > 1 else large_gemv(dev)
+        cpu = None
+        if world == 1 and not args.no_cpu_baseline:
+            cpu = cpu_baseline(chain, args.cpu_seconds)
+        wbytes = chain.bytes_per_token * (world if args.mode == "rowsplit" else 1)
+        result = {
+            "metric": "tg128 tok/s + Q4_K GEMV achieved-HBM-GB/s, TinyLlama-1.1B Q4_K_M @1 GPU",
+            "value": round(value, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 4),
+            "higher_is_better": True, "scaling": "weak" if args.mode == "replicas" else "strong",
+            "vs_baseline": None, "dtype": "q4_K/q6_K x q8_K (u4/u6*i8 dot4 -> i32, f32 combine)",
+            "data": "synthetic (random valid K-quant blocks of the real shapes; random f32 activations)",
+            "config": {"workload": f"{args.model} Q4_K_M decode matmul chain (tg, 1 token/step)",
+                       "weights_MB_per_token": round(wbytes / 1e6, 1),
+                       "launches_per_token": chain.launches(),
+                       "parallelism": (f"replicas x{world}" if args.mode == "replicas" else f"rowsplit{world}"),
+                       "hipgraph": not args.no_graph},
+            "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
+            "effective_GBps": round(value * chain.bytes_per_token / 1e9 / (world if args.mode == "replicas" else 1), 1),
+            "roofline": roof,
+            "kernels": kernels,
+            "gemv_large": large,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        import torch.distributed as dist
+        dist.destroy_process_group()
+    return result
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,425 @@
+// kq_api.hip — C-ABI of libggml_mi355x.so: argument checking, launch planning and
+// the ggml-surface mirrors (vec_dot / from_float / mul_mat). Declared in
+// include/ggml_mi355x.h.
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include <hip/hip_ext.h>
+
+#include "kq_common.h"
+#include "kq_internal.h"
+
+namespace kq {
+
+template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
+__global__ void kq_gemv(const GemvArgs a);
+__global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
+
+namespace {
+
+std::once_flag g_dev_once;
+int g_dev_ok = 0;
+int g_num_cus = 256;
+
+void probe_device() {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
+    if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+        fprintf(stderr, "ggml_mi355x: device %d is %s, this library is built for gfx950 only\n", dev,
+                prop.gcnArchName);
+        return;
+    }
+    g_num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    g_dev_ok = 1;
+}
+
+typedef void (*gemv_fn)(const GemvArgs);
+
+template <int NCOL, bool FUSEDQ, bool DEBUG>
+gemv_fn pick_tm(int tmask) {
+    switch (tmask) {
+        case 1: return kq_gemv<NCOL, FUSEDQ, DEBUG, 1>;
+        case 2: return kq_gemv<NCOL, FUSEDQ, DEBUG, 2>;
+        case 4: return kq_gemv<NCOL, FUSEDQ, DEBUG, 4>;
+        default: return kq_gemv<NCOL, FUSEDQ, DEBUG, 7>;
+    }
+}
+
+gemv_fn pick_gemv(int ncol, bool fusedq, bool debug, int tmask) {
+    if (debug) return pick_tm<1, false, true>(tmask);
+    if (fusedq) return pick_tm<1, true, false>(tmask);
+    switch (ncol) {
+        case 1: return pick_tm<1, false, false>(tmask);
+        case 2: return pick_tm<2, false, false>(tmask);
+        case 4: return pick_tm<4, false, false>(tmask);
+        default: return pick_tm<8, false, false>(tmask);
+    }
+}
+
+int type_bit(int type) {
+    return type == Q4_K ? 1 : type == Q5_K ? 2 : type == Q6_K ? 4 : 0;
+}
+
+constexpr size_t kMaxLds = 64 * 1024;
+
+}  // namespace
+
+int device_ok() {
+    std::call_once(g_dev_once, probe_device);
+    return g_dev_ok;
+}
+
+int num_cus() {
+    device_ok();
+    return g_num_cus;
+}
+
+int choose_ncol(int64_t M, int nb) {
+    if (M <= 1) return 1;
+    const int cands[4] = {8, 4, 2, 1};
+    for (int i = 0; i < 4; ++i) {
+        const int nc = cands[i];
+        if (nc > M && nc > 1) continue;
+        if ((size_t)lds_layout(nc, nb).total <= kMaxLds) return nc;
+    }
+    return 1;
+}
+
+// Validates descriptors and fills the launch arguments. Returns MI355X_OK or an error.
+int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int ncol, GemvArgs &a,
+              dim3 &grid, size_t &lds, int &tmask) {
+    if (n_desc < 1 || n_desc > MI355X_MAX_FUSED) return MI355X_E_INVAL;
+    if (K <= 0 || K % QK != 0 || M < 0) return MI355X_E_INVAL;
+    const int64_t nb = K / QK;
+    if (nb > 0x7fffffff / 8) return MI355X_E_INVAL;
+    memset(&a, 0, sizeof(a));
+    a.n_desc = n_desc;
+    a.nb = (int)nb;
+    a.R = nb >= 8 ? 1 : (int)(8 / nb);
+    a.S = nb >= 8 ? (int)((nb + 7) / 8) : 1;
+    a.m_total = (int)M;
+    tmask = 0;
+    int64_t tasks = 0;
+    for (int i = 0; i < n_desc; ++i) {
+        const int bb = block_bytes(d[i].type);
+        if (!bb) return MI355X_E_UNSUPPORTED;
+        if (d[i].n_rows < 0 || d[i].n_rows > 0x7fffffff) return MI355X_E_INVAL;
+        if (d[i].n_rows > 0) {
+            if (!d[i].w || !d[i].y) return MI355X_E_INVAL;
+            if (((uintptr_t)d[i].w & 3u) != 0) return MI355X_E_INVAL;
+            if (d[i].row_stride < (size_t)(nb * bb) || (d[i].row_stride & 1u)) return MI355X_E_INVAL;
+            if (d[i].type != Q6_K && (d[i].row_stride & 3u)) return MI355X_E_INVAL;
+        }
+        a.type[i] = d[i].type;
+        a.n_rows[i] = (int)d[i].n_rows;
+        a.w[i] = (const uint8_t *)d[i].w;
+        a.row_stride[i] = (int64_t)d[i].row_stride;
+        a.y[i] = d[i].y;
+        a.task_prefix[i] = (int)tasks;
+        tasks += (d[i].n_rows + a.R - 1) / a.R;
+        tmask |= type_bit(d[i].type);
+    }
+    if (tasks > 0x7fffffff) return MI355X_E_INVAL;
+    a.task_prefix[n_desc] = (int)tasks;
+    for (int i = n_desc; i < MI355X_MAX_FUSED; ++i) a.task_prefix[i] = (int)tasks;
+    a.tasks_total = (int)tasks;
+    if (tmask != 1 && tmask != 2 && tmask != 4) tmask = 7;
+    const LdsLayout L = lds_layout(ncol, (int)nb);
+    if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
+    lds = (size_t)L.total;
+    const int64_t wgs_needed = (tasks + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    const int64_t cap = (int64_t)num_cus() * 4;
+    grid = dim3((unsigned)(wgs_needed < cap ? (wgs_needed > 0 ? wgs_needed : 1) : cap),
+                (unsigned)((M + ncol - 1) / ncol), 1);
+    return MI355X_OK;
+}
+
+// ------------------------------------------------------------ launch timing
+namespace {
+struct TimedLaunch {
+    std::string kernel;
+    double bytes;
+    hipEvent_t start, stop;
+};
+std::mutex g_tmu;
+bool g_timing = false;
+std::vector<TimedLaunch> g_tlog;
+std::vector<std::pair<hipEvent_t, hipEvent_t>> g_tpool;
+size_t g_tpool_used = 0;
+
+bool capturing(hipStream_t s) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(s, &st) != hipSuccess) return false;
+    return st != hipStreamCaptureStatusNone;
+}
+
+// Returns true (and the events) when this launch should be timed.
+bool timing_slot(hipStream_t s, hipEvent_t &a, hipEvent_t &b) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    if (!g_timing || capturing(s)) return false;
+    if (g_tpool_used == g_tpool.size()) {
+        hipEvent_t e0, e1;
+        if (hipEventCreate(&e0) != hipSuccess) return false;
+        if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return false; }
+        g_tpool.push_back({e0, e1});
+    }
+    a = g_tpool[g_tpool_used].first;
+    b = g_tpool[g_tpool_used].second;
+    ++g_tpool_used;
+    return true;
+}
+
+void timing_log(const char *kernel, double bytes, hipEvent_t a, hipEvent_t b) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_tlog.push_back({kernel, bytes, a, b});
+}
+
+std::string gemv_name(int ncol, bool fusedq, bool debug, int tmask) {
+    return "kq::kq_gemv<" + std::to_string(ncol) + ", " + (fusedq ? "true" : "false") + ", " +
+           (debug ? "true" : "false") + ", " + std::to_string(tmask) + ">";
+}
+
+double gemv_bytes(const GemvArgs &a, bool fusedq) {
+    double w = 0, y = 0;
+    for (int i = 0; i < a.n_desc; ++i) {
+        w += (double)a.n_rows[i] * a.nb * block_bytes(a.type[i]);
+        y += (double)a.n_rows[i] * 4.0 * a.m_total;
+    }
+    const double x = fusedq ? (double)a.nb * QK * 4.0 * a.m_total : (double)a.nb * 292.0 * a.m_total;
+    return w + x + y;
+}
+}  // namespace
+
+int launch_gemv(const GemvArgs &a, dim3 grid, size_t lds, int ncol, bool fusedq, bool debug, int tmask,
+                hipStream_t stream) {
+    if (a.tasks_total == 0 || a.m_total == 0) return MI355X_OK;
+    gemv_fn fn = pick_gemv(ncol, fusedq, debug, tmask);
+    hipEvent_t e0, e1;
+    if (timing_slot(stream, e0, e1)) {
+        hipExtLaunchKernelGGL(fn, grid, dim3(WG_THREADS), (uint32_t)lds, stream, e0, e1, 0, a);
+        timing_log(gemv_name(ncol, fusedq, debug, tmask).c_str(), gemv_bytes(a, fusedq), e0, e1);
+    } else {
+        hipLaunchKernelGGL(fn, grid, dim3(WG_THREADS), lds, stream, a);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
+                    hipStream_t stream) {
+    const int64_t nb = k / QK;
+    const int64_t nblocks = nb * nrows;
+    if (nblocks == 0) return MI355X_OK;
+    const int64_t wgs = (nblocks + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    hipEvent_t e0, e1;
+    if (timing_slot(stream, e0, e1)) {
+        hipExtLaunchKernelGGL(kq_quantize_q8K, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, e0, e1, 0, x,
+                              x_stride_floats, (uint8_t *)y, (int)nb, nblocks);
+        timing_log("kq::kq_quantize_q8K", (double)nblocks * (QK * 4.0 + 292.0), e0, e1);
+    } else {
+        hipLaunchKernelGGL(kq_quantize_q8K, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, x, x_stride_floats,
+                           (uint8_t *)y, (int)nb, nblocks);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+}  // namespace kq
+
+using namespace kq;
+
+extern "C" {
+
+size_t mi355x_row_size(int type, int64_t k) {
+    if (k < 0 || k % QK) return 0;
+    const int64_t nb = k / QK;
+    if (type == MI355X_TYPE_Q8_K) return (size_t)(nb * 292);
+    if (type == MI355X_TYPE_F32) return (size_t)(k * 4);
+    return (size_t)(nb * block_bytes(type));
+}
+
+const char *mi355x_version(void) { return "ggml-mi355x 0.1.0 (gfx950, wave64, K-quant GEMV)"; }
+
+int mi355x_device_available(void) { return device_ok(); }
+
+int mi355x_quantize_q8_K(const float *x, size_t x_stride, void *y, int64_t k, int64_t nrows, void *stream) {
+    if (k <= 0 || k % QK || nrows < 0) return MI355X_E_INVAL;
+    if (nrows == 0) return MI355X_OK;
+    if (!x || !y || (x_stride & 3u) || ((uintptr_t)x & 3u) || ((uintptr_t)y & 3u)) return MI355X_E_INVAL;
+    if (nrows > 1 && x_stride < (size_t)k * 4) return MI355X_E_INVAL;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_quantize(x, (int64_t)(x_stride / 4), y, k, nrows, (hipStream_t)stream);
+}
+
+static void die(const char *fn, const char *msg) {
+    fprintf(stderr, "%s: %s\n", fn, msg);
+    abort();
+}
+
+void mi355x_quantize_row_q8_K(const float *x, void *y, int64_t k) {
+    if (k % QK) die(__func__, "k % QK_K != 0");
+    const int rc = mi355x_quantize_q8_K(x, (size_t)k * 4, y, k, 1, nullptr);
+    if (rc) die(__func__, "launch failed");
+    if (hipStreamSynchronize(nullptr) != hipSuccess) die(__func__, "hipStreamSynchronize failed");
+}
+
+size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, int64_t ne11) {
+    (void)ne01;
+    if (!block_bytes(src0_type) || ne00 <= 0 || ne00 % QK || ne11 < 0) return 0;
+    if (ne11 <= 1) return 0;
+    const size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * 292;
+    return (bytes + 255) & ~(size_t)255;
+}
+
+int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
+                      const void *src1_q8, int64_t ne11, size_t nb11, float *dst, size_t nb1, void *stream) {
+    if (ne11 < 0 || ne01 < 0) return MI355X_E_INVAL;
+    if (ne11 == 0 || ne01 == 0) return MI355X_OK;
+    if (!src1_q8 || ((uintptr_t)src1_q8 & 3u) || (nb11 & 3u) || ((uintptr_t)dst & 3u) || (nb1 & 3u))
+        return MI355X_E_INVAL;
+    if (ne00 <= 0 || ne00 % QK) return MI355X_E_INVAL;
+    if (ne11 > 1 && (nb11 < (size_t)(ne00 / QK) * 292 || nb1 < (size_t)ne01 * 4)) return MI355X_E_INVAL;
+    if (ne11 > 0x7fffffff) return MI355X_E_INVAL;
+    mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
+    const int ncol = choose_ncol(ne11, (int)(ne00 / QK));
+    GemvArgs a;
+    dim3 grid;
+    size_t lds;
+    int tmask;
+    int rc = plan_gemv(&d, 1, ne00, ne11, ncol, a, grid, lds, tmask);
+    if (rc) return rc;
+    a.xq = (const uint8_t *)src1_q8;
+    a.xq_col_stride = (int64_t)nb11;
+    a.y_col_stride[0] = (int64_t)(nb1 / 4);
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_gemv(a, grid, lds, ncol, false, false, tmask, (hipStream_t)stream);
+}
+
+int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01, const float *src1,
+                   int64_t ne11, size_t nb11, float *dst, size_t nb1, void *workspace, size_t workspace_size,
+                   void *stream) {
+    if (ne11 < 0 || ne01 < 0 || ne00 <= 0 || ne00 % QK) return MI355X_E_INVAL;
+    if (!block_bytes(src0_type)) return MI355X_E_UNSUPPORTED;
+    if (ne11 == 0 || ne01 == 0) return MI355X_OK;
+    if (!src1 || ((uintptr_t)src1 & 3u) || (nb11 & 3u) || !dst || ((uintptr_t)dst & 3u) || (nb1 & 3u))
+        return MI355X_E_INVAL;
+    if (ne11 > 1 && (nb11 < (size_t)ne00 * 4 || nb1 < (size_t)ne01 * 4)) return MI355X_E_INVAL;
+    if (ne11 == 1) {
+        mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
+        GemvArgs a;
+        dim3 grid;
+        size_t lds;
+        int tmask;
+        int rc = plan_gemv(&d, 1, ne00, 1, 1, a, grid, lds, tmask);
+        if (rc) return rc;
+        a.x = src1;
+        a.x_col_stride = (int64_t)(nb11 / 4);
+        a.y_col_stride[0] = (int64_t)(nb1 / 4);
+        if (!device_ok()) return MI355X_E_NODEVICE;
+        return launch_gemv(a, grid, lds, 1, true, false, tmask, (hipStream_t)stream);
+    }
+    const size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
+    if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    int rc = launch_quantize(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream);
+    if (rc) return rc;
+    const size_t q8_row = (size_t)(ne00 / QK) * 292;
+    return mi355x_mul_mat_q8(src0_type, src0, ne00, ne01, nb01, workspace, ne11, q8_row, dst, nb1, stream);
+}
+
+int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k, void *stream) {
+    if (!descs || !x || ((uintptr_t)x & 3u)) return MI355X_E_INVAL;
+    GemvArgs a;
+    dim3 grid;
+    size_t lds;
+    int tmask;
+    int rc = plan_gemv(descs, n_desc, k, 1, 1, a, grid, lds, tmask);
+    if (rc) return rc;
+    for (int i = 0; i < n_desc; ++i)
+        if (descs[i].y && ((uintptr_t)descs[i].y & 3u)) return MI355X_E_INVAL;
+    a.x = x;
+    a.x_col_stride = k;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_gemv(a, grid, lds, 1, true, false, tmask, (hipStream_t)stream);
+}
+
+int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
+                                const void *src1_q8, int32_t *out, void *stream) {
+    if (!out || !src1_q8 || ((uintptr_t)src1_q8 & 3u)) return MI355X_E_INVAL;
+    if (ne01 == 0) return MI355X_OK;
+    // the DEBUG kernel stores only the partials; dst is a placeholder
+    const int64_t nb = ne00 / QK;
+    float *dst = (float *)out;
+    mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
+    GemvArgs a;
+    dim3 grid;
+    size_t lds;
+    int tmask;
+    int rc = plan_gemv(&d, 1, ne00, 1, 1, a, grid, lds, tmask);
+    if (rc) return rc;
+    a.xq = (const uint8_t *)src1_q8;
+    a.xq_col_stride = (int64_t)(nb * 292);
+    a.dbg = out;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_gemv(a, grid, lds, 1, false, true, tmask, (hipStream_t)stream);
+}
+
+int mi355x_timing_enable(int enable) {
+    std::lock_guard<std::mutex> lk(g_tmu);
+    g_timing = enable != 0;
+    g_tlog.clear();
+    g_tpool_used = 0;
+    return MI355X_OK;
+}
+
+int mi355x_timing_read(mi355x_launch_timing *out, int max) {
+    if (hipDeviceSynchronize() != hipSuccess) return MI355X_E_NODEVICE;
+    std::lock_guard<std::mutex> lk(g_tmu);
+    const int n = (int)g_tlog.size();
+    for (int i = 0; i < n && i < max && out; ++i) {
+        memset(out[i].kernel, 0, sizeof(out[i].kernel));
+        strncpy(out[i].kernel, g_tlog[i].kernel.c_str(), sizeof(out[i].kernel) - 1);
+        out[i].bytes = g_tlog[i].bytes;
+        float ms = 0.f;
+        if (hipEventElapsedTime(&ms, g_tlog[i].start, g_tlog[i].stop) != hipSuccess) ms = -1.f;
+        out[i].ms = ms;
+    }
+    return n;
+}
+
+static void vec_dot_dev(int type, const char *fn, int n, float *s, const void *vx, const void *vy, int nrc) {
+    if (nrc != 1) die(fn, "nrc != 1 unsupported (reference configuration: nrows == 1)");
+    if (n <= 0 || n % QK) die(fn, "n % QK_K != 0");
+    if (!device_ok()) die(fn, "no gfx950 device");
+    const int rc = mi355x_mul_mat_q8(type, vx, n, 1, mi355x_row_size(type, n), vy, 1,
+                                     mi355x_row_size(MI355X_TYPE_Q8_K, n), s, 4, nullptr);
+    if (rc) die(fn, "launch failed");
+    if (hipStreamSynchronize(nullptr) != hipSuccess) die(fn, "hipStreamSynchronize failed");
+}
+
+void mi355x_vec_dot_q4_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx, const void *vy, size_t by,
+                              int nrc) {
+    (void)bs; (void)bx; (void)by;
+    vec_dot_dev(MI355X_TYPE_Q4_K, __func__, n, s, vx, vy, nrc);
+}
+void mi355x_vec_dot_q5_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx, const void *vy, size_t by,
+                              int nrc) {
+    (void)bs; (void)bx; (void)by;
+    vec_dot_dev(MI355X_TYPE_Q5_K, __func__, n, s, vx, vy, nrc);
+}
+void mi355x_vec_dot_q6_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx, const void *vy, size_t by,
+                              int nrc) {
+    (void)bs; (void)bx; (void)by;
+    vec_dot_dev(MI355X_TYPE_Q6_K, __func__, n, s, vx, vy, nrc);
+}
+
+}  // extern "C"

@@ -1,0 +1,67 @@
+// kq_common.h — shared device/host definitions for the gfx950 K-quant kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "ggml_mi355x.h"
+
+namespace kq {
+
+constexpr int QK = 256;
+constexpr int WAVE = 64;
+constexpr int WG_THREADS = 256;     // 4 waves per workgroup
+constexpr int WAVES_PER_WG = WG_THREADS / WAVE;
+constexpr int LANES_PER_BLOCK = 8;  // 8 lanes cooperate on one superblock
+constexpr int BLOCKS_PER_STEP = WAVE / LANES_PER_BLOCK;  // 8 superblocks per wave-step
+constexpr int ACT_QS_STRIDE = 272;  // LDS bytes per activation superblock (256 + 16 pad)
+constexpr int MAX_NCOL = 8;
+
+constexpr int Q4_K = MI355X_TYPE_Q4_K;
+constexpr int Q5_K = MI355X_TYPE_Q5_K;
+constexpr int Q6_K = MI355X_TYPE_Q6_K;
+
+__host__ __device__ constexpr int block_bytes(int type) {
+    return type == Q4_K ? 144 : type == Q5_K ? 176 : type == Q6_K ? 210 : 0;
+}
+
+// Argument block of the GEMV / small-M kernel (passed by value).
+struct GemvArgs {
+    int n_desc;
+    int nb;           // K / 256
+    int R;            // rows per task (1 when nb >= 8, else floor(8/nb))
+    int S;            // wave-steps per task
+    int m_total;      // activation columns in total (grid.y covers ceil(m_total/NCOL))
+    int tasks_total;
+    int task_prefix[MI355X_MAX_FUSED + 1];
+    int type[MI355X_MAX_FUSED];
+    int n_rows[MI355X_MAX_FUSED];
+    const uint8_t *w[MI355X_MAX_FUSED];
+    int64_t row_stride[MI355X_MAX_FUSED];  // bytes
+    float *y[MI355X_MAX_FUSED];
+    int64_t y_col_stride[MI355X_MAX_FUSED];  // floats between dst columns
+    const float *x;       // f32 input (FUSEDQ): column j at x + j*x_col_stride
+    int64_t x_col_stride; // floats
+    const uint8_t *xq;    // Q8_K input (!FUSEDQ): column j at xq + j*xq_col_stride
+    int64_t xq_col_stride; // bytes
+    int32_t *dbg;         // debug partials (DEBUG builds of the kernel only)
+};
+
+// LDS layout of one workgroup (dynamic shared memory).
+struct LdsLayout {
+    int act_qs, act_bs, act_d, recs, total;
+};
+
+__host__ __device__ inline LdsLayout lds_layout(int ncol, int nb) {
+    LdsLayout L;
+    L.act_qs = 0;
+    L.act_bs = ncol * nb * ACT_QS_STRIDE;
+    L.act_d = L.act_bs + ncol * nb * 32;
+    int recs = L.act_d + ncol * nb * 4;
+    recs = (recs + 15) & ~15;
+    L.recs = recs;
+    L.total = recs + WAVES_PER_WG * ncol * BLOCKS_PER_STEP * 16;
+    return L;
+}
+
+}  // namespace kq

@@ -1,0 +1,490 @@
+// kq_kernels.hip — gfx950 (CDNA4, wave64) kernels for the ggml K-quant MUL_MAT hot path.
+//
+// Replaces, on the device, the reference's
+//   ggml_vec_dot_q4_K_q8_K (NEON, README.md:686-779; optimized README.md:1455-1480),
+//   ggml_vec_dot_q6_K_q8_K (README.md:369, out.folded:160), the Q5_K sibling,
+//   quantize_row_q8_K_ref (out.folded:184-186) and the row loop of
+//   ggml_compute_forward_mul_mat / _one_chunk (README.md:136-137, ggml-cpu.c:1389/:1194).
+//
+// Numerics contract: every integer quantity (Q8_K qs/bsums/d, 6-bit scale and
+// min unpack, nibble x int8 dots, bsums x mins) is bit-exact; the per-row fp32
+// accumulation is carried out in superblock order with exactly the reference's
+// operations (fmsub/fmadd, README.md:551/:614), so outputs are bit-identical to
+// the reference NEON function. The kernel file is compiled with
+// -ffp-contract=off: only the explicit fmaf() calls fuse.
+//
+// Work decomposition (decode GEMV, HBM-bound): 8 lanes own one 144-B superblock
+// (lane p reads qs[16p..16p+16) with one 16-B load plus the 16-B header), so one
+// wave-step streams 8 consecutive superblocks (1152 B) of a row. The activation
+// row is quantized to Q8_K once per workgroup straight into LDS; each lane
+// dots its 32 nibbles against 2 x 16 B of LDS activations with v_dot4_i32_i8,
+// the 8 lanes reduce with 3 DPP adds, and the group leader drops
+// {sumi, summins, d, dmin} into a per-wave LDS record. One lane per row then
+// runs the serial fp32 chain over the records in superblock order.
+#include "kq_common.h"
+
+namespace kq {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f32x4a __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ u32x4 gload16(const uint8_t *p) { return *(const u32x4a *)p; }
+__device__ __forceinline__ uint32_t gload4(const uint8_t *p) { return *(const uint32_t *)p; }
+
+__device__ __forceinline__ float h2f(uint32_t h16) {
+    _Float16 h;
+    uint16_t b = (uint16_t)h16;
+    __builtin_memcpy(&h, &b, 2);
+    return (float)h;
+}
+
+__device__ __forceinline__ int sdot4(uint32_t a, uint32_t b, int c) {
+    return __builtin_amdgcn_sdot4((int)a, (int)b, c, false);
+}
+
+// Sum over the 8 lanes of an aligned lane-octet (DPP only, no LDS).
+__device__ __forceinline__ int octet_sum(int v) {
+    v += __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);   // quad_perm [1,0,3,2]
+    v += __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);   // quad_perm [2,3,0,1]
+    v += __builtin_amdgcn_mov_dpp(v, 0x141, 0xF, 0xF, true);  // row_half_mirror
+    return v;
+}
+
+__device__ __forceinline__ void wave_lds_fence() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ __forceinline__ float wave_max_f32(float v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+    return v;
+}
+__device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
+        v = w < v ? w : v;
+    }
+    return v;
+}
+
+// nearest_int(iscale * x) with the multiply-add contracted (aarch64 gcc build of
+// quantize_row_q8_K_ref): 12582912.f = 1.5*2^23 rounds to integer, RNE.
+__device__ __forceinline__ int nearest_int_fused(float iscale, float x) {
+    const float v = __builtin_fmaf(iscale, x, 12582912.f);
+    const int i = __float_as_int(v);
+    return (i & 0x007fffff) - 0x00400000;
+}
+
+// One Q8_K superblock quantized by one wave (quantize_row_q8_K_ref semantics):
+// lane l owns x[4l..4l+3]. Returns packed qs of the lane, the 16-element bsum
+// (valid on every lane of each lane-quad), and d (uniform).
+struct Q8Lane {
+    uint32_t qs4;
+    int bsum;
+    float d;
+};
+
+__device__ __forceinline__ Q8Lane quant_block_wave(const float *xb, int lane) {
+    const f32x4a v = *(const f32x4a *)(xb + 4 * lane);
+    const float a0 = fabsf(v.x), a1 = fabsf(v.y), a2 = fabsf(v.z), a3 = fabsf(v.w);
+    // amax; NaN never wins (fmaxf drops NaN, as `ax > amax` is false for NaN)
+    const float m = wave_max_f32(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
+    Q8Lane r;
+    if (m == 0.f) {  // wave-uniform: the `if (!amax)` branch
+        r.qs4 = 0;
+        r.bsum = 0;
+        r.d = 0.f;
+        return r;
+    }
+    // first index j with |x_j| == amax (serial `if (ax > amax)` keeps the first);
+    // key = 2*j + sign(x_j)
+    uint32_t key = 0xffffffffu;
+    const uint32_t base = 8u * (uint32_t)lane;
+    if (a3 == m) key = base + 6u + (v.w < 0.f ? 1u : 0u);
+    if (a2 == m) key = base + 4u + (v.z < 0.f ? 1u : 0u);
+    if (a1 == m) key = base + 2u + (v.y < 0.f ? 1u : 0u);
+    if (a0 == m) key = base + 0u + (v.x < 0.f ? 1u : 0u);
+    key = wave_min_u32(key);
+    const float maxv = (key & 1u) ? -m : m;
+    const float iscale = -127.f / maxv;  // correctly rounded (-fhip-fp32-correctly-rounded-divide-sqrt)
+    int q0 = nearest_int_fused(iscale, v.x);
+    int q1 = nearest_int_fused(iscale, v.y);
+    int q2 = nearest_int_fused(iscale, v.z);
+    int q3 = nearest_int_fused(iscale, v.w);
+    // y.qs[j] = MIN(127, v) stored as int8 (truncating, as the C assignment does when
+    // an overflowed iscale drives v below -128); bsums sum the stored int8 values.
+    q0 = (int)(int8_t)(q0 < 127 ? q0 : 127);
+    q1 = (int)(int8_t)(q1 < 127 ? q1 : 127);
+    q2 = (int)(int8_t)(q2 < 127 ? q2 : 127);
+    q3 = (int)(int8_t)(q3 < 127 ? q3 : 127);
+    r.qs4 = (uint32_t)(q0 & 0xff) | ((uint32_t)(q1 & 0xff) << 8) | ((uint32_t)(q2 & 0xff) << 16) |
+            ((uint32_t)(q3 & 0xff) << 24);
+    int s = q0 + q1 + q2 + q3;
+    s += __builtin_amdgcn_mov_dpp(s, 0xB1, 0xF, 0xF, true);
+    s += __builtin_amdgcn_mov_dpp(s, 0x4E, 0xF, 0xF, true);
+    r.bsum = s;
+    r.d = 1.f / iscale;
+    return r;
+}
+
+// ------------------------------------------------------------------ Q8_K quantize kernel
+// One wave per superblock; y rows are contiguous (nb blocks of 292 B).
+__global__ void __launch_bounds__(WG_THREADS) kq_quantize_q8K(const float *__restrict__ x, int64_t x_stride,
+                                                              uint8_t *__restrict__ y, int nb, int64_t nblocks) {
+    const int lane = threadIdx.x & 63;
+    const int64_t bi = (int64_t)blockIdx.x * WAVES_PER_WG + (threadIdx.x >> 6);
+    if (bi >= nblocks) return;
+    const int64_t row = bi / nb;
+    const int b = (int)(bi - row * nb);
+    const float *xb = x + row * x_stride + (int64_t)b * QK;
+    const Q8Lane q = quant_block_wave(xb, lane);
+    uint8_t *yb = y + bi * 292;
+    *(uint32_t *)(yb + 4 + 4 * lane) = q.qs4;
+    if ((lane & 3) == 0) *(int16_t *)(yb + 260 + 2 * (lane >> 2)) = (int16_t)q.bsum;
+    if (lane == 0) *(float *)yb = q.d;
+}
+
+// ------------------------------------------------------------------ per-type lane kernels
+// Register image of one lane's share of one superblock.
+struct Regs {
+    u32x4 a, b, c;
+    uint32_t e0, e1, e2, dh;
+};
+
+// Q4_K: lane p owns qs[16p, 16p+16): elements 64j+16h+[0,16) (low nibbles,
+// sub-block 2j) and 64j+32+16h+[0,16) (high nibbles, sub-block 2j+1), j=p>>1, h=p&1.
+__device__ __forceinline__ void load_q4K(Regs &r, const uint8_t *blk, int p) {
+    r.a = gload16(blk);               // d, dmin, scales[0..11]
+    r.b = gload16(blk + 16 + 16 * p); // qs
+}
+__device__ __forceinline__ void load_q5K(Regs &r, const uint8_t *blk, int p) {
+    r.a = gload16(blk);                      // d, dmin, scales
+    r.b = gload16(blk + 16 + 16 * (p & 1));  // qh[16h .. 16h+16)
+    r.c = gload16(blk + 48 + 16 * p);        // qs
+}
+// Q6_K blocks are 210 B, so odd blocks sit at 2 mod 4: load 4-B aligned words
+// (plus one extra word) and realign with v_alignbyte. Every word read lies
+// inside the block.
+__device__ __forceinline__ void load_q6K(Regs &r, const uint8_t *blk, int p) {
+    const uint32_t s = (uint32_t)((uintptr_t)blk & 3u);  // 0 or 2
+    const uint8_t *b4 = blk - s;
+    const int n = p >> 2, part = p & 3;
+    const int fql = 16 * p;
+    const int fqh = 128 + 32 * n + 16 * (part & 1);
+    r.a = gload16(b4 + fql);
+    r.e0 = gload4(b4 + fql + 12 + 2 * s);
+    r.b = gload16(b4 + fqh);
+    r.e1 = gload4(b4 + fqh + 12 + 2 * s);
+    r.c = gload16(b4 + 192);
+    r.e2 = gload4(b4 + 204 + 2 * s);
+    r.dh = *(const uint16_t *)(blk + 208);
+}
+
+__device__ __forceinline__ u32x4 realign(u32x4 v, uint32_t ex, uint32_t s) {
+    u32x4 o;
+    o.x = __builtin_amdgcn_alignbyte(v.y, v.x, s);
+    o.y = __builtin_amdgcn_alignbyte(v.z, v.y, s);
+    o.z = __builtin_amdgcn_alignbyte(v.w, v.z, s);
+    o.w = __builtin_amdgcn_alignbyte(ex, v.w, s);
+    return o;
+}
+
+__device__ __forceinline__ int dot16(u32x4 q, u32x4 a) {
+    int d = sdot4(q.x, a.x, 0);
+    d = sdot4(q.y, a.y, d);
+    d = sdot4(q.z, a.z, d);
+    d = sdot4(q.w, a.w, d);
+    return d;
+}
+
+// 6-bit scales/mins of a Q4_K/Q5_K header (get_scale_min_k4 / README.md:732-739).
+struct ScMn {
+    int sc_lo, sc_hi, mn;
+};
+__device__ __forceinline__ ScMn scales_k4(u32x4 hdr, int p) {
+    const int j = p >> 1;
+    const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
+    const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
+    const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
+    const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
+    const uint32_t sw = (j < 2) ? s03 : s47;
+    const uint32_t sh = (uint32_t)((2 * j) & 3) * 8u;
+    ScMn r;
+    r.sc_lo = (int)((sw >> sh) & 0xffu);
+    r.sc_hi = (int)((sw >> (sh + 8u)) & 0xffu);
+    const uint32_t mw = (p < 4) ? m03 : m47;
+    r.mn = (int)((mw >> ((uint32_t)(p & 3) * 8u)) & 0xffu);
+    return r;
+}
+
+// Lane partials against one activation column held in LDS.
+//   aq: LDS qs of the activation superblock (256 B), abs: its 16 bsums.
+__device__ __forceinline__ void lane_q4K(const Regs &r, const uint8_t *aq, const int16_t *abs, int p,
+                                         int &isum, int &imin) {
+    const int j = p >> 1, h = p & 1;
+    const ScMn s = scales_k4(r.a, p);
+    const u32x4 alo = *(const u32x4 *)(aq + 64 * j + 16 * h);
+    const u32x4 ahi = *(const u32x4 *)(aq + 64 * j + 32 + 16 * h);
+    const u32x4 lo = r.b & 0x0f0f0f0fu;
+    const u32x4 hi = (r.b >> 4) & 0x0f0f0f0fu;
+    isum = dot16(lo, alo) * s.sc_lo + dot16(hi, ahi) * s.sc_hi;
+    const uint32_t bs2 = *(const uint32_t *)(abs + 2 * p);
+    imin = ((int)(int16_t)(bs2 & 0xffffu) + (int)(int16_t)(bs2 >> 16)) * s.mn;
+}
+
+__device__ __forceinline__ void lane_q5K(const Regs &r, const uint8_t *aq, const int16_t *abs, int p,
+                                         int &isum, int &imin) {
+    const int j = p >> 1, h = p & 1;
+    const ScMn s = scales_k4(r.a, p);
+    const u32x4 alo = *(const u32x4 *)(aq + 64 * j + 16 * h);
+    const u32x4 ahi = *(const u32x4 *)(aq + 64 * j + 32 + 16 * h);
+    const uint32_t sl = (uint32_t)(2 * j), shh = (uint32_t)(2 * j + 1);
+    const u32x4 lo = (r.c & 0x0f0f0f0fu) | (((r.b >> sl) & 0x01010101u) << 4);
+    const u32x4 hi = ((r.c >> 4) & 0x0f0f0f0fu) | (((r.b >> shh) & 0x01010101u) << 4);
+    isum = dot16(lo, alo) * s.sc_lo + dot16(hi, ahi) * s.sc_hi;
+    const uint32_t bs2 = *(const uint32_t *)(abs + 2 * p);
+    imin = ((int)(int16_t)(bs2 & 0xffffu) + (int)(int16_t)(bs2 >> 16)) * s.mn;
+}
+
+__device__ __forceinline__ int sbyte(u32x4 w, int idx) {
+    const uint32_t d = (idx < 4) ? w.x : (idx < 8) ? w.y : (idx < 12) ? w.z : w.w;
+    return (int)(int8_t)((d >> ((uint32_t)(idx & 3) * 8u)) & 0xffu);
+}
+
+// Q6_K lane p: ql[16p..16p+16) of half n=p>>2; part=p&3 selects low/high 32 of the
+// half: low nibbles -> elements 128n+32(part>>1)+16(part&1)+[0,16), high nibbles
+// the same +64; qh bits (part>>1)*2 and +4.
+__device__ __forceinline__ void lane_q6K(const Regs &r, const uint8_t *aq, const int16_t *abs, int p,
+                                         int &isum, int &imin, uint32_t &dh) {
+    const int n = p >> 2, part = p & 3;
+    const u32x4 L = r.a, H = r.b, SC = r.c;
+    const uint32_t shl = (uint32_t)(part >> 1) * 2u;
+    const u32x4 qlo = (L & 0x0f0f0f0fu) | (((H >> shl) & 0x03030303u) << 4);
+    const u32x4 qhi = ((L >> 4) & 0x0f0f0f0fu) | (((H >> (shl + 4u)) & 0x03030303u) << 4);
+    const int elo = 128 * n + 32 * (part >> 1) + 16 * (part & 1);
+    const u32x4 alo = *(const u32x4 *)(aq + elo);
+    const u32x4 ahi = *(const u32x4 *)(aq + elo + 64);
+    const int sb = elo >> 4;
+    isum = dot16(qlo, alo) * sbyte(SC, sb) + dot16(qhi, ahi) * sbyte(SC, sb + 4);
+    const uint32_t bs2 = *(const uint32_t *)(abs + 2 * p);
+    imin = (int)(int16_t)(bs2 & 0xffffu) * sbyte(SC, 2 * p) + (int)(int16_t)(bs2 >> 16) * sbyte(SC, 2 * p + 1);
+    dh = r.dh;
+}
+
+// Per-block record consumed by the fp32 chain.
+struct Rec {
+    int a, b;
+    float c, e;
+};
+
+// The reference's per-superblock fp32 update, by type.
+__device__ __forceinline__ float chain_step(int type, const Rec &r, float s) {
+    if (type == Q4_K) {
+        s = fmaf(-(float)r.b, r.e, s);  // sumf -= dmin * summins   (fmsub, README.md:551)
+        s = fmaf((float)r.a, r.c, s);   // sumf += d * sumi         (fmadd, README.md:614)
+    } else if (type == Q5_K) {
+        const float t = fmaf(r.c, (float)r.a, -(r.e * (float)r.b));  // d*sumi - dmin*sumi_mins
+        s = s + t;
+    } else {                             // Q6_K: sum += d_all*y.d*(isum - 32*isum_mins)
+        s = fmaf(r.c, (float)r.a, s);
+    }
+    return s;
+}
+
+struct StepInfo {
+    int m, row0, rows;
+};
+
+__device__ __forceinline__ StepInfo task_info(const GemvArgs &a, int t) {
+    int m = 0;
+#pragma unroll
+    for (int i = 1; i < MI355X_MAX_FUSED; ++i)
+        if (i < a.n_desc && t >= a.task_prefix[i]) m = i;
+    StepInfo si;
+    si.m = m;
+    si.row0 = (t - a.task_prefix[m]) * a.R;
+    const int left = a.n_rows[m] - si.row0;
+    si.rows = left < a.R ? left : a.R;
+    return si;
+}
+
+// TMASK: bit0 Q4_K, bit1 Q5_K, bit2 Q6_K (types compiled into this instance).
+template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
+__global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int nb = a.nb;
+    const LdsLayout L = lds_layout(NCOL, nb);
+    uint8_t *act_qs = smem + L.act_qs;
+    int16_t *act_bs = (int16_t *)(smem + L.act_bs);
+    float *act_d = (float *)(smem + L.act_d);
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int g = lane >> 3, p = lane & 7;
+    Rec *recs = (Rec *)(smem + L.recs) + wave * NCOL * BLOCKS_PER_STEP;
+
+    const int col0 = blockIdx.y * NCOL;
+    const int ncol = (a.m_total - col0) < NCOL ? (a.m_total - col0) : NCOL;
+
+    const int nwaves = gridDim.x * WAVES_PER_WG;
+    const int wgid = blockIdx.x * WAVES_PER_WG + wave;
+    const int my_tasks = a.tasks_total > wgid ? (a.tasks_total - wgid + nwaves - 1) / nwaves : 0;
+    const int S = a.S, R = a.R;
+    const int Q = my_tasks * S;
+
+    int lane_row = 0, lane_blk = g;
+    if (R > 1) {
+        lane_row = g / nb;
+        lane_blk = g - lane_row * nb;
+    }
+
+    constexpr int U = 4;
+    Regs regs[U];
+
+    auto issue = [&](int q0) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = q0 + u;
+            if (q < Q) {
+                const int k = q / S, s = q - k * S;
+                const StepInfo si = task_info(a, wgid + k * nwaves);
+                const int type = a.type[si.m];
+                const int blk = (R == 1) ? 8 * s + g : lane_blk;
+                const bool valid = (R == 1) ? (blk < nb) : (g < R * nb && lane_row < si.rows);
+                if (valid) {
+                    const uint8_t *bp = a.w[si.m] + (int64_t)(si.row0 + lane_row) * a.row_stride[si.m] +
+                                        (int64_t)blk * block_bytes(type);
+                    if ((TMASK & 1) && type == Q4_K) load_q4K(regs[u], bp, p);
+                    else if ((TMASK & 2) && type == Q5_K) load_q5K(regs[u], bp, p);
+                    else if ((TMASK & 4) && type == Q6_K) load_q6K(regs[u], bp, p);
+                }
+            }
+        }
+    };
+
+    // Weights for the first batch are in flight while the activation is staged.
+    issue(0);
+
+    if (FUSEDQ) {
+        for (int b = wave; b < nb; b += WAVES_PER_WG) {
+            const Q8Lane q = quant_block_wave(a.x + (int64_t)col0 * a.x_col_stride + (int64_t)b * QK, lane);
+            *(uint32_t *)(act_qs + b * ACT_QS_STRIDE + 4 * lane) = q.qs4;
+            if ((lane & 3) == 0) act_bs[b * 16 + (lane >> 2)] = (int16_t)q.bsum;
+            if (lane == 0) act_d[b] = q.d;
+        }
+    } else {
+        const int per_col = nb * 73;
+        for (int i = threadIdx.x; i < ncol * per_col; i += WG_THREADS) {
+            const int c = i / per_col;
+            const int rem = i - c * per_col;
+            const int b = rem / 73;
+            const int dw = rem - b * 73;
+            const uint32_t v = gload4(a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)b * 292 + 4 * dw);
+            const int cb = c * nb + b;
+            if (dw == 0) act_d[cb] = __uint_as_float(v);
+            else if (dw <= 64) *(uint32_t *)(act_qs + cb * ACT_QS_STRIDE + 4 * (dw - 1)) = v;
+            else *(uint32_t *)(act_bs + cb * 16 + 2 * (dw - 65)) = v;
+        }
+    }
+    __syncthreads();
+
+    float acc = 0.f;  // running fp32 chain of this lane's (row, column)
+
+    for (int q0 = 0; q0 < Q; q0 += U) {
+        if (q0 > 0) issue(q0);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int q = q0 + u;
+            if (q >= Q) break;
+            const int k = q / S, s = q - k * S;
+            const StepInfo si = task_info(a, wgid + k * nwaves);
+            const int type = a.type[si.m];
+            const int blk = (R == 1) ? 8 * s + g : lane_blk;
+            const bool valid = (R == 1) ? (blk < nb) : (g < R * nb && lane_row < si.rows);
+            const int cblk = valid ? blk : 0;
+            Regs rr = regs[u];
+            uint32_t q6s = 0;
+            if ((TMASK & 4) && type == Q6_K) {
+                // realign the 2-mod-4 blocks (see load_q6K)
+                const uint8_t *bp = a.w[si.m] + (int64_t)(si.row0 + lane_row) * a.row_stride[si.m] +
+                                    (int64_t)cblk * 210;
+                q6s = (uint32_t)((uintptr_t)bp & 3u);
+                rr.a = realign(rr.a, rr.e0, q6s);
+                rr.b = realign(rr.b, rr.e1, q6s);
+                rr.c = realign(rr.c, rr.e2, q6s);
+            }
+#pragma unroll
+            for (int c = 0; c < NCOL; ++c) {
+                if (c < ncol) {
+                    const int cb = c * nb + cblk;
+                    const uint8_t *aq = act_qs + cb * ACT_QS_STRIDE;
+                    const int16_t *ab = act_bs + cb * 16;
+                    int isum = 0, imin = 0;
+                    uint32_t dh = 0;
+                    if ((TMASK & 1) && type == Q4_K) lane_q4K(rr, aq, ab, p, isum, imin);
+                    else if ((TMASK & 2) && type == Q5_K) lane_q5K(rr, aq, ab, p, isum, imin);
+                    else if ((TMASK & 4) && type == Q6_K) lane_q6K(rr, aq, ab, p, isum, imin, dh);
+                    isum = octet_sum(isum);
+                    imin = octet_sum(imin);
+                    if (p == 0 && valid) {
+                        const float yd = act_d[cb];
+                        Rec rec;
+                        if (type == Q6_K) {
+                            rec.a = isum - 32 * imin;
+                            rec.b = 0;
+                            rec.c = h2f(dh) * yd;
+                            rec.e = 0.f;
+                        } else {
+                            rec.a = isum;
+                            rec.b = imin;
+                            rec.c = yd * h2f(rr.a.x & 0xffffu);
+                            rec.e = yd * h2f(rr.a.x >> 16);
+                        }
+                        recs[c * BLOCKS_PER_STEP + g] = rec;
+                        if (DEBUG && c == 0) {
+                            const int64_t o = ((int64_t)(si.row0 + lane_row) * nb + blk) * 2;
+                            a.dbg[o] = isum;
+                            a.dbg[o + 1] = imin;
+                        }
+                    }
+                }
+            }
+            wave_lds_fence();
+            // serial fp32 chain, superblock order
+            if (R == 1) {
+                if (lane < ncol) {
+                    if (s == 0) acc = 0.f;
+                    const int cnt = (nb - 8 * s) < 8 ? (nb - 8 * s) : 8;
+                    for (int i = 0; i < cnt; ++i) acc = chain_step(type, recs[lane * BLOCKS_PER_STEP + i], acc);
+                    if (!DEBUG && s == S - 1) a.y[si.m][(int64_t)lane * a.y_col_stride[si.m] + si.row0] = acc;
+                }
+            } else {
+                const int c = lane / R, r = lane - c * R;
+                if (!DEBUG && c < ncol && r < si.rows) {
+                    float v = 0.f;
+                    for (int i = 0; i < nb; ++i) v = chain_step(type, recs[c * BLOCKS_PER_STEP + r * nb + i], v);
+                    a.y[si.m][(int64_t)c * a.y_col_stride[si.m] + si.row0 + r] = v;
+                }
+            }
+            wave_lds_fence();
+        }
+    }
+}
+
+// ------------------------------------------------------------------ explicit instances
+#define KQ_GEMV_INST(NC, FQ, DB, TM) \
+    template __global__ void kq_gemv<NC, FQ, DB, TM>(const GemvArgs a);
+
+#define KQ_GEMV_INST_TM(NC, FQ, DB) \
+    KQ_GEMV_INST(NC, FQ, DB, 1) KQ_GEMV_INST(NC, FQ, DB, 2) KQ_GEMV_INST(NC, FQ, DB, 4) KQ_GEMV_INST(NC, FQ, DB, 7)
+
+KQ_GEMV_INST_TM(1, true, false)
+KQ_GEMV_INST_TM(1, false, false)
+KQ_GEMV_INST_TM(2, false, false)
+KQ_GEMV_INST_TM(4, false, false)
+KQ_GEMV_INST_TM(8, false, false)
+KQ_GEMV_INST_TM(1, false, true)
+
+}  // namespace kq

@@ -1,0 +1,330 @@
+"""ggml_mi355x — Python host mirror of the ggml K-quant MUL_MAT operator surface,
+bound to libggml_mi355x.so (HIP, gfx950) through its C-ABI (include/ggml_mi355x.h).
+
+The names follow ggml: ``vec_dot_q4_K_q8_K`` (ggml_vec_dot_t, README.md:449),
+``quantize_row_q8_K`` (from_float of Q8_K), ``mul_mat`` (ggml_compute_forward_mul_mat,
+ggml-cpu.c:1389) and a ``Backend`` mirroring ggml-backend's device interface
+(graph_compute, ggml-cpu.cpp:186). PyTorch is only plumbing here: device
+buffers and the current HIP stream handle. There is no CPU fallback: if the
+shared library or a gfx950 device is missing, every compute call raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+PKG_ROOT = os.path.dirname(HERE)
+LIB_PATH = os.path.join(PKG_ROOT, "lib", "libggml_mi355x.so")
+
+TYPE_F32, TYPE_Q4_K, TYPE_Q5_K, TYPE_Q6_K, TYPE_Q8_K = 0, 12, 13, 14, 15
+QK_K = 256
+BLOCK_BYTES = {TYPE_Q4_K: 144, TYPE_Q5_K: 176, TYPE_Q6_K: 210, TYPE_Q8_K: 292}
+TYPE_NAMES = {TYPE_Q4_K: "q4_K", TYPE_Q5_K: "q5_K", TYPE_Q6_K: "q6_K", TYPE_Q8_K: "q8_K", TYPE_F32: "f32"}
+MAX_FUSED = 4
+OP_NONE, OP_MUL_MAT = 0, 1
+
+# Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).
+EXPORTED_SYMBOLS = (
+    "mi355x_row_size", "mi355x_version", "mi355x_device_available",
+    "mi355x_quantize_row_q8_K", "mi355x_vec_dot_q4_K_q8_K", "mi355x_vec_dot_q5_K_q8_K",
+    "mi355x_vec_dot_q6_K_q8_K", "mi355x_quantize_q8_K", "mi355x_mul_mat_workspace_size",
+    "mi355x_mul_mat", "mi355x_mul_mat_q8", "mi355x_gemv_fused", "mi355x_debug_block_partials",
+    "mi355x_backend_init", "mi355x_backend_free", "mi355x_backend_name", "mi355x_backend_stream",
+    "mi355x_backend_alloc", "mi355x_backend_free_buffer", "mi355x_backend_set_tensor",
+    "mi355x_backend_get_tensor", "mi355x_backend_synchronize", "mi355x_backend_supports_op",
+    "mi355x_backend_graph_compute", "mi355x_timing_enable", "mi355x_timing_read",
+)
+
+
+class Mi355xError(RuntimeError):
+    pass
+
+
+class GemvDesc(ctypes.Structure):
+    _fields_ = [("type", ctypes.c_int), ("w", ctypes.c_void_p), ("n_rows", ctypes.c_int64),
+                ("row_stride", ctypes.c_size_t), ("y", ctypes.c_void_p)]
+
+
+class LaunchTiming(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_char * 96), ("bytes", ctypes.c_double), ("ms", ctypes.c_float)]
+
+
+class Tensor(ctypes.Structure):
+    pass
+
+
+Tensor._fields_ = [("type", ctypes.c_int), ("op", ctypes.c_int), ("ne", ctypes.c_int64 * 4),
+                   ("nb", ctypes.c_size_t * 4), ("src", ctypes.POINTER(Tensor) * 2), ("data", ctypes.c_void_p)]
+
+_lib = None
+
+
+def lib():
+    """Load libggml_mi355x.so (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise Mi355xError(f"{LIB_PATH} missing: run __graft_entry__.build() (make -C ggml-neon-opt_amd)")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, sz, i64, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int
+    L.mi355x_row_size.argtypes = [i32, i64]
+    L.mi355x_row_size.restype = sz
+    L.mi355x_version.restype = ctypes.c_char_p
+    L.mi355x_device_available.restype = i32
+    L.mi355x_quantize_row_q8_K.argtypes = [vp, vp, i64]
+    for n in ("q4_K", "q5_K", "q6_K"):
+        getattr(L, f"mi355x_vec_dot_{n}_q8_K").argtypes = [i32, vp, sz, vp, sz, vp, sz, i32]
+    L.mi355x_quantize_q8_K.argtypes = [vp, sz, vp, i64, i64, vp]
+    L.mi355x_quantize_q8_K.restype = i32
+    L.mi355x_mul_mat_workspace_size.argtypes = [i32, i64, i64, i64]
+    L.mi355x_mul_mat_workspace_size.restype = sz
+    L.mi355x_mul_mat.argtypes = [i32, vp, i64, i64, sz, vp, i64, sz, vp, sz, vp, sz, vp]
+    L.mi355x_mul_mat.restype = i32
+    L.mi355x_mul_mat_q8.argtypes = [i32, vp, i64, i64, sz, vp, i64, sz, vp, sz, vp]
+    L.mi355x_mul_mat_q8.restype = i32
+    L.mi355x_gemv_fused.argtypes = [ctypes.POINTER(GemvDesc), i32, vp, i64, vp]
+    L.mi355x_gemv_fused.restype = i32
+    L.mi355x_debug_block_partials.argtypes = [i32, vp, i64, i64, sz, vp, vp, vp]
+    L.mi355x_debug_block_partials.restype = i32
+    L.mi355x_backend_init.argtypes = [i32]
+    L.mi355x_backend_init.restype = vp
+    L.mi355x_backend_free.argtypes = [vp]
+    L.mi355x_backend_name.argtypes = [vp]
+    L.mi355x_backend_name.restype = ctypes.c_char_p
+    L.mi355x_backend_stream.argtypes = [vp]
+    L.mi355x_backend_stream.restype = vp
+    L.mi355x_backend_alloc.argtypes = [vp, sz]
+    L.mi355x_backend_alloc.restype = vp
+    L.mi355x_backend_free_buffer.argtypes = [vp, vp]
+    L.mi355x_backend_set_tensor.argtypes = [vp, vp, vp, sz]
+    L.mi355x_backend_set_tensor.restype = i32
+    L.mi355x_backend_get_tensor.argtypes = [vp, vp, vp, sz]
+    L.mi355x_backend_get_tensor.restype = i32
+    L.mi355x_backend_synchronize.argtypes = [vp]
+    L.mi355x_backend_synchronize.restype = i32
+    L.mi355x_backend_supports_op.argtypes = [ctypes.POINTER(Tensor)]
+    L.mi355x_backend_supports_op.restype = i32
+    L.mi355x_backend_graph_compute.argtypes = [vp, ctypes.POINTER(ctypes.POINTER(Tensor)), i32, i32]
+    L.mi355x_backend_graph_compute.restype = i32
+    L.mi355x_timing_enable.argtypes = [i32]
+    L.mi355x_timing_enable.restype = i32
+    L.mi355x_timing_read.argtypes = [ctypes.POINTER(LaunchTiming), i32]
+    L.mi355x_timing_read.restype = i32
+    _lib = L
+    return L
+
+
+def timing_enable(enable=True):
+    """Start (and clear) or stop per-launch kernel timing (hipExtLaunchKernelGGL events)."""
+    lib().mi355x_timing_enable(1 if enable else 0)
+
+
+def timing_read():
+    """Synchronize the device; return [(kernel_name, algorithmic_bytes, ms), ...]."""
+    n = lib().mi355x_timing_read(None, 0)
+    if n < 0:
+        raise Mi355xError(f"mi355x_timing_read failed ({n})")
+    buf = (LaunchTiming * max(n, 1))()
+    n = lib().mi355x_timing_read(buf, n)
+    return [(buf[i].kernel.decode(), buf[i].bytes, buf[i].ms) for i in range(n)]
+
+
+def version() -> str:
+    return lib().mi355x_version().decode()
+
+
+def device_available() -> bool:
+    return bool(lib().mi355x_device_available())
+
+
+def row_size(type_: int, k: int) -> int:
+    return int(lib().mi355x_row_size(type_, k))
+
+
+def _check(rc: int, what: str):
+    if rc != 0:
+        raise Mi355xError(f"{what} failed with status {rc}")
+
+
+def _require_device():
+    if not device_available():
+        raise Mi355xError("no gfx950 device visible: the HIP path cannot run (there is no CPU fallback)")
+
+
+def _stream(stream):
+    if stream is not None:
+        return ctypes.c_void_p(stream)
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+# ----------------------------------------------------------- tensor helpers
+def _torch():
+    import torch
+    return torch
+
+
+def quantize_q8_K(x, out=None, stream=None):
+    """x: (M, K) float32 cuda tensor -> (M, K/256*292) uint8 cuda tensor (Q8_K rows)."""
+    torch = _torch()
+    _require_device()
+    if x.dim() == 1:
+        x = x[None]
+    assert x.dtype == torch.float32 and x.is_cuda and x.stride(1) == 1
+    M, K = x.shape
+    if out is None:
+        out = torch.empty((M, K // QK_K * 292), dtype=torch.uint8, device=x.device)
+    _check(lib().mi355x_quantize_q8_K(x.data_ptr(), x.stride(0) * 4, out.data_ptr(), K, M, _stream(stream)),
+           "mi355x_quantize_q8_K")
+    return out
+
+
+def mul_mat(type_, w, K, x, out=None, workspace=None, stream=None):
+    """dst (M, N) = mul_mat(w (N rows of `type_`), x (M, K) f32), ggml semantics."""
+    torch = _torch()
+    _require_device()
+    if x.dim() == 1:
+        x = x[None]
+    M = x.shape[0]
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+    ws = int(lib().mi355x_mul_mat_workspace_size(type_, K, N, M))
+    if ws and (workspace is None or workspace.numel() < ws):
+        workspace = torch.empty(ws, dtype=torch.uint8, device=x.device)
+    _check(lib().mi355x_mul_mat(type_, w.data_ptr(), K, N, w.stride(0), x.data_ptr(), M, x.stride(0) * 4,
+                                out.data_ptr(), out.stride(0) * 4,
+                                workspace.data_ptr() if ws else None, ws, _stream(stream)), "mi355x_mul_mat")
+    return out
+
+
+def mul_mat_q8(type_, w, K, q8, out=None, stream=None):
+    torch = _torch()
+    _require_device()
+    if q8.dim() == 1:
+        q8 = q8[None]
+    M = q8.shape[0]
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=torch.float32, device=q8.device)
+    _check(lib().mi355x_mul_mat_q8(type_, w.data_ptr(), K, N, w.stride(0), q8.data_ptr(), M, q8.stride(0),
+                                   out.data_ptr(), out.stride(0) * 4, _stream(stream)), "mi355x_mul_mat_q8")
+    return out
+
+
+def gemv_fused(mats, x, stream=None):
+    """mats: list of (type, w tensor (N, rowbytes), y tensor (N,) f32); x: (K,) f32. One launch."""
+    _require_device()
+    n = len(mats)
+    descs = (GemvDesc * n)()
+    for i, (t, w, y) in enumerate(mats):
+        descs[i] = GemvDesc(t, w.data_ptr(), w.shape[0], w.stride(0), y.data_ptr())
+    K = x.shape[-1]
+    _check(lib().mi355x_gemv_fused(descs, n, x.data_ptr(), K, _stream(stream)), "mi355x_gemv_fused")
+
+
+def block_partials(type_, w, K, q8_row, stream=None):
+    """Per-superblock integer partials -> (N, nb, 2) int32 cuda tensor."""
+    torch = _torch()
+    _require_device()
+    N = w.shape[0]
+    out = torch.zeros((N, K // QK_K, 2), dtype=torch.int32, device=w.device)
+    _check(lib().mi355x_debug_block_partials(type_, w.data_ptr(), K, N, w.stride(0), q8_row.data_ptr(),
+                                             out.data_ptr(), _stream(stream)), "mi355x_debug_block_partials")
+    return out
+
+
+# ------------------------------------------- raw ggml surface (device pointers)
+def vec_dot_q4_K_q8_K(n, s, bs, vx, bx, vy, by, nrc):
+    lib().mi355x_vec_dot_q4_K_q8_K(n, s, bs, vx, bx, vy, by, nrc)
+
+
+def vec_dot_q5_K_q8_K(n, s, bs, vx, bx, vy, by, nrc):
+    lib().mi355x_vec_dot_q5_K_q8_K(n, s, bs, vx, bx, vy, by, nrc)
+
+
+def vec_dot_q6_K_q8_K(n, s, bs, vx, bx, vy, by, nrc):
+    lib().mi355x_vec_dot_q6_K_q8_K(n, s, bs, vx, bx, vy, by, nrc)
+
+
+def quantize_row_q8_K(x, y, k):
+    lib().mi355x_quantize_row_q8_K(x, y, k)
+
+
+# ------------------------------------------------------------ backend mirror
+class Backend:
+    """ggml-backend device mirror: own stream, device buffers, graph_compute."""
+
+    def __init__(self, device=0):
+        _require_device()
+        self.h = lib().mi355x_backend_init(device)
+        if not self.h:
+            raise Mi355xError("mi355x_backend_init failed")
+        self._keep = []
+
+    @property
+    def name(self):
+        return lib().mi355x_backend_name(self.h).decode()
+
+    @property
+    def stream(self):
+        return lib().mi355x_backend_stream(self.h)
+
+    def alloc(self, size):
+        p = lib().mi355x_backend_alloc(self.h, size)
+        if not p:
+            raise Mi355xError("alloc failed")
+        return p
+
+    def free_buffer(self, p):
+        lib().mi355x_backend_free_buffer(self.h, p)
+
+    def set_tensor(self, dst, host_array):
+        import numpy as np
+        a = np.ascontiguousarray(host_array)
+        self._keep.append(a)  # keep alive until synchronize
+        _check(lib().mi355x_backend_set_tensor(self.h, dst, a.ctypes.data, a.nbytes), "set_tensor")
+
+    def get_tensor(self, host_array, src):
+        _check(lib().mi355x_backend_get_tensor(self.h, host_array.ctypes.data, src, host_array.nbytes),
+               "get_tensor")
+
+    def synchronize(self):
+        _check(lib().mi355x_backend_synchronize(self.h), "synchronize")
+        self._keep.clear()
+
+    def graph_compute(self, nodes, use_graph=True):
+        arr = (ctypes.POINTER(Tensor) * len(nodes))(*[ctypes.pointer(n) for n in nodes])
+        return int(lib().mi355x_backend_graph_compute(self.h, arr, len(nodes), 1 if use_graph else 0))
+
+    def close(self):
+        if self.h:
+            lib().mi355x_backend_free(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def supports_op(t: Tensor) -> bool:
+    return bool(lib().mi355x_backend_supports_op(ctypes.byref(t)))
+
+
+def make_tensor(type_, ne0, ne1, data, row_stride=None, op=OP_NONE, src0=None, src1=None) -> Tensor:
+    """2-D ggml-style tensor descriptor: ne0 elements per row, ne1 rows, row stride nb1 bytes."""
+    t = Tensor()
+    t.type = type_
+    t.op = op
+    nb0 = BLOCK_BYTES.get(type_, 4)
+    nb1 = row_stride if row_stride is not None else (ne0 // QK_K * nb0 if type_ in BLOCK_BYTES else ne0 * 4)
+    t.ne[0], t.ne[1], t.ne[2], t.ne[3] = ne0, ne1, 1, 1
+    t.nb[0], t.nb[1], t.nb[2], t.nb[3] = nb0, nb1, nb1 * ne1, nb1 * ne1
+    t.src[0] = ctypes.pointer(src0) if src0 is not None else ctypes.POINTER(Tensor)()
+    t.src[1] = ctypes.pointer(src1) if src1 is not None else ctypes.POINTER(Tensor)()
+    t.data = data
+    return t

@@ -1,0 +1,227 @@
+/*
+ * ggml_mi355x.h — C-ABI of the MI355X (gfx950) K-quant mat-vec / mat-mat hot path.
+ *
+ * This is the drop-in boundary for ggml's quantized MUL_MAT path
+ * (ggml_compute_forward_mul_mat -> type_traits_cpu[src0].vec_dot, here
+ * ggml_vec_dot_q4_K_q8_K). Every entry point is plain C: pointers, sizes,
+ * an opaque HIP stream handle (hipStream_t passed as void*, NULL = default
+ * stream). No torch or C++ types cross this boundary.
+ *
+ * Reference interfaces replaced (file:line in /root/reference, which quotes the
+ * un-vendored llama.cpp @ a3cb0474):
+ *   - ggml_vec_dot_t               README.md:449, :686  (ggml-cpu/arch/arm/quants.c:2059)
+ *   - quantize_row_q8_K(_ref)      artifacts/perf/out.folded:184-186
+ *   - ggml_compute_forward_mul_mat README.md:137, :157  (ggml-cpu.c:1389, one_chunk :1194)
+ *   - ggml_backend_cpu_graph_compute README.md:162      (ggml-cpu.cpp:186) -> mi355x_backend_graph_compute
+ *
+ * Memory: every data pointer below is DEVICE memory (hipMalloc / torch cuda
+ * tensor) unless stated otherwise. Weight blocks are stored exactly as GGUF /
+ * ggml stores them (no repack): rows of contiguous superblocks.
+ *
+ * Errors: functions returning int return 0 on success, a negative
+ * MI355X_E* code for argument errors, or a positive hipError_t value. The
+ * ggml-surface mirrors that return void (vec_dot, from_float) abort with a
+ * message on invalid arguments, as GGML_ASSERT does upstream.
+ */
+#ifndef GGML_MI355X_H
+#define GGML_MI355X_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ------------------------------------------------------------------ formats */
+/* Super-block size and block layouts: identical to ggml-common.h. Offsets
+ * are proven by the reference disassembly: block_q4_K stride 0x90
+ * (README.md:460, :611), d @0 (:529 "[x7,#-144]"), dmin @2 (:507), scales @4
+ * (:472 "#-140", :488 "#-132"), qs @16 (:480 "x7-0x80"); block_q8_K stride 0x124
+ * (:610), d @0 (:522), qs @4 (:459), bsums @260 (:492 "[x11,#256]"). */
+#define MI355X_QK_K 256
+#define MI355X_K_SCALE_SIZE 12
+
+typedef uint16_t mi355x_half; /* IEEE binary16 bits (ggml_half) */
+
+typedef struct {
+    mi355x_half d;                       /* super-block scale for quantized scales */
+    mi355x_half dmin;                    /* super-block scale for quantized mins   */
+    uint8_t scales[MI355X_K_SCALE_SIZE]; /* 8 x 6-bit scales + 8 x 6-bit mins      */
+    uint8_t qs[MI355X_QK_K / 2];         /* 4-bit quants                           */
+} mi355x_block_q4_K;                     /* 144 bytes, 4.5 bpw */
+
+typedef struct {
+    mi355x_half d;
+    mi355x_half dmin;
+    uint8_t scales[MI355X_K_SCALE_SIZE];
+    uint8_t qh[MI355X_QK_K / 8];         /* 5th bit of each quant */
+    uint8_t qs[MI355X_QK_K / 2];         /* low 4 bits            */
+} mi355x_block_q5_K;                     /* 176 bytes, 5.5 bpw */
+
+typedef struct {
+    uint8_t ql[MI355X_QK_K / 2];         /* low 4 bits             */
+    uint8_t qh[MI355X_QK_K / 4];         /* high 2 bits            */
+    int8_t scales[MI355X_QK_K / 16];     /* 8-bit sub-block scales */
+    mi355x_half d;                       /* super-block scale      */
+} mi355x_block_q6_K;                     /* 210 bytes, 6.5625 bpw */
+
+typedef struct {
+    float d;                             /* delta (negative when the block max is positive) */
+    int8_t qs[MI355X_QK_K];              /* quants                                          */
+    int16_t bsums[MI355X_QK_K / 16];     /* sums of 16 consecutive quants                    */
+} mi355x_block_q8_K;                     /* 292 bytes */
+
+/* ggml_type values (ggml.h enum ggml_type) for the types this path handles. */
+enum mi355x_type {
+    MI355X_TYPE_F32  = 0,
+    MI355X_TYPE_Q4_K = 12,
+    MI355X_TYPE_Q5_K = 13,
+    MI355X_TYPE_Q6_K = 14,
+    MI355X_TYPE_Q8_K = 15,
+};
+
+enum mi355x_status {
+    MI355X_OK           = 0,
+    MI355X_E_INVAL      = -1,  /* bad shape / stride / type                    */
+    MI355X_E_UNSUPPORTED = -2, /* combination not implemented on this device   */
+    MI355X_E_WORKSPACE  = -3,  /* workspace missing or too small               */
+    MI355X_E_NODEVICE   = -4,  /* no gfx950 device / HIP runtime unavailable   */
+};
+
+/* Bytes of one row of `type` with `k` elements (ggml_row_size). k % 256 == 0. */
+size_t mi355x_row_size(int type, int64_t k);
+
+/* Library / kernel-object identification (for logs and tests). */
+const char *mi355x_version(void);
+/* 1 when a gfx950 device is visible and the code object loads, else 0. */
+int mi355x_device_available(void);
+
+/* ------------------------------------------------ ggml operator surface */
+/* Device mirror of ggml_from_float_t for GGML_TYPE_Q8_K
+ * (type_traits_cpu[Q8_K].from_float = quantize_row_q8_K -> quantize_row_q8_K_ref).
+ * x: k floats, y: k/256 block_q8_K. Bit-exact with the reference
+ * (aarch64 build: iscale*x + 12582912.f contracted to one fma). Runs on the
+ * default stream and returns after completion. Aborts if k % 256 != 0. */
+void mi355x_quantize_row_q8_K(const float *x, void *y, int64_t k);
+
+/* Device mirror of ggml_vec_dot_t for Q4_K x Q8_K / Q5_K x Q8_K / Q6_K x Q8_K
+ * (README.md:449: void (int n, float *s, size_t bs, const void *vx, size_t bx,
+ * const void *vy, size_t by, int nrc)). n % 256 == 0, nrc == 1 (the measured
+ * reference configuration: no I8MM, README.md:677, so nrows == 1); bs/bx/by are
+ * unused exactly as upstream. s, vx, vy are device pointers. Runs on the default
+ * stream and returns after completion. The Q4_K result is bit-identical to the
+ * reference NEON function's fp32 output (README.md:725-777, fmsub :551, fmadd :614). */
+void mi355x_vec_dot_q4_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx,
+                              const void *vy, size_t by, int nrc);
+void mi355x_vec_dot_q5_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx,
+                              const void *vy, size_t by, int nrc);
+void mi355x_vec_dot_q6_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx,
+                              const void *vy, size_t by, int nrc);
+
+/* ----------------------------------------------------- stream-level API */
+/* Quantize `nrows` f32 rows of k elements (row stride x_stride bytes) into
+ * contiguous Q8_K rows (k/256 blocks each). Async on `stream`. */
+int mi355x_quantize_q8_K(const float *x, size_t x_stride, void *y, int64_t k, int64_t nrows,
+                         void *stream);
+
+/* MUL_MAT for src0 in {Q4_K, Q5_K, Q6_K}: dst[N x M] = src0[N x K] . src1[K x M]
+ * with ggml conventions: src0 row i at src0 + i*nb01 (ne00 = K, ne01 = N);
+ * src1 column j (ggml row j of src1) at src1 + j*nb11, K floats; dst column j at
+ * dst + j*nb1, N floats. Semantics = ggml_compute_forward_mul_mat: src1 is first
+ * quantized to Q8_K (bit-exact), then every dst element is vec_dot(row, col).
+ * M == 1 quantizes inside the GEMV kernel (no workspace needed); M > 1 needs a
+ * workspace of mi355x_mul_mat_workspace_size() bytes. Async on `stream`. */
+size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, int64_t ne11);
+int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
+                   const float *src1, int64_t ne11, size_t nb11,
+                   float *dst, size_t nb1,
+                   void *workspace, size_t workspace_size, void *stream);
+
+/* Same, with src1 already quantized to Q8_K rows (vec_dot_type), each
+ * ne00/256 blocks, column j at src1_q8 + j*nb11. No workspace. */
+int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
+                      const void *src1_q8, int64_t ne11, size_t nb11,
+                      float *dst, size_t nb1, void *stream);
+
+/* Fused decode GEMV over up to MI355X_MAX_FUSED matrices that share one f32
+ * input vector x (K floats): e.g. attn_q/attn_k/attn_v, or ffn_gate/ffn_up.
+ * One launch; x is quantized to Q8_K once per workgroup in LDS. Each matrix
+ * may have its own K-quant type. Equivalent to n separate mi355x_mul_mat calls
+ * with ne11 == 1 (bit-identical results). */
+#define MI355X_MAX_FUSED 4
+typedef struct {
+    int type;            /* MI355X_TYPE_Q4_K / Q5_K / Q6_K */
+    const void *w;       /* device: N rows of K/256 blocks  */
+    int64_t n_rows;      /* N                                */
+    size_t row_stride;   /* nb01 in bytes                    */
+    float *y;            /* device: N floats                 */
+} mi355x_gemv_desc;
+int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k,
+                      void *stream);
+
+/* Debug/parity hook: per-superblock integer partials of a Q4_K/Q5_K/Q6_K x Q8_K
+ * dot, as the GEMV kernel computes them. For each row r and superblock b:
+ * out[2*(r*nb+b)+0] = sumi (sum_j sc_j * dot_j), out[...+1] = summins
+ * (sum_g bsums_g * m_{g/2}; for Q6_K: sum_g bsums_g * sc_g). Device pointers. */
+int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, int64_t ne01,
+                                size_t nb01, const void *src1_q8, int32_t *out, void *stream);
+
+/* ------------------------------------------------------------ profiling */
+/* Per-launch kernel timing. While enabled, every GEMV/quantize launch made
+ * outside a stream capture goes through hipExtLaunchKernelGGL with a start and
+ * a stop event (the kernel's own begin/end timestamps, as rocprofv3's kernel
+ * trace reports them) and is logged with its kernel name and ALGORITHMIC bytes
+ * (weights + f32/Q8_K activations read + f32 outputs written).
+ * mi355x_timing_enable(1) clears the log; mi355x_timing_read synchronizes the
+ * device and copies up to `max` entries, returning the number logged. */
+typedef struct {
+    char kernel[96];
+    double bytes;
+    float ms;
+} mi355x_launch_timing;
+int mi355x_timing_enable(int enable);
+int mi355x_timing_read(mi355x_launch_timing *out, int max);
+
+/* --------------------------------------------- ggml-backend mirror (C++) */
+/* A minimal mirror of ggml-backend's device/buffer/graph interface
+ * (ggml-backend-impl.h [U]; CPU sibling ggml-cpu.cpp:186, README.md:162),
+ * enough for a ggml adapter to forward MUL_MAT nodes. */
+enum mi355x_op { MI355X_OP_NONE = 0, MI355X_OP_MUL_MAT = 1 };
+
+typedef struct mi355x_tensor {
+    int type;                      /* enum mi355x_type                          */
+    int op;                        /* enum mi355x_op                            */
+    int64_t ne[4];                 /* elements per dim (ggml order)            */
+    size_t nb[4];                  /* bytes per dim                            */
+    struct mi355x_tensor *src[2];  /* MUL_MAT: src[0] weights, src[1] f32 input */
+    void *data;                    /* device pointer                            */
+} mi355x_tensor;
+
+typedef struct mi355x_backend *mi355x_backend_t;
+
+mi355x_backend_t mi355x_backend_init(int device);        /* NULL on failure */
+void mi355x_backend_free(mi355x_backend_t backend);
+const char *mi355x_backend_name(mi355x_backend_t backend);
+void *mi355x_backend_stream(mi355x_backend_t backend);   /* hipStream_t */
+void *mi355x_backend_alloc(mi355x_backend_t backend, size_t size); /* device buffer */
+void mi355x_backend_free_buffer(mi355x_backend_t backend, void *ptr);
+int mi355x_backend_set_tensor(mi355x_backend_t backend, void *dst, const void *host_src,
+                              size_t size);              /* async H2D, bytes unchanged */
+int mi355x_backend_get_tensor(mi355x_backend_t backend, void *host_dst, const void *src,
+                              size_t size);              /* async D2H */
+int mi355x_backend_synchronize(mi355x_backend_t backend);
+int mi355x_backend_supports_op(const mi355x_tensor *op); /* 1 / 0 */
+/* Runs nodes in order on the backend stream. Consecutive MUL_MAT nodes with
+ * ne11 == 1 that share src[1] are fused into one launch. When `use_graph` is
+ * non-zero the launch sequence is captured once into a hipGraph and replayed
+ * on later calls with the same node list (same pointers and shapes).
+ * Returns 0 (GGML_STATUS_SUCCESS) or an error code. */
+int mi355x_backend_graph_compute(mi355x_backend_t backend, mi355x_tensor *const *nodes,
+                                 int n_nodes, int use_graph);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* GGML_MI355X_H */

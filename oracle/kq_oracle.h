@@ -1,0 +1,80 @@
+/*
+ * kq_oracle.h — CPU ORACLE (test infrastructure only).
+ *
+ * Scalar C restatement of the reference's K-quant dot-product path, used ONLY by
+ * tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg, as the checker
+ * (never as the thing measured or shipped). The product path
+ * (ggml-neon-opt_amd/) never links or calls this code.
+ *
+ * Parity status: the reference (/root/reference) ships no tests, fixtures or
+ * golden vectors for this path and its llama.cpp submodule is not vendored, so
+ * the oracle is "parity unpinned" against reference-produced outputs. It is
+ * pinned instead to (1) the reference's own quoted NEON source
+ * (README.md:686-779, optimized form :1455-1480), (2) its disassembly, which
+ * fixes struct offsets and the FP contraction (fmsub README.md:551, fmadd :614),
+ * and (3) an independent numpy restatement (oracle/kq_oracle_np.py) checked
+ * bit-for-bit against this C code by tests/test_oracle.py; golden vectors made
+ * from it are committed under tests/golden/ with their generator script.
+ */
+#ifndef KQ_ORACLE_H
+#define KQ_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KQO_QK_K 256
+
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qs[128]; } kqo_block_q4_K;
+typedef struct { uint16_t d, dmin; uint8_t scales[12]; uint8_t qh[32]; uint8_t qs[128]; } kqo_block_q5_K;
+typedef struct { uint8_t ql[128]; uint8_t qh[64]; int8_t scales[16]; uint16_t d; } kqo_block_q6_K;
+typedef struct { float d; int8_t qs[256]; int16_t bsums[16]; } kqo_block_q8_K;
+
+float kqo_fp16_to_fp32(uint16_t h);
+uint16_t kqo_fp32_to_fp16(float f); /* round-to-nearest-even, for generators */
+
+/* quantize_row_q8_K_ref. fused=1: iscale*x + 12582912.f contracted into one
+ * fma, as gcc -O2 -std=gnu11 (fp-contract=fast) builds it for aarch64, the
+ * reference's build (README.md:673). fused=0: ISO-C two roundings. */
+void kqo_quantize_row_q8_K(const float *x, kqo_block_q8_K *y, int64_t k, int fused);
+
+void kqo_dequantize_row_q4_K(const kqo_block_q4_K *x, float *y, int64_t k);
+void kqo_dequantize_row_q5_K(const kqo_block_q5_K *x, float *y, int64_t k);
+void kqo_dequantize_row_q6_K(const kqo_block_q6_K *x, float *y, int64_t k);
+
+/* ggml_vec_dot_t-shaped: (n, s, bs, vx, bx, vy, by, nrc); nrc must be 1. */
+void kqo_vec_dot_q4_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                const void *vy, size_t by, int nrc);
+void kqo_vec_dot_q4_K_q8_K_generic(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                   const void *vy, size_t by, int nrc);
+void kqo_vec_dot_q5_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                const void *vy, size_t by, int nrc);
+void kqo_vec_dot_q6_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                const void *vy, size_t by, int nrc);
+void kqo_vec_dot_q6_K_q8_K_generic(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                   const void *vy, size_t by, int nrc);
+
+/* Per-superblock integer partials (sumi, summins) of row . col, out[2*b+{0,1}].
+ * Q6_K: (isum with unsigned 0..63 quants, isum_mins = sum bsums_g*sc_g). */
+void kqo_block_partials(int type, int n, const void *vx, const void *vy, int32_t *out);
+
+/* Restated ggml_compute_forward_mul_mat (ggml-cpu.c:1389) for src0 K-quant,
+ * src1 f32: quantize src1 (per-thread slices), barrier, 64/16-row chunks handed
+ * out by an atomic counter, one_chunk 16x16 blocking calling vec_dot per
+ * (row, col). pthreads, n_threads >= 1. dst[j*N + i] (dst column j contiguous).
+ * variant: 0 = NEON-order dot, 1 = generic dot. Returns 0 on success. */
+int kqo_mul_mat(int type, const void *src0, int64_t K, int64_t N, size_t nb01,
+                const float *src1, int64_t M, size_t nb11, float *dst,
+                int n_threads, int variant);
+
+/* Same, with src1 already in Q8_K (M rows of K/256 blocks, contiguous). */
+int kqo_mul_mat_q8(int type, const void *src0, int64_t K, int64_t N, size_t nb01,
+                   const void *src1_q8, int64_t M, float *dst, int n_threads, int variant);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,102 @@
+"""CPU checks of the C-ABI library: it loads, exports every symbol the header
+declares, and its host-side logic (sizes, argument validation, supports_op)
+behaves — without launching anything."""
+import os
+import re
+import subprocess
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADER = os.path.join(ROOT, "include", "ggml_mi355x.h")
+
+
+def header_functions():
+    src = open(HEADER).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"\b(mi355x_[a-z0-9_A-Z]+)\s*\(", src)))
+
+
+def test_header_symbols_exported():
+    import ggml_mi355x as g
+    g.lib()
+    names = header_functions()
+    assert len(names) >= 20
+    assert sorted(g.EXPORTED_SYMBOLS) == names
+    out = subprocess.run(["nm", "-D", "--defined-only", g.LIB_PATH], capture_output=True, text=True).stdout
+    exported = set(l.split()[-1] for l in out.splitlines() if l.strip())
+    missing = [n for n in names if n not in exported]
+    assert not missing, missing
+
+
+def test_library_is_gfx950_code_object():
+    import ggml_mi355x as g
+    blob = open(g.LIB_PATH, "rb").read()
+    assert b"amdgcn-amd-amdhsa--gfx950" in blob
+    for other in (b"--gfx942", b"--gfx90a", b"--gfx1100"):
+        assert other not in blob
+    assert "gfx950" in g.version()
+
+
+def test_row_sizes():
+    import ggml_mi355x as g
+    assert g.row_size(g.TYPE_Q4_K, 2048) == 8 * 144
+    assert g.row_size(g.TYPE_Q5_K, 2048) == 8 * 176
+    assert g.row_size(g.TYPE_Q6_K, 5632) == 22 * 210
+    assert g.row_size(g.TYPE_Q8_K, 4096) == 16 * 292
+    assert g.row_size(g.TYPE_Q4_K, 100) == 0
+
+
+def test_argument_validation_without_device():
+    import ggml_mi355x as g
+    L = g.lib()
+    # K not a multiple of 256
+    assert L.mi355x_mul_mat(12, 0x1000, 300, 4, 144, 0x2000, 1, 1200, 0x3000, 16, None, 0, None) == -1
+    # unsupported src0 type
+    assert L.mi355x_mul_mat(2, 0x1000, 256, 4, 144, 0x2000, 1, 1024, 0x3000, 16, None, 0, None) == -2
+    # empty shapes are a no-op success
+    assert L.mi355x_mul_mat(12, 0x1000, 256, 0, 144, 0x2000, 1, 1024, 0x3000, 16, None, 0, None) == 0
+    assert L.mi355x_mul_mat(12, 0x1000, 256, 4, 144, 0x2000, 0, 1024, 0x3000, 16, None, 0, None) == 0
+    # M > 1 needs a workspace
+    assert L.mi355x_mul_mat(12, 0x1000, 256, 4, 144, 0x2000, 3, 1024, 0x3000, 16, None, 0, None) == -3
+    assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 5) == ((5 * 8 * 292 + 255) // 256) * 256
+    # misaligned weights
+    descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1002, 4, 144, 0x3000))
+    assert L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None) == -1
+    # row stride too small
+    descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1000, 4, 100, 0x3000))
+    assert L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None) == -1
+    # no device here -> the HIP path reports it instead of falling back
+    descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1000, 4, 144, 0x3000))
+    rc = L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None)
+    assert rc == (0 if g.device_available() else -4)
+
+
+def test_supports_op():
+    import ggml_mi355x as g
+    g.lib()
+    K, N, M = 2048, 64, 1
+    w = g.make_tensor(g.TYPE_Q4_K, K, N, 0x1000)
+    x = g.make_tensor(g.TYPE_F32, K, M, 0x2000)
+    y = g.make_tensor(g.TYPE_F32, N, M, 0x3000, op=g.OP_MUL_MAT, src0=w, src1=x)
+    assert g.supports_op(y)
+    for bad_type in (0, 2, 8, 15):
+        wb = g.make_tensor(bad_type, K, N, 0x1000)
+        assert not g.supports_op(g.make_tensor(g.TYPE_F32, N, M, 0x3000, op=g.OP_MUL_MAT, src0=wb, src1=x))
+    xb = g.make_tensor(g.TYPE_F32, K + 256, M, 0x2000)
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, N, M, 0x3000, op=g.OP_MUL_MAT, src0=w, src1=xb))
+    w3 = g.make_tensor(g.TYPE_Q6_K, K, N, 0x1000)
+    w3.ne[2] = 2
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, N, M, 0x3000, op=g.OP_MUL_MAT, src0=w3, src1=x))
+
+
+def test_product_has_no_oracle_dependency():
+    """The shipped package must not import or link the oracle."""
+    pkg = os.path.join(ROOT, "ggml-neon-opt_amd")
+    for dp, _, fns in os.walk(pkg):
+        for fn in fns:
+            if fn.endswith((".py", ".hip", ".h", ".cpp", "Makefile")):
+                txt = open(os.path.join(dp, fn), errors="ignore").read()
+                assert "kq_oracle" not in txt and "oracle/" not in txt, fn
+    out = subprocess.run(["ldd", os.path.join(pkg, "lib", "libggml_mi355x.so")], capture_output=True, text=True)
+    assert "oracle" not in out.stdout

@@ -1,0 +1,248 @@
+"""GPU parity: the HIP path (through the C-ABI) against the CPU oracle.
+
+Bar: Q8_K bytes, integer block partials and — because the kernel evaluates the
+reference's per-superblock fp32 chain in order — the fp32 outputs of Q4_K and
+Q6_K are compared BIT-EXACT with the oracle's NEON-order restatement. Q5_K's fp
+order is unpinned upstream [U]; it is checked bit-exact against this build's
+documented choice and with a tolerance against the dequantized float dot.
+"""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def t(a, dev):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(dev)
+
+
+def bits_equal(a, b):
+    a = np.asarray(a, np.float32)
+    b = np.asarray(b, np.float32)
+    return a.shape == b.shape and bool((a.view(np.uint32) == b.view(np.uint32)).all())
+
+
+def first_mismatch(a, b):
+    a = np.asarray(a, np.float32).ravel()
+    b = np.asarray(b, np.float32).ravel()
+    idx = np.nonzero(a.view(np.uint32) != b.view(np.uint32))[0]
+    return (len(idx), idx[:5].tolist(), a[idx[:5]].tolist(), b[idx[:5]].tolist()) if len(idx) else None
+
+
+# ---------------------------------------------------------------- Q8_K quantizer
+def test_quantize_golden_edges(dev, oracle):
+    import ggml_mi355x as g
+    z = np.load(os.path.join(GOLDEN, "q8K_edges.npz"))
+    got = g.quantize_q8_K(t(z["x"], dev)).cpu().numpy()
+    assert (got == z["q8"]).all()
+
+
+@pytest.mark.parametrize("K", [256, 2048, 14336])
+def test_quantize_random(dev, oracle, K):
+    import ggml_mi355x as g
+    rng = np.random.default_rng(K)
+    x = (rng.standard_normal((7, K)) * rng.uniform(1e-6, 1e6, (7, 1))).astype(np.float32)
+    x[0, :256] = 0
+    x[1, 3] = np.float32(-np.abs(x[1, :256]).max() * 1.0)  # force a sign tie for the max
+    got = g.quantize_q8_K(t(x, dev)).cpu().numpy()
+    assert (got == oracle.quantize_q8_K(x)).all()
+
+
+def test_quantize_row_q8_K_surface(dev, oracle):
+    """ggml from_float mirror (raw device pointers, default stream, synchronous)."""
+    import torch
+    import ggml_mi355x as g
+    x = np.random.default_rng(2).standard_normal(1024).astype(np.float32)
+    xd = t(x, dev)
+    y = torch.zeros(4 * 292, dtype=torch.uint8, device=dev)
+    torch.cuda.synchronize()
+    g.quantize_row_q8_K(xd.data_ptr(), y.data_ptr(), 1024)
+    assert (y.cpu().numpy() == oracle.quantize_q8_K(x)[0]).all()
+
+
+# ---------------------------------------------------------------- golden fixtures
+@pytest.mark.parametrize("name", ["q4K_k256_n16_m2", "q4K_k2048_n16_m2", "q4K_k5632_n8_m1",
+                                  "q5K_k2048_n16_m2", "q6K_k2048_n16_m2", "q6K_k768_n9_m3"])
+def test_golden(dev, name):
+    import ggml_mi355x as g
+    z = np.load(os.path.join(GOLDEN, name + ".npz"))
+    typ, K = int(z["type"]), int(z["K"])
+    w = t(z["w"], dev)
+    x = t(z["x"], dev)
+    q8 = g.quantize_q8_K(x).cpu().numpy()
+    assert (q8 == z["q8"]).all()
+    got = g.mul_mat(typ, w, K, x).cpu().numpy()
+    assert bits_equal(got, z["dst"]), first_mismatch(got, z["dst"])
+    for j in range(x.shape[0]):
+        p = g.block_partials(typ, w, K, t(z["q8"][j], dev)).cpu().numpy()
+        assert (p == z["partials"][j]).all()
+    # the single-column GEMV (fused quantization) agrees with column 0
+    y0 = g.mul_mat(typ, w, K, x[0:1]).cpu().numpy()
+    assert bits_equal(y0, z["dst"][0:1])
+
+
+# ---------------------------------------------------------------- shapes sweep
+SHAPES = [(256, 1), (256, 13), (512, 64), (768, 33), (1792, 7), (2048, 1), (2048, 130), (2304, 9),
+          (4096, 96), (5632, 40), (14336, 24)]
+
+
+@pytest.mark.parametrize("type_", [12, 13, 14])
+@pytest.mark.parametrize("K,N", SHAPES)
+def test_gemv_bit_exact(dev, oracle, npo, type_, K, N):
+    import ggml_mi355x as g
+    rng = np.random.default_rng(K * 31 + N + type_)
+    w = npo.random_blocks(rng, type_, N, K)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    got = g.mul_mat(type_, t(w, dev), K, t(x, dev)).cpu().numpy()
+    ref = oracle.mul_mat(type_, w, x)
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
+@pytest.mark.parametrize("type_", [12, 14])
+@pytest.mark.parametrize("M", [2, 3, 4, 5, 8, 9, 17])
+def test_small_batch_bit_exact(dev, oracle, npo, type_, M):
+    import ggml_mi355x as g
+    K, N = 2048, 77
+    rng = np.random.default_rng(M * 101 + type_)
+    w = npo.random_blocks(rng, type_, N, K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    got = g.mul_mat(type_, t(w, dev), K, t(x, dev)).cpu().numpy()
+    ref = oracle.mul_mat(type_, w, x)
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
+def test_strided_rows_and_columns(dev, oracle, npo):
+    """Non-contiguous src0 rows (nb01 > row size) and padded src1/dst columns."""
+    import torch
+    import ggml_mi355x as g
+    K, N, M = 1024, 50, 3
+    rng = np.random.default_rng(77)
+    w = npo.random_blocks(rng, 12, N, K)
+    wpad = np.zeros((N, w.shape[1] + 64), np.uint8)
+    wpad[:, :w.shape[1]] = w
+    x = rng.standard_normal((M, K + 64)).astype(np.float32)
+    out = torch.full((M, N + 16), -1.0, device=dev)
+    wd = t(wpad, dev)
+    xd = t(x, dev)
+    L = g.lib()
+    ws = torch.empty(g.lib().mi355x_mul_mat_workspace_size(12, K, N, M), dtype=torch.uint8, device=dev)
+    rc = L.mi355x_mul_mat(12, wd.data_ptr(), K, N, wpad.shape[1], xd.data_ptr(), M, (K + 64) * 4,
+                          out.data_ptr(), (N + 16) * 4, ws.data_ptr(), ws.numel(),
+                          torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    got = out.cpu().numpy()
+    ref = oracle.mul_mat(12, w, np.ascontiguousarray(x[:, :K]))
+    assert bits_equal(got[:, :N], ref)
+    assert (got[:, N:] == -1.0).all()  # nothing written past ne0
+
+
+def test_vec_dot_surface(dev, oracle, npo):
+    """ggml_vec_dot_t mirror on device pointers (n, s, bs, vx, bx, vy, by, nrc=1)."""
+    import torch
+    import ggml_mi355x as g
+    rng = np.random.default_rng(4)
+    K = 4096
+    for typ, fn in ((12, g.vec_dot_q4_K_q8_K), (13, g.vec_dot_q5_K_q8_K), (14, g.vec_dot_q6_K_q8_K)):
+        w = npo.random_blocks(rng, typ, 1, K)
+        x = rng.standard_normal((1, K)).astype(np.float32)
+        q8 = oracle.quantize_q8_K(x)
+        wd, qd = t(w, dev), t(q8, dev)
+        s = torch.zeros(1, device=dev)
+        torch.cuda.synchronize()
+        fn(K, s.data_ptr(), 0, wd.data_ptr(), 0, qd.data_ptr(), 0, 1)
+        ref = oracle.vec_dot(typ, w[0], q8[0], K)
+        assert bits_equal(s.cpu().numpy(), np.float32(ref))
+
+
+def test_fused_mixed_types_equal_separate(dev, oracle, npo):
+    """attn_q (Q4_K) + attn_k (Q4_K) + attn_v (Q6_K) in one launch == three mul_mats."""
+    import torch
+    import ggml_mi355x as g
+    K = 2048
+    rng = np.random.default_rng(12)
+    specs = [(12, 2048), (12, 256), (14, 256), (13, 100)]
+    ws = [npo.random_blocks(rng, ty, n, K) for ty, n in specs]
+    x = rng.standard_normal(K).astype(np.float32)
+    ys = [torch.full((n,), np.nan, device=dev) for _, n in specs]
+    g.gemv_fused([(ty, t(w, dev), y) for (ty, _), w, y in zip(specs, ws, ys)], t(x, dev))
+    for (ty, _), w, y in zip(specs, ws, ys):
+        ref = oracle.mul_mat(ty, w, x[None])[0]
+        assert bits_equal(y.cpu().numpy(), ref)
+
+
+# ---------------------------------------------------------------- full-size properties
+@pytest.mark.parametrize("K,N", [(4096, 14336), (14336, 4096), (8192, 1024)])
+def test_full_size_rows_subset(dev, oracle, npo, K, N):
+    """Llama-3-8B/70B-shaped GEMVs: every row on the GPU; a hashed subset of rows
+    re-computed by the oracle must match bit-for-bit; all outputs finite."""
+    import ggml_mi355x as g
+    rng = np.random.default_rng(N + K)
+    w = npo.random_blocks(rng, 12, N, K)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    got = g.mul_mat(12, t(w, dev), K, t(x, dev)).cpu().numpy()[0]
+    assert np.isfinite(got).all()
+    rows = np.unique(rng.integers(0, N, 97))
+    ref = oracle.mul_mat(12, w[rows], x)[0]
+    assert bits_equal(got[rows], ref)
+
+
+def test_linearity_in_activation_scale(dev, npo):
+    """Scaling x by a power of two leaves qs/bsums unchanged and scales d exactly, so
+    the output scales exactly (size-independent property at the full TinyLlama ffn shape)."""
+    import ggml_mi355x as g
+    K, N = 2048, 5632
+    rng = np.random.default_rng(8)
+    w = t(npo.random_blocks(rng, 12, N, K), dev)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    y1 = g.mul_mat(12, w, K, t(x, dev)).cpu().numpy()
+    y2 = g.mul_mat(12, w, K, t(x * np.float32(4.0), dev)).cpu().numpy()
+    assert bits_equal(y2, y1 * np.float32(4.0))
+
+
+def test_backend_graph_compute(dev, oracle, npo):
+    """ggml-backend mirror: MUL_MAT nodes (fusable q/k/v + a batched node), eager
+    and hipGraph-replayed, identical to the oracle."""
+    import ggml_mi355x as g
+    K = 2048
+    rng = np.random.default_rng(21)
+    be = g.Backend(0)
+    assert be.name.startswith("MI355X")
+    specs = [(12, 512), (12, 128), (14, 128)]
+    ws = [npo.random_blocks(rng, ty, n, K) for ty, n in specs]
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    xb = rng.standard_normal((6, K)).astype(np.float32)
+    bufs = []
+
+    def up(a):
+        p = be.alloc(a.nbytes)
+        be.set_tensor(p, a)
+        bufs.append(p)
+        return p
+
+    wt = [g.make_tensor(ty, K, n, up(w)) for (ty, n), w in zip(specs, ws)]
+    xt = g.make_tensor(g.TYPE_F32, K, 1, up(x))
+    xbt = g.make_tensor(g.TYPE_F32, K, 6, up(xb))
+    outs = [g.make_tensor(g.TYPE_F32, n, 1, be.alloc(n * 4), op=g.OP_MUL_MAT, src0=w_, src1=xt)
+            for (ty, n), w_ in zip(specs, wt)]
+    outs.append(g.make_tensor(g.TYPE_F32, 512, 6, be.alloc(512 * 6 * 4), op=g.OP_MUL_MAT, src0=wt[0], src1=xbt))
+    for use_graph in (0, 1, 1):
+        assert be.graph_compute(outs, use_graph=use_graph) == 0
+        be.synchronize()
+        for (ty, n), w, o in zip(specs, ws, outs[:3]):
+            h = np.zeros(n, np.float32)
+            be.get_tensor(h, o.data)
+            be.synchronize()
+            assert bits_equal(h, oracle.mul_mat(ty, w, x)[0])
+        h = np.zeros((6, 512), np.float32)
+        be.get_tensor(h, outs[3].data)
+        be.synchronize()
+        assert bits_equal(h, oracle.mul_mat(12, ws[0], xb))
+    for o in outs:
+        be.free_buffer(o.data)
+    for p in bufs:
+        be.free_buffer(p)
+    be.close()

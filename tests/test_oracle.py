@@ -1,0 +1,132 @@
+"""CPU tests of the oracle (test infrastructure): C restatement vs independent numpy
+restatement, committed golden vectors, quantizer edge cases, the restated
+mul_mat scheduler. No GPU needed."""
+import hashlib
+import json
+import os
+
+import numpy as np
+import pytest
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+TYPES = (12, 13, 14)
+
+
+@pytest.mark.parametrize("type_", TYPES)
+@pytest.mark.parametrize("K", [256, 768, 2048, 5632])
+def test_c_vs_numpy_bit_exact(oracle, npo, type_, K):
+    rng = np.random.default_rng(1000 + type_ * 7 + K)
+    w = npo.random_blocks(rng, type_, 23, K)
+    x = rng.standard_normal((3, K)).astype(np.float32) * np.float32(rng.uniform(1e-3, 1e3))
+    q8 = oracle.quantize_q8_K(x)
+    assert (q8 == npo.q8_K_to_bytes(npo.quantize_q8_K(x))).all()
+    got = oracle.mul_mat(type_, w, x)
+    ref = npo.mul_mat_q8(w, type_, K, npo.q8_K_from_bytes(q8, K // 256))
+    assert (got.view(np.uint32) == ref.view(np.uint32)).all()
+    a, b = npo.block_partials(w, type_, K, npo.q8_K_from_bytes(q8, K // 256))
+    for j in range(3):
+        p = oracle.block_partials(type_, w, q8[j], K)
+        assert (p[..., 0] == a[:, j]).all() and (p[..., 1] == b[:, j]).all()
+
+
+def test_golden_manifest_and_replay(oracle):
+    manifest = json.load(open(os.path.join(GOLDEN, "MANIFEST.json")))
+    assert len(manifest) >= 7
+    for name, sha in manifest.items():
+        path = os.path.join(GOLDEN, name + ".npz")
+        assert hashlib.sha256(open(path, "rb").read()).hexdigest() == sha, name
+        z = np.load(path)  # allow_pickle defaults to False
+        if name == "q8K_edges":
+            assert (oracle.quantize_q8_K(z["x"]) == z["q8"]).all()
+            assert (oracle.quantize_q8_K(z["x"], fused=False) == z["q8_unfused"]).all()
+            continue
+        t, K = int(z["type"]), int(z["K"])
+        assert (oracle.quantize_q8_K(z["x"]) == z["q8"]).all(), name
+        got = oracle.mul_mat(t, z["w"], z["x"])
+        assert (got.view(np.uint32) == z["dst"].view(np.uint32)).all(), name
+        for j in range(z["x"].shape[0]):
+            assert (oracle.block_partials(t, z["w"], z["q8"][j], K) == z["partials"][j]).all()
+
+
+def test_q8K_zero_block_and_ties(oracle, npo):
+    x = np.zeros((1, 512), np.float32)
+    x[0, 256 + 10] = -2.0
+    x[0, 256 + 20] = 2.0
+    q = npo.q8_K_from_bytes(oracle.quantize_q8_K(x), 2)
+    assert q["d"][0, 0] == 0 and (q["qs"][0, 0] == 0).all() and (q["bsums"][0, 0] == 0).all()
+    # first max is -2 -> iscale = +63.5 -> element 10 -> -127, element 20 -> +127 (clamped)
+    assert q["qs"][0, 1, 10] == -127 and q["qs"][0, 1, 20] == 127
+    assert q["d"][0, 1] > 0
+
+
+def test_q8K_max_is_negative_127(oracle, npo):
+    rng = np.random.default_rng(5)
+    x = rng.standard_normal((4, 1024)).astype(np.float32)
+    q = npo.q8_K_from_bytes(oracle.quantize_q8_K(x), 4)
+    xb = x.reshape(4, 4, 256)
+    idx = np.abs(xb).argmax(-1)
+    qv = np.take_along_axis(q["qs"], idx[..., None], -1)[..., 0]
+    assert (qv == -127).all()  # iscale = -127/max maps the block max to -127
+    assert (q["qs"] >= -127).all() and (q["qs"] <= 127).all()
+    assert (q["bsums"] == q["qs"].reshape(4, 4, 16, 16).astype(np.int32).sum(-1)).all()
+
+
+def test_fused_vs_unfused_nearest_int_differ_rarely(oracle):
+    rng = np.random.default_rng(11)
+    x = rng.standard_normal((64, 4096)).astype(np.float32)
+    a = oracle.quantize_q8_K(x, fused=True)
+    b = oracle.quantize_q8_K(x, fused=False)
+    frac = (a != b).mean()
+    assert frac < 1e-3  # double rounding is rare, but the build choice is pinned
+
+
+@pytest.mark.parametrize("type_", [12, 14])
+def test_neon_vs_generic_order(oracle, npo, type_):
+    """The generic restatement (8 float lanes) shares every integer with the NEON one
+    and differs only in fp32 rounding order."""
+    rng = np.random.default_rng(7)
+    K = 4096
+    w = npo.random_blocks(rng, type_, 64, K)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    neon = oracle.mul_mat(type_, w, x, variant="neon")
+    gen = oracle.mul_mat(type_, w, x, variant="generic")
+    a, b = npo.block_partials(w, type_, K, npo.q8_K_from_bytes(oracle.quantize_q8_K(x), K // 256))
+    scale = np.abs(neon).max() + 1e-30
+    assert np.max(np.abs(neon - gen)) <= 1e-5 * scale
+
+
+@pytest.mark.parametrize("type_", TYPES)
+def test_dot_matches_dequantized_float_dot(oracle, npo, type_):
+    """Semantic check of the block layouts: vec_dot == dequant(w) . dequant(q8) up to fp32 rounding."""
+    rng = np.random.default_rng(3)
+    K = 2048
+    w = npo.random_blocks(rng, type_, 32, K)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    q8 = oracle.quantize_q8_K(x)
+    qq = npo.q8_K_from_bytes(q8, K // 256)
+    xd = (qq["qs"].astype(np.float64) * qq["d"][..., None].astype(np.float64)).reshape(1, K)
+    wd = npo.dequantize(w, type_, K)
+    ref = wd @ xd[0]
+    got = oracle.mul_mat(type_, w, x)[0]
+    assert np.max(np.abs(got - ref)) <= 1e-5 * (np.abs(wd) @ np.abs(xd[0])).max()
+    # the C dequant restatement agrees with the numpy one
+    assert np.allclose(oracle.dequantize(type_, w, K), wd, rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.parametrize("n_threads", [2, 3, 8])
+def test_mul_mat_threading_is_bit_identical(oracle, npo, n_threads):
+    rng = np.random.default_rng(9)
+    K, N = 2048, 300
+    w = npo.random_blocks(rng, 12, N, K)
+    x = rng.standard_normal((5, K)).astype(np.float32)
+    one = oracle.mul_mat(12, w, x, n_threads=1)
+    many = oracle.mul_mat(12, w, x, n_threads=n_threads)
+    assert (one.view(np.uint32) == many.view(np.uint32)).all()
+
+
+def test_fp16_roundtrip(oracle):
+    L = oracle.lib()
+    for h in [0x0000, 0x0001, 0x03FF, 0x0400, 0x3C00, 0x7BFF, 0x8001, 0xFBFF]:
+        f = L.kqo_fp16_to_fp32(h)
+        assert np.float32(f) == np.uint16(h).view(np.float16).astype(np.float32)
+        assert L.kqo_fp32_to_fp16(f) == h
