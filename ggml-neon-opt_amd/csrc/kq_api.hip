@@ -71,6 +71,20 @@ int type_bit(int type) {
 
 constexpr size_t kMaxLds = 64 * 1024;
 
+// Workgroups of one kernel resident per CU (registers / LDS), cached per (fn, lds).
+int resident_wgs(gemv_fn fn, size_t lds) {
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<const void *, size_t>, int>> cache;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &e : cache)
+        if (e.first.first == (const void *)fn && e.first.second == lds) return e.second;
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, WG_THREADS, lds) != hipSuccess || n <= 0) n = 2;
+    if (n > 8) n = 8;
+    cache.push_back({{(const void *)fn, lds}, n});
+    return n;
+}
+
 }  // namespace
 
 int device_ok() {
@@ -137,7 +151,8 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
     if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
     lds = (size_t)L.total;
     const int64_t wgs_needed = (tasks + WAVES_PER_WG - 1) / WAVES_PER_WG;
-    const int64_t cap = (int64_t)num_cus() * 4;
+    // one wave of resident workgroups (persistent-style grid-stride over row tasks)
+    const int64_t cap = (int64_t)num_cus() * resident_wgs(pick_gemv(ncol, M == 1 && ncol == 1, false, tmask), lds);
     grid = dim3((unsigned)(wgs_needed < cap ? (wgs_needed > 0 ? wgs_needed : 1) : cap),
                 (unsigned)((M + ncol - 1) / ncol), 1);
     return MI355X_OK;

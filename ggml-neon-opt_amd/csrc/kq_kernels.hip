@@ -57,18 +57,28 @@ __device__ __forceinline__ void wave_lds_fence() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Full-wave reductions with DPP only (no LDS crossbar): quad swaps, 8/16-lane
+// mirrors, then row_bcast15/row_bcast31 fold the four rows into lane 63.
+template <typename Op>
+__device__ __forceinline__ int wave_reduce_dpp(int v, Op op) {
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0xB1, 0xF, 0xF, false));   // quad_perm [1,0,3,2]
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x4E, 0xF, 0xF, false));   // quad_perm [2,3,0,1]
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x141, 0xF, 0xF, false));  // row_half_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x140, 0xF, 0xF, false));  // row_mirror
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x142, 0xA, 0xF, false));  // row_bcast:15
+    v = op(v, __builtin_amdgcn_update_dpp(v, v, 0x143, 0xC, 0xF, false));  // row_bcast:31
+    return __builtin_amdgcn_readlane(v, 63);
+}
+
 __device__ __forceinline__ float wave_max_f32(float v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
-    return v;
+    // |x| values are non-negative (or NaN): their int bit patterns order like the floats.
+    // NaN must never win (serial `ax > amax` is false for NaN): map NaN to 0.
+    int b = (v == v) ? __float_as_int(v) : 0;
+    b = wave_reduce_dpp(b, [](int a, int c) { return a > c ? a : c; });
+    return __int_as_float(b);
 }
 __device__ __forceinline__ uint32_t wave_min_u32(uint32_t v) {
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        uint32_t w = (uint32_t)__shfl_xor((int)v, o, 64);
-        v = w < v ? w : v;
-    }
-    return v;
+    return (uint32_t)wave_reduce_dpp((int)v, [](int a, int c) { return (uint32_t)a < (uint32_t)c ? a : c; });
 }
 
 // nearest_int(iscale * x) with the multiply-add contracted (aarch64 gcc build of
@@ -92,7 +102,7 @@ __device__ __forceinline__ Q8Lane quant_block_wave(const float *xb, int lane) {
     const f32x4a v = *(const f32x4a *)(xb + 4 * lane);
     const float a0 = fabsf(v.x), a1 = fabsf(v.y), a2 = fabsf(v.z), a3 = fabsf(v.w);
     // amax; NaN never wins (fmaxf drops NaN, as `ax > amax` is false for NaN)
-    const float m = wave_max_f32(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));
+    const float m = wave_max_f32(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));  // fmaxf drops NaN
     Q8Lane r;
     if (m == 0.f) {  // wave-uniform: the `if (!amax)` branch
         r.qs4 = 0;
@@ -340,10 +350,12 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         lane_blk = g - lane_row * nb;
     }
 
-    constexpr int U = 4;
-    Regs regs[U];
+    // Steps in flight per buffer; two buffers alternate so the next batch's loads
+    // are in flight while the current batch is computed.
+    constexpr int U = (TMASK & 4) ? 2 : 4;
+    Regs ra[U], rb[U];
 
-    auto issue = [&](int q0) {
+    auto issue = [&](Regs (&regs)[U], int q0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int q = q0 + u;
@@ -364,36 +376,9 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         }
     };
 
-    // Weights for the first batch are in flight while the activation is staged.
-    issue(0);
-
-    if (FUSEDQ) {
-        for (int b = wave; b < nb; b += WAVES_PER_WG) {
-            const Q8Lane q = quant_block_wave(a.x + (int64_t)col0 * a.x_col_stride + (int64_t)b * QK, lane);
-            *(uint32_t *)(act_qs + b * ACT_QS_STRIDE + 4 * lane) = q.qs4;
-            if ((lane & 3) == 0) act_bs[b * 16 + (lane >> 2)] = (int16_t)q.bsum;
-            if (lane == 0) act_d[b] = q.d;
-        }
-    } else {
-        const int per_col = nb * 73;
-        for (int i = threadIdx.x; i < ncol * per_col; i += WG_THREADS) {
-            const int c = i / per_col;
-            const int rem = i - c * per_col;
-            const int b = rem / 73;
-            const int dw = rem - b * 73;
-            const uint32_t v = gload4(a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)b * 292 + 4 * dw);
-            const int cb = c * nb + b;
-            if (dw == 0) act_d[cb] = __uint_as_float(v);
-            else if (dw <= 64) *(uint32_t *)(act_qs + cb * ACT_QS_STRIDE + 4 * (dw - 1)) = v;
-            else *(uint32_t *)(act_bs + cb * 16 + 2 * (dw - 65)) = v;
-        }
-    }
-    __syncthreads();
-
     float acc = 0.f;  // running fp32 chain of this lane's (row, column)
 
-    for (int q0 = 0; q0 < Q; q0 += U) {
-        if (q0 > 0) issue(q0);
+    auto compute = [&](Regs (&regs)[U], int q0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int q = q0 + u;
@@ -405,12 +390,11 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
             const bool valid = (R == 1) ? (blk < nb) : (g < R * nb && lane_row < si.rows);
             const int cblk = valid ? blk : 0;
             Regs rr = regs[u];
-            uint32_t q6s = 0;
             if ((TMASK & 4) && type == Q6_K) {
                 // realign the 2-mod-4 blocks (see load_q6K)
                 const uint8_t *bp = a.w[si.m] + (int64_t)(si.row0 + lane_row) * a.row_stride[si.m] +
                                     (int64_t)cblk * 210;
-                q6s = (uint32_t)((uintptr_t)bp & 3u);
+                const uint32_t q6s = (uint32_t)((uintptr_t)bp & 3u);
                 rr.a = realign(rr.a, rr.e0, q6s);
                 rr.b = realign(rr.b, rr.e1, q6s);
                 rr.c = realign(rr.c, rr.e2, q6s);
@@ -452,24 +436,71 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
                 }
             }
             wave_lds_fence();
-            // serial fp32 chain, superblock order
+            // serial fp32 chain in superblock order: all 8 records are read at once,
+            // then the dependent fmas run back to back
             if (R == 1) {
                 if (lane < ncol) {
                     if (s == 0) acc = 0.f;
                     const int cnt = (nb - 8 * s) < 8 ? (nb - 8 * s) : 8;
-                    for (int i = 0; i < cnt; ++i) acc = chain_step(type, recs[lane * BLOCKS_PER_STEP + i], acc);
-                    if (!DEBUG && s == S - 1) a.y[si.m][(int64_t)lane * a.y_col_stride[si.m] + si.row0] = acc;
+                    Rec rv[BLOCKS_PER_STEP];
+#pragma unroll
+                    for (int i = 0; i < BLOCKS_PER_STEP; ++i) rv[i] = recs[lane * BLOCKS_PER_STEP + i];
+#pragma unroll
+                    for (int i = 0; i < BLOCKS_PER_STEP; ++i)
+                        if (i < cnt) acc = chain_step(type, rv[i], acc);
+                    if (!DEBUG && s == S - 1)
+                        a.y[si.m][(int64_t)(col0 + lane) * a.y_col_stride[si.m] + si.row0] = acc;
                 }
             } else {
                 const int c = lane / R, r = lane - c * R;
                 if (!DEBUG && c < ncol && r < si.rows) {
+                    Rec rv[BLOCKS_PER_STEP];
+#pragma unroll
+                    for (int i = 0; i < BLOCKS_PER_STEP; ++i)
+                        rv[i] = recs[c * BLOCKS_PER_STEP + ((r * nb + i) & (BLOCKS_PER_STEP - 1))];
                     float v = 0.f;
-                    for (int i = 0; i < nb; ++i) v = chain_step(type, recs[c * BLOCKS_PER_STEP + r * nb + i], v);
-                    a.y[si.m][(int64_t)c * a.y_col_stride[si.m] + si.row0 + r] = v;
+#pragma unroll
+                    for (int i = 0; i < BLOCKS_PER_STEP; ++i)
+                        if (i < nb) v = chain_step(type, rv[i], v);
+                    a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = v;
                 }
             }
             wave_lds_fence();
         }
+    };
+
+    // Weights for the first batch are in flight while the activation is staged.
+    issue(ra, 0);
+
+    if (FUSEDQ) {
+        for (int b = wave; b < nb; b += WAVES_PER_WG) {
+            const Q8Lane q = quant_block_wave(a.x + (int64_t)col0 * a.x_col_stride + (int64_t)b * QK, lane);
+            *(uint32_t *)(act_qs + b * ACT_QS_STRIDE + 4 * lane) = q.qs4;
+            if ((lane & 3) == 0) act_bs[b * 16 + (lane >> 2)] = (int16_t)q.bsum;
+            if (lane == 0) act_d[b] = q.d;
+        }
+    } else {
+        const int per_col = nb * 73;
+        for (int i = threadIdx.x; i < ncol * per_col; i += WG_THREADS) {
+            const int c = i / per_col;
+            const int rem = i - c * per_col;
+            const int b = rem / 73;
+            const int dw = rem - b * 73;
+            const uint32_t v = gload4(a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)b * 292 + 4 * dw);
+            const int cb = c * nb + b;
+            if (dw == 0) act_d[cb] = __uint_as_float(v);
+            else if (dw <= 64) *(uint32_t *)(act_qs + cb * ACT_QS_STRIDE + 4 * (dw - 1)) = v;
+            else *(uint32_t *)(act_bs + cb * 16 + 2 * (dw - 65)) = v;
+        }
+    }
+    __syncthreads();
+
+    for (int q0 = 0; q0 < Q; q0 += 2 * U) {
+        issue(rb, q0 + U);
+        compute(ra, q0);
+        if (q0 + U >= Q) break;
+        issue(ra, q0 + 2 * U);
+        compute(rb, q0 + U);
     }
 }
 

@@ -23,6 +23,8 @@ def t(a, dev):
 def bits_equal(a, b):
     a = np.asarray(a, np.float32)
     b = np.asarray(b, np.float32)
+    if a.size == b.size:
+        b = b.reshape(a.shape)
     return a.shape == b.shape and bool((a.view(np.uint32) == b.view(np.uint32)).all())
 
 
