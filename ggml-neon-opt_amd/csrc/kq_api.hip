@@ -16,7 +16,9 @@
 
 namespace kq {
 
-template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
+enum { MODE_ROWS = 0, MODE_BLOCKS = 1 };
+
+template <int MODE, int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void kq_gemv(const GemvArgs a);
 __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 
@@ -42,32 +44,29 @@ void probe_device() {
     g_dev_ok = 1;
 }
 
-typedef void (*gemv_fn)(const GemvArgs);
-
-template <int NCOL, bool FUSEDQ, bool DEBUG>
+template <int MODE, int NCOL, bool FUSEDQ, bool DEBUG>
 gemv_fn pick_tm(int tmask) {
     switch (tmask) {
-        case 1: return kq_gemv<NCOL, FUSEDQ, DEBUG, 1>;
-        case 2: return kq_gemv<NCOL, FUSEDQ, DEBUG, 2>;
-        case 4: return kq_gemv<NCOL, FUSEDQ, DEBUG, 4>;
-        default: return kq_gemv<NCOL, FUSEDQ, DEBUG, 7>;
+        case 1: return kq_gemv<MODE, NCOL, FUSEDQ, DEBUG, 1>;
+        case 4: return kq_gemv<MODE, NCOL, FUSEDQ, DEBUG, 4>;
+        default: return kq_gemv<MODE, NCOL, FUSEDQ, DEBUG, 7>;
     }
 }
 
-gemv_fn pick_gemv(int ncol, bool fusedq, bool debug, int tmask) {
-    if (debug) return pick_tm<1, false, true>(tmask);
-    if (fusedq) return pick_tm<1, true, false>(tmask);
+gemv_fn pick_gemv(int mode, int ncol, bool fusedq, bool debug, int tmask) {
+    if (mode == MODE_BLOCKS)
+        return fusedq ? pick_tm<MODE_BLOCKS, 1, true, false>(tmask) : pick_tm<MODE_BLOCKS, 1, false, false>(tmask);
+    if (debug) return pick_tm<MODE_ROWS, 1, false, true>(tmask);
+    if (fusedq) return pick_tm<MODE_ROWS, 1, true, false>(tmask);
     switch (ncol) {
-        case 1: return pick_tm<1, false, false>(tmask);
-        case 2: return pick_tm<2, false, false>(tmask);
-        case 4: return pick_tm<4, false, false>(tmask);
-        default: return pick_tm<8, false, false>(tmask);
+        case 1: return pick_tm<MODE_ROWS, 1, false, false>(tmask);
+        case 2: return pick_tm<MODE_ROWS, 2, false, false>(tmask);
+        case 4: return pick_tm<MODE_ROWS, 4, false, false>(tmask);
+        default: return pick_tm<MODE_ROWS, 8, false, false>(tmask);
     }
 }
 
-int type_bit(int type) {
-    return type == Q4_K ? 1 : type == Q5_K ? 2 : type == Q6_K ? 4 : 0;
-}
+int type_bit(int type) { return type == Q4_K ? 1 : type == Q5_K ? 2 : type == Q6_K ? 4 : 0; }
 
 constexpr size_t kMaxLds = 64 * 1024;
 
@@ -85,81 +84,7 @@ int resident_wgs(gemv_fn fn, size_t lds) {
     return n;
 }
 
-}  // namespace
-
-int device_ok() {
-    std::call_once(g_dev_once, probe_device);
-    return g_dev_ok;
-}
-
-int num_cus() {
-    device_ok();
-    return g_num_cus;
-}
-
-int choose_ncol(int64_t M, int nb) {
-    if (M <= 1) return 1;
-    const int cands[4] = {8, 4, 2, 1};
-    for (int i = 0; i < 4; ++i) {
-        const int nc = cands[i];
-        if (nc > M && nc > 1) continue;
-        if ((size_t)lds_layout(nc, nb).total <= kMaxLds) return nc;
-    }
-    return 1;
-}
-
-// Validates descriptors and fills the launch arguments. Returns MI355X_OK or an error.
-int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int ncol, GemvArgs &a,
-              dim3 &grid, size_t &lds, int &tmask) {
-    if (n_desc < 1 || n_desc > MI355X_MAX_FUSED) return MI355X_E_INVAL;
-    if (K <= 0 || K % QK != 0 || M < 0) return MI355X_E_INVAL;
-    const int64_t nb = K / QK;
-    if (nb > 0x7fffffff / 8) return MI355X_E_INVAL;
-    memset(&a, 0, sizeof(a));
-    a.n_desc = n_desc;
-    a.nb = (int)nb;
-    a.R = nb >= 8 ? 1 : (int)(8 / nb);
-    a.S = nb >= 8 ? (int)((nb + 7) / 8) : 1;
-    a.m_total = (int)M;
-    tmask = 0;
-    int64_t tasks = 0;
-    for (int i = 0; i < n_desc; ++i) {
-        const int bb = block_bytes(d[i].type);
-        if (!bb) return MI355X_E_UNSUPPORTED;
-        if (d[i].n_rows < 0 || d[i].n_rows > 0x7fffffff) return MI355X_E_INVAL;
-        if (d[i].n_rows > 0) {
-            if (!d[i].w || !d[i].y) return MI355X_E_INVAL;
-            if (((uintptr_t)d[i].w & 3u) != 0) return MI355X_E_INVAL;
-            if (d[i].row_stride < (size_t)(nb * bb) || (d[i].row_stride & 1u)) return MI355X_E_INVAL;
-            if (d[i].type != Q6_K && (d[i].row_stride & 3u)) return MI355X_E_INVAL;
-        }
-        a.type[i] = d[i].type;
-        a.n_rows[i] = (int)d[i].n_rows;
-        a.w[i] = (const uint8_t *)d[i].w;
-        a.row_stride[i] = (int64_t)d[i].row_stride;
-        a.y[i] = d[i].y;
-        a.task_prefix[i] = (int)tasks;
-        tasks += (d[i].n_rows + a.R - 1) / a.R;
-        tmask |= type_bit(d[i].type);
-    }
-    if (tasks > 0x7fffffff) return MI355X_E_INVAL;
-    a.task_prefix[n_desc] = (int)tasks;
-    for (int i = n_desc; i < MI355X_MAX_FUSED; ++i) a.task_prefix[i] = (int)tasks;
-    a.tasks_total = (int)tasks;
-    if (tmask != 1 && tmask != 2 && tmask != 4) tmask = 7;
-    const LdsLayout L = lds_layout(ncol, (int)nb);
-    if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
-    lds = (size_t)L.total;
-    const int64_t wgs_needed = (tasks + WAVES_PER_WG - 1) / WAVES_PER_WG;
-    // one wave of resident workgroups (persistent-style grid-stride over row tasks)
-    const int64_t cap = (int64_t)num_cus() * resident_wgs(pick_gemv(ncol, M == 1 && ncol == 1, false, tmask), lds);
-    grid = dim3((unsigned)(wgs_needed < cap ? (wgs_needed > 0 ? wgs_needed : 1) : cap),
-                (unsigned)((M + ncol - 1) / ncol), 1);
-    return MI355X_OK;
-}
-
 // ------------------------------------------------------------ launch timing
-namespace {
 struct TimedLaunch {
     std::string kernel;
     double bytes;
@@ -184,7 +109,10 @@ bool timing_slot(hipStream_t s, hipEvent_t &a, hipEvent_t &b) {
     if (g_tpool_used == g_tpool.size()) {
         hipEvent_t e0, e1;
         if (hipEventCreate(&e0) != hipSuccess) return false;
-        if (hipEventCreate(&e1) != hipSuccess) { hipEventDestroy(e0); return false; }
+        if (hipEventCreate(&e1) != hipSuccess) {
+            hipEventDestroy(e0);
+            return false;
+        }
         g_tpool.push_back({e0, e1});
     }
     a = g_tpool[g_tpool_used].first;
@@ -193,16 +121,19 @@ bool timing_slot(hipStream_t s, hipEvent_t &a, hipEvent_t &b) {
     return true;
 }
 
-void timing_log(const char *kernel, double bytes, hipEvent_t a, hipEvent_t b) {
+void timing_log(const std::string &kernel, double bytes, hipEvent_t a, hipEvent_t b) {
     std::lock_guard<std::mutex> lk(g_tmu);
     g_tlog.push_back({kernel, bytes, a, b});
 }
 
-std::string gemv_name(int ncol, bool fusedq, bool debug, int tmask) {
-    return "kq::kq_gemv<" + std::to_string(ncol) + ", " + (fusedq ? "true" : "false") + ", " +
-           (debug ? "true" : "false") + ", " + std::to_string(tmask) + ">";
+// Same spelling as rocprofv3's kernel names (kernel-trace "Kernel_Name").
+std::string gemv_name(const GemvPlan &pl) {
+    return std::string("kq::kq_gemv<") + std::to_string(pl.mode) + ", " + std::to_string(pl.ncol) + ", " +
+           (pl.fusedq ? "true" : "false") + ", " + (pl.debug ? "true" : "false") + ", " + std::to_string(pl.tmask) +
+           ">";
 }
 
+// Algorithmic bytes of one launch: weights + activations read + f32 outputs.
 double gemv_bytes(const GemvArgs &a, bool fusedq) {
     double w = 0, y = 0;
     for (int i = 0; i < a.n_desc; ++i) {
@@ -212,18 +143,123 @@ double gemv_bytes(const GemvArgs &a, bool fusedq) {
     const double x = fusedq ? (double)a.nb * QK * 4.0 * a.m_total : (double)a.nb * 292.0 * a.m_total;
     return w + x + y;
 }
+
 }  // namespace
 
-int launch_gemv(const GemvArgs &a, dim3 grid, size_t lds, int ncol, bool fusedq, bool debug, int tmask,
-                hipStream_t stream) {
+int device_ok() {
+    std::call_once(g_dev_once, probe_device);
+    return g_dev_ok;
+}
+
+int num_cus() {
+    device_ok();
+    return g_num_cus;
+}
+
+int choose_ncol(int64_t M, int nb) {
+    if (M <= 1) return 1;
+    const int cands[4] = {8, 4, 2, 1};
+    for (int i = 0; i < 4; ++i) {
+        const int nc = cands[i];
+        if (nc > M && nc > 1) continue;
+        if ((size_t)lds_layout(nc, nb, 0).total <= kMaxLds / 2) return nc;
+    }
+    return 1;
+}
+
+// MODE_BLOCKS (one row per wave) only pays when N is too small to give every CU
+// a few 8-row tasks. MI355X_GEMV_MODE=rows|blocks forces a mode (experiments).
+int choose_mode(int64_t total_rows, int64_t nb, int64_t M) {
+    static int forced = -2;
+    if (forced == -2) {
+        const char *e = getenv("MI355X_GEMV_MODE");
+        forced = !e ? -1 : (strcmp(e, "rows") == 0 ? MODE_ROWS : strcmp(e, "blocks") == 0 ? MODE_BLOCKS : -1);
+    }
+    if (M > 1 || nb < 8) return MODE_ROWS;
+    if (forced >= 0) return forced;
+    return (total_rows / 8 >= (int64_t)num_cus() * 4) ? MODE_ROWS : MODE_BLOCKS;
+}
+
+// Validates descriptors and fills the launch plan. Returns MI355X_OK or an error.
+int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int ncol, bool fusedq, bool debug,
+              GemvPlan &pl) {
+    GemvArgs &a = pl.a;
+    if (n_desc < 1 || n_desc > MI355X_MAX_FUSED) return MI355X_E_INVAL;
+    if (K <= 0 || K % QK != 0 || M < 0) return MI355X_E_INVAL;
+    const int64_t nb = K / QK;
+    if (nb > 0x7fffffff / 8) return MI355X_E_INVAL;
+    memset(&a, 0, sizeof(a));
+    int64_t total_rows = 0;
+    int tmask = 0;
+    for (int i = 0; i < n_desc; ++i) {
+        const int bb = block_bytes(d[i].type);
+        if (!bb) return MI355X_E_UNSUPPORTED;
+        if (d[i].n_rows < 0 || d[i].n_rows > 0x7fffffff) return MI355X_E_INVAL;
+        if (d[i].n_rows > 0) {
+            if (!d[i].w || !d[i].y) return MI355X_E_INVAL;
+            if (((uintptr_t)d[i].w & 3u) != 0) return MI355X_E_INVAL;
+            if (d[i].row_stride < (size_t)(nb * bb) || (d[i].row_stride & 1u)) return MI355X_E_INVAL;
+            if (d[i].type != Q6_K && (d[i].row_stride & 3u)) return MI355X_E_INVAL;
+        }
+        total_rows += d[i].n_rows;
+        tmask |= type_bit(d[i].type);
+    }
+    if (tmask != 1 && tmask != 4) tmask = 7;
+    const int mode = debug ? MODE_ROWS : choose_mode(total_rows, nb, M);
+    a.n_desc = n_desc;
+    a.nb = (int)nb;
+    a.R = mode == MODE_ROWS ? BLOCKS_PER_STEP : 1;
+    a.S = mode == MODE_ROWS ? (int)nb : (int)((nb + 7) / 8);
+    a.m_total = (int)M;
+    int64_t tasks = 0;
+    for (int i = 0; i < n_desc; ++i) {
+        a.type[i] = d[i].type;
+        a.n_rows[i] = (int)d[i].n_rows;
+        a.w[i] = (const uint8_t *)d[i].w;
+        a.row_stride[i] = (int64_t)d[i].row_stride;
+        a.y[i] = d[i].y;
+        a.task_prefix[i] = (int)tasks;
+        tasks += (d[i].n_rows + a.R - 1) / a.R;
+    }
+    if (tasks > 0x7fffffff) return MI355X_E_INVAL;
+    for (int i = n_desc; i <= MI355X_MAX_FUSED; ++i) a.task_prefix[i] = (int)tasks;
+    a.tasks_total = (int)tasks;
+    pl.mode = mode;
+    pl.ncol = ncol;
+    pl.fusedq = fusedq;
+    pl.debug = debug;
+    pl.tmask = tmask;
+    pl.fn = pick_gemv(mode, ncol, fusedq, debug, tmask);
+    const int64_t wgs_needed = (tasks + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    // at most one wave of resident workgroups; each wave grid-strides over row tasks
+    const int64_t base_lds = lds_layout(ncol, (int)nb, 0).total;
+    if ((size_t)base_lds > kMaxLds) return MI355X_E_UNSUPPORTED;
+    int64_t wgs = (int64_t)num_cus() * resident_wgs(pl.fn, (size_t)base_lds + 2048);
+    if (wgs > wgs_needed) wgs = wgs_needed > 0 ? wgs_needed : 1;
+    // staged outputs: bound the tasks per wave so the LDS output area stays small
+    const int rt = a.R;
+    int64_t tpw = (tasks + wgs * WAVES_PER_WG - 1) / (wgs * WAVES_PER_WG);
+    while (tpw * rt * ncol * 4 * WAVES_PER_WG > 8192 && tpw > 1) {
+        wgs *= 2;
+        tpw = (tasks + wgs * WAVES_PER_WG - 1) / (wgs * WAVES_PER_WG);
+    }
+    a.out_per_wave = (int)(tpw * rt * ncol);
+    const LdsLayout L = lds_layout(ncol, (int)nb, a.out_per_wave);
+    if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
+    pl.lds = (size_t)L.total;
+    pl.grid = dim3((unsigned)wgs, (unsigned)((M + ncol - 1) / ncol), 1);
+    return MI355X_OK;
+}
+
+int launch_gemv(const GemvPlan &pl, hipStream_t stream) {
+    const GemvArgs &a = pl.a;
     if (a.tasks_total == 0 || a.m_total == 0) return MI355X_OK;
-    gemv_fn fn = pick_gemv(ncol, fusedq, debug, tmask);
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
-        hipExtLaunchKernelGGL(fn, grid, dim3(WG_THREADS), (uint32_t)lds, stream, e0, e1, 0, a);
-        timing_log(gemv_name(ncol, fusedq, debug, tmask).c_str(), gemv_bytes(a, fusedq), e0, e1);
+        hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), (uint32_t)pl.lds, stream, e0, e1, 0, a);
+        timing_log(gemv_name(pl), gemv_bytes(a, pl.fusedq), e0, e1);
     } else {
-        hipLaunchKernelGGL(fn, grid, dim3(WG_THREADS), lds, stream, a);
+        hipLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), pl.lds, stream, a);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
@@ -306,17 +342,14 @@ int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne0
     if (ne11 > 0x7fffffff) return MI355X_E_INVAL;
     mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
     const int ncol = choose_ncol(ne11, (int)(ne00 / QK));
-    GemvArgs a;
-    dim3 grid;
-    size_t lds;
-    int tmask;
-    int rc = plan_gemv(&d, 1, ne00, ne11, ncol, a, grid, lds, tmask);
+    GemvPlan pl;
+    int rc = plan_gemv(&d, 1, ne00, ne11, ncol, false, false, pl);
     if (rc) return rc;
-    a.xq = (const uint8_t *)src1_q8;
-    a.xq_col_stride = (int64_t)nb11;
-    a.y_col_stride[0] = (int64_t)(nb1 / 4);
+    pl.a.xq = (const uint8_t *)src1_q8;
+    pl.a.xq_col_stride = (int64_t)nb11;
+    pl.a.y_col_stride[0] = (int64_t)(nb1 / 4);
     if (!device_ok()) return MI355X_E_NODEVICE;
-    return launch_gemv(a, grid, lds, ncol, false, false, tmask, (hipStream_t)stream);
+    return launch_gemv(pl, (hipStream_t)stream);
 }
 
 int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01, const float *src1,
@@ -330,17 +363,14 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     if (ne11 > 1 && (nb11 < (size_t)ne00 * 4 || nb1 < (size_t)ne01 * 4)) return MI355X_E_INVAL;
     if (ne11 == 1) {
         mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
-        GemvArgs a;
-        dim3 grid;
-        size_t lds;
-        int tmask;
-        int rc = plan_gemv(&d, 1, ne00, 1, 1, a, grid, lds, tmask);
+        GemvPlan pl;
+        int rc = plan_gemv(&d, 1, ne00, 1, 1, true, false, pl);
         if (rc) return rc;
-        a.x = src1;
-        a.x_col_stride = (int64_t)(nb11 / 4);
-        a.y_col_stride[0] = (int64_t)(nb1 / 4);
+        pl.a.x = src1;
+        pl.a.x_col_stride = (int64_t)(nb11 / 4);
+        pl.a.y_col_stride[0] = (int64_t)(nb1 / 4);
         if (!device_ok()) return MI355X_E_NODEVICE;
-        return launch_gemv(a, grid, lds, 1, true, false, tmask, (hipStream_t)stream);
+        return launch_gemv(pl, (hipStream_t)stream);
     }
     const size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
@@ -353,18 +383,15 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
 
 int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k, void *stream) {
     if (!descs || !x || ((uintptr_t)x & 3u)) return MI355X_E_INVAL;
-    GemvArgs a;
-    dim3 grid;
-    size_t lds;
-    int tmask;
-    int rc = plan_gemv(descs, n_desc, k, 1, 1, a, grid, lds, tmask);
+    GemvPlan pl;
+    int rc = plan_gemv(descs, n_desc, k, 1, 1, true, false, pl);
     if (rc) return rc;
     for (int i = 0; i < n_desc; ++i)
         if (descs[i].y && ((uintptr_t)descs[i].y & 3u)) return MI355X_E_INVAL;
-    a.x = x;
-    a.x_col_stride = k;
+    pl.a.x = x;
+    pl.a.x_col_stride = k;
     if (!device_ok()) return MI355X_E_NODEVICE;
-    return launch_gemv(a, grid, lds, 1, true, false, tmask, (hipStream_t)stream);
+    return launch_gemv(pl, (hipStream_t)stream);
 }
 
 int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
@@ -375,17 +402,14 @@ int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, i
     const int64_t nb = ne00 / QK;
     float *dst = (float *)out;
     mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
-    GemvArgs a;
-    dim3 grid;
-    size_t lds;
-    int tmask;
-    int rc = plan_gemv(&d, 1, ne00, 1, 1, a, grid, lds, tmask);
+    GemvPlan pl;
+    int rc = plan_gemv(&d, 1, ne00, 1, 1, false, true, pl);
     if (rc) return rc;
-    a.xq = (const uint8_t *)src1_q8;
-    a.xq_col_stride = (int64_t)(nb * 292);
-    a.dbg = out;
+    pl.a.xq = (const uint8_t *)src1_q8;
+    pl.a.xq_col_stride = (int64_t)(nb * 292);
+    pl.a.dbg = out;
     if (!device_ok()) return MI355X_E_NODEVICE;
-    return launch_gemv(a, grid, lds, 1, false, true, tmask, (hipStream_t)stream);
+    return launch_gemv(pl, (hipStream_t)stream);
 }
 
 int mi355x_timing_enable(int enable) {

@@ -33,6 +33,7 @@ struct GemvArgs {
     int S;            // wave-steps per task
     int m_total;      // activation columns in total (grid.y covers ceil(m_total/NCOL))
     int tasks_total;
+    int out_per_wave;     // LDS floats per wave for staged outputs (tasks_per_wave * R * NCOL)
     int task_prefix[MI355X_MAX_FUSED + 1];
     int type[MI355X_MAX_FUSED];
     int n_rows[MI355X_MAX_FUSED];
@@ -49,10 +50,10 @@ struct GemvArgs {
 
 // LDS layout of one workgroup (dynamic shared memory).
 struct LdsLayout {
-    int act_qs, act_bs, act_d, recs, total;
+    int act_qs, act_bs, act_d, recs, outs, total;
 };
 
-__host__ __device__ inline LdsLayout lds_layout(int ncol, int nb) {
+__host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wave) {
     LdsLayout L;
     L.act_qs = 0;
     L.act_bs = ncol * nb * ACT_QS_STRIDE;
@@ -60,7 +61,8 @@ __host__ __device__ inline LdsLayout lds_layout(int ncol, int nb) {
     int recs = L.act_d + ncol * nb * 4;
     recs = (recs + 15) & ~15;
     L.recs = recs;
-    L.total = recs + WAVES_PER_WG * ncol * BLOCKS_PER_STEP * 16;
+    L.outs = recs + WAVES_PER_WG * ncol * BLOCKS_PER_STEP * 16;
+    L.total = L.outs + WAVES_PER_WG * out_per_wave * 4;
     return L;
 }
 

@@ -98,8 +98,7 @@ struct Q8Lane {
     float d;
 };
 
-__device__ __forceinline__ Q8Lane quant_block_wave(const float *xb, int lane) {
-    const f32x4a v = *(const f32x4a *)(xb + 4 * lane);
+__device__ __forceinline__ Q8Lane quant_values_wave(const f32x4a v, int lane) {
     const float a0 = fabsf(v.x), a1 = fabsf(v.y), a2 = fabsf(v.z), a3 = fabsf(v.w);
     // amax; NaN never wins (fmaxf drops NaN, as `ax > amax` is false for NaN)
     const float m = wave_max_f32(fmaxf(fmaxf(a0, a1), fmaxf(a2, a3)));  // fmaxf drops NaN
@@ -139,6 +138,10 @@ __device__ __forceinline__ Q8Lane quant_block_wave(const float *xb, int lane) {
     r.bsum = s;
     r.d = 1.f / iscale;
     return r;
+}
+
+__device__ __forceinline__ Q8Lane quant_block_wave(const float *xb, int lane) {
+    return quant_values_wave(*(const f32x4a *)(xb + 4 * lane), lane);
 }
 
 // ------------------------------------------------------------------ Q8_K quantize kernel
@@ -309,6 +312,8 @@ struct StepInfo {
     int m, row0, rows;
 };
 
+// Task t -> (matrix, first row, rows in task). All inputs are wave-uniform, so this
+// runs on the scalar unit with scalar loads from the kernel-argument segment.
 __device__ __forceinline__ StepInfo task_info(const GemvArgs &a, int t) {
     int m = 0;
 #pragma unroll
@@ -322,164 +327,260 @@ __device__ __forceinline__ StepInfo task_info(const GemvArgs &a, int t) {
     return si;
 }
 
-// TMASK: bit0 Q4_K, bit1 Q5_K, bit2 Q6_K (types compiled into this instance).
-template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
+template <int TMASK>
+__device__ __forceinline__ void load_block(Regs &r, const uint8_t *bp, int type, int p) {
+    if (TMASK == 1) { load_q4K(r, bp, p); return; }
+    if (TMASK == 4) { load_q6K(r, bp, p); return; }
+    if (type == Q4_K) load_q4K(r, bp, p);
+    else if (type == Q5_K) load_q5K(r, bp, p);
+    else load_q6K(r, bp, p);
+}
+
+template <int TMASK>
+__device__ __forceinline__ void lane_partials(const Regs &rr, const uint8_t *aq, const int16_t *ab, int type, int p,
+                                              int &isum, int &imin, uint32_t &dh) {
+    if (TMASK == 1 || (TMASK != 4 && type == Q4_K)) lane_q4K(rr, aq, ab, p, isum, imin);
+    else if (TMASK != 4 && type == Q5_K) lane_q5K(rr, aq, ab, p, isum, imin);
+    else lane_q6K(rr, aq, ab, p, isum, imin, dh);
+}
+
+// The reference's per-superblock fp32 update from the integer partials.
+__device__ __forceinline__ float chain_update(int type, int isum, int imin, const Regs &rr, uint32_t dh, float yd,
+                                              float s) {
+    Rec r;
+    if (type == Q6_K) {
+        r.a = isum - 32 * imin;
+        r.b = 0;
+        r.c = h2f(dh) * yd;   // d_all * y.d
+        r.e = 0.f;
+    } else {
+        r.a = isum;
+        r.b = imin;
+        r.c = yd * h2f(rr.a.x & 0xffffu);  // y.d * fp16(x.d)
+        r.e = yd * h2f(rr.a.x >> 16);      // y.d * fp16(x.dmin)
+    }
+    return chain_step(type, r, s);
+}
+
+enum { MODE_ROWS = 0, MODE_BLOCKS = 1 };
+
+// Walks one wave's (task, step) sequence without divisions: task info (matrix,
+// type, per-lane row base) is refreshed only when the task changes. Past the
+// last step it stays on the last step (the clamped "tail" loads re-read it).
+template <int MODE>
+struct Cursor {
+    int k, s;             // task ordinal within this wave, step within task
+    int m, type, bb;      // matrix index, its type and block bytes
+    int row0, rows;       // first row and rows of the task
+    bool valid;           // this lane's octet maps to a real row / block
+    const uint8_t *base;  // this lane's row base (+ task's first block for BLOCKS)
+
+    __device__ __forceinline__ void load_task(const GemvArgs &a, int t, int g) {
+        const StepInfo si = task_info(a, t);
+        m = si.m;
+        row0 = si.row0;
+        rows = si.rows;
+        type = a.type[m];
+        bb = block_bytes(type);
+        int row = row0;
+        if (MODE == MODE_ROWS) row += (g < rows ? g : 0);
+        base = a.w[m] + (int64_t)row * a.row_stride[m];
+    }
+    __device__ __forceinline__ void start(const GemvArgs &a, int wgid, int g) {
+        k = 0;
+        s = 0;
+        load_task(a, wgid, g);
+    }
+    // advance to the next step; returns false (and stays put) past the end
+    __device__ __forceinline__ void next(const GemvArgs &a, int S, int my_tasks, int wgid, int nwaves, int g) {
+        if (s + 1 < S) {
+            ++s;
+        } else if (k + 1 < my_tasks) {
+            ++k;
+            s = 0;
+            load_task(a, wgid + k * nwaves, g);
+        }
+    }
+    __device__ __forceinline__ const uint8_t *block(int nb, int g, int &blk) {
+        if (MODE == MODE_ROWS) {
+            valid = g < rows;
+            blk = s;
+        } else {
+            blk = BLOCKS_PER_STEP * s + g;
+            valid = blk < nb;
+            blk = valid ? blk : nb - 1;
+        }
+        return base + (int64_t)blk * bb;
+    }
+};
+
+// Decode / small-batch GEMV.
+//   MODE_ROWS:   a task is 8 rows; octet g owns row row0+g and walks its superblocks
+//                in order (one superblock per wave-step), keeping the fp32 chain in
+//                registers. All octets read the same activation superblock (LDS broadcast).
+//   MODE_BLOCKS: a task is 1 row; octet g takes superblock 8s+g of step s; the octet
+//                leaders drop records into LDS and one lane runs the chain over the 8
+//                records of the step. Used when N is too small to give every CU
+//                enough 8-row tasks.
+// Loads run D steps ahead through a ring of registers; addresses past the end are
+// clamped to valid blocks so every step issues the same loads (counted vmcnt waits).
+template <int MODE, int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int nb = a.nb;
-    const LdsLayout L = lds_layout(NCOL, nb);
+    const LdsLayout L = lds_layout(NCOL, nb, a.out_per_wave);
     uint8_t *act_qs = smem + L.act_qs;
     int16_t *act_bs = (int16_t *)(smem + L.act_bs);
     float *act_d = (float *)(smem + L.act_d);
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int lane = threadIdx.x & 63;
+    // wave index made provably uniform so that every per-step quantity (task, matrix,
+    // descriptor fields) lives in SGPRs and is fetched with scalar loads
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int g = lane >> 3, p = lane & 7;
     Rec *recs = (Rec *)(smem + L.recs) + wave * NCOL * BLOCKS_PER_STEP;
+    // Results are staged in LDS [task k][col][row-in-task] and written after the
+    // loop: a global store inside the pipelined loop would force vmcnt drains.
+    float *outs = (float *)(smem + L.outs) + wave * a.out_per_wave;
 
     const int col0 = blockIdx.y * NCOL;
     const int ncol = (a.m_total - col0) < NCOL ? (a.m_total - col0) : NCOL;
-
     const int nwaves = gridDim.x * WAVES_PER_WG;
     const int wgid = blockIdx.x * WAVES_PER_WG + wave;
     const int my_tasks = a.tasks_total > wgid ? (a.tasks_total - wgid + nwaves - 1) / nwaves : 0;
-    const int S = a.S, R = a.R;
+    const int S = MODE == MODE_ROWS ? nb : (nb + BLOCKS_PER_STEP - 1) / BLOCKS_PER_STEP;
+    constexpr int RT = MODE == MODE_ROWS ? BLOCKS_PER_STEP : 1;  // rows per task
     const int Q = my_tasks * S;
 
-    int lane_row = 0, lane_blk = g;
-    if (R > 1) {
-        lane_row = g / nb;
-        lane_blk = g - lane_row * nb;
-    }
+    constexpr int D = (TMASK & 4) ? 3 : 4;  // steps in flight
+    Regs ring[D];
+    Cursor<MODE> ic, cc;  // issue and compute cursors
 
-    // Steps in flight per buffer; two buffers alternate so the next batch's loads
-    // are in flight while the current batch is computed.
-    constexpr int U = (TMASK & 4) ? 2 : 4;
-    Regs ra[U], rb[U];
-
-    auto issue = [&](Regs (&regs)[U], int q0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = q0 + u;
-            if (q < Q) {
-                const int k = q / S, s = q - k * S;
-                const StepInfo si = task_info(a, wgid + k * nwaves);
-                const int type = a.type[si.m];
-                const int blk = (R == 1) ? 8 * s + g : lane_blk;
-                const bool valid = (R == 1) ? (blk < nb) : (g < R * nb && lane_row < si.rows);
-                if (valid) {
-                    const uint8_t *bp = a.w[si.m] + (int64_t)(si.row0 + lane_row) * a.row_stride[si.m] +
-                                        (int64_t)blk * block_bytes(type);
-                    if ((TMASK & 1) && type == Q4_K) load_q4K(regs[u], bp, p);
-                    else if ((TMASK & 2) && type == Q5_K) load_q5K(regs[u], bp, p);
-                    else if ((TMASK & 4) && type == Q6_K) load_q6K(regs[u], bp, p);
-                }
-            }
-        }
+    auto issue = [&](Regs &r) {
+        int blk;
+        const uint8_t *bp = ic.block(nb, g, blk);
+        load_block<TMASK>(r, bp, ic.type, p);
+        ic.next(a, S, my_tasks, wgid, nwaves, g);
     };
 
-    float acc = 0.f;  // running fp32 chain of this lane's (row, column)
+    float acc[NCOL];
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c) acc[c] = 0.f;
 
-    auto compute = [&](Regs (&regs)[U], int q0) {
+    auto compute = [&](const Regs &r, const bool live) {
+        int blk;
+        const uint8_t *bp = cc.block(nb, g, blk);
+        const int type = cc.type, s = cc.s;
+        const bool valid = cc.valid;
+        Regs rr = r;
+        if ((TMASK & 4) && type == Q6_K) {
+            const uint32_t sh = (uint32_t)((uintptr_t)bp & 3u);  // realign 2-mod-4 blocks
+            rr.a = realign(rr.a, rr.e0, sh);
+            rr.b = realign(rr.b, rr.e1, sh);
+            rr.c = realign(rr.c, rr.e2, sh);
+        }
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int q = q0 + u;
-            if (q >= Q) break;
-            const int k = q / S, s = q - k * S;
-            const StepInfo si = task_info(a, wgid + k * nwaves);
-            const int type = a.type[si.m];
-            const int blk = (R == 1) ? 8 * s + g : lane_blk;
-            const bool valid = (R == 1) ? (blk < nb) : (g < R * nb && lane_row < si.rows);
-            const int cblk = valid ? blk : 0;
-            Regs rr = regs[u];
-            if ((TMASK & 4) && type == Q6_K) {
-                // realign the 2-mod-4 blocks (see load_q6K)
-                const uint8_t *bp = a.w[si.m] + (int64_t)(si.row0 + lane_row) * a.row_stride[si.m] +
-                                    (int64_t)cblk * 210;
-                const uint32_t q6s = (uint32_t)((uintptr_t)bp & 3u);
-                rr.a = realign(rr.a, rr.e0, q6s);
-                rr.b = realign(rr.b, rr.e1, q6s);
-                rr.c = realign(rr.c, rr.e2, q6s);
-            }
-#pragma unroll
-            for (int c = 0; c < NCOL; ++c) {
-                if (c < ncol) {
-                    const int cb = c * nb + cblk;
-                    const uint8_t *aq = act_qs + cb * ACT_QS_STRIDE;
-                    const int16_t *ab = act_bs + cb * 16;
-                    int isum = 0, imin = 0;
-                    uint32_t dh = 0;
-                    if ((TMASK & 1) && type == Q4_K) lane_q4K(rr, aq, ab, p, isum, imin);
-                    else if ((TMASK & 2) && type == Q5_K) lane_q5K(rr, aq, ab, p, isum, imin);
-                    else if ((TMASK & 4) && type == Q6_K) lane_q6K(rr, aq, ab, p, isum, imin, dh);
-                    isum = octet_sum(isum);
-                    imin = octet_sum(imin);
-                    if (p == 0 && valid) {
-                        const float yd = act_d[cb];
-                        Rec rec;
-                        if (type == Q6_K) {
-                            rec.a = isum - 32 * imin;
-                            rec.b = 0;
-                            rec.c = h2f(dh) * yd;
-                            rec.e = 0.f;
-                        } else {
-                            rec.a = isum;
-                            rec.b = imin;
-                            rec.c = yd * h2f(rr.a.x & 0xffffu);
-                            rec.e = yd * h2f(rr.a.x >> 16);
-                        }
-                        recs[c * BLOCKS_PER_STEP + g] = rec;
-                        if (DEBUG && c == 0) {
-                            const int64_t o = ((int64_t)(si.row0 + lane_row) * nb + blk) * 2;
-                            a.dbg[o] = isum;
-                            a.dbg[o + 1] = imin;
-                        }
+        for (int c = 0; c < NCOL; ++c) {
+            if (c < ncol) {
+                const int cb = c * nb + blk;
+                int isum = 0, imin = 0;
+                uint32_t dh = rr.dh;
+                lane_partials<TMASK>(rr, act_qs + cb * ACT_QS_STRIDE, act_bs + cb * 16, type, p, isum, imin, dh);
+                isum = octet_sum(isum);
+                imin = octet_sum(imin);
+                const float yd = act_d[cb];
+                if (MODE == MODE_ROWS) {
+                    // every lane of the octet holds the same sums: all 8 run the chain
+                    acc[c] = chain_update(type, isum, imin, rr, dh, yd, acc[c]);
+                    if (DEBUG && c == 0 && p == 0 && valid && live) {
+                        const int64_t o = ((int64_t)(cc.row0 + g) * nb + blk) * 2;
+                        a.dbg[o] = isum;
+                        a.dbg[o + 1] = imin;
                     }
+                    if (s == S - 1) {
+                        if (!DEBUG && p == 0 && live) outs[(cc.k * NCOL + c) * RT + g] = acc[c];
+                        acc[c] = 0.f;
+                    }
+                } else if (p == 0 && valid) {  // BLOCKS: records of this step
+                    Rec rec;
+                    if (type == Q6_K) {
+                        rec.a = isum - 32 * imin;
+                        rec.b = 0;
+                        rec.c = h2f(dh) * yd;
+                        rec.e = 0.f;
+                    } else {
+                        rec.a = isum;
+                        rec.b = imin;
+                        rec.c = yd * h2f(rr.a.x & 0xffffu);
+                        rec.e = yd * h2f(rr.a.x >> 16);
+                    }
+                    recs[c * BLOCKS_PER_STEP + g] = rec;
                 }
             }
+        }
+        if (MODE == MODE_BLOCKS) {
             wave_lds_fence();
-            // serial fp32 chain in superblock order: all 8 records are read at once,
-            // then the dependent fmas run back to back
-            if (R == 1) {
-                if (lane < ncol) {
-                    if (s == 0) acc = 0.f;
-                    const int cnt = (nb - 8 * s) < 8 ? (nb - 8 * s) : 8;
-                    Rec rv[BLOCKS_PER_STEP];
+            if (lane < ncol) {
+                const int cnt = (nb - BLOCKS_PER_STEP * s) < BLOCKS_PER_STEP ? (nb - BLOCKS_PER_STEP * s)
+                                                                            : BLOCKS_PER_STEP;
+                Rec rv[BLOCKS_PER_STEP];
 #pragma unroll
-                    for (int i = 0; i < BLOCKS_PER_STEP; ++i) rv[i] = recs[lane * BLOCKS_PER_STEP + i];
+                for (int i = 0; i < BLOCKS_PER_STEP; ++i) rv[i] = recs[lane * BLOCKS_PER_STEP + i];
+                float v = s == 0 ? 0.f : acc[0];
 #pragma unroll
-                    for (int i = 0; i < BLOCKS_PER_STEP; ++i)
-                        if (i < cnt) acc = chain_step(type, rv[i], acc);
-                    if (!DEBUG && s == S - 1)
-                        a.y[si.m][(int64_t)(col0 + lane) * a.y_col_stride[si.m] + si.row0] = acc;
-                }
-            } else {
-                const int c = lane / R, r = lane - c * R;
-                if (!DEBUG && c < ncol && r < si.rows) {
-                    Rec rv[BLOCKS_PER_STEP];
-#pragma unroll
-                    for (int i = 0; i < BLOCKS_PER_STEP; ++i)
-                        rv[i] = recs[c * BLOCKS_PER_STEP + ((r * nb + i) & (BLOCKS_PER_STEP - 1))];
-                    float v = 0.f;
-#pragma unroll
-                    for (int i = 0; i < BLOCKS_PER_STEP; ++i)
-                        if (i < nb) v = chain_step(type, rv[i], v);
-                    a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = v;
-                }
+                for (int i = 0; i < BLOCKS_PER_STEP; ++i)
+                    if (i < cnt) v = chain_step(type, rv[i], v);
+                acc[0] = v;
+                if (!DEBUG && live && s == S - 1) outs[cc.k * NCOL + lane] = v;
             }
             wave_lds_fence();
         }
+        cc.next(a, S, my_tasks, wgid, nwaves, g);
     };
 
-    // Weights for the first batch are in flight while the activation is staged.
-    issue(ra, 0);
-
+    // Activation loads go out first, then the first D weight steps, so both
+    // latencies overlap; the activation is then quantized / staged into LDS.
+    // Every load below is unconditional (clamped addresses): the compiler can then
+    // count outstanding loads exactly and wait only for the ones it consumes.
+    const int t0 = wgid < a.tasks_total ? wgid : a.tasks_total - 1;
     if (FUSEDQ) {
-        for (int b = wave; b < nb; b += WAVES_PER_WG) {
-            const Q8Lane q = quant_block_wave(a.x + (int64_t)col0 * a.x_col_stride + (int64_t)b * QK, lane);
-            *(uint32_t *)(act_qs + b * ACT_QS_STRIDE + 4 * lane) = q.qs4;
-            if ((lane & 3) == 0) act_bs[b * 16 + (lane >> 2)] = (int16_t)q.bsum;
-            if (lane == 0) act_d[b] = q.d;
+        constexpr int XB = 8;  // superblocks per wave per batch (8 float4 registers)
+        const float *xc = a.x + (int64_t)col0 * a.x_col_stride;
+        f32x4a xv[XB];
+#pragma unroll
+        for (int i = 0; i < XB; ++i) {
+            const int b = min(wave + i * WAVES_PER_WG, nb - 1);
+            xv[i] = *(const f32x4a *)(xc + (int64_t)b * QK + 4 * lane);
+        }
+        ic.start(a, t0, g);
+        cc.start(a, t0, g);
+#pragma unroll
+        for (int j = 0; j < D; ++j) issue(ring[j]);
+        auto quant_batch = [&](int b0) {
+#pragma unroll
+            for (int i = 0; i < XB; ++i) {
+                const int b = b0 + i * WAVES_PER_WG;
+                if (b < nb) {
+                    const Q8Lane q = quant_values_wave(xv[i], lane);
+                    *(uint32_t *)(act_qs + b * ACT_QS_STRIDE + 4 * lane) = q.qs4;
+                    if ((lane & 3) == 0) act_bs[b * 16 + (lane >> 2)] = (int16_t)q.bsum;
+                    if (lane == 0) act_d[b] = q.d;
+                }
+            }
+        };
+        quant_batch(wave);  // first batch straight-line: its waits skip the weight loads
+        for (int b0 = wave + XB * WAVES_PER_WG; b0 < nb; b0 += XB * WAVES_PER_WG) {  // K > 8192 only
+#pragma unroll
+            for (int i = 0; i < XB; ++i) {
+                const int b = min(b0 + i * WAVES_PER_WG, nb - 1);
+                xv[i] = *(const f32x4a *)(xc + (int64_t)b * QK + 4 * lane);
+            }
+            quant_batch(b0);
         }
     } else {
+        ic.start(a, t0, g);
+        cc.start(a, t0, g);
+#pragma unroll
+        for (int j = 0; j < D; ++j) issue(ring[j]);
         const int per_col = nb * 73;
         for (int i = threadIdx.x; i < ncol * per_col; i += WG_THREADS) {
             const int c = i / per_col;
@@ -495,27 +596,44 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     }
     __syncthreads();
 
-    for (int q0 = 0; q0 < Q; q0 += 2 * U) {
-        issue(rb, q0 + U);
-        compute(ra, q0);
-        if (q0 + U >= Q) break;
-        issue(ra, q0 + 2 * U);
-        compute(rb, q0 + U);
+    // Steps padded to a multiple of D: the ring loop body is straight-line code.
+    // Padding steps recompute the clamped last step and never store (live == false).
+    const int Qp = (Q + D - 1) / D * D;
+    for (int q0 = 0; q0 < Qp; q0 += D) {
+#pragma unroll
+        for (int j = 0; j < D; ++j) {
+            compute(ring[j], q0 + j < Q);
+            issue(ring[j]);
+        }
+    }
+
+    // flush the staged results: task k of this wave -> rows row0..row0+RT-1, NCOL columns
+    if (!DEBUG && my_tasks > 0) {
+        wave_lds_fence();
+        for (int k = 0; k < my_tasks; ++k) {
+            const StepInfo si = task_info(a, wgid + k * nwaves);
+            for (int i = lane; i < NCOL * RT; i += WAVE) {
+                const int c = i / RT, r = i - c * RT;
+                if (c < ncol && r < si.rows)
+                    a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = outs[k * NCOL * RT + i];
+            }
+        }
     }
 }
 
 // ------------------------------------------------------------------ explicit instances
-#define KQ_GEMV_INST(NC, FQ, DB, TM) \
-    template __global__ void kq_gemv<NC, FQ, DB, TM>(const GemvArgs a);
+#define KQ_GEMV_INST(MD, NC, FQ, DB, TM) \
+    template __global__ void kq_gemv<MD, NC, FQ, DB, TM>(const GemvArgs a);
+#define KQ_GEMV_INST_TM(MD, NC, FQ, DB) \
+    KQ_GEMV_INST(MD, NC, FQ, DB, 1) KQ_GEMV_INST(MD, NC, FQ, DB, 4) KQ_GEMV_INST(MD, NC, FQ, DB, 7)
 
-#define KQ_GEMV_INST_TM(NC, FQ, DB) \
-    KQ_GEMV_INST(NC, FQ, DB, 1) KQ_GEMV_INST(NC, FQ, DB, 2) KQ_GEMV_INST(NC, FQ, DB, 4) KQ_GEMV_INST(NC, FQ, DB, 7)
-
-KQ_GEMV_INST_TM(1, true, false)
-KQ_GEMV_INST_TM(1, false, false)
-KQ_GEMV_INST_TM(2, false, false)
-KQ_GEMV_INST_TM(4, false, false)
-KQ_GEMV_INST_TM(8, false, false)
-KQ_GEMV_INST_TM(1, false, true)
+KQ_GEMV_INST_TM(MODE_ROWS, 1, true, false)
+KQ_GEMV_INST_TM(MODE_ROWS, 1, false, false)
+KQ_GEMV_INST_TM(MODE_ROWS, 2, false, false)
+KQ_GEMV_INST_TM(MODE_ROWS, 4, false, false)
+KQ_GEMV_INST_TM(MODE_ROWS, 8, false, false)
+KQ_GEMV_INST_TM(MODE_ROWS, 1, false, true)
+KQ_GEMV_INST_TM(MODE_BLOCKS, 1, true, false)
+KQ_GEMV_INST_TM(MODE_BLOCKS, 1, false, false)
 
 }  // namespace kq

@@ -1,0 +1,64 @@
+"""GEMV microbenchmark: achieved algorithmic GB/s per shape/type, kernel timestamps
+from the library's launch-timing hook (hipExtLaunchKernelGGL events). Weight buffers
+rotate over > 600 MB so the 256 MB Infinity Cache cannot serve them."""
+import json
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ggml-neon-opt_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import ggml_mi355x as g  # noqa: E402
+from bench import random_kquant  # noqa: E402
+
+SHAPES = [("tl q/o", 12, 2048, 2048), ("tl qkv-fused", 12, 2048, 2560), ("tl gate", 12, 2048, 5632),
+          ("tl down", 12, 5632, 2048), ("tl out q6", 14, 2048, 32000), ("l3 up", 12, 4096, 14336),
+          ("l3 down", 12, 14336, 4096), ("70b down", 12, 28672, 8192), ("l3 q6 down", 14, 14336, 4096)]
+
+
+def run(reps=20):
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(1)
+    out = []
+    for label, typ, K, N in SHAPES:
+        nbytes = N * (K // 256) * g.BLOCK_BYTES[typ]
+        nbuf = max(2, int(np.ceil(640e6 / nbytes)))
+        ws = [random_kquant(typ, N, K, gen, dev) for _ in range(nbuf)]
+        x = torch.randn(1, K, device=dev, generator=gen)
+        y = torch.empty(1, N, device=dev)
+        for w in ws:
+            g.mul_mat(typ, w, K, x, out=y)
+        g.timing_enable(True)
+        for r in range(reps):
+            g.mul_mat(typ, ws[r % nbuf], K, x, out=y)
+        rows = g.timing_read()
+        g.timing_enable(False)
+        ms = np.array([r[2] for r in rows])
+        b = rows[0][1]
+        med = float(np.median(ms))
+        out.append({"shape": label, "type": typ, "K": K, "N": N, "kernel": rows[0][0], "MB": round(b / 1e6, 2),
+                    "us": round(med * 1e3, 2), "GBps": round(b / (med * 1e-3) / 1e9, 1)})
+        del ws
+        torch.cuda.empty_cache()
+    return out
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 1 and sys.argv[1] == "child":
+        print(json.dumps(run()))
+        sys.exit(0)
+    for mode in ("auto", "rows", "blocks"):
+        env = dict(os.environ)
+        if mode != "auto":
+            env["MI355X_GEMV_MODE"] = mode
+        r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)
+        if r.returncode != 0:
+            print(r.stderr[-2000:])
+            sys.exit(r.returncode)
+        for row in json.loads(r.stdout.strip().splitlines()[-1]):
+            print(f"{mode:6s} {row['shape']:14s} K={row['K']:6d} N={row['N']:6d} {row['MB']:8.2f} MB "
+                  f"{row['us']:8.2f} us {row['GBps']:8.1f} GB/s  {row['kernel']}")
