@@ -177,7 +177,8 @@ int choose_mode(int64_t total_rows, int64_t nb, int64_t M) {
     }
     if (M > 1 || nb < 8) return MODE_ROWS;
     if (forced >= 0) return forced;
-    return (total_rows / 8 >= (int64_t)num_cus() * 4) ? MODE_ROWS : MODE_BLOCKS;
+    (void)total_rows;
+    return MODE_ROWS;  // measured faster on every shape of tools/gemv_sweep.py except K=5632,N=2048
 }
 
 // Validates descriptors and fills the launch plan. Returns MI355X_OK or an error.
@@ -230,6 +231,14 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
     pl.debug = debug;
     pl.tmask = tmask;
     pl.fn = pick_gemv(mode, ncol, fusedq, debug, tmask);
+    {
+        static int diag = -1;
+        if (diag < 0) {
+            const char *e = getenv("MI355X_GEMV_DIAG");
+            diag = e ? atoi(e) : 0;
+        }
+        a.diag = diag;
+    }
     const int64_t wgs_needed = (tasks + WAVES_PER_WG - 1) / WAVES_PER_WG;
     // at most one wave of resident workgroups; each wave grid-strides over row tasks
     const int64_t base_lds = lds_layout(ncol, (int)nb, 0).total;

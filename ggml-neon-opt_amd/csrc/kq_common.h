@@ -34,6 +34,7 @@ struct GemvArgs {
     int m_total;      // activation columns in total (grid.y covers ceil(m_total/NCOL))
     int tasks_total;
     int out_per_wave;     // LDS floats per wave for staged outputs (tasks_per_wave * R * NCOL)
+    int diag;             // diagnostics: bit0 = stop after the activation prologue
     int task_prefix[MI355X_MAX_FUSED + 1];
     int type[MI355X_MAX_FUSED];
     int n_rows[MI355X_MAX_FUSED];

@@ -345,8 +345,11 @@ __device__ __forceinline__ void lane_partials(const Regs &rr, const uint8_t *aq,
 }
 
 // The reference's per-superblock fp32 update from the integer partials.
+template <int TMASK>
 __device__ __forceinline__ float chain_update(int type, int isum, int imin, const Regs &rr, uint32_t dh, float yd,
                                               float s) {
+    if (TMASK == 1) type = Q4_K;
+    if (TMASK == 4) type = Q6_K;
     Rec r;
     if (type == Q6_K) {
         r.a = isum - 32 * imin;
@@ -451,7 +454,9 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     constexpr int RT = MODE == MODE_ROWS ? BLOCKS_PER_STEP : 1;  // rows per task
     const int Q = my_tasks * S;
 
-    constexpr int D = (TMASK & 4) ? 3 : 4;  // steps in flight
+    // steps in flight: 8 x 1152 B per wave for Q4_K (enough bytes in flight per CU
+    // even at one or two waves per CU); Q6_K steps hold 16 registers, so fewer
+    constexpr int D = (TMASK & 4) ? 5 : 8;
     Regs ring[D];
     Cursor<MODE> ic, cc;  // issue and compute cursors
 
@@ -490,7 +495,7 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
                 const float yd = act_d[cb];
                 if (MODE == MODE_ROWS) {
                     // every lane of the octet holds the same sums: all 8 run the chain
-                    acc[c] = chain_update(type, isum, imin, rr, dh, yd, acc[c]);
+                    acc[c] = chain_update<TMASK>(type, isum, imin, rr, dh, yd, acc[c]);
                     if (DEBUG && c == 0 && p == 0 && valid && live) {
                         const int64_t o = ((int64_t)(cc.row0 + g) * nb + blk) * 2;
                         a.dbg[o] = isum;
@@ -526,9 +531,10 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
 #pragma unroll
                 for (int i = 0; i < BLOCKS_PER_STEP; ++i) rv[i] = recs[lane * BLOCKS_PER_STEP + i];
                 float v = s == 0 ? 0.f : acc[0];
+                const int ctype = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : type;
 #pragma unroll
                 for (int i = 0; i < BLOCKS_PER_STEP; ++i)
-                    if (i < cnt) v = chain_step(type, rv[i], v);
+                    if (i < cnt) v = chain_step(ctype, rv[i], v);
                 acc[0] = v;
                 if (!DEBUG && live && s == S - 1) outs[cc.k * NCOL + lane] = v;
             }
@@ -595,6 +601,8 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         }
     }
     __syncthreads();
+
+    if (a.diag & 1) return;  // diagnostics: prologue only
 
     // Steps padded to a multiple of D: the ring loop body is straight-line code.
     // Padding steps recompute the clamped last step and never store (live == false).

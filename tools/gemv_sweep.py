@@ -49,11 +49,15 @@ def run(reps=20):
 
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "child":
+        sys.argv = sys.argv[:1]
         print(json.dumps(run()))
         sys.exit(0)
-    for mode in ("auto", "rows", "blocks"):
+    modes = sys.argv[1:] or ["auto", "rows", "blocks", "prologue"]
+    for mode in modes:
         env = dict(os.environ)
-        if mode != "auto":
+        if mode == "prologue":
+            env["MI355X_GEMV_DIAG"] = "1"
+        elif mode != "auto":
             env["MI355X_GEMV_MODE"] = mode
         r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:
