@@ -16,9 +16,7 @@
 
 namespace kq {
 
-enum { MODE_ROWS = 0, MODE_BLOCKS = 1 };
-
-template <int MODE, int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
+template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void kq_gemv(const GemvArgs a);
 __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 
@@ -44,25 +42,23 @@ void probe_device() {
     g_dev_ok = 1;
 }
 
-template <int MODE, int NCOL, bool FUSEDQ, bool DEBUG>
+template <int NCOL, bool FUSEDQ, bool DEBUG>
 gemv_fn pick_tm(int tmask) {
     switch (tmask) {
-        case 1: return kq_gemv<MODE, NCOL, FUSEDQ, DEBUG, 1>;
-        case 4: return kq_gemv<MODE, NCOL, FUSEDQ, DEBUG, 4>;
-        default: return kq_gemv<MODE, NCOL, FUSEDQ, DEBUG, 7>;
+        case 1: return kq_gemv<NCOL, FUSEDQ, DEBUG, 1>;
+        case 4: return kq_gemv<NCOL, FUSEDQ, DEBUG, 4>;
+        default: return kq_gemv<NCOL, FUSEDQ, DEBUG, 7>;
     }
 }
 
-gemv_fn pick_gemv(int mode, int ncol, bool fusedq, bool debug, int tmask) {
-    if (mode == MODE_BLOCKS)
-        return fusedq ? pick_tm<MODE_BLOCKS, 1, true, false>(tmask) : pick_tm<MODE_BLOCKS, 1, false, false>(tmask);
-    if (debug) return pick_tm<MODE_ROWS, 1, false, true>(tmask);
-    if (fusedq) return pick_tm<MODE_ROWS, 1, true, false>(tmask);
+gemv_fn pick_gemv(int ncol, bool fusedq, bool debug, int tmask) {
+    if (debug) return pick_tm<1, false, true>(tmask);
+    if (fusedq) return pick_tm<1, true, false>(tmask);
     switch (ncol) {
-        case 1: return pick_tm<MODE_ROWS, 1, false, false>(tmask);
-        case 2: return pick_tm<MODE_ROWS, 2, false, false>(tmask);
-        case 4: return pick_tm<MODE_ROWS, 4, false, false>(tmask);
-        default: return pick_tm<MODE_ROWS, 8, false, false>(tmask);
+        case 1: return pick_tm<1, false, false>(tmask);
+        case 2: return pick_tm<2, false, false>(tmask);
+        case 4: return pick_tm<4, false, false>(tmask);
+        default: return pick_tm<8, false, false>(tmask);
     }
 }
 
@@ -128,9 +124,8 @@ void timing_log(const std::string &kernel, double bytes, hipEvent_t a, hipEvent_
 
 // Same spelling as rocprofv3's kernel names (kernel-trace "Kernel_Name").
 std::string gemv_name(const GemvPlan &pl) {
-    return std::string("kq::kq_gemv<") + std::to_string(pl.mode) + ", " + std::to_string(pl.ncol) + ", " +
-           (pl.fusedq ? "true" : "false") + ", " + (pl.debug ? "true" : "false") + ", " + std::to_string(pl.tmask) +
-           ">";
+    return std::string("kq::kq_gemv<") + std::to_string(pl.ncol) + ", " + (pl.fusedq ? "true" : "false") + ", " +
+           (pl.debug ? "true" : "false") + ", " + std::to_string(pl.tmask) + ">";
 }
 
 // Algorithmic bytes of one launch: weights + activations read + f32 outputs.
@@ -162,23 +157,9 @@ int choose_ncol(int64_t M, int nb) {
     for (int i = 0; i < 4; ++i) {
         const int nc = cands[i];
         if (nc > M && nc > 1) continue;
-        if ((size_t)lds_layout(nc, nb, 0).total <= kMaxLds / 2) return nc;
+        if ((size_t)lds_layout(nc, nb, 8 * nc).total <= kMaxLds / 2) return nc;
     }
     return 1;
-}
-
-// MODE_BLOCKS (one row per wave) only pays when N is too small to give every CU
-// a few 8-row tasks. MI355X_GEMV_MODE=rows|blocks forces a mode (experiments).
-int choose_mode(int64_t total_rows, int64_t nb, int64_t M) {
-    static int forced = -2;
-    if (forced == -2) {
-        const char *e = getenv("MI355X_GEMV_MODE");
-        forced = !e ? -1 : (strcmp(e, "rows") == 0 ? MODE_ROWS : strcmp(e, "blocks") == 0 ? MODE_BLOCKS : -1);
-    }
-    if (M > 1 || nb < 8) return MODE_ROWS;
-    if (forced >= 0) return forced;
-    (void)total_rows;
-    return MODE_ROWS;  // measured faster on every shape of tools/gemv_sweep.py except K=5632,N=2048
 }
 
 // Validates descriptors and fills the launch plan. Returns MI355X_OK or an error.
@@ -206,11 +187,9 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
         tmask |= type_bit(d[i].type);
     }
     if (tmask != 1 && tmask != 4) tmask = 7;
-    const int mode = debug ? MODE_ROWS : choose_mode(total_rows, nb, M);
     a.n_desc = n_desc;
     a.nb = (int)nb;
-    a.R = mode == MODE_ROWS ? BLOCKS_PER_STEP : 1;
-    a.S = mode == MODE_ROWS ? (int)nb : (int)((nb + 7) / 8);
+    a.R = BLOCKS_PER_STEP;
     a.m_total = (int)M;
     int64_t tasks = 0;
     for (int i = 0; i < n_desc; ++i) {
@@ -225,12 +204,11 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
     if (tasks > 0x7fffffff) return MI355X_E_INVAL;
     for (int i = n_desc; i <= MI355X_MAX_FUSED; ++i) a.task_prefix[i] = (int)tasks;
     a.tasks_total = (int)tasks;
-    pl.mode = mode;
     pl.ncol = ncol;
     pl.fusedq = fusedq;
     pl.debug = debug;
     pl.tmask = tmask;
-    pl.fn = pick_gemv(mode, ncol, fusedq, debug, tmask);
+    pl.fn = pick_gemv(ncol, fusedq, debug, tmask);
     {
         static int diag = -1;
         if (diag < 0) {
@@ -239,21 +217,19 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
         }
         a.diag = diag;
     }
-    const int64_t wgs_needed = (tasks + WAVES_PER_WG - 1) / WAVES_PER_WG;
-    // at most one wave of resident workgroups; each wave grid-strides over row tasks
+    // One workgroup per 8-row task, at most one round of resident workgroups; each
+    // workgroup strides over tasks. Staged outputs bound the tasks per workgroup.
     const int64_t base_lds = lds_layout(ncol, (int)nb, 0).total;
     if ((size_t)base_lds > kMaxLds) return MI355X_E_UNSUPPORTED;
-    int64_t wgs = (int64_t)num_cus() * resident_wgs(pl.fn, (size_t)base_lds + 2048);
-    if (wgs > wgs_needed) wgs = wgs_needed > 0 ? wgs_needed : 1;
-    // staged outputs: bound the tasks per wave so the LDS output area stays small
-    const int rt = a.R;
-    int64_t tpw = (tasks + wgs * WAVES_PER_WG - 1) / (wgs * WAVES_PER_WG);
-    while (tpw * rt * ncol * 4 * WAVES_PER_WG > 8192 && tpw > 1) {
+    int64_t wgs = (int64_t)num_cus() * resident_wgs(pl.fn, (size_t)base_lds + 1024);
+    if (wgs > tasks) wgs = tasks > 0 ? tasks : 1;
+    int64_t tpw = (tasks + wgs - 1) / wgs;
+    while (tpw * 8 * ncol * 4 > 4096 && tpw > 1) {
         wgs *= 2;
-        tpw = (tasks + wgs * WAVES_PER_WG - 1) / (wgs * WAVES_PER_WG);
+        tpw = (tasks + wgs - 1) / wgs;
     }
-    a.out_per_wave = (int)(tpw * rt * ncol);
-    const LdsLayout L = lds_layout(ncol, (int)nb, a.out_per_wave);
+    a.out_per_wg = (int)(tpw * 8 * ncol);
+    const LdsLayout L = lds_layout(ncol, (int)nb, a.out_per_wg);
     if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
     pl.lds = (size_t)L.total;
     pl.grid = dim3((unsigned)wgs, (unsigned)((M + ncol - 1) / ncol), 1);

@@ -29,12 +29,11 @@ __host__ __device__ constexpr int block_bytes(int type) {
 struct GemvArgs {
     int n_desc;
     int nb;           // K / 256
-    int R;            // rows per task (1 when nb >= 8, else floor(8/nb))
-    int S;            // wave-steps per task
+    int R;            // rows per task (8: one per lane octet)
     int m_total;      // activation columns in total (grid.y covers ceil(m_total/NCOL))
     int tasks_total;
-    int out_per_wave;     // LDS floats per wave for staged outputs (tasks_per_wave * R * NCOL)
-    int diag;             // diagnostics: bit0 = stop after the activation prologue
+    int out_per_wg;   // LDS floats for staged outputs (tasks_per_wg * 8 * NCOL)
+    int diag;         // diagnostics: bit0 prologue only, bit1 empty, bit2 no prologue weight loads
     int task_prefix[MI355X_MAX_FUSED + 1];
     int type[MI355X_MAX_FUSED];
     int n_rows[MI355X_MAX_FUSED];
@@ -51,19 +50,20 @@ struct GemvArgs {
 
 // LDS layout of one workgroup (dynamic shared memory).
 struct LdsLayout {
-    int act_qs, act_bs, act_d, recs, outs, total;
+    int act_qs, act_bs, act_d, recs, outs, spw, total;
 };
 
-__host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wave) {
+__host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg) {
     LdsLayout L;
+    L.spw = (nb + WAVES_PER_WG - 1) / WAVES_PER_WG;  // max superblocks per wave per task
     L.act_qs = 0;
     L.act_bs = ncol * nb * ACT_QS_STRIDE;
     L.act_d = L.act_bs + ncol * nb * 32;
     int recs = L.act_d + ncol * nb * 4;
     recs = (recs + 15) & ~15;
-    L.recs = recs;
-    L.outs = recs + WAVES_PER_WG * ncol * BLOCKS_PER_STEP * 16;
-    L.total = L.outs + WAVES_PER_WG * out_per_wave * 4;
+    L.recs = recs;  // 2 task slots x 3 waves x ncol x 8 rows x spw records of 16 B
+    L.outs = recs + 2 * (WAVES_PER_WG - 1) * ncol * 8 * L.spw * 16;
+    L.total = L.outs + out_per_wg * 4;
     return L;
 }
 

@@ -15,7 +15,7 @@ struct GemvPlan {
     dim3 grid;
     size_t lds;
     gemv_fn fn;
-    int mode, ncol, tmask;
+    int ncol, tmask;
     bool fusedq, debug;
 };
 int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int ncol, bool fusedq, bool debug,

@@ -365,18 +365,22 @@ __device__ __forceinline__ float chain_update(int type, int isum, int imin, cons
     return chain_step(type, r, s);
 }
 
-enum { MODE_ROWS = 0, MODE_BLOCKS = 1 };
+// K-range of wave w when a task's nb superblocks are split over the 4 waves.
+__device__ __forceinline__ void wave_krange(int nb, int w, int &lo, int &cnt) {
+    const int q = nb / WAVES_PER_WG, r = nb % WAVES_PER_WG;
+    cnt = q + (w < r ? 1 : 0);
+    lo = w * q + (w < r ? w : r);
+}
 
-// Walks one wave's (task, step) sequence without divisions: task info (matrix,
-// type, per-lane row base) is refreshed only when the task changes. Past the
-// last step it stays on the last step (the clamped "tail" loads re-read it).
-template <int MODE>
+// Walks one wave's (task, step) sequence without divisions. Task info (matrix,
+// type, per-lane row base) is refreshed only when the task changes; past the last
+// step the cursor stays on it (the clamped tail loads re-read a valid block).
 struct Cursor {
-    int k, s;             // task ordinal within this wave, step within task
+    int k, s;             // task ordinal within this workgroup, step within the wave's K range
     int m, type, bb;      // matrix index, its type and block bytes
     int row0, rows;       // first row and rows of the task
-    bool valid;           // this lane's octet maps to a real row / block
-    const uint8_t *base;  // this lane's row base (+ task's first block for BLOCKS)
+    bool valid;           // this lane's octet maps to a real row
+    const uint8_t *base;  // this lane's row base
 
     __device__ __forceinline__ void load_task(const GemvArgs &a, int t, int g) {
         const StepInfo si = task_info(a, t);
@@ -385,104 +389,109 @@ struct Cursor {
         rows = si.rows;
         type = a.type[m];
         bb = block_bytes(type);
-        int row = row0;
-        if (MODE == MODE_ROWS) row += (g < rows ? g : 0);
-        base = a.w[m] + (int64_t)row * a.row_stride[m];
+        valid = g < rows;
+        base = a.w[m] + (int64_t)(row0 + (valid ? g : 0)) * a.row_stride[m];
     }
-    __device__ __forceinline__ void start(const GemvArgs &a, int wgid, int g) {
+    __device__ __forceinline__ void start(const GemvArgs &a, int t, int g) {
         k = 0;
         s = 0;
-        load_task(a, wgid, g);
+        load_task(a, t, g);
     }
-    // advance to the next step; returns false (and stays put) past the end
-    __device__ __forceinline__ void next(const GemvArgs &a, int S, int my_tasks, int wgid, int nwaves, int g) {
+    __device__ __forceinline__ void next(const GemvArgs &a, int S, int my_tasks, int t0, int stride, int g) {
         if (s + 1 < S) {
             ++s;
         } else if (k + 1 < my_tasks) {
             ++k;
             s = 0;
-            load_task(a, wgid + k * nwaves, g);
+            load_task(a, t0 + k * stride, g);
         }
-    }
-    __device__ __forceinline__ const uint8_t *block(int nb, int g, int &blk) {
-        if (MODE == MODE_ROWS) {
-            valid = g < rows;
-            blk = s;
-        } else {
-            blk = BLOCKS_PER_STEP * s + g;
-            valid = blk < nb;
-            blk = valid ? blk : nb - 1;
-        }
-        return base + (int64_t)blk * bb;
     }
 };
 
-// Decode / small-batch GEMV.
-//   MODE_ROWS:   a task is 8 rows; octet g owns row row0+g and walks its superblocks
-//                in order (one superblock per wave-step), keeping the fp32 chain in
-//                registers. All octets read the same activation superblock (LDS broadcast).
-//   MODE_BLOCKS: a task is 1 row; octet g takes superblock 8s+g of step s; the octet
-//                leaders drop records into LDS and one lane runs the chain over the 8
-//                records of the step. Used when N is too small to give every CU
-//                enough 8-row tasks.
-// Loads run D steps ahead through a ring of registers; addresses past the end are
-// clamped to valid blocks so every step issues the same loads (counted vmcnt waits).
-template <int MODE, int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
+// Decode / small-batch GEMV (dst[c][row] for NCOL activation columns).
+//
+// A workgroup owns 8-row tasks (octet g of every wave <-> row row0+g). The task's
+// nb superblocks are split into 4 contiguous K-ranges, one per wave, so a task
+// takes nb/4 wave-steps of 8 superblocks x 144 B. Wave 0 keeps the fp32 chain of
+// its range in registers; waves 1-3 store exact per-superblock records (the
+// operands of the reference's fmas) in LDS; after one s_barrier per task (no
+// vmcnt drain), wave 0 continues the chain through them in superblock order.
+// Each wave quantizes / stages only the activation superblocks of its own
+// K-range, so no barrier is needed before the main loop.
+// Weight loads run D steps ahead through a register ring; addresses past the end
+// are clamped to valid blocks so every step issues the same loads (exact vmcnt).
+template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.diag & 2) return;  // diagnostics: empty launch (same grid / LDS)
     const int nb = a.nb;
-    const LdsLayout L = lds_layout(NCOL, nb, a.out_per_wave);
+    const LdsLayout L = lds_layout(NCOL, nb, a.out_per_wg);
     uint8_t *act_qs = smem + L.act_qs;
     int16_t *act_bs = (int16_t *)(smem + L.act_bs);
     float *act_d = (float *)(smem + L.act_d);
+    Rec *recs = (Rec *)(smem + L.recs);  // [slot 2][wave-1 3][NCOL][row 8][spw]
+    float *outs = (float *)(smem + L.outs);  // [task k][NCOL][row 8], wave 0 only
     const int lane = threadIdx.x & 63;
-    // wave index made provably uniform so that every per-step quantity (task, matrix,
-    // descriptor fields) lives in SGPRs and is fetched with scalar loads
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform
     const int g = lane >> 3, p = lane & 7;
-    Rec *recs = (Rec *)(smem + L.recs) + wave * NCOL * BLOCKS_PER_STEP;
-    // Results are staged in LDS [task k][col][row-in-task] and written after the
-    // loop: a global store inside the pipelined loop would force vmcnt drains.
-    float *outs = (float *)(smem + L.outs) + wave * a.out_per_wave;
+    const int spw = L.spw;
 
     const int col0 = blockIdx.y * NCOL;
     const int ncol = (a.m_total - col0) < NCOL ? (a.m_total - col0) : NCOL;
-    const int nwaves = gridDim.x * WAVES_PER_WG;
-    const int wgid = blockIdx.x * WAVES_PER_WG + wave;
-    const int my_tasks = a.tasks_total > wgid ? (a.tasks_total - wgid + nwaves - 1) / nwaves : 0;
-    const int S = MODE == MODE_ROWS ? nb : (nb + BLOCKS_PER_STEP - 1) / BLOCKS_PER_STEP;
-    constexpr int RT = MODE == MODE_ROWS ? BLOCKS_PER_STEP : 1;  // rows per task
+    const int t0 = blockIdx.x, tstride = gridDim.x;
+    const int my_tasks = a.tasks_total > t0 ? (a.tasks_total - t0 + tstride - 1) / tstride : 0;
+    int lo, S;
+    wave_krange(nb, wave, lo, S);
     const int Q = my_tasks * S;
 
-    // steps in flight: 8 x 1152 B per wave for Q4_K (enough bytes in flight per CU
-    // even at one or two waves per CU); Q6_K steps hold 16 registers, so fewer
+    // steps in flight: 8 x 1152 B per wave for Q4_K; Q6_K steps hold 16 registers
     constexpr int D = (TMASK & 4) ? 5 : 8;
     Regs ring[D];
-    Cursor<MODE> ic, cc;  // issue and compute cursors
+    Cursor ic, cc;  // issue and compute cursors
 
     auto issue = [&](Regs &r) {
-        int blk;
-        const uint8_t *bp = ic.block(nb, g, blk);
-        load_block<TMASK>(r, bp, ic.type, p);
-        ic.next(a, S, my_tasks, wgid, nwaves, g);
+        load_block<TMASK>(r, ic.base + (int64_t)(lo + ic.s) * ic.bb, ic.type, p);
+        ic.next(a, S, my_tasks, t0, tstride, g);
     };
 
     float acc[NCOL];
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) acc[c] = 0.f;
 
+    auto task_end = [&](const Cursor &cu) {
+        // every wave: make this task's records visible, then meet the other waves
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (wave == 0) {
+            const Rec *rs = recs + (cu.k & 1) * (WAVES_PER_WG - 1) * NCOL * 8 * spw;
+#pragma unroll
+            for (int c = 0; c < NCOL; ++c) {
+                if (c < ncol) {
+                    float v = acc[c];
+                    for (int w = 1; w < WAVES_PER_WG; ++w) {
+                        int wlo, wcnt;
+                        wave_krange(nb, w, wlo, wcnt);
+                        const Rec *rw = rs + (((w - 1) * NCOL + c) * 8 + g) * spw;
+                        const int ctype = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : cu.type;
+                        for (int i = 0; i < wcnt; ++i) v = chain_step(ctype, rw[i], v);
+                    }
+                    if (!DEBUG && p == 0) outs[(cu.k * NCOL + c) * 8 + g] = v;
+                    acc[c] = 0.f;
+                }
+            }
+        }
+    };
+
     auto compute = [&](const Regs &r, const bool live) {
-        int blk;
-        const uint8_t *bp = cc.block(nb, g, blk);
-        const int type = cc.type, s = cc.s;
+        const int type = cc.type, s = cc.s, blk = lo + s;
         const bool valid = cc.valid;
         Regs rr = r;
         if ((TMASK & 4) && type == Q6_K) {
-            const uint32_t sh = (uint32_t)((uintptr_t)bp & 3u);  // realign 2-mod-4 blocks
-            rr.a = realign(rr.a, rr.e0, sh);
+            const uint32_t sh = (uint32_t)((uintptr_t)(cc.base + (int64_t)blk * cc.bb) & 3u);
+            rr.a = realign(rr.a, rr.e0, sh);  // realign 2-mod-4 blocks
             rr.b = realign(rr.b, rr.e1, sh);
             rr.c = realign(rr.c, rr.e2, sh);
         }
+        Rec *rw = recs + (((cc.k & 1) * (WAVES_PER_WG - 1) + (wave - 1)) * NCOL * 8 + g) * spw + s;
 #pragma unroll
         for (int c = 0; c < NCOL; ++c) {
             if (c < ncol) {
@@ -493,21 +502,12 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
                 isum = octet_sum(isum);
                 imin = octet_sum(imin);
                 const float yd = act_d[cb];
-                if (MODE == MODE_ROWS) {
+                if (wave == 0) {
                     // every lane of the octet holds the same sums: all 8 run the chain
                     acc[c] = chain_update<TMASK>(type, isum, imin, rr, dh, yd, acc[c]);
-                    if (DEBUG && c == 0 && p == 0 && valid && live) {
-                        const int64_t o = ((int64_t)(cc.row0 + g) * nb + blk) * 2;
-                        a.dbg[o] = isum;
-                        a.dbg[o + 1] = imin;
-                    }
-                    if (s == S - 1) {
-                        if (!DEBUG && p == 0 && live) outs[(cc.k * NCOL + c) * RT + g] = acc[c];
-                        acc[c] = 0.f;
-                    }
-                } else if (p == 0 && valid) {  // BLOCKS: records of this step
+                } else if (p == 0) {
                     Rec rec;
-                    if (type == Q6_K) {
+                    if ((TMASK == 4) || (TMASK != 1 && type == Q6_K)) {
                         rec.a = isum - 32 * imin;
                         rec.b = 0;
                         rec.c = h2f(dh) * yd;
@@ -518,54 +518,45 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
                         rec.c = yd * h2f(rr.a.x & 0xffffu);
                         rec.e = yd * h2f(rr.a.x >> 16);
                     }
-                    recs[c * BLOCKS_PER_STEP + g] = rec;
+                    rw[c * 8 * spw] = rec;
+                }
+                if (DEBUG && c == 0 && p == 0 && valid && live) {
+                    const int64_t o = ((int64_t)(cc.row0 + g) * nb + blk) * 2;
+                    a.dbg[o] = isum;
+                    a.dbg[o + 1] = imin;
                 }
             }
         }
-        if (MODE == MODE_BLOCKS) {
-            wave_lds_fence();
-            if (lane < ncol) {
-                const int cnt = (nb - BLOCKS_PER_STEP * s) < BLOCKS_PER_STEP ? (nb - BLOCKS_PER_STEP * s)
-                                                                            : BLOCKS_PER_STEP;
-                Rec rv[BLOCKS_PER_STEP];
-#pragma unroll
-                for (int i = 0; i < BLOCKS_PER_STEP; ++i) rv[i] = recs[lane * BLOCKS_PER_STEP + i];
-                float v = s == 0 ? 0.f : acc[0];
-                const int ctype = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : type;
-#pragma unroll
-                for (int i = 0; i < BLOCKS_PER_STEP; ++i)
-                    if (i < cnt) v = chain_step(ctype, rv[i], v);
-                acc[0] = v;
-                if (!DEBUG && live && s == S - 1) outs[cc.k * NCOL + lane] = v;
-            }
-            wave_lds_fence();
-        }
-        cc.next(a, S, my_tasks, wgid, nwaves, g);
+        if (live && s == S - 1) task_end(cc);
+        cc.next(a, S, my_tasks, t0, tstride, g);
     };
 
+    // ---- prologue: this wave's activation superblocks [lo, lo+S) -> LDS.
     // Activation loads go out first, then the first D weight steps, so both
-    // latencies overlap; the activation is then quantized / staged into LDS.
-    // Every load below is unconditional (clamped addresses): the compiler can then
-    // count outstanding loads exactly and wait only for the ones it consumes.
-    const int t0 = wgid < a.tasks_total ? wgid : a.tasks_total - 1;
+    // latencies overlap. Every load is unconditional (clamped addresses): the
+    // compiler then counts outstanding loads exactly and waits only for what it uses.
+    const int tfirst = t0 < a.tasks_total ? t0 : a.tasks_total - 1;
+    const int last_blk = S > 0 ? lo + S - 1 : 0;
     if (FUSEDQ) {
-        constexpr int XB = 8;  // superblocks per wave per batch (8 float4 registers)
+        constexpr int XB = 4;  // superblocks per batch (4 float4 registers)
         const float *xc = a.x + (int64_t)col0 * a.x_col_stride;
         f32x4a xv[XB];
 #pragma unroll
         for (int i = 0; i < XB; ++i) {
-            const int b = min(wave + i * WAVES_PER_WG, nb - 1);
+            const int b = min(lo + i, last_blk);
             xv[i] = *(const f32x4a *)(xc + (int64_t)b * QK + 4 * lane);
         }
-        ic.start(a, t0, g);
-        cc.start(a, t0, g);
+        ic.start(a, tfirst, g);
+        cc.start(a, tfirst, g);
+        if (!(a.diag & 4)) {  // diagnostics bit2: no weight loads in the prologue
 #pragma unroll
-        for (int j = 0; j < D; ++j) issue(ring[j]);
+            for (int j = 0; j < D; ++j) issue(ring[j]);
+        }
         auto quant_batch = [&](int b0) {
 #pragma unroll
             for (int i = 0; i < XB; ++i) {
-                const int b = b0 + i * WAVES_PER_WG;
-                if (b < nb) {
+                const int b = b0 + i;
+                if (b < lo + S) {
                     const Q8Lane q = quant_values_wave(xv[i], lane);
                     *(uint32_t *)(act_qs + b * ACT_QS_STRIDE + 4 * lane) = q.qs4;
                     if ((lane & 3) == 0) act_bs[b * 16 + (lane >> 2)] = (int16_t)q.bsum;
@@ -573,75 +564,75 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
                 }
             }
         };
-        quant_batch(wave);  // first batch straight-line: its waits skip the weight loads
-        for (int b0 = wave + XB * WAVES_PER_WG; b0 < nb; b0 += XB * WAVES_PER_WG) {  // K > 8192 only
+        quant_batch(lo);  // first batch straight-line: its waits skip the weight loads
+        for (int b0 = lo + XB; b0 < lo + S; b0 += XB) {
 #pragma unroll
             for (int i = 0; i < XB; ++i) {
-                const int b = min(b0 + i * WAVES_PER_WG, nb - 1);
+                const int b = min(b0 + i, last_blk);
                 xv[i] = *(const f32x4a *)(xc + (int64_t)b * QK + 4 * lane);
             }
             quant_batch(b0);
         }
     } else {
-        ic.start(a, t0, g);
-        cc.start(a, t0, g);
+        ic.start(a, tfirst, g);
+        cc.start(a, tfirst, g);
 #pragma unroll
         for (int j = 0; j < D; ++j) issue(ring[j]);
-        const int per_col = nb * 73;
-        for (int i = threadIdx.x; i < ncol * per_col; i += WG_THREADS) {
-            const int c = i / per_col;
-            const int rem = i - c * per_col;
-            const int b = rem / 73;
-            const int dw = rem - b * 73;
-            const uint32_t v = gload4(a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)b * 292 + 4 * dw);
-            const int cb = c * nb + b;
-            if (dw == 0) act_d[cb] = __uint_as_float(v);
-            else if (dw <= 64) *(uint32_t *)(act_qs + cb * ACT_QS_STRIDE + 4 * (dw - 1)) = v;
-            else *(uint32_t *)(act_bs + cb * 16 + 2 * (dw - 65)) = v;
+        // Q8_K blocks of this wave's K-range: 73 dwords each (d, 64 qs words, 8 bsum words)
+        for (int c = 0; c < ncol; ++c) {
+            const uint8_t *src = a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)lo * 292;
+            for (int i = lane; i < S * 73; i += WAVE) {
+                const int b = i / 73, dw = i - b * 73;
+                const uint32_t v = gload4(src + (int64_t)b * 292 + 4 * dw);
+                const int cb = c * nb + lo + b;
+                if (dw == 0) act_d[cb] = __uint_as_float(v);
+                else if (dw <= 64) *(uint32_t *)(act_qs + cb * ACT_QS_STRIDE + 4 * (dw - 1)) = v;
+                else *(uint32_t *)(act_bs + cb * 16 + 2 * (dw - 65)) = v;
+            }
         }
     }
-    __syncthreads();
+    wave_lds_fence();  // this wave's staged activations before its own reads
 
     if (a.diag & 1) return;  // diagnostics: prologue only
 
-    // Steps padded to a multiple of D: the ring loop body is straight-line code.
-    // Padding steps recompute the clamped last step and never store (live == false).
-    const int Qp = (Q + D - 1) / D * D;
-    for (int q0 = 0; q0 < Qp; q0 += D) {
+    // ---- main loop. Steps padded to a multiple of D: the ring loop body is
+    // straight-line code; padding steps re-run the clamped last step and never
+    // store (live == false). Waves without a K-range still meet every task barrier.
+    if (S > 0) {
+        const int Qp = (Q + D - 1) / D * D;
+        for (int q0 = 0; q0 < Qp; q0 += D) {
 #pragma unroll
-        for (int j = 0; j < D; ++j) {
-            compute(ring[j], q0 + j < Q);
-            issue(ring[j]);
+            for (int j = 0; j < D; ++j) {
+                compute(ring[j], q0 + j < Q);
+                issue(ring[j]);
+            }
         }
+    } else {
+        for (int k = 0; k < my_tasks; ++k) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
 
-    // flush the staged results: task k of this wave -> rows row0..row0+RT-1, NCOL columns
-    if (!DEBUG && my_tasks > 0) {
+    // ---- flush wave 0's staged results: task k -> rows row0..row0+7, NCOL columns
+    if (!DEBUG && wave == 0 && my_tasks > 0) {
         wave_lds_fence();
         for (int k = 0; k < my_tasks; ++k) {
-            const StepInfo si = task_info(a, wgid + k * nwaves);
-            for (int i = lane; i < NCOL * RT; i += WAVE) {
-                const int c = i / RT, r = i - c * RT;
-                if (c < ncol && r < si.rows)
-                    a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = outs[k * NCOL * RT + i];
-            }
+            const StepInfo si = task_info(a, t0 + k * tstride);
+            const int i = lane;  // NCOL * 8 <= 64
+            const int c = i >> 3, r = i & 7;
+            if (c < ncol && r < si.rows)
+                a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = outs[k * NCOL * 8 + i];
         }
     }
 }
 
 // ------------------------------------------------------------------ explicit instances
-#define KQ_GEMV_INST(MD, NC, FQ, DB, TM) \
-    template __global__ void kq_gemv<MD, NC, FQ, DB, TM>(const GemvArgs a);
-#define KQ_GEMV_INST_TM(MD, NC, FQ, DB) \
-    KQ_GEMV_INST(MD, NC, FQ, DB, 1) KQ_GEMV_INST(MD, NC, FQ, DB, 4) KQ_GEMV_INST(MD, NC, FQ, DB, 7)
+#define KQ_GEMV_INST(NC, FQ, DB, TM) template __global__ void kq_gemv<NC, FQ, DB, TM>(const GemvArgs a);
+#define KQ_GEMV_INST_TM(NC, FQ, DB) KQ_GEMV_INST(NC, FQ, DB, 1) KQ_GEMV_INST(NC, FQ, DB, 4) KQ_GEMV_INST(NC, FQ, DB, 7)
 
-KQ_GEMV_INST_TM(MODE_ROWS, 1, true, false)
-KQ_GEMV_INST_TM(MODE_ROWS, 1, false, false)
-KQ_GEMV_INST_TM(MODE_ROWS, 2, false, false)
-KQ_GEMV_INST_TM(MODE_ROWS, 4, false, false)
-KQ_GEMV_INST_TM(MODE_ROWS, 8, false, false)
-KQ_GEMV_INST_TM(MODE_ROWS, 1, false, true)
-KQ_GEMV_INST_TM(MODE_BLOCKS, 1, true, false)
-KQ_GEMV_INST_TM(MODE_BLOCKS, 1, false, false)
+KQ_GEMV_INST_TM(1, true, false)
+KQ_GEMV_INST_TM(1, false, false)
+KQ_GEMV_INST_TM(2, false, false)
+KQ_GEMV_INST_TM(4, false, false)
+KQ_GEMV_INST_TM(8, false, false)
+KQ_GEMV_INST_TM(1, false, true)
 
 }  // namespace kq

@@ -57,6 +57,10 @@ if __name__ == "__main__":
         env = dict(os.environ)
         if mode == "prologue":
             env["MI355X_GEMV_DIAG"] = "1"
+        elif mode == "empty":
+            env["MI355X_GEMV_DIAG"] = "2"
+        elif mode == "quantonly":
+            env["MI355X_GEMV_DIAG"] = "5"
         elif mode != "auto":
             env["MI355X_GEMV_MODE"] = mode
         r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)
