@@ -66,6 +66,9 @@ int type_bit(int type) { return type == Q4_K ? 1 : type == Q5_K ? 2 : type == Q6
 
 constexpr size_t kMaxLds = 64 * 1024;
 
+uint64_t *g_stamps = nullptr;  // diagnostics (mi355x_diag_stamps)
+int64_t g_stamps_cap = 0;
+
 // Workgroups of one kernel resident per CU (registers / LDS), cached per (fn, lds).
 int resident_wgs(gemv_fn fn, size_t lds) {
     static std::mutex mu;
@@ -157,7 +160,7 @@ int choose_ncol(int64_t M, int nb) {
     for (int i = 0; i < 4; ++i) {
         const int nc = cands[i];
         if (nc > M && nc > 1) continue;
-        if ((size_t)lds_layout(nc, nb, 8 * nc).total <= kMaxLds / 2) return nc;
+        if ((size_t)lds_layout(nc, nb, 8 * nc, false, 8 * 16 * 14, 4).total <= kMaxLds) return nc;
     }
     return 1;
 }
@@ -216,10 +219,28 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
             diag = e ? atoi(e) : 0;
         }
         a.diag = diag;
+        static int ring_env = -1;
+        if (ring_env < 0) {
+            const char *e = getenv("MI355X_GEMV_RING");
+            ring_env = e ? atoi(e) : 0;
+        }
+        a.ring_override = ring_env;
     }
+    a.stamps = g_stamps;
+    a.stamps_cap = g_stamps_cap;
     // One workgroup per 8-row task, at most one round of resident workgroups; each
-    // workgroup strides over tasks. Staged outputs bound the tasks per workgroup.
-    const int64_t base_lds = lds_layout(ncol, (int)nb, 0).total;
+    // workgroup strides over tasks. Ring depth: as deep as LDS allows 2+ resident
+    // workgroups per CU. Staged outputs bound the tasks per workgroup.
+    const int slot = tmask == 1 ? 8 * 16 * 9 : 8 * 16 * 14;
+    const int dcands[3] = {tmask == 1 ? 8 : 6, tmask == 1 ? 6 : 5, 4};
+    int D = 4;
+    for (int i = 0; i < 3; ++i) {
+        D = dcands[i];
+        if ((size_t)lds_layout(ncol, (int)nb, 8 * ncol, fusedq, slot, D).total <= kMaxLds / 2) break;
+    }
+    if (a.ring_override > 0) D = a.ring_override < 8 ? a.ring_override : 8;
+    a.ring = D;
+    const int64_t base_lds = lds_layout(ncol, (int)nb, 0, fusedq, slot, D).total;
     if ((size_t)base_lds > kMaxLds) return MI355X_E_UNSUPPORTED;
     int64_t wgs = (int64_t)num_cus() * resident_wgs(pl.fn, (size_t)base_lds + 1024);
     if (wgs > tasks) wgs = tasks > 0 ? tasks : 1;
@@ -229,7 +250,7 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
         tpw = (tasks + wgs - 1) / wgs;
     }
     a.out_per_wg = (int)(tpw * 8 * ncol);
-    const LdsLayout L = lds_layout(ncol, (int)nb, a.out_per_wg);
+    const LdsLayout L = lds_layout(ncol, (int)nb, a.out_per_wg, fusedq, slot, D);
     if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
     pl.lds = (size_t)L.total;
     pl.grid = dim3((unsigned)wgs, (unsigned)((M + ncol - 1) / ncol), 1);
@@ -395,6 +416,12 @@ int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, i
     pl.a.dbg = out;
     if (!device_ok()) return MI355X_E_NODEVICE;
     return launch_gemv(pl, (hipStream_t)stream);
+}
+
+int mi355x_diag_stamps(void *buf, size_t bytes) {
+    g_stamps = (uint64_t *)buf;
+    g_stamps_cap = buf ? (int64_t)(bytes / 8) : 0;
+    return MI355X_OK;
 }
 
 int mi355x_timing_enable(int enable) {

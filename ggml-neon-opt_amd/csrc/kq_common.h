@@ -33,7 +33,9 @@ struct GemvArgs {
     int m_total;      // activation columns in total (grid.y covers ceil(m_total/NCOL))
     int tasks_total;
     int out_per_wg;   // LDS floats for staged outputs (tasks_per_wg * 8 * NCOL)
-    int diag;         // diagnostics: bit0 prologue only, bit1 empty, bit2 no prologue weight loads
+    int diag;         // diagnostics: bit0 prologue only, bit1 empty
+    int ring;         // LDS ring depth D (weight steps in flight per wave)
+    int ring_override; // host-side experiment knob (MI355X_GEMV_RING), 0 = auto
     int task_prefix[MI355X_MAX_FUSED + 1];
     int type[MI355X_MAX_FUSED];
     int n_rows[MI355X_MAX_FUSED];
@@ -46,23 +48,28 @@ struct GemvArgs {
     const uint8_t *xq;    // Q8_K input (!FUSEDQ): column j at xq + j*xq_col_stride
     int64_t xq_col_stride; // bytes
     int32_t *dbg;         // debug partials (DEBUG builds of the kernel only)
+    uint64_t *stamps;     // diagnostics: per-wave s_memrealtime stamps (or null)
+    int64_t stamps_cap;   // entries available in stamps
 };
 
 // LDS layout of one workgroup (dynamic shared memory).
+//   ring: per wave D slots of `slot` bytes (8 rows x one superblock)
+//   act:  per wave, its K-range of activations (f32 staging / raw Q8_K per column)
+//   recs: 2 task slots x 3 waves x ncol x 8 rows x spw exact chain records
+//   outs: staged results of wave 0 (tasks_per_wg x ncol x 8 floats)
 struct LdsLayout {
-    int act_qs, act_bs, act_d, recs, outs, spw, total;
+    int ring, act, act_per_wave, act_col, recs, outs, spw, total;
 };
 
-__host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg) {
+__host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg, bool fusedq, int slot, int D) {
     LdsLayout L;
     L.spw = (nb + WAVES_PER_WG - 1) / WAVES_PER_WG;  // max superblocks per wave per task
-    L.act_qs = 0;
-    L.act_bs = ncol * nb * ACT_QS_STRIDE;
-    L.act_d = L.act_bs + ncol * nb * 32;
-    int recs = L.act_d + ncol * nb * 4;
-    recs = (recs + 15) & ~15;
-    L.recs = recs;  // 2 task slots x 3 waves x ncol x 8 rows x spw records of 16 B
-    L.outs = recs + 2 * (WAVES_PER_WG - 1) * ncol * 8 * L.spw * 16;
+    L.ring = 0;
+    L.act = WAVES_PER_WG * D * slot;
+    L.act_col = (L.spw * 292 + 16 + 15) & ~15;
+    L.act_per_wave = fusedq ? L.spw * 1024 : ncol * L.act_col;
+    L.recs = L.act + WAVES_PER_WG * L.act_per_wave;
+    L.outs = L.recs + 2 * (WAVES_PER_WG - 1) * ncol * 8 * L.spw * 16;
     L.total = L.outs + out_per_wg * 4;
     return L;
 }

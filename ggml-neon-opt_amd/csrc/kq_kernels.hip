@@ -13,21 +13,23 @@
 // the reference NEON function. The kernel file is compiled with
 // -ffp-contract=off: only the explicit fmaf() calls fuse.
 //
-// Work decomposition (decode GEMV, HBM-bound): 8 lanes own one 144-B superblock
-// (lane p reads qs[16p..16p+16) with one 16-B load plus the 16-B header), so one
-// wave-step streams 8 consecutive superblocks (1152 B) of a row. The activation
-// row is quantized to Q8_K once per workgroup straight into LDS; each lane
-// dots its 32 nibbles against 2 x 16 B of LDS activations with v_dot4_i32_i8,
-// the 8 lanes reduce with 3 DPP adds, and the group leader drops
-// {sumi, summins, d, dmin} into a per-wave LDS record. One lane per row then
-// runs the serial fp32 chain over the records in superblock order.
+// Work decomposition (decode GEMV, HBM-bound; details at kq_gemv below): a
+// workgroup owns 8-row tasks, its 4 waves split each task's superblocks into
+// K-ranges, weights stream into per-wave LDS rings by LDS-DMA
+// (global_load_lds_dwordx4), 8 lanes own one superblock and dot their 32 quants
+// against LDS activations with v_dot4_i32_i8, 3 DPP adds reduce an octet, and
+// the reference's fp32 chain runs in superblock order (wave 0 in registers,
+// waves 1-3 through exact LDS records).
 #include "kq_common.h"
 
 namespace kq {
 
+
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 typedef uint32_t u32x4a __attribute__((ext_vector_type(4), aligned(4)));
 typedef float f32x4a __attribute__((ext_vector_type(4), aligned(4)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+#define LDS __attribute__((address_space(3)))
 
 __device__ __forceinline__ u32x4 gload16(const uint8_t *p) { return *(const u32x4a *)p; }
 __device__ __forceinline__ uint32_t gload4(const uint8_t *p) { return *(const uint32_t *)p; }
@@ -168,35 +170,6 @@ struct Regs {
     uint32_t e0, e1, e2, dh;
 };
 
-// Q4_K: lane p owns qs[16p, 16p+16): elements 64j+16h+[0,16) (low nibbles,
-// sub-block 2j) and 64j+32+16h+[0,16) (high nibbles, sub-block 2j+1), j=p>>1, h=p&1.
-__device__ __forceinline__ void load_q4K(Regs &r, const uint8_t *blk, int p) {
-    r.a = gload16(blk);               // d, dmin, scales[0..11]
-    r.b = gload16(blk + 16 + 16 * p); // qs
-}
-__device__ __forceinline__ void load_q5K(Regs &r, const uint8_t *blk, int p) {
-    r.a = gload16(blk);                      // d, dmin, scales
-    r.b = gload16(blk + 16 + 16 * (p & 1));  // qh[16h .. 16h+16)
-    r.c = gload16(blk + 48 + 16 * p);        // qs
-}
-// Q6_K blocks are 210 B, so odd blocks sit at 2 mod 4: load 4-B aligned words
-// (plus one extra word) and realign with v_alignbyte. Every word read lies
-// inside the block.
-__device__ __forceinline__ void load_q6K(Regs &r, const uint8_t *blk, int p) {
-    const uint32_t s = (uint32_t)((uintptr_t)blk & 3u);  // 0 or 2
-    const uint8_t *b4 = blk - s;
-    const int n = p >> 2, part = p & 3;
-    const int fql = 16 * p;
-    const int fqh = 128 + 32 * n + 16 * (part & 1);
-    r.a = gload16(b4 + fql);
-    r.e0 = gload4(b4 + fql + 12 + 2 * s);
-    r.b = gload16(b4 + fqh);
-    r.e1 = gload4(b4 + fqh + 12 + 2 * s);
-    r.c = gload16(b4 + 192);
-    r.e2 = gload4(b4 + 204 + 2 * s);
-    r.dh = *(const uint16_t *)(blk + 208);
-}
-
 __device__ __forceinline__ u32x4 realign(u32x4 v, uint32_t ex, uint32_t s) {
     u32x4 o;
     o.x = __builtin_amdgcn_alignbyte(v.y, v.x, s);
@@ -235,13 +208,14 @@ __device__ __forceinline__ ScMn scales_k4(u32x4 hdr, int p) {
 }
 
 // Lane partials against one activation column held in LDS.
-//   aq: LDS qs of the activation superblock (256 B), abs: its 16 bsums.
+//   aq: LDS qs of the activation superblock (256 B, 4-byte aligned: raw Q8_K
+//   layout), abs: its 16 bsums (4-byte aligned).
 __device__ __forceinline__ void lane_q4K(const Regs &r, const uint8_t *aq, const int16_t *abs, int p,
                                          int &isum, int &imin) {
     const int j = p >> 1, h = p & 1;
     const ScMn s = scales_k4(r.a, p);
-    const u32x4 alo = *(const u32x4 *)(aq + 64 * j + 16 * h);
-    const u32x4 ahi = *(const u32x4 *)(aq + 64 * j + 32 + 16 * h);
+    const u32x4 alo = *(const u32x4a *)(aq + 64 * j + 16 * h);
+    const u32x4 ahi = *(const u32x4a *)(aq + 64 * j + 32 + 16 * h);
     const u32x4 lo = r.b & 0x0f0f0f0fu;
     const u32x4 hi = (r.b >> 4) & 0x0f0f0f0fu;
     isum = dot16(lo, alo) * s.sc_lo + dot16(hi, ahi) * s.sc_hi;
@@ -253,8 +227,8 @@ __device__ __forceinline__ void lane_q5K(const Regs &r, const uint8_t *aq, const
                                          int &isum, int &imin) {
     const int j = p >> 1, h = p & 1;
     const ScMn s = scales_k4(r.a, p);
-    const u32x4 alo = *(const u32x4 *)(aq + 64 * j + 16 * h);
-    const u32x4 ahi = *(const u32x4 *)(aq + 64 * j + 32 + 16 * h);
+    const u32x4 alo = *(const u32x4a *)(aq + 64 * j + 16 * h);
+    const u32x4 ahi = *(const u32x4a *)(aq + 64 * j + 32 + 16 * h);
     const uint32_t sl = (uint32_t)(2 * j), shh = (uint32_t)(2 * j + 1);
     const u32x4 lo = (r.c & 0x0f0f0f0fu) | (((r.b >> sl) & 0x01010101u) << 4);
     const u32x4 hi = ((r.c >> 4) & 0x0f0f0f0fu) | (((r.b >> shh) & 0x01010101u) << 4);
@@ -279,8 +253,8 @@ __device__ __forceinline__ void lane_q6K(const Regs &r, const uint8_t *aq, const
     const u32x4 qlo = (L & 0x0f0f0f0fu) | (((H >> shl) & 0x03030303u) << 4);
     const u32x4 qhi = ((L >> 4) & 0x0f0f0f0fu) | (((H >> (shl + 4u)) & 0x03030303u) << 4);
     const int elo = 128 * n + 32 * (part >> 1) + 16 * (part & 1);
-    const u32x4 alo = *(const u32x4 *)(aq + elo);
-    const u32x4 ahi = *(const u32x4 *)(aq + elo + 64);
+    const u32x4 alo = *(const u32x4a *)(aq + elo);
+    const u32x4 ahi = *(const u32x4a *)(aq + elo + 64);
     const int sb = elo >> 4;
     isum = dot16(qlo, alo) * sbyte(SC, sb) + dot16(qhi, ahi) * sbyte(SC, sb + 4);
     const uint32_t bs2 = *(const uint32_t *)(abs + 2 * p);
@@ -327,13 +301,59 @@ __device__ __forceinline__ StepInfo task_info(const GemvArgs &a, int t) {
     return si;
 }
 
+
+// ------------------------------------------------------------------ weight streaming
+// Pieces (16 B) per superblock in the LDS ring: Q4_K 9 (144 B), Q5_K 11 (176 B),
+// Q6_K 14 (210 B fetched from the 16-B boundary below the block: 224 B).
+__host__ __device__ constexpr int pieces_of(int type) { return type == Q4_K ? 9 : type == Q5_K ? 11 : 14; }
+__host__ __device__ constexpr int slot_bytes(int tmask) { return 8 * 16 * (tmask == 1 ? 9 : 14); }
+
+__device__ __forceinline__ void dma16(const void *src, LDS void *dst) {
+    __builtin_amdgcn_global_load_lds(src, dst, 16, 0, 0);
+}
+
+template <int N>
+__device__ __forceinline__ void vm_wait() {
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// Wait until at most `steps` ring steps (2 DMA instructions each) are in flight.
+__device__ __forceinline__ void vm_wait_steps(int steps) {
+    switch (steps) {
+        case 0: vm_wait<0>(); break;
+        case 1: vm_wait<2>(); break;
+        case 2: vm_wait<4>(); break;
+        case 3: vm_wait<6>(); break;
+        case 4: vm_wait<8>(); break;
+        case 5: vm_wait<10>(); break;
+        case 6: vm_wait<12>(); break;
+        case 7: vm_wait<14>(); break;
+        default: vm_wait<16>(); break;
+    }
+}
+
+// Register image of one lane's share of a superblock, read from its LDS ring slot.
+//   region: LDS bytes of row g's superblock copy; sh: byte offset of the block
+//   inside the region (Q6_K: block start mod 16; 0 otherwise).
 template <int TMASK>
-__device__ __forceinline__ void load_block(Regs &r, const uint8_t *bp, int type, int p) {
-    if (TMASK == 1) { load_q4K(r, bp, p); return; }
-    if (TMASK == 4) { load_q6K(r, bp, p); return; }
-    if (type == Q4_K) load_q4K(r, bp, p);
-    else if (type == Q5_K) load_q5K(r, bp, p);
-    else load_q6K(r, bp, p);
+__device__ __forceinline__ void lds_block(Regs &r, const uint8_t *region, uint32_t sh, int type, int p) {
+    if (TMASK == 1 || (TMASK != 4 && type == Q4_K)) {
+        r.a = *(const u32x4 *)(region);
+        r.b = *(const u32x4 *)(region + 16 + 16 * p);
+    } else if (TMASK != 4 && type == Q5_K) {
+        r.a = *(const u32x4 *)(region);
+        r.b = *(const u32x4 *)(region + 16 + 16 * (p & 1));
+        r.c = *(const u32x4 *)(region + 48 + 16 * p);
+    } else {
+        const int n = p >> 2, part = p & 3;
+        const uint32_t s4 = sh & 3u;
+        const uint8_t *b = region + (sh & ~3u);
+        const int fql = 16 * p, fqh = 128 + 32 * n + 16 * (part & 1);
+        r.a = realign(*(const u32x4a *)(b + fql), *(const uint32_t *)(b + fql + 16), s4);
+        r.b = realign(*(const u32x4a *)(b + fqh), *(const uint32_t *)(b + fqh + 16), s4);
+        r.c = realign(*(const u32x4a *)(b + 192), *(const uint32_t *)(b + 208), s4);
+        r.dh = (*(const uint32_t *)(b + 208) >> (8u * s4)) & 0xffffu;
+    }
 }
 
 template <int TMASK>
@@ -344,17 +364,16 @@ __device__ __forceinline__ void lane_partials(const Regs &rr, const uint8_t *aq,
     else lane_q6K(rr, aq, ab, p, isum, imin, dh);
 }
 
-// The reference's per-superblock fp32 update from the integer partials.
+// Exact record of one superblock: the operands of the reference's fp32 update.
 template <int TMASK>
-__device__ __forceinline__ float chain_update(int type, int isum, int imin, const Regs &rr, uint32_t dh, float yd,
-                                              float s) {
+__device__ __forceinline__ Rec make_rec(int type, int isum, int imin, const Regs &rr, uint32_t dh, float yd) {
     if (TMASK == 1) type = Q4_K;
     if (TMASK == 4) type = Q6_K;
     Rec r;
     if (type == Q6_K) {
         r.a = isum - 32 * imin;
         r.b = 0;
-        r.c = h2f(dh) * yd;   // d_all * y.d
+        r.c = h2f(dh) * yd;  // d_all * y.d
         r.e = 0.f;
     } else {
         r.a = isum;
@@ -362,79 +381,80 @@ __device__ __forceinline__ float chain_update(int type, int isum, int imin, cons
         r.c = yd * h2f(rr.a.x & 0xffffu);  // y.d * fp16(x.d)
         r.e = yd * h2f(rr.a.x >> 16);      // y.d * fp16(x.dmin)
     }
-    return chain_step(type, r, s);
+    return r;
 }
 
 // K-range of wave w when a task's nb superblocks are split over the 4 waves.
-__device__ __forceinline__ void wave_krange(int nb, int w, int &lo, int &cnt) {
+__host__ __device__ __forceinline__ void wave_krange(int nb, int w, int &lo, int &cnt) {
     const int q = nb / WAVES_PER_WG, r = nb % WAVES_PER_WG;
     cnt = q + (w < r ? 1 : 0);
     lo = w * q + (w < r ? w : r);
 }
 
-// Walks one wave's (task, step) sequence without divisions. Task info (matrix,
-// type, per-lane row base) is refreshed only when the task changes; past the last
-// step the cursor stays on it (the clamped tail loads re-read a valid block).
-struct Cursor {
-    int k, s;             // task ordinal within this workgroup, step within the wave's K range
-    int m, type, bb;      // matrix index, its type and block bytes
-    int row0, rows;       // first row and rows of the task
-    bool valid;           // this lane's octet maps to a real row
-    const uint8_t *base;  // this lane's row base
+// Per-task state of a lane: consumer row (octet g) and the two DMA pieces it fetches.
+struct TaskLane {
+    int m, type, bb, P, row0, rows;  // wave-uniform
+    bool valid;                      // octet g maps to a real row
+    const uint8_t *crow;             // consumer row base
+    const uint8_t *drow[2];          // DMA piece rows (instruction 0: lane, 1: lane + 64)
+    int dj[2];                       // DMA piece index within the block
+    bool dact1;                      // lane active in DMA instruction 1
 
-    __device__ __forceinline__ void load_task(const GemvArgs &a, int t, int g) {
+    __device__ __forceinline__ void load(const GemvArgs &a, int t, int lane) {
         const StepInfo si = task_info(a, t);
         m = si.m;
         row0 = si.row0;
         rows = si.rows;
         type = a.type[m];
         bb = block_bytes(type);
+        P = pieces_of(type);
+        const int g = lane >> 3;
         valid = g < rows;
-        base = a.w[m] + (int64_t)(row0 + (valid ? g : 0)) * a.row_stride[m];
-    }
-    __device__ __forceinline__ void start(const GemvArgs &a, int t, int g) {
-        k = 0;
-        s = 0;
-        load_task(a, t, g);
-    }
-    __device__ __forceinline__ void next(const GemvArgs &a, int S, int my_tasks, int t0, int stride, int g) {
-        if (s + 1 < S) {
-            ++s;
-        } else if (k + 1 < my_tasks) {
-            ++k;
-            s = 0;
-            load_task(a, t0 + k * stride, g);
+        const uint8_t *w = a.w[m];
+        const int64_t rs = a.row_stride[m];
+        crow = w + (int64_t)(row0 + (valid ? g : rows - 1)) * rs;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const int pi = lane + 64 * i;
+            const int gi = pi / P;
+            dj[i] = pi - gi * P;
+            drow[i] = w + (int64_t)(row0 + (gi < rows ? gi : rows - 1)) * rs;
         }
+        dact1 = lane + 64 < 8 * P;
     }
 };
 
-// Decode / small-batch GEMV (dst[c][row] for NCOL activation columns).
+// Decode / small-batch GEMV: dst[c][row] for NCOL activation columns.
 //
-// A workgroup owns 8-row tasks (octet g of every wave <-> row row0+g). The task's
-// nb superblocks are split into 4 contiguous K-ranges, one per wave, so a task
-// takes nb/4 wave-steps of 8 superblocks x 144 B. Wave 0 keeps the fp32 chain of
-// its range in registers; waves 1-3 store exact per-superblock records (the
-// operands of the reference's fmas) in LDS; after one s_barrier per task (no
-// vmcnt drain), wave 0 continues the chain through them in superblock order.
-// Each wave quantizes / stages only the activation superblocks of its own
-// K-range, so no barrier is needed before the main loop.
-// Weight loads run D steps ahead through a register ring; addresses past the end
-// are clamped to valid blocks so every step issues the same loads (exact vmcnt).
+// Work: a workgroup owns 8-row tasks (octet g of every wave <-> row row0+g). The
+// task's nb superblocks are split into 4 contiguous K-ranges, one per wave.
+// Weights: each wave streams its range through a ring of D LDS slots; a step is
+// one superblock of each of the 8 rows, fetched as 16-B pieces by two
+// global_load_lds_dwordx4 (every piece 16-B aligned, so no access can cross a
+// page) and waited for with a counted s_waitcnt vmcnt. The loop is not unrolled:
+// the slot is an LDS address, so prefetch depth costs no registers and the code
+// stays small (the instruction footprint dominates short launches).
+// Activations: each wave stages only its own K-range: f32 by LDS-DMA, quantized
+// in place into raw 292-B Q8_K blocks (FUSEDQ), or raw Q8_K bytes by LDS-DMA.
+// Chain: wave 0 keeps the fp32 chain of its range in registers; waves 1-3 store
+// exact records; after one s_barrier per task (no vmcnt drain) wave 0 continues
+// the chain through them in superblock order and stages the 8 results.
 template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     if (a.diag & 2) return;  // diagnostics: empty launch (same grid / LDS)
-    const int nb = a.nb;
-    const LdsLayout L = lds_layout(NCOL, nb, a.out_per_wg);
-    uint8_t *act_qs = smem + L.act_qs;
-    int16_t *act_bs = (int16_t *)(smem + L.act_bs);
-    float *act_d = (float *)(smem + L.act_d);
-    Rec *recs = (Rec *)(smem + L.recs);  // [slot 2][wave-1 3][NCOL][row 8][spw]
-    float *outs = (float *)(smem + L.outs);  // [task k][NCOL][row 8], wave 0 only
+    const int nb = a.nb, D = a.ring;
+    constexpr int SLOT = slot_bytes(TMASK);
+    const LdsLayout L = lds_layout(NCOL, nb, a.out_per_wg, FUSEDQ, SLOT, D);
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);  // provably uniform
     const int g = lane >> 3, p = lane & 7;
     const int spw = L.spw;
+    uint8_t *ring = smem + L.ring + wave * D * SLOT;
+    uint8_t *act = smem + L.act + wave * L.act_per_wave;
+    Rec *recs = (Rec *)(smem + L.recs);      // [slot 2][wave-1 3][NCOL][row 8][spw]
+    float *outs = (float *)(smem + L.outs);  // [task k][NCOL][row 8], wave 0 only
 
     const int col0 = blockIdx.y * NCOL;
     const int ncol = (a.m_total - col0) < NCOL ? (a.m_total - col0) : NCOL;
@@ -443,26 +463,50 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     int lo, S;
     wave_krange(nb, wave, lo, S);
     const int Q = my_tasks * S;
+    // byte offset of each column's first raw Q8_K block inside its LDS region
+    int actsh[NCOL];
+#pragma unroll
+    for (int c = 0; c < NCOL; ++c)
+        actsh[c] = FUSEDQ ? 0 : (int)((uintptr_t)(a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)lo * 292) & 15);
 
-    // steps in flight: 8 x 1152 B per wave for Q4_K; Q6_K steps hold 16 registers
-    constexpr int D = (TMASK & 4) ? 5 : 8;
-    Regs ring[D];
-    Cursor ic, cc;  // issue and compute cursors
-
-    auto issue = [&](Regs &r) {
-        load_block<TMASK>(r, ic.base + (int64_t)(lo + ic.s) * ic.bb, ic.type, p);
-        ic.next(a, S, my_tasks, t0, tstride, g);
+    // ---- issue cursor: step q -> (task k, step s); DMA into slot q % D
+    TaskLane it;
+    int ik = 0, is = 0, iq = 0;
+    auto issue = [&]() {
+        const int blk = lo + is;
+        uint8_t *slot = ring + (iq % D) * SLOT;
+        const int type = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : it.type;
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            const uint8_t *src;
+            if (type == Q6_K) {
+                const uintptr_t blkp = (uintptr_t)(it.drow[i] + (int64_t)blk * 210);
+                src = (const uint8_t *)(blkp & ~(uintptr_t)15) + 16 * it.dj[i];
+            } else {
+                src = it.drow[i] + (int64_t)blk * it.bb + 16 * it.dj[i];
+            }
+            if (i == 0 || it.dact1) dma16(src, (LDS void *)(slot + 1024 * i));
+        }
+        ++iq;
+        if (++is == S) {
+            is = 0;
+            if (++ik < my_tasks) it.load(a, t0 + ik * tstride, lane);
+        }
     };
 
+    // ---- compute cursor
+    TaskLane ct;
+    int ck = 0, cs = 0;
     float acc[NCOL];
 #pragma unroll
     for (int c = 0; c < NCOL; ++c) acc[c] = 0.f;
 
-    auto task_end = [&](const Cursor &cu) {
+    auto task_end = [&]() {
         // every wave: make this task's records visible, then meet the other waves
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (wave == 0) {
-            const Rec *rs = recs + (cu.k & 1) * (WAVES_PER_WG - 1) * NCOL * 8 * spw;
+            const Rec *rs = recs + (ck & 1) * (WAVES_PER_WG - 1) * NCOL * 8 * spw;
+            const int ctype = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : ct.type;
 #pragma unroll
             for (int c = 0; c < NCOL; ++c) {
                 if (c < ncol) {
@@ -471,155 +515,124 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
                         int wlo, wcnt;
                         wave_krange(nb, w, wlo, wcnt);
                         const Rec *rw = rs + (((w - 1) * NCOL + c) * 8 + g) * spw;
-                        const int ctype = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : cu.type;
                         for (int i = 0; i < wcnt; ++i) v = chain_step(ctype, rw[i], v);
                     }
-                    if (!DEBUG && p == 0) outs[(cu.k * NCOL + c) * 8 + g] = v;
+                    if (!DEBUG && p == 0) outs[(ck * NCOL + c) * 8 + g] = v;
                     acc[c] = 0.f;
                 }
             }
         }
     };
 
-    auto compute = [&](const Regs &r, const bool live) {
-        const int type = cc.type, s = cc.s, blk = lo + s;
-        const bool valid = cc.valid;
-        Regs rr = r;
-        if ((TMASK & 4) && type == Q6_K) {
-            const uint32_t sh = (uint32_t)((uintptr_t)(cc.base + (int64_t)blk * cc.bb) & 3u);
-            rr.a = realign(rr.a, rr.e0, sh);  // realign 2-mod-4 blocks
-            rr.b = realign(rr.b, rr.e1, sh);
-            rr.c = realign(rr.c, rr.e2, sh);
-        }
-        Rec *rw = recs + (((cc.k & 1) * (WAVES_PER_WG - 1) + (wave - 1)) * NCOL * 8 + g) * spw + s;
+    auto compute = [&](int q) {
+        const int blk = lo + cs;
+        const int type = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : ct.type;
+        const uint8_t *slot = ring + (q % D) * SLOT;
+        uint32_t sh = 0;
+        if (type == Q6_K) sh = (uint32_t)((uintptr_t)(ct.crow + (int64_t)blk * 210) & 15u);
+        Regs rr;
+        lds_block<TMASK>(rr, slot + g * ct.P * 16, sh, type, p);
+        Rec *rw = recs + (((ck & 1) * (WAVES_PER_WG - 1) + (wave - 1)) * NCOL * 8 + g) * spw + cs;
 #pragma unroll
         for (int c = 0; c < NCOL; ++c) {
             if (c < ncol) {
-                const int cb = c * nb + blk;
+                const uint8_t *ab = act + c * L.act_col + actsh[c] + cs * 292;  // raw Q8_K block
                 int isum = 0, imin = 0;
                 uint32_t dh = rr.dh;
-                lane_partials<TMASK>(rr, act_qs + cb * ACT_QS_STRIDE, act_bs + cb * 16, type, p, isum, imin, dh);
+                lane_partials<TMASK>(rr, ab + 4, (const int16_t *)(ab + 260), type, p, isum, imin, dh);
                 isum = octet_sum(isum);
                 imin = octet_sum(imin);
-                const float yd = act_d[cb];
-                if (wave == 0) {
-                    // every lane of the octet holds the same sums: all 8 run the chain
-                    acc[c] = chain_update<TMASK>(type, isum, imin, rr, dh, yd, acc[c]);
-                } else if (p == 0) {
-                    Rec rec;
-                    if ((TMASK == 4) || (TMASK != 1 && type == Q6_K)) {
-                        rec.a = isum - 32 * imin;
-                        rec.b = 0;
-                        rec.c = h2f(dh) * yd;
-                        rec.e = 0.f;
-                    } else {
-                        rec.a = isum;
-                        rec.b = imin;
-                        rec.c = yd * h2f(rr.a.x & 0xffffu);
-                        rec.e = yd * h2f(rr.a.x >> 16);
-                    }
-                    rw[c * 8 * spw] = rec;
-                }
-                if (DEBUG && c == 0 && p == 0 && valid && live) {
-                    const int64_t o = ((int64_t)(cc.row0 + g) * nb + blk) * 2;
+                const float yd = *(const float *)ab;
+                const Rec rec = make_rec<TMASK>(type, isum, imin, rr, dh, yd);
+                if (wave == 0) acc[c] = chain_step(type, rec, acc[c]);  // all 8 lanes of the octet
+                else if (p == 0) rw[c * 8 * spw] = rec;
+                if (DEBUG && c == 0 && p == 0 && ct.valid) {
+                    const int64_t o = ((int64_t)(ct.row0 + g) * nb + blk) * 2;
                     a.dbg[o] = isum;
                     a.dbg[o + 1] = imin;
                 }
             }
         }
-        if (live && s == S - 1) task_end(cc);
-        cc.next(a, S, my_tasks, t0, tstride, g);
+        if (++cs == S) {
+            task_end();
+            cs = 0;
+            if (++ck < my_tasks) ct.load(a, t0 + ck * tstride, lane);
+        }
     };
 
-    // ---- prologue: this wave's activation superblocks [lo, lo+S) -> LDS.
-    // Activation loads go out first, then the first D weight steps, so both
-    // latencies overlap. Every load is unconditional (clamped addresses): the
-    // compiler then counts outstanding loads exactly and waits only for what it uses.
+    // ---- prologue: activation K-range of this wave -> LDS, first D weight steps in flight
     const int tfirst = t0 < a.tasks_total ? t0 : a.tasks_total - 1;
-    const int last_blk = S > 0 ? lo + S - 1 : 0;
+    it.load(a, tfirst, lane);
+    ct = it;
     if (FUSEDQ) {
-        constexpr int XB = 4;  // superblocks per batch (4 float4 registers)
-        const float *xc = a.x + (int64_t)col0 * a.x_col_stride;
-        f32x4a xv[XB];
-#pragma unroll
-        for (int i = 0; i < XB; ++i) {
-            const int b = min(lo + i, last_blk);
-            xv[i] = *(const f32x4a *)(xc + (int64_t)b * QK + 4 * lane);
-        }
-        ic.start(a, tfirst, g);
-        cc.start(a, tfirst, g);
-        if (!(a.diag & 4)) {  // diagnostics bit2: no weight loads in the prologue
-#pragma unroll
-            for (int j = 0; j < D; ++j) issue(ring[j]);
-        }
-        auto quant_batch = [&](int b0) {
-#pragma unroll
-            for (int i = 0; i < XB; ++i) {
-                const int b = b0 + i;
-                if (b < lo + S) {
-                    const Q8Lane q = quant_values_wave(xv[i], lane);
-                    *(uint32_t *)(act_qs + b * ACT_QS_STRIDE + 4 * lane) = q.qs4;
-                    if ((lane & 3) == 0) act_bs[b * 16 + (lane >> 2)] = (int16_t)q.bsum;
-                    if (lane == 0) act_d[b] = q.d;
-                }
-            }
-        };
-        quant_batch(lo);  // first batch straight-line: its waits skip the weight loads
-        for (int b0 = lo + XB; b0 < lo + S; b0 += XB) {
-#pragma unroll
-            for (int i = 0; i < XB; ++i) {
-                const int b = min(b0 + i, last_blk);
-                xv[i] = *(const f32x4a *)(xc + (int64_t)b * QK + 4 * lane);
-            }
-            quant_batch(b0);
-        }
+        const float *xc = a.x + (int64_t)col0 * a.x_col_stride + (int64_t)lo * QK;
+        for (int i = 0; i < S; ++i) dma16(xc + (int64_t)i * QK + 4 * lane, (LDS void *)(act + 1024 * i));
     } else {
-        ic.start(a, tfirst, g);
-        cc.start(a, tfirst, g);
-#pragma unroll
-        for (int j = 0; j < D; ++j) issue(ring[j]);
-        // Q8_K blocks of this wave's K-range: 73 dwords each (d, 64 qs words, 8 bsum words)
         for (int c = 0; c < ncol; ++c) {
-            const uint8_t *src = a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)lo * 292;
-            for (int i = lane; i < S * 73; i += WAVE) {
-                const int b = i / 73, dw = i - b * 73;
-                const uint32_t v = gload4(src + (int64_t)b * 292 + 4 * dw);
-                const int cb = c * nb + lo + b;
-                if (dw == 0) act_d[cb] = __uint_as_float(v);
-                else if (dw <= 64) *(uint32_t *)(act_qs + cb * ACT_QS_STRIDE + 4 * (dw - 1)) = v;
-                else *(uint32_t *)(act_bs + cb * 16 + 2 * (dw - 65)) = v;
+            const uintptr_t start = (uintptr_t)(a.xq + (int64_t)(col0 + c) * a.xq_col_stride + (int64_t)lo * 292);
+            const uint8_t *s16 = (const uint8_t *)(start & ~(uintptr_t)15);
+            const int np = (int)((S * 292 + (start & 15) + 15) / 16);
+            for (int k = 0; k * 64 < np; ++k) {
+                const int pc = k * 64 + lane;
+                if (pc < np) dma16(s16 + 16 * pc, (LDS void *)(act + c * L.act_col + 1024 * k));
             }
         }
     }
+    const int pre = Q < D ? Q : D;
+    for (int j = 0; j < pre; ++j) issue();
+    vm_wait_steps(pre);  // activation DMAs are older than the ring's 2*pre
+    if (FUSEDQ) {
+        // quantize in place: block i's f32 staging [1024i, 1024i+1024) -> raw Q8_K [292i, 292i+292)
+#pragma unroll 1
+        for (int i = 0; i < S; ++i) {
+            const f32x4 v = *(const f32x4 *)(act + 1024 * i + 16 * lane);
+            const Q8Lane q = quant_values_wave(v, lane);
+            uint8_t *qb = act + 292 * i;
+            *(uint32_t *)(qb + 4 + 4 * lane) = q.qs4;
+            if ((lane & 3) == 0) *(int16_t *)(qb + 260 + 2 * (lane >> 2)) = (int16_t)q.bsum;
+            if (lane == 0) *(float *)qb = q.d;
+        }
+    }
     wave_lds_fence();  // this wave's staged activations before its own reads
-
+    uint64_t st1 = 0, st2 = 0;
+    if (a.stamps) {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        st1 = __builtin_amdgcn_s_memrealtime();
+    }
     if (a.diag & 1) return;  // diagnostics: prologue only
 
-    // ---- main loop. Steps padded to a multiple of D: the ring loop body is
-    // straight-line code; padding steps re-run the clamped last step and never
-    // store (live == false). Waves without a K-range still meet every task barrier.
+    // ---- main loop: wait for step q's slot, compute it, refill the slot with step q+D
     if (S > 0) {
-        const int Qp = (Q + D - 1) / D * D;
-        for (int q0 = 0; q0 < Qp; q0 += D) {
-#pragma unroll
-            for (int j = 0; j < D; ++j) {
-                compute(ring[j], q0 + j < Q);
-                issue(ring[j]);
-            }
+#pragma unroll 1
+        for (int q = 0; q < Q; ++q) {
+            // steps issued after q: min(D, Q - q) - 1 (debug stores also count: wait for all)
+            vm_wait_steps(DEBUG ? 0 : (Q - q < D ? Q - q : D) - 1);
+            compute(q);
+            if (q + D < Q) issue();
         }
     } else {
         for (int k = 0; k < my_tasks; ++k) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
+    if (a.stamps) st2 = __builtin_amdgcn_s_memrealtime();
 
     // ---- flush wave 0's staged results: task k -> rows row0..row0+7, NCOL columns
     if (!DEBUG && wave == 0 && my_tasks > 0) {
         wave_lds_fence();
         for (int k = 0; k < my_tasks; ++k) {
             const StepInfo si = task_info(a, t0 + k * tstride);
-            const int i = lane;  // NCOL * 8 <= 64
-            const int c = i >> 3, r = i & 7;
+            const int c = lane >> 3, r = lane & 7;  // NCOL * 8 <= 64
             if (c < ncol && r < si.rows)
-                a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = outs[k * NCOL * 8 + i];
+                a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = outs[k * NCOL * 8 + lane];
+        }
+    }
+    if (a.stamps) {
+        const int64_t o = ((int64_t)blockIdx.x * WAVES_PER_WG + wave) * 4;
+        if (lane == 0 && o + 3 < a.stamps_cap) {
+            const uint64_t st3 = __builtin_amdgcn_s_memrealtime();
+            a.stamps[o] = st0;
+            a.stamps[o + 1] = st1;
+            a.stamps[o + 2] = st2;
+            a.stamps[o + 3] = st3;
         }
     }
 }

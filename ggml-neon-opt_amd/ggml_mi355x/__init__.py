@@ -15,7 +15,7 @@ import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
-LIB_PATH = os.path.join(PKG_ROOT, "lib", "libggml_mi355x.so")
+LIB_PATH = os.environ.get("MI355X_LIB") or os.path.join(PKG_ROOT, "lib", "libggml_mi355x.so")
 
 TYPE_F32, TYPE_Q4_K, TYPE_Q5_K, TYPE_Q6_K, TYPE_Q8_K = 0, 12, 13, 14, 15
 QK_K = 256
@@ -33,7 +33,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_backend_init", "mi355x_backend_free", "mi355x_backend_name", "mi355x_backend_stream",
     "mi355x_backend_alloc", "mi355x_backend_free_buffer", "mi355x_backend_set_tensor",
     "mi355x_backend_get_tensor", "mi355x_backend_synchronize", "mi355x_backend_supports_op",
-    "mi355x_backend_graph_compute", "mi355x_timing_enable", "mi355x_timing_read",
+    "mi355x_backend_graph_compute", "mi355x_timing_enable", "mi355x_timing_read", "mi355x_diag_stamps",
 )
 
 
@@ -112,6 +112,8 @@ def lib():
     L.mi355x_timing_enable.restype = i32
     L.mi355x_timing_read.argtypes = [ctypes.POINTER(LaunchTiming), i32]
     L.mi355x_timing_read.restype = i32
+    L.mi355x_diag_stamps.argtypes = [vp, sz]
+    L.mi355x_diag_stamps.restype = i32
     _lib = L
     return L
 

@@ -182,6 +182,11 @@ typedef struct {
 } mi355x_launch_timing;
 int mi355x_timing_enable(int enable);
 int mi355x_timing_read(mi355x_launch_timing *out, int max);
+/* Diagnostics: while `buf` (device memory, `bytes` long) is set, GEMV launches
+ * record per-wave s_memrealtime stamps (100 MHz) at kernel entry, after the
+ * activation prologue, after the main loop and at exit: 4 x uint64 per wave,
+ * indexed [(blockIdx.x * 4 + wave) * 4 + i]. NULL disables. Not for production. */
+int mi355x_diag_stamps(void *buf, size_t bytes);
 
 /* --------------------------------------------- ggml-backend mirror (C++) */
 /* A minimal mirror of ggml-backend's device/buffer/graph interface

@@ -1,0 +1,52 @@
+"""In-kernel timeline of one GEMV launch (diagnostic build path): per-wave
+s_memrealtime stamps at entry / after prologue / after main loop / exit."""
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "ggml-neon-opt_amd")]
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+import ggml_mi355x as g  # noqa: E402
+from bench import random_kquant  # noqa: E402
+
+SHAPES = [("tl q", 12, 2048, 2048), ("tl 8rows", 12, 2048, 8), ("tl gate+up", 12, 2048, 11264),
+          ("tl down", 12, 5632, 2048), ("70b down", 12, 28672, 8192)]
+
+
+def main():
+    dev = torch.device("cuda:0")
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(3)
+    buf = torch.zeros(1 << 20, dtype=torch.int64, device=dev)
+    for label, typ, K, N in SHAPES:
+        ws = [random_kquant(typ, N, K, gen, dev) for _ in range(max(2, int(600e6 // (N * K // 256 * 144))))]
+        x = torch.randn(1, K, device=dev)
+        y = torch.empty(1, N, device=dev)
+        for w in ws:
+            g.mul_mat(typ, w, K, x, out=y)
+        res = []
+        for r in range(5):
+            buf.zero_()
+            torch.cuda.synchronize()
+            # warm the clocks with a burst; stamps of the LAST launch of the burst survive
+            for i in range(60):
+                if i == 59:
+                    g.lib().mi355x_diag_stamps(buf.data_ptr(), buf.numel() * 8)
+                g.mul_mat(typ, ws[(r * 60 + i) % len(ws)], K, x, out=y)
+            torch.cuda.synchronize()
+            g.lib().mi355x_diag_stamps(None, 0)
+            st = buf.cpu().numpy().astype(np.int64).reshape(-1, 4)
+            st = st[st[:, 0] != 0]
+            t0 = st[:, 0].min()
+            rel = (st - t0) * 10 / 1000.0  # 100 MHz ticks -> us
+            res.append((len(st), rel[:, 0].max(), np.median(rel[:, 1] - rel[:, 0]), np.max(rel[:, 1] - rel[:, 0]),
+                        np.median(rel[:, 2] - rel[:, 1]), np.max(rel[:, 2] - rel[:, 1]), rel[:, 3].max()))
+        a = np.array(res)[1:].mean(0)
+        print(f"{label:12s} waves={int(a[0]):5d} start_spread={a[1]:5.2f}us prologue med/max={a[2]:5.2f}/{a[3]:5.2f} "
+              f"loop med/max={a[4]:6.2f}/{a[5]:6.2f} end={a[6]:6.2f}us")
+
+
+if __name__ == "__main__":
+    main()
