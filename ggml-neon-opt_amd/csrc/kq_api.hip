@@ -64,7 +64,9 @@ gemv_fn pick_gemv(int ncol, bool fusedq, bool debug, int tmask) {
 
 int type_bit(int type) { return type == Q4_K ? 1 : type == Q5_K ? 2 : type == Q6_K ? 4 : 0; }
 
-constexpr size_t kMaxLds = 64 * 1024;
+constexpr size_t kMaxLds = 160 * 1024;   // LDS per CU (one workgroup may use it all)
+constexpr size_t kTargetLds = 80 * 1024; // aim for >= 2 resident workgroups per CU
+constexpr int64_t kFusedQMaxNb = 32;      // in-kernel quantization up to K = 8192
 
 uint64_t *g_stamps = nullptr;  // diagnostics (mi355x_diag_stamps)
 int64_t g_stamps_cap = 0;
@@ -160,7 +162,7 @@ int choose_ncol(int64_t M, int nb) {
     for (int i = 0; i < 4; ++i) {
         const int nc = cands[i];
         if (nc > M && nc > 1) continue;
-        if ((size_t)lds_layout(nc, nb, 8 * nc, false, 8 * 16 * 14, 4).total <= kMaxLds) return nc;
+        if ((size_t)lds_layout(nc, nb, 8 * nc, false, 8 * 16 * 14, 4).total <= kTargetLds) return nc;
     }
     return 1;
 }
@@ -236,7 +238,7 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
     int D = 4;
     for (int i = 0; i < 3; ++i) {
         D = dcands[i];
-        if ((size_t)lds_layout(ncol, (int)nb, 8 * ncol, fusedq, slot, D).total <= kMaxLds / 2) break;
+        if ((size_t)lds_layout(ncol, (int)nb, 8 * ncol, fusedq, slot, D).total <= kTargetLds) break;
     }
     if (a.ring_override > 0) D = a.ring_override < 8 ? a.ring_override : 8;
     a.ring = D;
@@ -257,9 +259,22 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
     return MI355X_OK;
 }
 
+// Dynamic LDS above 64 KB must be opted into per kernel.
+void allow_lds(gemv_fn fn, size_t lds) {
+    if (lds <= 64 * 1024) return;
+    static std::mutex mu;
+    static std::vector<std::pair<const void *, size_t>> done;
+    std::lock_guard<std::mutex> lk(mu);
+    for (auto &e : done)
+        if (e.first == (const void *)fn && e.second >= lds) return;
+    hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
+    done.push_back({(const void *)fn, kMaxLds});
+}
+
 int launch_gemv(const GemvPlan &pl, hipStream_t stream) {
     const GemvArgs &a = pl.a;
     if (a.tasks_total == 0 || a.m_total == 0) return MI355X_OK;
+    allow_lds(pl.fn, pl.lds);
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
         hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), (uint32_t)pl.lds, stream, e0, e1, 0, a);
@@ -332,9 +347,14 @@ void mi355x_quantize_row_q8_K(const float *x, void *y, int64_t k) {
 size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, int64_t ne11) {
     (void)ne01;
     if (!block_bytes(src0_type) || ne00 <= 0 || ne00 % QK || ne11 < 0) return 0;
-    if (ne11 <= 1) return 0;
+    if (ne11 == 0 || (ne11 == 1 && ne00 / QK <= kFusedQMaxNb)) return 0;
     const size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * 292;
     return (bytes + 255) & ~(size_t)255;
+}
+
+size_t mi355x_gemv_fused_workspace_size(int64_t k) {
+    if (k <= 0 || k % QK || k / QK <= kFusedQMaxNb) return 0;
+    return ((size_t)(k / QK) * 292 + 255) & ~(size_t)255;
 }
 
 int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
@@ -367,7 +387,7 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     if (!src1 || ((uintptr_t)src1 & 3u) || (nb11 & 3u) || !dst || ((uintptr_t)dst & 3u) || (nb1 & 3u))
         return MI355X_E_INVAL;
     if (ne11 > 1 && (nb11 < (size_t)ne00 * 4 || nb1 < (size_t)ne01 * 4)) return MI355X_E_INVAL;
-    if (ne11 == 1) {
+    if (ne11 == 1 && ne00 / QK <= kFusedQMaxNb && ((uintptr_t)src1 & 15u) == 0) {
         mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
         GemvPlan pl;
         int rc = plan_gemv(&d, 1, ne00, 1, 1, true, false, pl);
@@ -378,7 +398,8 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
         if (!device_ok()) return MI355X_E_NODEVICE;
         return launch_gemv(pl, (hipStream_t)stream);
     }
-    const size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
+    size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
+    if (need == 0) need = (size_t)ne11 * (size_t)(ne00 / QK) * 292;  // misaligned src1, M == 1
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
     if (!device_ok()) return MI355X_E_NODEVICE;
     int rc = launch_quantize(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream);
@@ -387,16 +408,29 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     return mi355x_mul_mat_q8(src0_type, src0, ne00, ne01, nb01, workspace, ne11, q8_row, dst, nb1, stream);
 }
 
-int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k, void *stream) {
+int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k, void *workspace,
+                      size_t workspace_size, void *stream) {
     if (!descs || !x || ((uintptr_t)x & 3u)) return MI355X_E_INVAL;
-    GemvPlan pl;
-    int rc = plan_gemv(descs, n_desc, k, 1, 1, true, false, pl);
-    if (rc) return rc;
-    for (int i = 0; i < n_desc; ++i)
+    if (k <= 0 || k % QK) return MI355X_E_INVAL;
+    for (int i = 0; i < n_desc && i < MI355X_MAX_FUSED; ++i)
         if (descs[i].y && ((uintptr_t)descs[i].y & 3u)) return MI355X_E_INVAL;
-    pl.a.x = x;
-    pl.a.x_col_stride = k;
+    const bool fusedq = k / QK <= kFusedQMaxNb && ((uintptr_t)x & 15u) == 0;
+    GemvPlan pl;
+    int rc = plan_gemv(descs, n_desc, k, 1, 1, fusedq, false, pl);
+    if (rc) return rc;
+    if (fusedq) {
+        pl.a.x = x;
+        pl.a.x_col_stride = k;
+        if (!device_ok()) return MI355X_E_NODEVICE;
+        return launch_gemv(pl, (hipStream_t)stream);
+    }
+    const size_t need = (size_t)(k / QK) * 292;
+    if (!workspace || workspace_size < need || ((uintptr_t)workspace & 3u)) return MI355X_E_WORKSPACE;
     if (!device_ok()) return MI355X_E_NODEVICE;
+    rc = launch_quantize(x, k, workspace, k, 1, (hipStream_t)stream);
+    if (rc) return rc;
+    pl.a.xq = (const uint8_t *)workspace;
+    pl.a.xq_col_stride = (int64_t)need;
     return launch_gemv(pl, (hipStream_t)stream);
 }
 

@@ -81,7 +81,8 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
                 d[k].row_stride = n->src[0]->nb[1];
                 d[k].y = (float *)n->data;
             }
-            rc = mi355x_gemv_fused(d, l.count, (const float *)x->data, w->ne[0], b->stream);
+            rc = mi355x_gemv_fused(d, l.count, (const float *)x->data, w->ne[0], b->workspace, b->workspace_size,
+                                   b->stream);
         } else {
             rc = mi355x_mul_mat(w->type, w->data, w->ne[0], w->ne[1], w->nb[1], (const float *)x->data, x->ne[1],
                                 x->nb[1], (float *)t->data, t->nb[1], b->workspace, b->workspace_size,
@@ -178,7 +179,11 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
         if (!mi355x_backend_supports_op(nodes[i])) return MI355X_E_UNSUPPORTED;
         if (nodes[i]->op == MI355X_OP_MUL_MAT) {
             const mi355x_tensor *w = nodes[i]->src[0];
-            const size_t need = mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], nodes[i]->src[1]->ne[1]);
+            size_t need = mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], nodes[i]->src[1]->ne[1]);
+            const size_t nf = mi355x_gemv_fused_workspace_size(w->ne[0]);
+            need = need > nf ? need : nf;
+            if (nodes[i]->src[1]->ne[1] == 1 && ((uintptr_t)nodes[i]->src[1]->data & 15u))
+                need = need > (size_t)(w->ne[0] / 256) * 292 ? need : (size_t)(w->ne[0] / 256) * 292;
             ws = need > ws ? need : ws;
         }
     }

@@ -400,6 +400,7 @@ struct TaskLane {
     int dj[2];                       // DMA piece index within the block
     bool dact1;                      // lane active in DMA instruction 1
 
+    template <int TMASK>
     __device__ __forceinline__ void load(const GemvArgs &a, int t, int lane) {
         const StepInfo si = task_info(a, t);
         m = si.m;
@@ -413,6 +414,8 @@ struct TaskLane {
         const uint8_t *w = a.w[m];
         const int64_t rs = a.row_stride[m];
         crow = w + (int64_t)(row0 + (valid ? g : rows - 1)) * rs;
+        if (TMASK == 1) P = 9;  // compile-time divisor below
+        if (TMASK == 4) P = 14;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             const int pi = lane + 64 * i;
@@ -471,10 +474,12 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
 
     // ---- issue cursor: step q -> (task k, step s); DMA into slot q % D
     TaskLane it;
-    int ik = 0, is = 0, iq = 0;
+    int ik = 0, is = 0;
+    uint8_t *const ring_end = ring + D * SLOT;
+    uint8_t *islot = ring;  // slot of the next issued step (wraps)
     auto issue = [&]() {
         const int blk = lo + is;
-        uint8_t *slot = ring + (iq % D) * SLOT;
+        uint8_t *slot = islot;
         const int type = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : it.type;
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
@@ -487,10 +492,10 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
             }
             if (i == 0 || it.dact1) dma16(src, (LDS void *)(slot + 1024 * i));
         }
-        ++iq;
+        islot = islot + SLOT == ring_end ? ring : islot + SLOT;
         if (++is == S) {
             is = 0;
-            if (++ik < my_tasks) it.load(a, t0 + ik * tstride, lane);
+            if (++ik < my_tasks) it.load<TMASK>(a, t0 + ik * tstride, lane);
         }
     };
 
@@ -524,10 +529,12 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         }
     };
 
-    auto compute = [&](int q) {
+    const uint8_t *cslot = ring;  // slot of the next computed step (wraps)
+    auto compute = [&]() {
         const int blk = lo + cs;
         const int type = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : ct.type;
-        const uint8_t *slot = ring + (q % D) * SLOT;
+        const uint8_t *slot = cslot;
+        cslot = cslot + SLOT == ring_end ? ring : cslot + SLOT;
         uint32_t sh = 0;
         if (type == Q6_K) sh = (uint32_t)((uintptr_t)(ct.crow + (int64_t)blk * 210) & 15u);
         Regs rr;
@@ -556,14 +563,16 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         if (++cs == S) {
             task_end();
             cs = 0;
-            if (++ck < my_tasks) ct.load(a, t0 + ck * tstride, lane);
+            if (++ck < my_tasks) ct.load<TMASK>(a, t0 + ck * tstride, lane);
         }
     };
 
     // ---- prologue: activation K-range of this wave -> LDS, first D weight steps in flight
     const int tfirst = t0 < a.tasks_total ? t0 : a.tasks_total - 1;
-    it.load(a, tfirst, lane);
+    it.load<TMASK>(a, tfirst, lane);
     ct = it;
+    uint64_t sa = 0, sb = 0, sc = 0;
+    if (a.stamps) sa = __builtin_amdgcn_s_memrealtime();
     if (FUSEDQ) {
         const float *xc = a.x + (int64_t)col0 * a.x_col_stride + (int64_t)lo * QK;
         for (int i = 0; i < S; ++i) dma16(xc + (int64_t)i * QK + 4 * lane, (LDS void *)(act + 1024 * i));
@@ -580,7 +589,9 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     }
     const int pre = Q < D ? Q : D;
     for (int j = 0; j < pre; ++j) issue();
+    if (a.stamps) sb = __builtin_amdgcn_s_memrealtime();
     vm_wait_steps(pre);  // activation DMAs are older than the ring's 2*pre
+    if (a.stamps) sc = __builtin_amdgcn_s_memrealtime();
     if (FUSEDQ) {
         // quantize in place: block i's f32 staging [1024i, 1024i+1024) -> raw Q8_K [292i, 292i+292)
 #pragma unroll 1
@@ -607,7 +618,7 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         for (int q = 0; q < Q; ++q) {
             // steps issued after q: min(D, Q - q) - 1 (debug stores also count: wait for all)
             vm_wait_steps(DEBUG ? 0 : (Q - q < D ? Q - q : D) - 1);
-            compute(q);
+            compute();
             if (q + D < Q) issue();
         }
     } else {
@@ -626,13 +637,16 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         }
     }
     if (a.stamps) {
-        const int64_t o = ((int64_t)blockIdx.x * WAVES_PER_WG + wave) * 4;
-        if (lane == 0 && o + 3 < a.stamps_cap) {
+        const int64_t o = ((int64_t)blockIdx.x * WAVES_PER_WG + wave) * 8;
+        if (lane == 0 && o + 7 < a.stamps_cap) {
             const uint64_t st3 = __builtin_amdgcn_s_memrealtime();
             a.stamps[o] = st0;
             a.stamps[o + 1] = st1;
             a.stamps[o + 2] = st2;
             a.stamps[o + 3] = st3;
+            a.stamps[o + 4] = sa;
+            a.stamps[o + 5] = sb;
+            a.stamps[o + 6] = sc;
         }
     }
 }

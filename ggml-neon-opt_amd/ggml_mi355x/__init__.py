@@ -34,6 +34,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_backend_alloc", "mi355x_backend_free_buffer", "mi355x_backend_set_tensor",
     "mi355x_backend_get_tensor", "mi355x_backend_synchronize", "mi355x_backend_supports_op",
     "mi355x_backend_graph_compute", "mi355x_timing_enable", "mi355x_timing_read", "mi355x_diag_stamps",
+    "mi355x_gemv_fused_workspace_size",
 )
 
 
@@ -84,7 +85,9 @@ def lib():
     L.mi355x_mul_mat.restype = i32
     L.mi355x_mul_mat_q8.argtypes = [i32, vp, i64, i64, sz, vp, i64, sz, vp, sz, vp]
     L.mi355x_mul_mat_q8.restype = i32
-    L.mi355x_gemv_fused.argtypes = [ctypes.POINTER(GemvDesc), i32, vp, i64, vp]
+    L.mi355x_gemv_fused.argtypes = [ctypes.POINTER(GemvDesc), i32, vp, i64, vp, sz, vp]
+    L.mi355x_gemv_fused_workspace_size.argtypes = [i64]
+    L.mi355x_gemv_fused_workspace_size.restype = sz
     L.mi355x_gemv_fused.restype = i32
     L.mi355x_debug_block_partials.argtypes = [i32, vp, i64, i64, sz, vp, vp, vp]
     L.mi355x_debug_block_partials.restype = i32
@@ -194,8 +197,10 @@ def mul_mat(type_, w, K, x, out=None, workspace=None, stream=None):
     if out is None:
         out = torch.empty((M, N), dtype=torch.float32, device=x.device)
     ws = int(lib().mi355x_mul_mat_workspace_size(type_, K, N, M))
+    if M == 1 and x.data_ptr() % 16:
+        ws = max(ws, K // QK_K * 292)
     if ws and (workspace is None or workspace.numel() < ws):
-        workspace = torch.empty(ws, dtype=torch.uint8, device=x.device)
+        workspace = _workspace(ws, x.device)
     _check(lib().mi355x_mul_mat(type_, w.data_ptr(), K, N, w.stride(0), x.data_ptr(), M, x.stride(0) * 4,
                                 out.data_ptr(), out.stride(0) * 4,
                                 workspace.data_ptr() if ws else None, ws, _stream(stream)), "mi355x_mul_mat")
@@ -216,15 +221,33 @@ def mul_mat_q8(type_, w, K, q8, out=None, stream=None):
     return out
 
 
-def gemv_fused(mats, x, stream=None):
-    """mats: list of (type, w tensor (N, rowbytes), y tensor (N,) f32); x: (K,) f32. One launch."""
+_ws_cache = {}
+
+
+def _workspace(nbytes, device):
+    torch = _torch()
+    key = str(device)
+    buf = _ws_cache.get(key)
+    if buf is None or buf.numel() < nbytes:
+        buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
+        _ws_cache[key] = buf
+    return buf
+
+
+def gemv_fused(mats, x, stream=None, workspace=None):
+    """mats: list of (type, w tensor (N, rowbytes), y tensor (N,) f32); x: (K,) f32. One launch
+    (two when K > 8192: Q8_K quantization into a workspace first)."""
     _require_device()
     n = len(mats)
     descs = (GemvDesc * n)()
     for i, (t, w, y) in enumerate(mats):
         descs[i] = GemvDesc(t, w.data_ptr(), w.shape[0], w.stride(0), y.data_ptr())
     K = x.shape[-1]
-    _check(lib().mi355x_gemv_fused(descs, n, x.data_ptr(), K, _stream(stream)), "mi355x_gemv_fused")
+    need = int(lib().mi355x_gemv_fused_workspace_size(K))
+    if need and (workspace is None or workspace.numel() < need):
+        workspace = _workspace(need, x.device)
+    _check(lib().mi355x_gemv_fused(descs, n, x.data_ptr(), K, workspace.data_ptr() if need else None, need,
+                                   _stream(stream)), "mi355x_gemv_fused")
 
 
 def block_partials(type_, w, K, q8_row, stream=None):

@@ -130,8 +130,9 @@ int mi355x_quantize_q8_K(const float *x, size_t x_stride, void *y, int64_t k, in
  * src1 column j (ggml row j of src1) at src1 + j*nb11, K floats; dst column j at
  * dst + j*nb1, N floats. Semantics = ggml_compute_forward_mul_mat: src1 is first
  * quantized to Q8_K (bit-exact), then every dst element is vec_dot(row, col).
- * M == 1 quantizes inside the GEMV kernel (no workspace needed); M > 1 needs a
- * workspace of mi355x_mul_mat_workspace_size() bytes. Async on `stream`. */
+ * M == 1 with K <= 8192 quantizes inside the GEMV kernel (no workspace); other
+ * shapes need a workspace of mi355x_mul_mat_workspace_size() bytes (the Q8_K
+ * copy of src1). Async on `stream`. */
 size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, int64_t ne11);
 int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
                    const float *src1, int64_t ne11, size_t nb11,
@@ -146,9 +147,11 @@ int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne0
 
 /* Fused decode GEMV over up to MI355X_MAX_FUSED matrices that share one f32
  * input vector x (K floats): e.g. attn_q/attn_k/attn_v, or ffn_gate/ffn_up.
- * One launch; x is quantized to Q8_K once per workgroup in LDS. Each matrix
- * may have its own K-quant type. Equivalent to n separate mi355x_mul_mat calls
- * with ne11 == 1 (bit-identical results). */
+ * Each matrix may have its own K-quant type. Equivalent to n separate
+ * mi355x_mul_mat calls with ne11 == 1 (bit-identical results). For K <= 8192
+ * x is quantized inside the GEMV (each wave quantizes its own K-range into LDS,
+ * one launch, no workspace); above that x is first quantized into `workspace`
+ * (mi355x_gemv_fused_workspace_size(k) bytes; 0 means none needed). */
 #define MI355X_MAX_FUSED 4
 typedef struct {
     int type;            /* MI355X_TYPE_Q4_K / Q5_K / Q6_K */
@@ -157,8 +160,9 @@ typedef struct {
     size_t row_stride;   /* nb01 in bytes                    */
     float *y;            /* device: N floats                 */
 } mi355x_gemv_desc;
+size_t mi355x_gemv_fused_workspace_size(int64_t k);
 int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k,
-                      void *stream);
+                      void *workspace, size_t workspace_size, void *stream);
 
 /* Debug/parity hook: per-superblock integer partials of a Q4_K/Q5_K/Q6_K x Q8_K
  * dot, as the GEMV kernel computes them. For each row r and superblock b:
@@ -184,8 +188,9 @@ int mi355x_timing_enable(int enable);
 int mi355x_timing_read(mi355x_launch_timing *out, int max);
 /* Diagnostics: while `buf` (device memory, `bytes` long) is set, GEMV launches
  * record per-wave s_memrealtime stamps (100 MHz) at kernel entry, after the
- * activation prologue, after the main loop and at exit: 4 x uint64 per wave,
- * indexed [(blockIdx.x * 4 + wave) * 4 + i]. NULL disables. Not for production. */
+ * activation prologue, after the main loop and at exit, then after the first
+ * task lookup, after the prologue DMAs are issued and after their wait:
+ * 8 x uint64 per wave, [(blockIdx.x * 4 + wave) * 8 + i]. NULL disables. */
 int mi355x_diag_stamps(void *buf, size_t bytes);
 
 /* --------------------------------------------- ggml-backend mirror (C++) */

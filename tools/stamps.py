@@ -12,7 +12,7 @@ import ggml_mi355x as g  # noqa: E402
 from bench import random_kquant  # noqa: E402
 
 SHAPES = [("tl q", 12, 2048, 2048), ("tl 8rows", 12, 2048, 8), ("tl gate+up", 12, 2048, 11264),
-          ("tl down", 12, 5632, 2048), ("70b down", 12, 28672, 8192)]
+          ("tl down", 12, 5632, 2048), ("tl out q6", 14, 2048, 32000)]
 
 
 def main():
@@ -37,15 +37,19 @@ def main():
                 g.mul_mat(typ, ws[(r * 60 + i) % len(ws)], K, x, out=y)
             torch.cuda.synchronize()
             g.lib().mi355x_diag_stamps(None, 0)
-            st = buf.cpu().numpy().astype(np.int64).reshape(-1, 4)
+            st = buf.cpu().numpy().astype(np.int64).reshape(-1, 8)
             st = st[st[:, 0] != 0]
             t0 = st[:, 0].min()
             rel = (st - t0) * 10 / 1000.0  # 100 MHz ticks -> us
-            res.append((len(st), rel[:, 0].max(), np.median(rel[:, 1] - rel[:, 0]), np.max(rel[:, 1] - rel[:, 0]),
-                        np.median(rel[:, 2] - rel[:, 1]), np.max(rel[:, 2] - rel[:, 1]), rel[:, 3].max()))
+            med = lambda v: float(np.median(v))  # noqa: E731
+            res.append((len(st), rel[:, 0].max(), med(rel[:, 4] - rel[:, 0]), med(rel[:, 5] - rel[:, 4]),
+                        med(rel[:, 6] - rel[:, 5]), med(rel[:, 1] - rel[:, 6]),
+                        med(rel[:, 1] - rel[:, 0]), med(rel[:, 2] - rel[:, 1]), np.max(rel[:, 2] - rel[:, 1]),
+                        rel[:, 3].max()))
         a = np.array(res)[1:].mean(0)
-        print(f"{label:12s} waves={int(a[0]):5d} start_spread={a[1]:5.2f}us prologue med/max={a[2]:5.2f}/{a[3]:5.2f} "
-              f"loop med/max={a[4]:6.2f}/{a[5]:6.2f} end={a[6]:6.2f}us")
+        print(f"{label:12s} waves={int(a[0]):5d} start_spread={a[1]:5.2f}us | lookup {a[2]:4.2f} issue {a[3]:4.2f} "
+              f"wait {a[4]:4.2f} quant {a[5]:4.2f} = prologue {a[6]:4.2f} | loop med/max={a[7]:5.2f}/{a[8]:5.2f} "
+              f"end={a[9]:6.2f}us")
 
 
 if __name__ == "__main__":
