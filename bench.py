@@ -162,9 +162,10 @@ def large_gemv(dev, reps=20):
             g.mul_mat(g.TYPE_Q4_K, ws[r % nbuf], K, x, out=y)
         rows = g.timing_read()
         g.timing_enable(False)
-        ms = [r[2] for r in rows]
-        b = rows[0][1]
-        out[label] = {"bytes": b, "us_median": float(np.median(ms) * 1e3),
+        per_call = len(rows) // reps  # K > 8192: Q8_K quantize launch + GEMV launch
+        ms = [sum(r[2] for r in rows[i * per_call:(i + 1) * per_call]) for i in range(reps)]
+        b = nbytes + K * 4 + N * 4
+        out[label] = {"bytes": b, "launches_per_call": per_call, "us_median": float(np.median(ms) * 1e3),
                       "GBps_median": b / (np.median(ms) * 1e-3) / 1e9,
                       "frac_median": b / (np.median(ms) * 1e-3) / 1e9 / HBM_PEAK_GBS}
         del ws

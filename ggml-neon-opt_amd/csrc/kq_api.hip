@@ -5,6 +5,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -19,6 +20,8 @@ namespace kq {
 template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void kq_gemv(const GemvArgs a);
 __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
+template <int TMASK, bool FUSEDQ>
+__global__ void kq_rows(const RowsArgs a);
 
 namespace {
 
@@ -72,16 +75,17 @@ uint64_t *g_stamps = nullptr;  // diagnostics (mi355x_diag_stamps)
 int64_t g_stamps_cap = 0;
 
 // Workgroups of one kernel resident per CU (registers / LDS), cached per (fn, lds).
-int resident_wgs(gemv_fn fn, size_t lds) {
+int resident_wgs(const void *fn, size_t lds) {
     static std::mutex mu;
     static std::vector<std::pair<std::pair<const void *, size_t>, int>> cache;
     std::lock_guard<std::mutex> lk(mu);
     for (auto &e : cache)
-        if (e.first.first == (const void *)fn && e.first.second == lds) return e.second;
+        if (e.first.first == fn && e.first.second == lds) return e.second;
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, WG_THREADS, lds) != hipSuccess || n <= 0) n = 2;
+    if (lds > 64 * 1024) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, WG_THREADS, lds) != hipSuccess || n <= 0) n = 1;
     if (n > 8) n = 8;
-    cache.push_back({{(const void *)fn, lds}, n});
+    cache.push_back({{fn, lds}, n});
     return n;
 }
 
@@ -176,7 +180,6 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
     const int64_t nb = K / QK;
     if (nb > 0x7fffffff / 8) return MI355X_E_INVAL;
     memset(&a, 0, sizeof(a));
-    int64_t total_rows = 0;
     int tmask = 0;
     for (int i = 0; i < n_desc; ++i) {
         const int bb = block_bytes(d[i].type);
@@ -188,7 +191,6 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
             if (d[i].row_stride < (size_t)(nb * bb) || (d[i].row_stride & 1u)) return MI355X_E_INVAL;
             if (d[i].type != Q6_K && (d[i].row_stride & 3u)) return MI355X_E_INVAL;
         }
-        total_rows += d[i].n_rows;
         tmask |= type_bit(d[i].type);
     }
     if (tmask != 1 && tmask != 4) tmask = 7;
@@ -240,11 +242,11 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
         D = dcands[i];
         if ((size_t)lds_layout(ncol, (int)nb, 8 * ncol, fusedq, slot, D).total <= kTargetLds) break;
     }
-    if (a.ring_override > 0) D = a.ring_override < 8 ? a.ring_override : 8;
+    if (a.ring_override > 0) D = a.ring_override < 13 ? a.ring_override : 13;
     a.ring = D;
     const int64_t base_lds = lds_layout(ncol, (int)nb, 0, fusedq, slot, D).total;
     if ((size_t)base_lds > kMaxLds) return MI355X_E_UNSUPPORTED;
-    int64_t wgs = (int64_t)num_cus() * resident_wgs(pl.fn, (size_t)base_lds + 1024);
+    int64_t wgs = (int64_t)num_cus() * resident_wgs((const void *)pl.fn, (size_t)base_lds + 1024);
     if (wgs > tasks) wgs = tasks > 0 ? tasks : 1;
     int64_t tpw = (tasks + wgs - 1) / wgs;
     while (tpw * 8 * ncol * 4 > 4096 && tpw > 1) {
@@ -260,25 +262,165 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
 }
 
 // Dynamic LDS above 64 KB must be opted into per kernel.
-void allow_lds(gemv_fn fn, size_t lds) {
+void allow_lds(const void *fn, size_t lds) {
     if (lds <= 64 * 1024) return;
     static std::mutex mu;
     static std::vector<std::pair<const void *, size_t>> done;
     std::lock_guard<std::mutex> lk(mu);
     for (auto &e : done)
-        if (e.first == (const void *)fn && e.second >= lds) return;
-    hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
-    done.push_back({(const void *)fn, kMaxLds});
+        if (e.first == fn && e.second >= lds) return;
+    hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
+    done.push_back({fn, kMaxLds});
 }
 
 int launch_gemv(const GemvPlan &pl, hipStream_t stream) {
     const GemvArgs &a = pl.a;
     if (a.tasks_total == 0 || a.m_total == 0) return MI355X_OK;
-    allow_lds(pl.fn, pl.lds);
+    allow_lds((const void *)pl.fn, pl.lds);
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
         hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), (uint32_t)pl.lds, stream, e0, e1, 0, a);
         timing_log(gemv_name(pl), gemv_bytes(a, pl.fusedq), e0, e1);
+    } else {
+        hipLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), pl.lds, stream, a);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+// ------------------------------------------------------------ row-stream decode GEMV
+std::atomic<int> g_impl{-1};
+bool rows_enabled() {
+    int v = g_impl.load();
+    if (v < 0) {
+        const char *e = getenv("MI355X_GEMV_IMPL");  // "tasks": force kq_gemv (A/B runs)
+        v = (e && strcmp(e, "tasks") == 0) ? MI355X_GEMV_TASKS : MI355X_GEMV_AUTO;
+        int expect = -1;
+        g_impl.compare_exchange_strong(expect, v);
+        v = g_impl.load();
+    }
+    return v == MI355X_GEMV_AUTO;
+}
+
+template <int TM, bool FQ>
+rows_fn rows_inst() {
+    return kq_rows<TM, FQ>;
+}
+
+rows_fn pick_rows(int tmask, bool fusedq) {
+    switch (tmask) {
+        case 1: return fusedq ? rows_inst<1, true>() : rows_inst<1, false>();
+        case 2: return fusedq ? rows_inst<2, true>() : rows_inst<2, false>();
+        case 4: return fusedq ? rows_inst<4, true>() : rows_inst<4, false>();
+        default: return fusedq ? rows_inst<7, true>() : rows_inst<7, false>();
+    }
+}
+
+int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, RowsPlan &pl) {
+    RowsArgs &a = pl.a;
+    if (n_desc < 1 || n_desc > MI355X_MAX_FUSED) return MI355X_E_INVAL;
+    if (K <= 0 || K % QK != 0) return MI355X_E_INVAL;
+    const int64_t nb = K / QK;
+    if (nb > 4096) return MI355X_E_UNSUPPORTED;
+    if (fusedq && nb > kFusedQMaxNb) return MI355X_E_UNSUPPORTED;
+    memset(&a, 0, sizeof(a));
+    int tmask = 0;
+    int64_t total_rows = 0;
+    for (int i = 0; i < n_desc; ++i) {
+        const int bb = block_bytes(d[i].type);
+        if (!bb) return MI355X_E_UNSUPPORTED;
+        if (d[i].n_rows < 0 || d[i].n_rows > 0x7fffffff) return MI355X_E_INVAL;
+        if (d[i].n_rows > 0) {
+            if (!d[i].w || !d[i].y) return MI355X_E_INVAL;
+            if (((uintptr_t)d[i].w & 3u) != 0) return MI355X_E_INVAL;
+            // one contiguous stream per wave; Q4_K/Q5_K superblocks 16-B aligned in LDS
+            if (d[i].row_stride != (size_t)(nb * bb)) return MI355X_E_UNSUPPORTED;
+            if (d[i].type != Q6_K && ((uintptr_t)d[i].w & 15u)) return MI355X_E_UNSUPPORTED;
+        }
+        total_rows += d[i].n_rows;
+        tmask |= type_bit(d[i].type);
+    }
+    if (tmask != 1 && tmask != 2 && tmask != 4) tmask = 7;
+    pl.tmask = tmask;
+    pl.fusedq = fusedq;
+    pl.fn = pick_rows(tmask, fusedq);
+    a.n_desc = n_desc;
+    a.nb = (int)nb;
+    for (int i = 0; i < n_desc; ++i) {
+        a.type[i] = d[i].type;
+        a.n_rows[i] = (int)d[i].n_rows;
+        a.w[i] = (const uint8_t *)d[i].w;
+        a.y[i] = d[i].y;
+    }
+    {
+        static int diag = -1, ring_env = -1;
+        if (diag < 0) {
+            const char *e = getenv("MI355X_GEMV_DIAG");
+            diag = e ? atoi(e) : 0;
+            e = getenv("MI355X_GEMV_RING");
+            ring_env = e ? atoi(e) : 0;
+        }
+        a.diag = diag;
+        a.ring = ring_env > 0 ? (ring_env < 12 ? ring_env : 12) : (tmask == 1 ? 6 : tmask == 2 ? 5 : 4);
+    }
+    a.stamps = g_stamps;
+    a.stamps_cap = g_stamps_cap;
+    const int slot = rows_slot(tmask);
+    // rows per chain batch: <= 128 records, batch ends on a step boundary (bR*nb % 8 == 0)
+    int g8 = 8;
+    while (nb % g8) g8 >>= 1;
+    const int u = 8 / g8;
+    int bR_full = (int)(128 / nb) / u * u;
+    if (bR_full < u) bR_full = u;
+    // rows per wave: fill the resident capacity once (no tail round of workgroups)
+    const int res = resident_wgs((const void *)pl.fn, (size_t)rows_layout((int)nb, slot, a.ring, bR_full, 64).total);
+    const int64_t cap_waves = (int64_t)num_cus() * res * WAVES_PER_WG;
+    int64_t rpw = (total_rows + cap_waves - 1) / cap_waves;
+    if (rpw < 1) rpw = 1;
+    while (true) {  // the per-matrix partition adds at most one partial wave per matrix
+        int64_t w = 0;
+        for (int i = 0; i < n_desc; ++i) w += (d[i].n_rows + rpw - 1) / rpw;
+        if (w <= cap_waves || rpw >= total_rows) break;
+        ++rpw;
+    }
+    if (rpw > 0x7fffffff / 64) return MI355X_E_UNSUPPORTED;
+    a.rpw = (int)rpw;
+    a.bR = rpw <= bR_full ? (int)rpw : bR_full;
+    int64_t waves = 0;
+    for (int i = 0; i < n_desc; ++i) {
+        a.wave_prefix[i] = (int)waves;
+        waves += (d[i].n_rows + rpw - 1) / rpw;
+    }
+    for (int i = n_desc; i <= MI355X_MAX_FUSED; ++i) a.wave_prefix[i] = (int)waves;
+    a.waves_total = (int)waves;
+    const RowsLayout L = rows_layout((int)nb, slot, a.ring, a.bR, a.rpw);
+    if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
+    pl.lds = (size_t)L.total;
+    pl.grid = dim3((unsigned)((waves + WAVES_PER_WG - 1) / WAVES_PER_WG), 1, 1);
+    return MI355X_OK;
+}
+
+std::string rows_name(const RowsPlan &pl) {
+    return std::string("kq::kq_rows<") + std::to_string(pl.tmask) + ", " + (pl.fusedq ? "true" : "false") + ">";
+}
+
+double rows_bytes(const RowsArgs &a, bool fusedq) {
+    double w = 0, y = 0;
+    for (int i = 0; i < a.n_desc; ++i) {
+        w += (double)a.n_rows[i] * a.nb * block_bytes(a.type[i]);
+        y += (double)a.n_rows[i] * 4.0;
+    }
+    return w + y + (fusedq ? (double)a.nb * QK * 4.0 : (double)a.nb * 292.0);
+}
+
+int launch_rows(const RowsPlan &pl, hipStream_t stream) {
+    const RowsArgs &a = pl.a;
+    if (a.waves_total == 0) return MI355X_OK;
+    allow_lds((const void *)pl.fn, pl.lds);
+    hipEvent_t e0, e1;
+    if (timing_slot(stream, e0, e1)) {
+        hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), (uint32_t)pl.lds, stream, e0, e1, 0, a);
+        timing_log(rows_name(pl), rows_bytes(a, pl.fusedq), e0, e1);
     } else {
         hipLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), pl.lds, stream, a);
     }
@@ -303,6 +445,49 @@ int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k,
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+// One activation column (decode): kq_rows when the rows are contiguous (always for
+// GGUF tensors), kq_gemv otherwise. x is quantized inside the GEMV for K <= 8192
+// (x 16-B aligned), else into `ws` first.
+int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *ws, size_t ws_size,
+            hipStream_t stream) {
+    const bool fusedq = k / QK <= kFusedQMaxNb && ((uintptr_t)x & 15u) == 0;
+    const size_t need = (size_t)(k / QK) * 292;
+    if (rows_enabled()) {
+        RowsPlan rp;
+        int rc = plan_rows(d, n, k, fusedq, rp);
+        if (rc == MI355X_OK) {
+            if (fusedq) {
+                rp.a.x = x;
+                if (!device_ok()) return MI355X_E_NODEVICE;
+                return launch_rows(rp, stream);
+            }
+            if (!ws || ws_size < need || ((uintptr_t)ws & 3u)) return MI355X_E_WORKSPACE;
+            if (!device_ok()) return MI355X_E_NODEVICE;
+            rc = launch_quantize(x, k, ws, k, 1, stream);
+            if (rc) return rc;
+            rp.a.xq = (const uint8_t *)ws;
+            return launch_rows(rp, stream);
+        }
+        if (rc != MI355X_E_UNSUPPORTED) return rc;
+    }
+    GemvPlan pl;
+    int rc = plan_gemv(d, n, k, 1, 1, fusedq, false, pl);
+    if (rc) return rc;
+    if (fusedq) {
+        pl.a.x = x;
+        pl.a.x_col_stride = k;
+        if (!device_ok()) return MI355X_E_NODEVICE;
+        return launch_gemv(pl, stream);
+    }
+    if (!ws || ws_size < need || ((uintptr_t)ws & 3u)) return MI355X_E_WORKSPACE;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    rc = launch_quantize(x, k, ws, k, 1, stream);
+    if (rc) return rc;
+    pl.a.xq = (const uint8_t *)ws;
+    pl.a.xq_col_stride = (int64_t)need;
+    return launch_gemv(pl, stream);
 }
 
 }  // namespace kq
@@ -367,6 +552,16 @@ int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne0
     if (ne11 > 1 && (nb11 < (size_t)(ne00 / QK) * 292 || nb1 < (size_t)ne01 * 4)) return MI355X_E_INVAL;
     if (ne11 > 0x7fffffff) return MI355X_E_INVAL;
     mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
+    if (ne11 == 1 && rows_enabled()) {
+        RowsPlan rp;
+        const int rc = plan_rows(&d, 1, ne00, false, rp);
+        if (rc == MI355X_OK) {
+            rp.a.xq = (const uint8_t *)src1_q8;
+            if (!device_ok()) return MI355X_E_NODEVICE;
+            return launch_rows(rp, (hipStream_t)stream);
+        }
+        if (rc != MI355X_E_UNSUPPORTED) return rc;
+    }
     const int ncol = choose_ncol(ne11, (int)(ne00 / QK));
     GemvPlan pl;
     int rc = plan_gemv(&d, 1, ne00, ne11, ncol, false, false, pl);
@@ -387,16 +582,9 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     if (!src1 || ((uintptr_t)src1 & 3u) || (nb11 & 3u) || !dst || ((uintptr_t)dst & 3u) || (nb1 & 3u))
         return MI355X_E_INVAL;
     if (ne11 > 1 && (nb11 < (size_t)ne00 * 4 || nb1 < (size_t)ne01 * 4)) return MI355X_E_INVAL;
-    if (ne11 == 1 && ne00 / QK <= kFusedQMaxNb && ((uintptr_t)src1 & 15u) == 0) {
+    if (ne11 == 1) {
         mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
-        GemvPlan pl;
-        int rc = plan_gemv(&d, 1, ne00, 1, 1, true, false, pl);
-        if (rc) return rc;
-        pl.a.x = src1;
-        pl.a.x_col_stride = (int64_t)(nb11 / 4);
-        pl.a.y_col_stride[0] = (int64_t)(nb1 / 4);
-        if (!device_ok()) return MI355X_E_NODEVICE;
-        return launch_gemv(pl, (hipStream_t)stream);
+        return gemv_m1(&d, 1, src1, ne00, workspace, workspace_size, (hipStream_t)stream);
     }
     size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
     if (need == 0) need = (size_t)ne11 * (size_t)(ne00 / QK) * 292;  // misaligned src1, M == 1
@@ -414,24 +602,7 @@ int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x,
     if (k <= 0 || k % QK) return MI355X_E_INVAL;
     for (int i = 0; i < n_desc && i < MI355X_MAX_FUSED; ++i)
         if (descs[i].y && ((uintptr_t)descs[i].y & 3u)) return MI355X_E_INVAL;
-    const bool fusedq = k / QK <= kFusedQMaxNb && ((uintptr_t)x & 15u) == 0;
-    GemvPlan pl;
-    int rc = plan_gemv(descs, n_desc, k, 1, 1, fusedq, false, pl);
-    if (rc) return rc;
-    if (fusedq) {
-        pl.a.x = x;
-        pl.a.x_col_stride = k;
-        if (!device_ok()) return MI355X_E_NODEVICE;
-        return launch_gemv(pl, (hipStream_t)stream);
-    }
-    const size_t need = (size_t)(k / QK) * 292;
-    if (!workspace || workspace_size < need || ((uintptr_t)workspace & 3u)) return MI355X_E_WORKSPACE;
-    if (!device_ok()) return MI355X_E_NODEVICE;
-    rc = launch_quantize(x, k, workspace, k, 1, (hipStream_t)stream);
-    if (rc) return rc;
-    pl.a.xq = (const uint8_t *)workspace;
-    pl.a.xq_col_stride = (int64_t)need;
-    return launch_gemv(pl, (hipStream_t)stream);
+    return gemv_m1(descs, n_desc, x, k, workspace, workspace_size, (hipStream_t)stream);
 }
 
 int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
@@ -450,6 +621,12 @@ int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, i
     pl.a.dbg = out;
     if (!device_ok()) return MI355X_E_NODEVICE;
     return launch_gemv(pl, (hipStream_t)stream);
+}
+
+int mi355x_gemv_impl(int impl) {
+    if (impl != MI355X_GEMV_AUTO && impl != MI355X_GEMV_TASKS) return MI355X_E_INVAL;
+    rows_enabled();  // resolve the environment default first
+    return g_impl.exchange(impl);
 }
 
 int mi355x_diag_stamps(void *buf, size_t bytes) {

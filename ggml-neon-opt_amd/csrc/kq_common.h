@@ -74,4 +74,55 @@ __host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg
     return L;
 }
 
+// ---------------------------------------------------------------- row-stream decode GEMV
+// Argument block of kq_rows (M = 1). Waves are partitioned per matrix: matrix d
+// owns global waves [wave_prefix[d], wave_prefix[d+1]); a wave owns `rpw`
+// consecutive rows (the last wave of a matrix fewer).
+struct RowsArgs {
+    int n_desc;
+    int nb;           // K / 256
+    int rpw;          // rows per wave
+    int waves_total;
+    int ring;         // LDS ring depth D (steps in flight per wave)
+    int bR;           // rows per chain batch (bR*nb % 8 == 0 unless bR >= rpw)
+    int diag;         // diagnostics: bit3 stream weights only
+    int wave_prefix[MI355X_MAX_FUSED + 1];
+    int type[MI355X_MAX_FUSED];
+    int n_rows[MI355X_MAX_FUSED];
+    const uint8_t *w[MI355X_MAX_FUSED];
+    float *y[MI355X_MAX_FUSED];
+    const float *x;       // f32 activation (FUSEDQ)
+    const uint8_t *xq;    // raw Q8_K activation row (!FUSEDQ)
+    uint64_t *stamps;
+    int64_t stamps_cap;
+};
+
+// One step = 8 consecutive superblocks of a wave's row stream, fetched as 16-B
+// granules from the 16-B boundary below them (+1 granule of slack): Q4_K 73,
+// Q5_K 89, Q6_K 106 granules; two LDS-DMA instructions per step for every type.
+__host__ __device__ constexpr int rows_gran(int type) { return 8 * block_bytes(type) / 16 + 1; }
+__host__ __device__ constexpr int rows_slot(int tmask) {
+    return 16 * ((tmask & 4) ? rows_gran(Q6_K) : (tmask & 2) ? rows_gran(Q5_K) : rows_gran(Q4_K));
+}
+
+//   act:  raw Q8_K activation (nb*292 B, +16 for a misaligned DMA source)
+//   ring: per wave D slots (+16 B tail slack for the Q6_K realign reads)
+//   recs: per wave bR*nb chain records (16 B), block-major [blk][row]
+//   outs: per wave rpw staged results
+struct RowsLayout {
+    int act, ring, ring_stride, recs, recs_stride, outs, outs_stride, total;
+};
+__host__ __device__ inline RowsLayout rows_layout(int nb, int slot, int D, int bR, int rpw) {
+    RowsLayout L;
+    L.act = 0;
+    L.ring = (nb * 292 + 32 + 15) & ~15;  // 16-B granules from the 16-B boundary below the row
+    L.ring_stride = D * slot + 16;
+    L.recs = L.ring + WAVES_PER_WG * L.ring_stride;
+    L.recs_stride = bR * nb * 16;
+    L.outs = L.recs + WAVES_PER_WG * L.recs_stride;
+    L.outs_stride = (rpw * 4 + 15) & ~15;
+    L.total = L.outs + WAVES_PER_WG * L.outs_stride;
+    return L;
+}
+
 }  // namespace kq

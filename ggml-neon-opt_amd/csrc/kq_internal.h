@@ -21,6 +21,20 @@ struct GemvPlan {
 int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int ncol, bool fusedq, bool debug,
               GemvPlan &pl);
 int launch_gemv(const GemvPlan &pl, hipStream_t stream);
+typedef void (*rows_fn)(const RowsArgs);
+struct RowsPlan {
+    RowsArgs a;
+    dim3 grid;
+    size_t lds;
+    rows_fn fn;
+    int tmask;
+    bool fusedq;
+};
+// Row-stream decode GEMV (kq_rows): returns MI355X_E_UNSUPPORTED when the rows are
+// not contiguous or not aligned for it (callers then use kq_gemv).
+int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, RowsPlan &pl);
+int launch_rows(const RowsPlan &pl, hipStream_t stream);
+bool rows_enabled();
 int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
                     hipStream_t stream);
 

@@ -34,7 +34,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_backend_alloc", "mi355x_backend_free_buffer", "mi355x_backend_set_tensor",
     "mi355x_backend_get_tensor", "mi355x_backend_synchronize", "mi355x_backend_supports_op",
     "mi355x_backend_graph_compute", "mi355x_timing_enable", "mi355x_timing_read", "mi355x_diag_stamps",
-    "mi355x_gemv_fused_workspace_size",
+    "mi355x_gemv_fused_workspace_size", "mi355x_gemv_impl",
 )
 
 
@@ -115,10 +115,24 @@ def lib():
     L.mi355x_timing_enable.restype = i32
     L.mi355x_timing_read.argtypes = [ctypes.POINTER(LaunchTiming), i32]
     L.mi355x_timing_read.restype = i32
+    L.mi355x_gemv_impl.argtypes = [i32]
+    L.mi355x_gemv_impl.restype = i32
     L.mi355x_diag_stamps.argtypes = [vp, sz]
     L.mi355x_diag_stamps.restype = i32
     _lib = L
     return L
+
+
+GEMV_AUTO, GEMV_TASKS = 0, 1
+
+
+def gemv_impl(impl):
+    """Select the decode GEMV kernel (GEMV_AUTO: row-stream kq_rows; GEMV_TASKS: kq_gemv).
+    Returns the previous selection."""
+    prev = lib().mi355x_gemv_impl(impl)
+    if prev < 0:
+        raise Mi355xError(f"mi355x_gemv_impl failed with status {prev}")
+    return prev
 
 
 def timing_enable(enable=True):

@@ -192,6 +192,12 @@ int mi355x_timing_read(mi355x_launch_timing *out, int max);
  * task lookup, after the prologue DMAs are issued and after their wait:
  * 8 x uint64 per wave, [(blockIdx.x * 4 + wave) * 8 + i]. NULL disables. */
 int mi355x_diag_stamps(void *buf, size_t bytes);
+/* Decode-GEMV implementation selector (A/B runs, parity of both paths):
+ * MI355X_GEMV_AUTO (row-stream kq_rows when rows are contiguous, else kq_gemv) or
+ * MI355X_GEMV_TASKS (always the 8-row-task kq_gemv). Returns the previous value. */
+#define MI355X_GEMV_AUTO 0
+#define MI355X_GEMV_TASKS 1
+int mi355x_gemv_impl(int impl);
 
 /* --------------------------------------------- ggml-backend mirror (C++) */
 /* A minimal mirror of ggml-backend's device/buffer/graph interface

@@ -34,3 +34,12 @@ def dev():
     assert g.device_available(), "gfx950 device / libggml_mi355x.so required for -m gpu tests"
     assert torch.cuda.is_available()
     return torch.device("cuda:0")
+
+
+@pytest.fixture(params=[0, 1], ids=["rows", "tasks"])
+def impl(request):
+    """Runs a decode-GEMV test on both kernels: kq_rows (default) and kq_gemv."""
+    import ggml_mi355x as g
+    prev = g.gemv_impl(request.param)
+    yield request.param
+    g.gemv_impl(prev)

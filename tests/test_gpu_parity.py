@@ -69,7 +69,7 @@ def test_quantize_row_q8_K_surface(dev, oracle):
 # ---------------------------------------------------------------- golden fixtures
 @pytest.mark.parametrize("name", ["q4K_k256_n16_m2", "q4K_k2048_n16_m2", "q4K_k5632_n8_m1",
                                   "q5K_k2048_n16_m2", "q6K_k2048_n16_m2", "q6K_k768_n9_m3"])
-def test_golden(dev, name):
+def test_golden(dev, name, impl):
     import ggml_mi355x as g
     z = np.load(os.path.join(GOLDEN, name + ".npz"))
     typ, K = int(z["type"]), int(z["K"])
@@ -94,7 +94,7 @@ SHAPES = [(256, 1), (256, 13), (512, 64), (768, 33), (1792, 7), (2048, 1), (2048
 
 @pytest.mark.parametrize("type_", [12, 13, 14])
 @pytest.mark.parametrize("K,N", SHAPES)
-def test_gemv_bit_exact(dev, oracle, npo, type_, K, N):
+def test_gemv_bit_exact(dev, oracle, npo, type_, K, N, impl):
     import ggml_mi355x as g
     rng = np.random.default_rng(K * 31 + N + type_)
     w = npo.random_blocks(rng, type_, N, K)
@@ -142,7 +142,7 @@ def test_strided_rows_and_columns(dev, oracle, npo):
     assert (got[:, N:] == -1.0).all()  # nothing written past ne0
 
 
-def test_vec_dot_surface(dev, oracle, npo):
+def test_vec_dot_surface(dev, oracle, npo, impl):
     """ggml_vec_dot_t mirror on device pointers (n, s, bs, vx, bx, vy, by, nrc=1)."""
     import torch
     import ggml_mi355x as g
@@ -160,7 +160,7 @@ def test_vec_dot_surface(dev, oracle, npo):
         assert bits_equal(s.cpu().numpy(), np.float32(ref))
 
 
-def test_fused_mixed_types_equal_separate(dev, oracle, npo):
+def test_fused_mixed_types_equal_separate(dev, oracle, npo, impl):
     """attn_q (Q4_K) + attn_k (Q4_K) + attn_v (Q6_K) in one launch == three mul_mats."""
     import torch
     import ggml_mi355x as g
@@ -177,18 +177,19 @@ def test_fused_mixed_types_equal_separate(dev, oracle, npo):
 
 
 # ---------------------------------------------------------------- full-size properties
-@pytest.mark.parametrize("K,N", [(4096, 14336), (14336, 4096), (8192, 1024)])
-def test_full_size_rows_subset(dev, oracle, npo, K, N):
+@pytest.mark.parametrize("type_", [12, 14])
+@pytest.mark.parametrize("K,N", [(4096, 14336), (14336, 4096), (8192, 1024), (5632, 16384), (768, 131072)])
+def test_full_size_rows_subset(dev, oracle, npo, K, N, type_, impl):
     """Llama-3-8B/70B-shaped GEMVs: every row on the GPU; a hashed subset of rows
     re-computed by the oracle must match bit-for-bit; all outputs finite."""
     import ggml_mi355x as g
     rng = np.random.default_rng(N + K)
-    w = npo.random_blocks(rng, 12, N, K)
+    w = npo.random_blocks(rng, type_, N, K)
     x = rng.standard_normal((1, K)).astype(np.float32)
-    got = g.mul_mat(12, t(w, dev), K, t(x, dev)).cpu().numpy()[0]
+    got = g.mul_mat(type_, t(w, dev), K, t(x, dev)).cpu().numpy()[0]
     assert np.isfinite(got).all()
-    rows = np.unique(rng.integers(0, N, 97))
-    ref = oracle.mul_mat(12, w[rows], x)[0]
+    rows = np.unique(np.concatenate([rng.integers(0, N, 97), [0, N - 1]]))
+    ref = oracle.mul_mat(type_, w[rows], x)[0]
     assert bits_equal(got[rows], ref)
 
 
@@ -248,3 +249,42 @@ def test_backend_graph_compute(dev, oracle, npo):
     for p in bufs:
         be.free_buffer(p)
     be.close()
+
+
+@pytest.mark.parametrize("type_,offset", [(14, 4), (14, 8), (12, 4), (13, 12)])
+def test_unaligned_weight_rows(dev, oracle, npo, type_, offset):
+    """Weights at a 4-B (not 16-B) aligned address: Q6_K streams from the 16-B boundary
+    below (kq_rows realigns in LDS); Q4_K/Q5_K fall back to kq_gemv. Bit-exact either way."""
+    import torch
+    import ggml_mi355x as g
+    K, N = 2048, 300
+    rng = np.random.default_rng(offset * 7 + type_)
+    w = npo.random_blocks(rng, type_, N, K)
+    buf = torch.zeros(w.size + 64, dtype=torch.uint8, device=dev)
+    buf[offset:offset + w.size] = t(w.reshape(-1), dev)
+    x = rng.standard_normal((1, K)).astype(np.float32)
+    xd = t(x, dev)
+    y = torch.full((N,), np.nan, device=dev)
+    L = g.lib()
+    rc = L.mi355x_mul_mat(type_, buf.data_ptr() + offset, K, N, w.shape[1], xd.data_ptr(), 1, K * 4,
+                          y.data_ptr(), N * 4, None, 0, torch.cuda.current_stream().cuda_stream)
+    assert rc == 0
+    ref = oracle.mul_mat(type_, w, x)[0]
+    assert bits_equal(y.cpu().numpy(), ref), first_mismatch(y.cpu().numpy(), ref)
+
+
+def test_fused_ragged_partition(dev, oracle, npo, impl):
+    """Four fused matrices with row counts that are not multiples of the rows per wave
+    (one partial wave per matrix), K with nb % 8 != 0 (chain batches cross rows)."""
+    import torch
+    import ggml_mi355x as g
+    K = 5632
+    rng = np.random.default_rng(99)
+    specs = [(12, 4099), (14, 1), (13, 777), (12, 2049)]
+    ws = [npo.random_blocks(rng, ty, n, K) for ty, n in specs]
+    x = rng.standard_normal(K).astype(np.float32)
+    ys = [torch.full((n,), np.nan, device=dev) for _, n in specs]
+    g.gemv_fused([(ty, t(w, dev), y) for (ty, _), w, y in zip(specs, ws, ys)], t(x, dev))
+    for (ty, _), w, y in zip(specs, ws, ys):
+        ref = oracle.mul_mat(ty, w, x[None])[0]
+        assert bits_equal(y.cpu().numpy(), ref), first_mismatch(y.cpu().numpy(), ref)

@@ -37,11 +37,12 @@ def run(reps=20):
             g.mul_mat(typ, ws[r % nbuf], K, x, out=y)
         rows = g.timing_read()
         g.timing_enable(False)
-        ms = np.array([r[2] for r in rows])
-        b = rows[0][1]
+        per_call = len(rows) // reps  # 2 launches (quantize + GEMV) above K = 8192
+        ms = np.array([sum(r[2] for r in rows[i * per_call:(i + 1) * per_call]) for i in range(reps)])
+        b = nbytes + K * 4 + N * 4  # algorithmic: weights + f32 activation + f32 output
         med = float(np.median(ms))
-        out.append({"shape": label, "type": typ, "K": K, "N": N, "kernel": rows[0][0], "MB": round(b / 1e6, 2),
-                    "us": round(med * 1e3, 2), "GBps": round(b / (med * 1e-3) / 1e9, 1)})
+        out.append({"shape": label, "type": typ, "K": K, "N": N, "kernel": "+".join(r[0] for r in rows[:per_call]),
+                    "MB": round(b / 1e6, 2), "us": round(med * 1e3, 2), "GBps": round(b / (med * 1e-3) / 1e9, 1)})
         del ws
         torch.cuda.empty_cache()
     return out
@@ -52,7 +53,7 @@ if __name__ == "__main__":
         sys.argv = sys.argv[:1]
         print(json.dumps(run()))
         sys.exit(0)
-    modes = sys.argv[1:] or ["auto", "rows", "blocks", "prologue"]
+    modes = sys.argv[1:] or ["auto", "prologue"]
     for mode in modes:
         env = dict(os.environ)
         if mode == "prologue":
@@ -61,6 +62,12 @@ if __name__ == "__main__":
             env["MI355X_GEMV_DIAG"] = "2"
         elif mode == "quantonly":
             env["MI355X_GEMV_DIAG"] = "5"
+        elif mode == "dmaonly":
+            env["MI355X_GEMV_DIAG"] = "8"
+        elif mode == "tasks":
+            env["MI355X_GEMV_IMPL"] = "tasks"
+        elif mode.startswith("ring"):
+            env["MI355X_GEMV_RING"] = mode[4:]
         elif mode != "auto":
             env["MI355X_GEMV_MODE"] = mode
         r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)

@@ -5,7 +5,7 @@ set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 STEPS=${STEPS:-64}
-timeout -k 10 600 python tools/gemv_sweep.py > gpurun_out/sweep.log 2>&1; rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.log
+timeout -k 10 600 python tools/gemv_sweep.py ${SWEEP_MODES:-auto tasks} > gpurun_out/sweep.log 2>&1; rc=$?; echo "sweep rc=$rc"; cat gpurun_out/sweep.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
 timeout -k 10 900 python -m pytest tests -m gpu -q -p no:cacheprovider ${PYTEST_ARGS:-} > gpurun_out/gpu_tests.log 2>&1
 rc=$?
