@@ -22,6 +22,7 @@ __global__ void kq_gemv(const GemvArgs a);
 __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TMASK, bool FUSEDQ>
 __global__ void kq_rows(const RowsArgs a);
+__global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 
 namespace {
 
@@ -353,27 +354,26 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
         a.y[i] = d[i].y;
     }
     {
-        static int diag = -1, ring_env = -1;
+        static int diag = -1, pre_env = -1;
         if (diag < 0) {
             const char *e = getenv("MI355X_GEMV_DIAG");
             diag = e ? atoi(e) : 0;
-            e = getenv("MI355X_GEMV_RING");
-            ring_env = e ? atoi(e) : 0;
+            e = getenv("MI355X_GEMV_PRE0");
+            pre_env = e ? atoi(e) : 1;
         }
         a.diag = diag;
-        a.ring = ring_env > 0 ? (ring_env < 12 ? ring_env : 12) : (tmask == 1 ? 6 : tmask == 2 ? 5 : 4);
+        a.pre0 = pre_env < 0 ? 0 : pre_env > 3 ? 3 : pre_env;
     }
     a.stamps = g_stamps;
     a.stamps_cap = g_stamps_cap;
-    const int slot = rows_slot(tmask);
-    // rows per chain batch: <= 128 records, batch ends on a step boundary (bR*nb % 8 == 0)
-    int g8 = 8;
-    while (nb % g8) g8 >>= 1;
-    const int u = 8 / g8;
+    // rows per chain batch: <= 128 records, batch ends on a step boundary (bR*nb % 16 == 0)
+    int g16 = ROWS_SB;
+    while (nb % g16) g16 >>= 1;
+    const int u = ROWS_SB / g16;
     int bR_full = (int)(128 / nb) / u * u;
     if (bR_full < u) bR_full = u;
     // rows per wave: fill the resident capacity once (no tail round of workgroups)
-    const int res = resident_wgs((const void *)pl.fn, (size_t)rows_layout((int)nb, slot, a.ring, bR_full, 64).total);
+    const int res = resident_wgs((const void *)pl.fn, (size_t)rows_layout((int)nb, tmask, bR_full, 64).total);
     const int64_t cap_waves = (int64_t)num_cus() * res * WAVES_PER_WG;
     int64_t rpw = (total_rows + cap_waves - 1) / cap_waves;
     if (rpw < 1) rpw = 1;
@@ -393,7 +393,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     }
     for (int i = n_desc; i <= MI355X_MAX_FUSED; ++i) a.wave_prefix[i] = (int)waves;
     a.waves_total = (int)waves;
-    const RowsLayout L = rows_layout((int)nb, slot, a.ring, a.bR, a.rpw);
+    const RowsLayout L = rows_layout((int)nb, tmask, a.bR, a.rpw);
     if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
     pl.lds = (size_t)L.total;
     pl.grid = dim3((unsigned)((waves + WAVES_PER_WG - 1) / WAVES_PER_WG), 1, 1);
@@ -410,7 +410,7 @@ double rows_bytes(const RowsArgs &a, bool fusedq) {
         w += (double)a.n_rows[i] * a.nb * block_bytes(a.type[i]);
         y += (double)a.n_rows[i] * 4.0;
     }
-    return w + y + (fusedq ? (double)a.nb * QK * 4.0 : (double)a.nb * 292.0);
+    return w + y + (fusedq ? (double)a.nb * QK * 4.0 : (double)a.nb * Q8L_STRIDE);
 }
 
 int launch_rows(const RowsPlan &pl, hipStream_t stream) {
@@ -423,6 +423,23 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
         timing_log(rows_name(pl), rows_bytes(a, pl.fusedq), e0, e1);
     } else {
         hipLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), pl.lds, stream, a);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+int launch_quantize_q8L(const float *x, int64_t k, void *y, hipStream_t stream) {
+    const int64_t nb = k / QK;
+    if (nb == 0) return MI355X_OK;
+    const int64_t wgs = (nb + 15) / 16;
+    hipEvent_t e0, e1;
+    if (timing_slot(stream, e0, e1)) {
+        hipExtLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, e0, e1, 0, x, k,
+                              (uint8_t *)y, (int)nb, nb);
+        timing_log("kq::kq_quantize_q8L", (double)nb * (QK * 4.0 + Q8L_STRIDE), e0, e1);
+    } else {
+        hipLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, x, k, (uint8_t *)y,
+                           (int)nb, nb);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
@@ -463,9 +480,10 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
                 if (!device_ok()) return MI355X_E_NODEVICE;
                 return launch_rows(rp, stream);
             }
-            if (!ws || ws_size < need || ((uintptr_t)ws & 3u)) return MI355X_E_WORKSPACE;
+            const size_t need_l = (size_t)(k / QK) * Q8L_STRIDE;
+            if (!ws || ws_size < need_l || ((uintptr_t)ws & 15u)) return MI355X_E_WORKSPACE;
             if (!device_ok()) return MI355X_E_NODEVICE;
-            rc = launch_quantize(x, k, ws, k, 1, stream);
+            rc = launch_quantize_q8L(x, k, ws, stream);
             if (rc) return rc;
             rp.a.xq = (const uint8_t *)ws;
             return launch_rows(rp, stream);
@@ -533,13 +551,13 @@ size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, 
     (void)ne01;
     if (!block_bytes(src0_type) || ne00 <= 0 || ne00 % QK || ne11 < 0) return 0;
     if (ne11 == 0 || (ne11 == 1 && ne00 / QK <= kFusedQMaxNb)) return 0;
-    const size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * 292;
+    const size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * (ne11 == 1 ? Q8L_STRIDE : 292);
     return (bytes + 255) & ~(size_t)255;
 }
 
 size_t mi355x_gemv_fused_workspace_size(int64_t k) {
     if (k <= 0 || k % QK || k / QK <= kFusedQMaxNb) return 0;
-    return ((size_t)(k / QK) * 292 + 255) & ~(size_t)255;
+    return ((size_t)(k / QK) * Q8L_STRIDE + 255) & ~(size_t)255;
 }
 
 int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,
@@ -552,16 +570,6 @@ int mi355x_mul_mat_q8(int src0_type, const void *src0, int64_t ne00, int64_t ne0
     if (ne11 > 1 && (nb11 < (size_t)(ne00 / QK) * 292 || nb1 < (size_t)ne01 * 4)) return MI355X_E_INVAL;
     if (ne11 > 0x7fffffff) return MI355X_E_INVAL;
     mi355x_gemv_desc d = {src0_type, src0, ne01, nb01, dst};
-    if (ne11 == 1 && rows_enabled()) {
-        RowsPlan rp;
-        const int rc = plan_rows(&d, 1, ne00, false, rp);
-        if (rc == MI355X_OK) {
-            rp.a.xq = (const uint8_t *)src1_q8;
-            if (!device_ok()) return MI355X_E_NODEVICE;
-            return launch_rows(rp, (hipStream_t)stream);
-        }
-        if (rc != MI355X_E_UNSUPPORTED) return rc;
-    }
     const int ncol = choose_ncol(ne11, (int)(ne00 / QK));
     GemvPlan pl;
     int rc = plan_gemv(&d, 1, ne00, ne11, ncol, false, false, pl);
@@ -587,7 +595,6 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
         return gemv_m1(&d, 1, src1, ne00, workspace, workspace_size, (hipStream_t)stream);
     }
     size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
-    if (need == 0) need = (size_t)ne11 * (size_t)(ne00 / QK) * 292;  // misaligned src1, M == 1
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
     if (!device_ok()) return MI355X_E_NODEVICE;
     int rc = launch_quantize(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream);

@@ -183,7 +183,7 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
             const size_t nf = mi355x_gemv_fused_workspace_size(w->ne[0]);
             need = need > nf ? need : nf;
             if (nodes[i]->src[1]->ne[1] == 1 && ((uintptr_t)nodes[i]->src[1]->data & 15u))
-                need = need > (size_t)(w->ne[0] / 256) * 292 ? need : (size_t)(w->ne[0] / 256) * 292;
+                need = need > (size_t)(w->ne[0] / 256) * kq::Q8L_STRIDE ? need : (size_t)(w->ne[0] / 256) * kq::Q8L_STRIDE;
             ws = need > ws ? need : ws;
         }
     }

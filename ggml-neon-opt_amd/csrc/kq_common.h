@@ -83,8 +83,8 @@ struct RowsArgs {
     int nb;           // K / 256
     int rpw;          // rows per wave
     int waves_total;
-    int ring;         // LDS ring depth D (steps in flight per wave)
-    int bR;           // rows per chain batch (bR*nb % 8 == 0 unless bR >= rpw)
+    int pre0;         // weight steps issued before the activation is quantized
+    int bR;           // rows per chain batch (bR*nb % 16 == 0 unless bR >= rpw)
     int diag;         // diagnostics: bit3 stream weights only
     int wave_prefix[MI355X_MAX_FUSED + 1];
     int type[MI355X_MAX_FUSED];
@@ -92,31 +92,41 @@ struct RowsArgs {
     const uint8_t *w[MI355X_MAX_FUSED];
     float *y[MI355X_MAX_FUSED];
     const float *x;       // f32 activation (FUSEDQ)
-    const uint8_t *xq;    // raw Q8_K activation row (!FUSEDQ)
+    const uint8_t *xq;    // Q8L activation row (!FUSEDQ), written by kq_quantize_q8L
     uint64_t *stamps;
     int64_t stamps_cap;
 };
 
-// One step = 8 consecutive superblocks of a wave's row stream, fetched as 16-B
-// granules from the 16-B boundary below them (+1 granule of slack): Q4_K 73,
-// Q5_K 89, Q6_K 106 granules; two LDS-DMA instructions per step for every type.
-__host__ __device__ constexpr int rows_gran(int type) { return 8 * block_bytes(type) / 16 + 1; }
-__host__ __device__ constexpr int rows_slot(int tmask) {
-    return 16 * ((tmask & 4) ? rows_gran(Q6_K) : (tmask & 2) ? rows_gran(Q5_K) : rows_gran(Q4_K));
+// One step = 16 consecutive superblocks of a wave's row stream (2304 / 2816 / 3360
+// B), fetched as 16-B granules from the 16-B boundary below them (+1 granule of
+// slack for a misaligned Q6_K stream): 145 / 177 / 211 granules = 3 / 3 / 4
+// LDS-DMA instructions. Ring depth per type keeps ~9-10 KB in flight per wave
+// (measured ceiling: 2-3 KB steps, ~96 KB per CU, nt -> 7.1 TB/s).
+constexpr int ROWS_SB = 16;     // superblocks per step (4 lanes each)
+constexpr int Q8L_STRIDE = 304; // LDS/workspace Q8_K block: d @0, qs @16, bsums @272 (16-B aligned)
+__host__ __device__ constexpr int rows_gran(int type) { return block_bytes(type) + 1; }
+__host__ __device__ constexpr int rows_slot(int type) { return 16 * rows_gran(type); }
+__host__ __device__ constexpr int rows_ni(int type) { return (rows_gran(type) + 63) / 64; }
+__host__ __device__ constexpr int rows_depth(int type) { return type == Q4_K ? 4 : 3; }
+__host__ __device__ constexpr int rows_ring_bytes(int type) { return rows_depth(type) * rows_slot(type); }
+__host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
+__host__ __device__ constexpr int rows_ring(int tmask) {
+    return 16 + cmax((tmask & 1) ? rows_ring_bytes(Q4_K) : 0,
+                     cmax((tmask & 2) ? rows_ring_bytes(Q5_K) : 0, (tmask & 4) ? rows_ring_bytes(Q6_K) : 0));
 }
 
-//   act:  raw Q8_K activation (nb*292 B, +16 for a misaligned DMA source)
-//   ring: per wave D slots (+16 B tail slack for the Q6_K realign reads)
+//   act:  Q8_K activation row in the aligned Q8L layout (nb * 304 B)
+//   ring: per wave, the ring of its type (+16 B tail slack for Q6_K realign reads)
 //   recs: per wave bR*nb chain records (16 B), block-major [blk][row]
 //   outs: per wave rpw staged results
 struct RowsLayout {
     int act, ring, ring_stride, recs, recs_stride, outs, outs_stride, total;
 };
-__host__ __device__ inline RowsLayout rows_layout(int nb, int slot, int D, int bR, int rpw) {
+__host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int rpw) {
     RowsLayout L;
     L.act = 0;
-    L.ring = (nb * 292 + 32 + 15) & ~15;  // 16-B granules from the 16-B boundary below the row
-    L.ring_stride = D * slot + 16;
+    L.ring = nb * Q8L_STRIDE;
+    L.ring_stride = rows_ring(tmask);
     L.recs = L.ring + WAVES_PER_WG * L.ring_stride;
     L.recs_stride = bR * nb * 16;
     L.outs = L.recs + WAVES_PER_WG * L.recs_stride;

@@ -260,12 +260,24 @@ __host__ __device__ constexpr int slot_bytes(int tmask) { return 8 * 16 * (tmask
 // s_waitcnt vmcnt(0) before it (seen in the ISA: it drained the whole ring each
 // step). Completion is tracked by hand with counted vmcnt waits instead; the
 // "memory" clobber keeps earlier LDS reads of a recycled slot ahead of the DMA.
-// s_nop: SALU write of M0 -> LDS-DMA needs one wait state.
+// s_nop: SALU write of M0 -> LDS-DMA needs one wait state. M0 is reserved by the
+// compiler (never allocated to values; set right before each instruction that
+// reads it), so clobbering it here is safe; the warning saying so is silenced.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void dma16(const void *src, LDS void *dst) {
     const uint32_t m0 = (uint32_t)(uintptr_t)dst;
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(src)
                  : "memory", "m0");
 }
+// Same, non-temporal (nt): for the once-read weight stream (measured on this part:
+// 6.2 -> 7.1 TB/s chip-wide, profiles/r01_lds_dma_stream_ceiling.txt).
+__device__ __forceinline__ void dma16_nt(const void *src, LDS void *dst) {
+    const uint32_t m0 = (uint32_t)(uintptr_t)dst;
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m0), "v"(src)
+                 : "memory", "m0");
+}
+#pragma clang diagnostic pop
 
 template <int N>
 __device__ __forceinline__ void vm_wait() {

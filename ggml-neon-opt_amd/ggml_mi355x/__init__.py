@@ -212,7 +212,7 @@ def mul_mat(type_, w, K, x, out=None, workspace=None, stream=None):
         out = torch.empty((M, N), dtype=torch.float32, device=x.device)
     ws = int(lib().mi355x_mul_mat_workspace_size(type_, K, N, M))
     if M == 1 and x.data_ptr() % 16:
-        ws = max(ws, K // QK_K * 292)
+        ws = max(ws, K // QK_K * 304)  # Q8L activation blocks (kq_rows)
     if ws and (workspace is None or workspace.numel() < ws):
         workspace = _workspace(ws, x.device)
     _check(lib().mi355x_mul_mat(type_, w.data_ptr(), K, N, w.stride(0), x.data_ptr(), M, x.stride(0) * 4,

@@ -61,7 +61,7 @@ def test_argument_validation_without_device():
     assert L.mi355x_mul_mat(12, 0x1000, 256, 4, 144, 0x2000, 3, 1024, 0x3000, 16, None, 0, None) == -3
     assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 5) == ((5 * 8 * 292 + 255) // 256) * 256
     assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 1) == 0
-    assert L.mi355x_mul_mat_workspace_size(12, 28672, 64, 1) == ((112 * 292 + 255) // 256) * 256
+    assert L.mi355x_mul_mat_workspace_size(12, 28672, 64, 1) == ((112 * 304 + 255) // 256) * 256
     # misaligned weights
     descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1002, 4, 144, 0x3000))
     assert L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None, 0, None) == -1
@@ -70,7 +70,7 @@ def test_argument_validation_without_device():
     assert L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None, 0, None) == -1
     # large K needs the Q8_K workspace
     assert L.mi355x_gemv_fused_workspace_size(2048) == 0
-    assert L.mi355x_gemv_fused_workspace_size(14336) == ((56 * 292 + 255) // 256) * 256
+    assert L.mi355x_gemv_fused_workspace_size(14336) == ((56 * 304 + 255) // 256) * 256
     descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1000, 4, 56 * 144, 0x3000))
     assert L.mi355x_gemv_fused(descs, 1, 0x2000, 14336, None, 0, None) == -3
     # no device here -> the HIP path reports it instead of falling back

@@ -12,10 +12,13 @@ import ggml_mi355x as g  # noqa: E402
 from bench import random_kquant  # noqa: E402
 
 SHAPES = [("tl q", 12, 2048, 2048), ("tl 8rows", 12, 2048, 8), ("tl gate+up", 12, 2048, 11264),
-          ("tl down", 12, 5632, 2048), ("tl out q6", 14, 2048, 32000)]
+          ("tl down", 12, 5632, 2048), ("tl out q6", 14, 2048, 32000), ("l3 up", 12, 4096, 14336),
+          ("70b down", 12, 28672, 8192)]
 
 
-def main():
+def main(impl):
+    g.gemv_impl(impl)
+    tag = "rows " if impl == 0 else "tasks"
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
     gen.manual_seed(3)
@@ -47,10 +50,11 @@ def main():
                         med(rel[:, 1] - rel[:, 0]), med(rel[:, 2] - rel[:, 1]), np.max(rel[:, 2] - rel[:, 1]),
                         rel[:, 3].max()))
         a = np.array(res)[1:].mean(0)
-        print(f"{label:12s} waves={int(a[0]):5d} start_spread={a[1]:5.2f}us | lookup {a[2]:4.2f} issue {a[3]:4.2f} "
+        print(f"{tag} {label:12s} waves={int(a[0]):5d} start_spread={a[1]:5.2f}us | lookup {a[2]:4.2f} issue {a[3]:4.2f} "
               f"wait {a[4]:4.2f} quant {a[5]:4.2f} = prologue {a[6]:4.2f} | loop med/max={a[7]:5.2f}/{a[8]:5.2f} "
               f"end={a[9]:6.2f}us")
 
 
 if __name__ == "__main__":
-    main()
+    for impl in (0, 1):
+        main(impl)
