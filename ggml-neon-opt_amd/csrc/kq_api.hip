@@ -70,7 +70,8 @@ int type_bit(int type) { return type == Q4_K ? 1 : type == Q5_K ? 2 : type == Q6
 
 constexpr size_t kMaxLds = 160 * 1024;   // LDS per CU (one workgroup may use it all)
 constexpr size_t kTargetLds = 80 * 1024; // aim for >= 2 resident workgroups per CU
-constexpr int64_t kFusedQMaxNb = 32;      // in-kernel quantization up to K = 8192
+constexpr int64_t kFusedQMaxNb = 32;      // kq_gemv: in-kernel quantization up to K = 8192
+constexpr int64_t kRowsFusedMaxNb = ROWS_QPASS * 4 * ROWS_WAVES;  // kq_rows: up to K = 36864
 
 uint64_t *g_stamps = nullptr;  // diagnostics (mi355x_diag_stamps)
 int64_t g_stamps_cap = 0;
@@ -323,10 +324,10 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     if (K <= 0 || K % QK != 0) return MI355X_E_INVAL;
     const int64_t nb = K / QK;
     if (nb > 4096) return MI355X_E_UNSUPPORTED;
-    if (fusedq && nb > kFusedQMaxNb) return MI355X_E_UNSUPPORTED;
+    if (fusedq && nb > kRowsFusedMaxNb) return MI355X_E_UNSUPPORTED;
     memset(&a, 0, sizeof(a));
     int tmask = 0;
-    int64_t total_rows = 0;
+    double bytes_total = 0;
     for (int i = 0; i < n_desc; ++i) {
         const int bb = block_bytes(d[i].type);
         if (!bb) return MI355X_E_UNSUPPORTED;
@@ -338,7 +339,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
             if (d[i].row_stride != (size_t)(nb * bb)) return MI355X_E_UNSUPPORTED;
             if (d[i].type != Q6_K && ((uintptr_t)d[i].w & 15u)) return MI355X_E_UNSUPPORTED;
         }
-        total_rows += d[i].n_rows;
+        bytes_total += (double)d[i].n_rows * bb;
         tmask |= type_bit(d[i].type);
     }
     if (tmask != 1 && tmask != 2 && tmask != 4) tmask = 7;
@@ -349,7 +350,6 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     a.nb = (int)nb;
     for (int i = 0; i < n_desc; ++i) {
         a.type[i] = d[i].type;
-        a.n_rows[i] = (int)d[i].n_rows;
         a.w[i] = (const uint8_t *)d[i].w;
         a.y[i] = d[i].y;
     }
@@ -366,37 +366,55 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     }
     a.stamps = g_stamps;
     a.stamps_cap = g_stamps_cap;
-    // rows per chain batch: <= 128 records, batch ends on a step boundary (bR*nb % 16 == 0)
-    int g16 = ROWS_SB;
-    while (nb % g16) g16 >>= 1;
-    const int u = ROWS_SB / g16;
-    int bR_full = (int)(128 / nb) / u * u;
-    if (bR_full < u) bR_full = u;
-    // rows per wave: fill the resident capacity once (no tail round of workgroups)
-    const int res = resident_wgs((const void *)pl.fn, (size_t)rows_layout((int)nb, tmask, bR_full, 64).total);
-    const int64_t cap_waves = (int64_t)num_cus() * res * WAVES_PER_WG;
-    int64_t rpw = (total_rows + cap_waves - 1) / cap_waves;
-    if (rpw < 1) rpw = 1;
-    while (true) {  // the per-matrix partition adds at most one partial wave per matrix
-        int64_t w = 0;
-        for (int i = 0; i < n_desc; ++i) w += (d[i].n_rows + rpw - 1) / rpw;
-        if (w <= cap_waves || rpw >= total_rows) break;
-        ++rpw;
-    }
-    if (rpw > 0x7fffffff / 64) return MI355X_E_UNSUPPORTED;
-    a.rpw = (int)rpw;
-    a.bR = rpw <= bR_full ? (int)rpw : bR_full;
+    // Waves: one workgroup of ROWS_WAVES per CU; each matrix gets waves in
+    // proportion to its bytes (never more waves than rows), rows split evenly.
+    const int64_t cap = (int64_t)num_cus() * ROWS_WAVES;
+    int64_t wv[MI355X_MAX_FUSED] = {0, 0, 0, 0};
     int64_t waves = 0;
     for (int i = 0; i < n_desc; ++i) {
+        if (d[i].n_rows == 0) continue;
+        const double share = (double)d[i].n_rows * block_bytes(d[i].type) / bytes_total;
+        int64_t w = (int64_t)(share * (double)cap);
+        if (w < 1) w = 1;
+        if (w > d[i].n_rows) w = d[i].n_rows;
+        wv[i] = w;
+        waves += w;
+    }
+    while (waves > cap) {  // the max(1, .) floors may overshoot by < n_desc: trim the largest
+        int big = 0;
+        for (int i = 1; i < n_desc; ++i)
+            if (wv[i] > wv[big]) big = i;
+        --wv[big];
+        --waves;
+    }
+    int64_t rpw = 0;
+    waves = 0;
+    for (int i = 0; i < n_desc; ++i) {
         a.wave_prefix[i] = (int)waves;
-        waves += (d[i].n_rows + rpw - 1) / rpw;
+        if (wv[i] > 0) {
+            a.rbase[i] = (int)(d[i].n_rows / wv[i]);
+            a.rrem[i] = (int)(d[i].n_rows % wv[i]);
+            const int64_t r = a.rbase[i] + (a.rrem[i] ? 1 : 0);
+            rpw = r > rpw ? r : rpw;
+        }
+        waves += wv[i];
     }
     for (int i = n_desc; i <= MI355X_MAX_FUSED; ++i) a.wave_prefix[i] = (int)waves;
     a.waves_total = (int)waves;
+    if (rpw > 0x7fffffff / 64) return MI355X_E_UNSUPPORTED;
+    a.rpw = (int)(rpw > 0 ? rpw : 1);
+    // rows per chain batch: ~ROWS_RECS records, batch ends on a step boundary (bR*nb % 16 == 0)
+    int g16 = ROWS_SB;
+    while (nb % g16) g16 >>= 1;
+    const int u = ROWS_SB / g16;
+    int bR_full = (int)(ROWS_RECS / nb) / u * u;
+    if (bR_full < u) bR_full = u;
+    a.bR = a.rpw <= bR_full ? a.rpw : bR_full;
     const RowsLayout L = rows_layout((int)nb, tmask, a.bR, a.rpw);
     if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
     pl.lds = (size_t)L.total;
-    pl.grid = dim3((unsigned)((waves + WAVES_PER_WG - 1) / WAVES_PER_WG), 1, 1);
+    const int64_t grid = waves < num_cus() ? waves : num_cus();
+    pl.grid = dim3((unsigned)(grid > 0 ? grid : 1), 1, 1);
     return MI355X_OK;
 }
 
@@ -407,8 +425,9 @@ std::string rows_name(const RowsPlan &pl) {
 double rows_bytes(const RowsArgs &a, bool fusedq) {
     double w = 0, y = 0;
     for (int i = 0; i < a.n_desc; ++i) {
-        w += (double)a.n_rows[i] * a.nb * block_bytes(a.type[i]);
-        y += (double)a.n_rows[i] * 4.0;
+        const double rows = (double)a.rbase[i] * (a.wave_prefix[i + 1] - a.wave_prefix[i]) + a.rrem[i];
+        w += rows * a.nb * block_bytes(a.type[i]);
+        y += rows * 4.0;
     }
     return w + y + (fusedq ? (double)a.nb * QK * 4.0 : (double)a.nb * Q8L_STRIDE);
 }
@@ -419,10 +438,10 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
     allow_lds((const void *)pl.fn, pl.lds);
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
-        hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), (uint32_t)pl.lds, stream, e0, e1, 0, a);
+        hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(ROWS_WAVES * 64), (uint32_t)pl.lds, stream, e0, e1, 0, a);
         timing_log(rows_name(pl), rows_bytes(a, pl.fusedq), e0, e1);
     } else {
-        hipLaunchKernelGGL(pl.fn, pl.grid, dim3(WG_THREADS), pl.lds, stream, a);
+        hipLaunchKernelGGL(pl.fn, pl.grid, dim3(ROWS_WAVES * 64), pl.lds, stream, a);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
@@ -473,9 +492,10 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
     const size_t need = (size_t)(k / QK) * 292;
     if (rows_enabled()) {
         RowsPlan rp;
-        int rc = plan_rows(d, n, k, fusedq, rp);
+        const bool rows_fq = k / QK <= kRowsFusedMaxNb && ((uintptr_t)x & 15u) == 0;
+        int rc = plan_rows(d, n, k, rows_fq, rp);
         if (rc == MI355X_OK) {
-            if (fusedq) {
+            if (rows_fq) {
                 rp.a.x = x;
                 if (!device_ok()) return MI355X_E_NODEVICE;
                 return launch_rows(rp, stream);

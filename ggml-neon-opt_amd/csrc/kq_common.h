@@ -75,20 +75,28 @@ __host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg
 }
 
 // ---------------------------------------------------------------- row-stream decode GEMV
-// Argument block of kq_rows (M = 1). Waves are partitioned per matrix: matrix d
-// owns global waves [wave_prefix[d], wave_prefix[d+1]); a wave owns `rpw`
-// consecutive rows (the last wave of a matrix fewer).
+// kq_rows (M = 1): one workgroup of ROWS_WAVES waves per CU. Global wave index
+// gw = wave * gridDim.x + blockIdx.x (active waves spread over every CU). Matrix d
+// owns global waves [wave_prefix[d], wave_prefix[d+1]); its j-th wave owns rows
+// [j*rbase[d] + min(j, rrem[d]), ...) — rbase[d] rows, one more for j < rrem[d].
+#ifndef KQ_ROWS_WAVES
+#define KQ_ROWS_WAVES 12
+#endif
+constexpr int ROWS_WAVES = KQ_ROWS_WAVES;
+constexpr int ROWS_QPASS = 3;  // fused-quantization passes of 4*ROWS_WAVES superblocks
+
 struct RowsArgs {
     int n_desc;
     int nb;           // K / 256
-    int rpw;          // rows per wave
+    int rpw;          // max rows per wave (LDS sizing)
     int waves_total;
     int pre0;         // weight steps issued before the activation is quantized
     int bR;           // rows per chain batch (bR*nb % 16 == 0 unless bR >= rpw)
     int diag;         // diagnostics: bit3 stream weights only
     int wave_prefix[MI355X_MAX_FUSED + 1];
+    int rbase[MI355X_MAX_FUSED];
+    int rrem[MI355X_MAX_FUSED];
     int type[MI355X_MAX_FUSED];
-    int n_rows[MI355X_MAX_FUSED];
     const uint8_t *w[MI355X_MAX_FUSED];
     float *y[MI355X_MAX_FUSED];
     const float *x;       // f32 activation (FUSEDQ)
@@ -100,14 +108,18 @@ struct RowsArgs {
 // One step = 16 consecutive superblocks of a wave's row stream (2304 / 2816 / 3360
 // B), fetched as 16-B granules from the 16-B boundary below them (+1 granule of
 // slack for a misaligned Q6_K stream): 145 / 177 / 211 granules = 3 / 3 / 4
-// LDS-DMA instructions. Ring depth per type keeps ~9-10 KB in flight per wave
-// (measured ceiling: 2-3 KB steps, ~96 KB per CU, nt -> 7.1 TB/s).
+// LDS-DMA instructions. Ring depth per type keeps 6.8-8.5 KB in flight per wave,
+// ~80-100 KB per CU (measured ceiling: 2-3 KB steps, ~96 KB per CU, nt -> 7.1 TB/s).
 constexpr int ROWS_SB = 16;     // superblocks per step (4 lanes each)
 constexpr int Q8L_STRIDE = 304; // LDS/workspace Q8_K block: d @0, qs @16, bsums @272 (16-B aligned)
+constexpr int ROWS_RECS = 64;   // chain records per wave per batch (soft cap)
 __host__ __device__ constexpr int rows_gran(int type) { return block_bytes(type) + 1; }
 __host__ __device__ constexpr int rows_slot(int type) { return 16 * rows_gran(type); }
 __host__ __device__ constexpr int rows_ni(int type) { return (rows_gran(type) + 63) / 64; }
-__host__ __device__ constexpr int rows_depth(int type) { return type == Q4_K ? 4 : 3; }
+#ifndef KQ_ROWS_DQ4
+#define KQ_ROWS_DQ4 3
+#endif
+__host__ __device__ constexpr int rows_depth(int type) { return type == Q4_K ? KQ_ROWS_DQ4 : type == Q5_K ? 3 : 2; }
 __host__ __device__ constexpr int rows_ring_bytes(int type) { return rows_depth(type) * rows_slot(type); }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int rows_ring(int tmask) {
@@ -127,11 +139,11 @@ __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int
     L.act = 0;
     L.ring = nb * Q8L_STRIDE;
     L.ring_stride = rows_ring(tmask);
-    L.recs = L.ring + WAVES_PER_WG * L.ring_stride;
+    L.recs = L.ring + ROWS_WAVES * L.ring_stride;
     L.recs_stride = bR * nb * 16;
-    L.outs = L.recs + WAVES_PER_WG * L.recs_stride;
+    L.outs = L.recs + ROWS_WAVES * L.recs_stride;
     L.outs_stride = (rpw * 4 + 15) & ~15;
-    L.total = L.outs + WAVES_PER_WG * L.outs_stride;
+    L.total = L.outs + ROWS_WAVES * L.outs_stride;
     return L;
 }
 

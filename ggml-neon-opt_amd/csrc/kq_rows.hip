@@ -57,18 +57,28 @@ __device__ __forceinline__ void quant16_store(const u32x4 v[4], int l, uint8_t *
         x[4 * k + 2] = __uint_as_float(v[k].z);
         x[4 * k + 3] = __uint_as_float(v[k].w);
     }
-    float m = 0.f;
+    // amax and the sign of the first x with |x| == amax: the largest positive and
+    // the largest negated value (both >= 0, NaN dropped by fmaxf); only a tie
+    // (+amax and -amax both present) needs the first-index scan.
+    float mp = 0.f, mn = 0.f;
 #pragma unroll
-    for (int k = 0; k < 16; ++k) m = fmaxf(m, fabsf(x[k]));  // fmaxf drops NaN
-    int mb = (m == m) ? __float_as_int(m) : 0;
-    mb = row16_reduce(mb, [](int a, int c) { return a > c ? a : c; });
-    m = __int_as_float(mb);
-    uint32_t key = 0xffffffffu;
+    for (int k = 0; k < 16; ++k) {
+        mp = fmaxf(mp, x[k]);
+        mn = fmaxf(mn, -x[k]);
+    }
+    const int mpb = row16_reduce(__float_as_int(mp), [](int a, int c) { return a > c ? a : c; });
+    const int mnb = row16_reduce(__float_as_int(mn), [](int a, int c) { return a > c ? a : c; });
+    const float m = __int_as_float(mpb > mnb ? mpb : mnb);
+    bool neg = mnb > mpb;
+    if (mpb == mnb && mpb != 0) {  // tie: serial `if (ax > amax)` keeps the first index
+        uint32_t key = 0xffffffffu;
 #pragma unroll
-    for (int k = 15; k >= 0; --k)
-        if (fabsf(x[k]) == m) key = 2u * (uint32_t)(16 * l + k) + (x[k] < 0.f ? 1u : 0u);
-    key = (uint32_t)row16_reduce((int)key, [](int a, int c) { return (uint32_t)a < (uint32_t)c ? a : c; });
-    const float maxv = (key & 1u) ? -m : m;
+        for (int k = 15; k >= 0; --k)
+            if (fabsf(x[k]) == m) key = 2u * (uint32_t)(16 * l + k) + (x[k] < 0.f ? 1u : 0u);
+        key = (uint32_t)row16_reduce((int)key, [](int a, int c) { return (uint32_t)a < (uint32_t)c ? a : c; });
+        neg = (key & 1u) != 0;
+    }
+    const float maxv = neg ? -m : m;
     const float iscale = -127.f / maxv;
     u32x4 q;
     q.x = qbyte(iscale, x[0]) | (qbyte(iscale, x[1]) << 8) | (qbyte(iscale, x[2]) << 16) | (qbyte(iscale, x[3]) << 24);
@@ -236,7 +246,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     constexpr int NI = rows_ni(TYPE);
     constexpr int SLOT = rows_slot(TYPE);
     constexpr int D = rows_depth(TYPE);
-    static_assert(D <= 4, "vm_wait_k covers 3 steps in flight");
+    static_assert(D >= 2 && D <= 4, "vm_wait_k covers 3 steps in flight");
     const int nb = a.nb, bR = a.bR;
     const int q = lane >> 2, s = lane & 3;
     uint8_t *const ring = smem + L.ring + wave * L.ring_stride;
@@ -276,13 +286,15 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 
     // ---- prologue: activation loads, pre0 weight steps, quantize, then the rest of the ring
     const int pre0 = T < a.pre0 ? T : a.pre0;  // 0..3
+    uint64_t sx = 0, sq = 0, sf = 0;  // diagnostics: x landed, quantized, first step computed
     if (FUSEDQ) {
-        u32x4 xv[2][4] = {};
-        const int qiters = (nb + 15) >> 4;  // 16 superblocks per workgroup pass
+        constexpr int PASS = 4 * ROWS_WAVES;  // superblocks per workgroup pass
+        u32x4 xv[ROWS_QPASS][4] = {};
+        const int qiters = (nb + PASS - 1) / PASS;
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
+        for (int i = 0; i < ROWS_QPASS; ++i) {
             if (i < qiters) {
-                int b = 16 * i + 4 * wave + (lane >> 4);
+                int b = PASS * i + 4 * wave + (lane >> 4);
                 b = b < nb ? b : nb - 1;
                 const float *xp = a.x + (int64_t)b * QK + 16 * (lane & 15);
 #pragma unroll
@@ -293,25 +305,32 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         vm_wait_k<NI>(pre0);  // the activation loads are older than pre0 weight steps
         // the loads above are invisible to the compiler: pin their registers past the wait
         asm volatile("" : "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[1][0]),
-                     "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]));
+                     "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]), "+v"(xv[2][0]), "+v"(xv[2][1]), "+v"(xv[2][2]),
+                     "+v"(xv[2][3]));
+        if (a.stamps) sx = __builtin_amdgcn_s_memrealtime();
+#pragma unroll 1
+        for (int i = 0; i < qiters; ++i) {  // one copy of the quantizer; pick the pass's registers
+            u32x4 cur[4];
 #pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            if (i < qiters) {
-                const int b = 16 * i + 4 * wave + (lane >> 4);
-                if (b < nb) quant16_store(xv[i], lane & 15, smem + L.act + Q8L_STRIDE * b);
-            }
+            for (int k = 0; k < 4; ++k) cur[k] = i == 0 ? xv[0][k] : i == 1 ? xv[1][k] : xv[2][k];
+            const int b = PASS * i + 4 * wave + (lane >> 4);
+            if (b < nb) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * b);
+        }
+        if (a.stamps) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            sq = __builtin_amdgcn_s_memrealtime();
         }
     } else {
         const int ng = nb * (Q8L_STRIDE / 16);
-        for (int j = wave; 64 * j < ng; j += WAVES_PER_WG) {
+        for (int j = wave; 64 * j < ng; j += ROWS_WAVES) {
             const int k = 64 * j + lane;
             if (k < ng) dma16(a.xq + 16 * k, (LDS void *)(smem + L.act + 1024 * j));
         }
         for (int j = 0; j < pre0; ++j) issue();
         vm_wait_k<NI>(pre0);
     }
-    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // Q8_K row complete (no vmcnt drain)
     while (it_ < D && it_ < T) issue();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // Q8_K row complete (no vmcnt drain)
     const uint64_t st1 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
 
     // ---- main loop
@@ -364,6 +383,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             }
         }
         if (it_ < T) issue();
+        if (a.stamps && t == 0) sf = __builtin_amdgcn_s_memrealtime();
         if (ROWS_SB * (t + 1) >= bend) {  // batch complete: replay its rows' chains, lane r <-> row r
             wave_lds_fence();
             const int nr = bR < ww.nrows - brow ? bR : ww.nrows - brow;
@@ -390,38 +410,38 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             if (k + lane < ww.nrows) y[k + lane] = outs[k + lane];
     }
     if (a.stamps) {
-        const int64_t o = ((int64_t)blockIdx.x * WAVES_PER_WG + wave) * 8;
+        const int64_t o = ((int64_t)blockIdx.x * ROWS_WAVES + wave) * 8;
         if (lane == 0 && o + 7 < a.stamps_cap) {
             a.stamps[o] = st0;
             a.stamps[o + 1] = st1;
             a.stamps[o + 2] = st2;
             a.stamps[o + 3] = __builtin_amdgcn_s_memrealtime();
-            a.stamps[o + 4] = st0;
-            a.stamps[o + 5] = st0;
-            a.stamps[o + 6] = st1;
+            a.stamps[o + 4] = sx;
+            a.stamps[o + 5] = sq;
+            a.stamps[o + 6] = sf;
         }
     }
 }
 
 template <int TMASK, bool FUSEDQ>
-__global__ void __launch_bounds__(WG_THREADS) kq_rows(const RowsArgs a) {
+__global__ void __launch_bounds__(ROWS_WAVES * 64) kq_rows(const RowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const RowsLayout L = rows_layout(a.nb, TMASK, a.bR, a.rpw);
 
-    const int gw = blockIdx.x * WAVES_PER_WG + wave;
+    const int gw = wave * gridDim.x + blockIdx.x;  // active waves spread over every CU
     WaveWork ww;
     int m = 0;
 #pragma unroll
     for (int i = 1; i < MI355X_MAX_FUSED; ++i)
         if (i < a.n_desc && gw >= a.wave_prefix[i]) m = i;
     ww.m = m;
-    ww.r0 = (gw - a.wave_prefix[m]) * a.rpw;
-    const int left = a.n_rows[m] - ww.r0;
-    ww.nrows = gw < a.waves_total ? (left < a.rpw ? left : a.rpw) : 0;
-    if (ww.nrows < 0) ww.nrows = 0;
+    const int j = gw - a.wave_prefix[m];
+    const int base = a.rbase[m], rem = a.rrem[m];
+    ww.r0 = j * base + (j < rem ? j : rem);
+    ww.nrows = gw < a.waves_total ? base + (j < rem ? 1 : 0) : 0;
 
     if (TMASK == 1) {
         rows_body<Q4_K, FUSEDQ>(a, ww, smem, L, wave, lane, st0);

@@ -72,7 +72,12 @@ def test_argument_validation_without_device():
     assert L.mi355x_gemv_fused_workspace_size(2048) == 0
     assert L.mi355x_gemv_fused_workspace_size(14336) == ((56 * 304 + 255) // 256) * 256
     descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1000, 4, 56 * 144, 0x3000))
-    assert L.mi355x_gemv_fused(descs, 1, 0x2000, 14336, None, 0, None) == -3
+    prev = L.mi355x_gemv_impl(1)  # kq_gemv quantizes K > 8192 into the workspace
+    try:
+        assert L.mi355x_gemv_fused(descs, 1, 0x2000, 14336, None, 0, None) == -3
+    finally:
+        L.mi355x_gemv_impl(prev)
+    assert L.mi355x_gemv_impl(7) == -1
     # no device here -> the HIP path reports it instead of falling back
     descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1000, 4, 144, 0x3000))
     rc = L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None, 0, None)

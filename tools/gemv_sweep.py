@@ -56,6 +56,11 @@ if __name__ == "__main__":
     modes = sys.argv[1:] or ["auto", "prologue"]
     for mode in modes:
         env = dict(os.environ)
+        for kv in mode.split(":"):  # generic overrides: "pre0=0", "lib=path", combined with ':'
+            if kv.startswith("pre0="):
+                env["MI355X_GEMV_PRE0"] = kv[5:]
+            elif kv.startswith("lib="):
+                env["MI355X_LIB"] = os.path.join(ROOT, kv[4:])
         if mode == "prologue":
             env["MI355X_GEMV_DIAG"] = "1"
         elif mode == "empty":
