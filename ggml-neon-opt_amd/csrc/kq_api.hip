@@ -375,8 +375,11 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
         if (d[i].n_rows == 0) continue;
         const double share = (double)d[i].n_rows * block_bytes(d[i].type) / bytes_total;
         int64_t w = (int64_t)(share * (double)cap);
+        // at least one full 16-superblock step per wave (short rows: several rows per wave)
+        const int64_t min_rows = (ROWS_SB + nb - 1) / nb;
+        const int64_t wmax = (d[i].n_rows + min_rows - 1) / min_rows;
+        if (w > wmax) w = wmax;
         if (w < 1) w = 1;
-        if (w > d[i].n_rows) w = d[i].n_rows;
         wv[i] = w;
         waves += w;
     }

@@ -285,7 +285,8 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     };
 
     // ---- prologue: activation loads, pre0 weight steps, quantize, then the rest of the ring
-    const int pre0 = T < a.pre0 ? T : a.pre0;  // 0..3
+    const int pre_cap = a.pre0 < D ? a.pre0 : D;  // never more than the ring holds
+    const int pre0 = T < pre_cap ? T : pre_cap;     // 0..3
     uint64_t sx = 0, sq = 0, sf = 0;  // diagnostics: x landed, quantized, first step computed
     if (FUSEDQ) {
         constexpr int PASS = 4 * ROWS_WAVES;  // superblocks per workgroup pass
@@ -293,7 +294,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         const int qiters = (nb + PASS - 1) / PASS;
 #pragma unroll
         for (int i = 0; i < ROWS_QPASS; ++i) {
-            if (i < qiters) {
+            if (i < qiters && PASS * i + 4 * wave < nb) {  // waves past the row load nothing
                 int b = PASS * i + 4 * wave + (lane >> 4);
                 b = b < nb ? b : nb - 1;
                 const float *xp = a.x + (int64_t)b * QK + 16 * (lane & 15);

@@ -112,3 +112,50 @@ def test_product_has_no_oracle_dependency():
                 assert "kq_oracle" not in txt and "oracle/" not in txt, fn
     out = subprocess.run(["ldd", os.path.join(pkg, "lib", "libggml_mi355x.so")], capture_output=True, text=True)
     assert "oracle" not in out.stdout
+
+
+def _gfx950_code_objects(path):
+    """gfx950 ELF code objects of every clang offload bundle in the shared library."""
+    import struct
+    data = open(path, "rb").read()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    objs, i = [], data.find(magic)
+    while i >= 0:
+        n = struct.unpack_from("<Q", data, i + 24)[0]
+        off = i + 32
+        for _ in range(n):
+            eo, es, tl = struct.unpack_from("<QQQ", data, off)
+            off += 24
+            triple = data[off:off + tl].decode(errors="replace")
+            off += tl
+            if "gfx950" in triple and es:
+                objs.append(data[i + eo:i + eo + es])
+        i = data.find(magic, i + 1)
+    return objs
+
+
+def test_kernels_do_not_spill_to_scratch(tmp_path):
+    """A scratch spill in a GEMV costs a vmcnt(0) drain of the weight ring per use
+    (seen once: -30 % tok/s). Every kernel must have private_segment_fixed_size 0."""
+    import re
+    import shutil
+    import subprocess
+    import ggml_mi355x as g
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not os.path.exists(readelf):
+        readelf = shutil.which("llvm-readelf")
+    assert readelf, "llvm-readelf not found"
+    objs = _gfx950_code_objects(g.LIB_PATH)
+    assert objs, "no gfx950 code object in the library"
+    kernels = 0
+    for k, obj in enumerate(objs):
+        p = tmp_path / f"co{k}.o"
+        p.write_bytes(obj)
+        notes = subprocess.run([readelf, "--notes", str(p)], capture_output=True, text=True, check=True).stdout
+        names = re.findall(r"\.name:\s+(\S+)", notes)
+        sizes = [int(v) for v in re.findall(r"\.private_segment_fixed_size:\s+(\d+)", notes)]
+        assert len(names) == len(sizes)
+        spilled = [n for n, sz in zip(names, sizes) if sz]
+        assert not spilled, f"kernels using scratch: {spilled}"
+        kernels += len(names)
+    assert kernels >= 20
