@@ -231,7 +231,8 @@ def main():
             import torch.distributed as dist
             dist.barrier()
 
-    if args.mode == "rowsplit" and world > 1:
+    use_backend = args.mode != "rowsplit"
+    if not use_backend:  # world 1 runs the same path with one shard (exercises StageGather)
         from ggml_mi355x.rowsplit import RowSplitChain
         runner = RowSplitChain(args.model, dev, rank, world, make_chain=Chain)
         chain = runner.chain
@@ -251,7 +252,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if args.mode != "rowsplit" or world == 1:
+    if use_backend:
         be.synchronize()
     barrier()
     torch.cuda.synchronize()
@@ -262,7 +263,7 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
-    if args.mode != "rowsplit" or world == 1:
+    if use_backend:
         be.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -281,7 +282,7 @@ def main():
         # roofline of the dominant kernel, from per-launch kernel timestamps
         roof = None
         per = {}
-        if args.mode != "rowsplit" or world == 1:
+        if use_backend:
             per = timed_kernel_stats(be, chain, tokens=4)
             dom = max(per, key=lambda k: per[k]["ms"])
             d = per[dom]
@@ -319,7 +320,7 @@ def main():
                        "weights_MB_per_token": round(wbytes / 1e6, 1),
                        "launches_per_token": chain.launches(),
                        "parallelism": (f"replicas x{world}" if args.mode == "replicas" else f"rowsplit{world}"),
-                       "hipgraph": not args.no_graph},
+                       "hipgraph": use_backend and not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
             "effective_GBps": round(value * chain.bytes_per_token / 1e9 / (world if args.mode == "replicas" else 1), 1),
             "roofline": roof,

@@ -23,6 +23,8 @@ __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, in
 template <int TMASK, bool FUSEDQ>
 __global__ void kq_rows(const RowsArgs a);
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
+template <int TYPE>
+__global__ void kq_mmq(const MmqArgs a);
 
 namespace {
 
@@ -450,21 +452,64 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
     return e == hipSuccess ? MI355X_OK : (int)e;
 }
 
-int launch_quantize_q8L(const float *x, int64_t k, void *y, hipStream_t stream) {
+int launch_quantize_q8L(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
+                        hipStream_t stream) {
     const int64_t nb = k / QK;
-    if (nb == 0) return MI355X_OK;
-    const int64_t wgs = (nb + 15) / 16;
+    const int64_t nblocks = nb * nrows;
+    if (nblocks == 0) return MI355X_OK;
+    const int64_t wgs = (nblocks + 15) / 16;
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
-        hipExtLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, e0, e1, 0, x, k,
-                              (uint8_t *)y, (int)nb, nb);
-        timing_log("kq::kq_quantize_q8L", (double)nb * (QK * 4.0 + Q8L_STRIDE), e0, e1);
+        hipExtLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, e0, e1, 0, x,
+                              x_stride_floats, (uint8_t *)y, (int)nb, nblocks);
+        timing_log("kq::kq_quantize_q8L", (double)nblocks * (QK * 4.0 + Q8L_STRIDE), e0, e1);
     } else {
-        hipLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, x, k, (uint8_t *)y,
-                           (int)nb, nb);
+        hipLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, x, x_stride_floats,
+                           (uint8_t *)y, (int)nb, nblocks);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+// ------------------------------------------------------------ batched MFMA path
+constexpr int64_t kMmqMinCols = 16;  // below this the NCOL GEMV streams the weights fewer times
+
+int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
+               float *y, int64_t y_col_stride, hipStream_t stream) {
+    MmqArgs a;
+    a.w = (const uint8_t *)w;
+    a.row_stride = (int64_t)row_stride;
+    a.n_rows = (int)N;
+    a.xq = xq;
+    a.nb = (int)(K / QK);
+    a.xq_col_stride = (int64_t)a.nb * Q8L_STRIDE;
+    a.m_cols = (int)M;
+    a.y = y;
+    a.y_col_stride = y_col_stride;
+    const void *fn = type == Q5_K ? (const void *)kq_mmq<Q5_K> : (const void *)kq_mmq<Q4_K>;
+    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * block_bytes(type));
+    allow_lds(fn, lds);
+    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64), 1);
+    hipEvent_t e0, e1;
+    const bool timed = timing_slot(stream, e0, e1);
+    void *args[] = {&a};
+    hipError_t e;
+    if (timed) {
+        e = hipExtLaunchKernel(fn, grid, dim3(256), args, lds, stream, e0, e1, 0);
+        timing_log(std::string("kq::kq_mmq<") + (type == Q5_K ? "13" : "12") + ">",
+                   (double)N * a.nb * block_bytes(type) + (double)M * a.nb * Q8L_STRIDE + (double)M * N * 4.0, e0, e1);
+    } else {
+        e = hipLaunchKernel(fn, grid, dim3(256), args, lds, stream);
+    }
+    if (e != hipSuccess) return (int)e;
+    e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+bool mmq_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M) {
+    if (!rows_enabled() || M < kMmqMinCols || N <= 0) return false;
+    if (type != Q4_K && type != Q5_K) return false;
+    return ((uintptr_t)w & 15u) == 0 && (row_stride & 15u) == 0 && N < (1ll << 31) && M < (1ll << 31);
 }
 
 int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
@@ -506,7 +551,7 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
             const size_t need_l = (size_t)(k / QK) * Q8L_STRIDE;
             if (!ws || ws_size < need_l || ((uintptr_t)ws & 15u)) return MI355X_E_WORKSPACE;
             if (!device_ok()) return MI355X_E_NODEVICE;
-            rc = launch_quantize_q8L(x, k, ws, stream);
+            rc = launch_quantize_q8L(x, k, ws, k, 1, stream);
             if (rc) return rc;
             rp.a.xq = (const uint8_t *)ws;
             return launch_rows(rp, stream);
@@ -574,7 +619,7 @@ size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, 
     (void)ne01;
     if (!block_bytes(src0_type) || ne00 <= 0 || ne00 % QK || ne11 < 0) return 0;
     if (ne11 == 0 || (ne11 == 1 && ne00 / QK <= kFusedQMaxNb)) return 0;
-    const size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * (ne11 == 1 ? Q8L_STRIDE : 292);
+    const size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * Q8L_STRIDE;  // >= raw 292-B blocks
     return (bytes + 255) & ~(size_t)255;
 }
 
@@ -619,6 +664,13 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     }
     size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
+    if (mmq_applies(src0_type, src0, ne01, nb01, ne11) && ((uintptr_t)workspace & 15u) == 0) {
+        if (!device_ok()) return MI355X_E_NODEVICE;
+        int rc = launch_quantize_q8L(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream);
+        if (rc) return rc;
+        return launch_mmq(src0_type, src0, ne00, ne01, nb01, (const uint8_t *)workspace, ne11, dst,
+                          (int64_t)(nb1 / 4), (hipStream_t)stream);
+    }
     if (!device_ok()) return MI355X_E_NODEVICE;
     int rc = launch_quantize(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream);
     if (rc) return rc;

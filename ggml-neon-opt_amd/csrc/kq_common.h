@@ -147,4 +147,18 @@ __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int
     return L;
 }
 
+// ---------------------------------------------------------------- batched (prefill) MFMA GEMM
+// kq_mmq (M > 1): 64 x 64 output tiles, Q8L activations in a workspace.
+struct MmqArgs {
+    const uint8_t *w;        // weight rows (16-B aligned, row_stride % 16 == 0)
+    int64_t row_stride;      // bytes
+    int n_rows;
+    const uint8_t *xq;       // Q8L activation columns
+    int64_t xq_col_stride;   // bytes (nb * 304)
+    int m_cols;
+    float *y;                // dst column j at y + j * y_col_stride
+    int64_t y_col_stride;    // floats
+    int nb;
+};
+
 }  // namespace kq

@@ -1,0 +1,170 @@
+// kq_mmq.hip — batched (prefill) K-quant x Q8_K matmul on MFMA, bit-exact.
+//
+// Replaces, for ne11 = M > 1 activation columns, the per-(row, column) vec_dot
+// calls of ggml_compute_forward_mul_mat_one_chunk (ggml-cpu.c:1194,
+// README.md:136) with int8 matrix cores while keeping the reference's numerics:
+//  * per 32-element sub-block j, v_mfma_i32_32x32x32_i8 gives the exact int32
+//    dot of 32 weight rows x 32 activation columns (K = 32 = one Q4_K sub-block);
+//    sumi += sc_j(row) * dot_j, exact int32 (README.md:754-771);
+//  * summins = sum_j mn_j(row) * (bsums[2j] + bsums[2j+1]) by f32 MFMA 32x32x2:
+//    integers below 2^24, so exact (README.md:741-744);
+//  * the fp32 chain per output element runs superblock by superblock in order,
+//    sumf = fmaf(-(float)summins, dmin, sumf); sumf = fmaf((float)sumi, d, sumf)
+//    (fmsub/fmadd, README.md:551/:614) -- the same ops as the GEMV kernels, so
+//    the result equals the oracle's mul_mat (and ggml's vec_dot loop) bit for bit.
+// Tiles: a workgroup of 4 waves owns 64 activation columns x 64 weight rows (2x2
+// waves of 32x32); each superblock's Q8L activation blocks (64 x 304 B) and weight
+// blocks (64 x 144/176 B) are double-buffered in LDS by LDS-DMA, a fixed number of
+// DMA instructions per wave and superblock so the wait is a constant vmcnt.
+// MFMA operand maps (verified with exact integer data, tools/mfma_layout_check.hip):
+//   i8 32x32x32: lane l (r = l&31, h = l>>5) holds A[r][16h+j], B[16h+j][r], j<16;
+//   f32 32x32x2: A[r][h], B[h][r]; C/D: col = r, row = (reg&3) + 8(reg>>2) + 4h.
+#include "kq_device.h"
+
+namespace kq {
+
+typedef int i32x4m __attribute__((ext_vector_type(4)));
+typedef int i32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int MMQ_TILE = 64;                 // columns x rows per workgroup
+constexpr int MMQ_A_BYTES = MMQ_TILE * Q8L_STRIDE;  // 19456 B per superblock
+constexpr int MMQ_A_INSTR = MMQ_A_BYTES / 1024;     // 19 DMA instructions (exact)
+
+__host__ __device__ constexpr int mmq_b_instr(int type) { return MMQ_TILE * block_bytes(type) / 1024; }  // 9 / 11
+__host__ __device__ constexpr int mmq_nw(int type) { return (MMQ_A_INSTR + mmq_b_instr(type) + 3) / 4; }
+__host__ __device__ constexpr int mmq_buf(int type) { return MMQ_A_BYTES + MMQ_TILE * block_bytes(type); }
+
+template <int TYPE>
+__global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
+    constexpr int BSZ = block_bytes(TYPE);
+    constexpr int NB_I = mmq_b_instr(TYPE);
+    constexpr int NW = mmq_nw(TYPE);
+    constexpr int BUF = mmq_buf(TYPE);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const int r = lane & 31, h = lane >> 5;
+    const int col0 = blockIdx.x * MMQ_TILE, row0 = blockIdx.y * MMQ_TILE;
+    const int nb = a.nb;
+
+    // ---- DMA plan: the superblock's 19 activation + NB_I weight instructions, NW per wave
+    auto issue = [&](int b) {
+        uint8_t *buf = smem + (b & 1) * BUF;
+#pragma unroll
+        for (int s = 0; s < NW; ++s) {
+            int t = wave + 4 * s;
+            if (t >= MMQ_A_INSTR + NB_I) t = MMQ_A_INSTR + NB_I - 1;  // pad: repeat the last one
+            const int g = 64 * (t < MMQ_A_INSTR ? t : t - MMQ_A_INSTR) + lane;  // granule in its tile
+            const uint8_t *src;
+            if (t < MMQ_A_INSTR) {
+                int c = g / (Q8L_STRIDE / 16);
+                const int piece = g - c * (Q8L_STRIDE / 16);
+                c = col0 + c < a.m_cols ? col0 + c : a.m_cols - 1;
+                src = a.xq + (int64_t)c * a.xq_col_stride + (int64_t)b * Q8L_STRIDE + 16 * piece;
+                dma16(src, (LDS void *)(buf + 1024 * t));
+            } else {
+                int rw = g / (BSZ / 16);
+                const int piece = g - rw * (BSZ / 16);
+                rw = row0 + rw < a.n_rows ? row0 + rw : a.n_rows - 1;
+                src = a.w + (int64_t)rw * a.row_stride + (int64_t)b * BSZ + 16 * piece;
+                dma16(src, (LDS void *)(buf + MMQ_A_BYTES + 1024 * (t - MMQ_A_INSTR)));
+            }
+        }
+    };
+
+    f32x16 sumf;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sumf[i] = 0.f;
+
+    issue(0);
+#pragma unroll 1
+    for (int b = 0; b < nb; ++b) {
+        if (b + 1 < nb) {
+            issue(b + 1);
+            vm_wait<NW>();  // superblock b's DMAs (older than b+1's NW) have landed
+        } else {
+            vm_wait<0>();
+        }
+        asm volatile("s_barrier" ::: "memory");  // every wave's part of superblock b
+        const uint8_t *buf = smem + (b & 1) * BUF;
+        const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;          // this lane's activation column
+        const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;   // this lane's weight row
+        const u32x4 hdr = *(const u32x4 *)Bt;
+        // 6-bit scales / mins of the lane's row (get_scale_min_k4, README.md:732-739)
+        const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
+        const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
+        const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
+        const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
+        i32x16 sumi;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sumi[i] = 0;
+        u32x4 qh = {0u, 0u, 0u, 0u};
+        if (TYPE == Q5_K) qh = *(const u32x4 *)(Bt + 16 + 16 * h);
+#pragma unroll
+        for (int jp = 0; jp < 4; ++jp) {
+            const u32x4 qv = *(const u32x4 *)(Bt + (TYPE == Q5_K ? 48 : 16) + 32 * jp + 16 * h);
+            u32x4 lo = qv & 0x0f0f0f0fu, hi = (qv >> 4) & 0x0f0f0f0fu;
+            if (TYPE == Q5_K) {
+                lo = lo | (((qh >> (uint32_t)(2 * jp)) & 0x01010101u) << 4);
+                hi = hi | (((qh >> (uint32_t)(2 * jp + 1)) & 0x01010101u) << 4);
+            }
+            const u32x4 alo = *(const u32x4 *)(At + 16 + 64 * jp + 16 * h);
+            const u32x4 ahi = *(const u32x4 *)(At + 48 + 64 * jp + 16 * h);
+            const uint32_t sw = jp < 2 ? s03 : s47;
+            const int sc_lo = (int)((sw >> (16u * (uint32_t)(jp & 1))) & 0xffu);
+            const int sc_hi = (int)((sw >> (16u * (uint32_t)(jp & 1) + 8u)) & 0xffu);
+            const i32x16 zero = {};
+            i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, zero, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sumi[i] += sc_lo * c[i];
+            c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&hi, zero, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sumi[i] += sc_hi * c[i];
+        }
+        // summins by f32 MFMA: A[m][k] = bsums[2k] + bsums[2k+1] (k = sub-block), B[k][n] = mn_k
+        f32x16 mins;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) mins[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+            const int k = 2 * s + h;
+            const uint32_t bs2 = *(const uint32_t *)(At + 272 + 4 * k);
+            const float av = (float)((int)(int16_t)(bs2 & 0xffffu) + (int)(int16_t)(bs2 >> 16));
+            const uint32_t mw = k < 4 ? m03 : m47;
+            const float bv = (float)((mw >> (8u * (uint32_t)(k & 3))) & 0xffu);
+            mins = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, mins, 0, 0, 0);
+        }
+        // the reference's fp32 update per element, superblock order
+        const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16);
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
+            if (TYPE == Q5_K) {
+                const float t = fmaf(yd * xd, (float)sumi[i], -((yd * xdm) * mins[i]));
+                sumf[i] = sumf[i] + t;
+            } else {
+                sumf[i] = fmaf(-mins[i], yd * xdm, sumf[i]);
+                sumf[i] = fmaf((float)sumi[i], yd * xd, sumf[i]);
+            }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer b&1 free for b+2
+    }
+
+    // ---- store: lane's weight row n, 16 activation columns
+    const int n = row0 + 32 * wn + r;
+    if (n < a.n_rows) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int m = col0 + 32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h;
+            if (m < a.m_cols) a.y[(int64_t)m * a.y_col_stride + n] = sumf[i];
+        }
+    }
+}
+
+template __global__ void kq_mmq<Q4_K>(const MmqArgs a);
+template __global__ void kq_mmq<Q5_K>(const MmqArgs a);
+
+}  // namespace kq

@@ -59,7 +59,7 @@ def test_argument_validation_without_device():
     assert L.mi355x_mul_mat(12, 0x1000, 256, 4, 144, 0x2000, 0, 1024, 0x3000, 16, None, 0, None) == 0
     # M > 1 needs a workspace
     assert L.mi355x_mul_mat(12, 0x1000, 256, 4, 144, 0x2000, 3, 1024, 0x3000, 16, None, 0, None) == -3
-    assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 5) == ((5 * 8 * 292 + 255) // 256) * 256
+    assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 5) == ((5 * 8 * 304 + 255) // 256) * 256
     assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 1) == 0
     assert L.mi355x_mul_mat_workspace_size(12, 28672, 64, 1) == ((112 * 304 + 255) // 256) * 256
     # misaligned weights

@@ -288,3 +288,36 @@ def test_fused_ragged_partition(dev, oracle, npo, impl):
     for (ty, _), w, y in zip(specs, ws, ys):
         ref = oracle.mul_mat(ty, w, x[None])[0]
         assert bits_equal(y.cpu().numpy(), ref), first_mismatch(y.cpu().numpy(), ref)
+
+
+# ---------------------------------------------------------------- batched (prefill) MFMA path
+@pytest.mark.parametrize("type_", [12, 13])
+@pytest.mark.parametrize("K,N,M", [(256, 64, 16), (2048, 100, 33), (4096, 130, 64), (5632, 77, 100),
+                                   (768, 5, 70), (2048, 64, 512)])
+def test_prefill_mfma_bit_exact(dev, oracle, npo, type_, K, N, M):
+    """M >= 16 columns go through kq_mmq (int8 MFMA per 32-element sub-block, f32 MFMA
+    for the mins, the reference's fp32 chain per element): identical to ggml's
+    per-(row, column) vec_dot loop."""
+    import ggml_mi355x as g
+    rng = np.random.default_rng(K + 7 * N + 13 * M + type_)
+    w = npo.random_blocks(rng, type_, N, K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    x[1, :256] = 0.0  # an all-zero activation block (d = 0)
+    got = g.mul_mat(type_, t(w, dev), K, t(x, dev)).cpu().numpy()
+    ref = oracle.mul_mat(type_, w, x)
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
+def test_prefill_full_size_subset(dev, oracle, npo):
+    """Llama-3-8B ffn_up at pp512: every output on the GPU, a column x row subset re-computed."""
+    import ggml_mi355x as g
+    K, N, M = 4096, 14336, 512
+    rng = np.random.default_rng(5)
+    w = npo.random_blocks(rng, 12, N, K)
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    got = g.mul_mat(12, t(w, dev), K, t(x, dev)).cpu().numpy()
+    assert got.shape == (M, N) and np.isfinite(got).all()
+    rows = np.unique(np.concatenate([rng.integers(0, N, 40), [0, N - 1]]))
+    cols = np.unique(np.concatenate([rng.integers(0, M, 24), [0, M - 1]]))
+    ref = oracle.mul_mat(12, w[rows], x[cols])
+    assert bits_equal(got[np.ix_(cols, rows)], ref)
