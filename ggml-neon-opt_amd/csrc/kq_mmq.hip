@@ -3,9 +3,12 @@
 // Replaces, for ne11 = M > 1 activation columns, the per-(row, column) vec_dot
 // calls of ggml_compute_forward_mul_mat_one_chunk (ggml-cpu.c:1194,
 // README.md:136) with int8 matrix cores while keeping the reference's numerics:
-//  * per 32-element sub-block j, v_mfma_i32_32x32x32_i8 gives the exact int32
-//    dot of 32 weight rows x 32 activation columns (K = 32 = one Q4_K sub-block);
-//    sumi += sc_j(row) * dot_j, exact int32 (README.md:754-771);
+//  * per 32-element sub-block j, v_mfma_i32_32x32x32_i8 gives exact int32 dots of
+//    32 weight rows x 32 activation columns (K = 32 = one Q4_K sub-block). Q4_K:
+//    the 6-bit scale is split into 3-bit halves folded into the weight operand
+//    (nibble*half <= 105 fits int8), so sumi = 8*S8 + S1 accumulates across all
+//    sub-blocks inside the matrix core; Q5_K: sumi += sc_j(row) * dot_j on VALU.
+//    Exact int32 either way (README.md:754-771);
 //  * summins = sum_j mn_j(row) * (bsums[2j] + bsums[2j+1]) by f32 MFMA 32x32x2:
 //    integers below 2^24, so exact (README.md:741-744);
 //  * the fp32 chain per output element runs superblock by superblock in order,
@@ -26,6 +29,18 @@ namespace kq {
 typedef int i32x4m __attribute__((ext_vector_type(4)));
 typedef int i32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef uint16_t u16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ u16x2 as_u16x2(uint32_t v) {
+    u16x2 r;
+    __builtin_memcpy(&r, &v, 4);
+    return r;
+}
+__device__ __forceinline__ uint32_t as_u32(u16x2 v) {
+    uint32_t r;
+    __builtin_memcpy(&r, &v, 4);
+    return r;
+}
 
 constexpr int MMQ_TILE = 64;                 // columns x rows per workgroup
 constexpr int MMQ_A_BYTES = MMQ_TILE * Q8L_STRIDE;  // 19456 B per superblock
@@ -97,7 +112,7 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
         const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
         const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
         const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
-        i32x16 sumi;
+        i32x16 sumi, s8 = {}, s1 = {};  // Q4_K: sumi = 8*s8 + s1 (scale split into 3-bit halves)
 #pragma unroll
         for (int i = 0; i < 16; ++i) sumi[i] = 0;
         u32x4 qh = {0u, 0u, 0u, 0u};
@@ -115,13 +130,40 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
             const uint32_t sw = jp < 2 ? s03 : s47;
             const int sc_lo = (int)((sw >> (16u * (uint32_t)(jp & 1))) & 0xffu);
             const int sc_hi = (int)((sw >> (16u * (uint32_t)(jp & 1) + 8u)) & 0xffu);
-            const i32x16 zero = {};
-            i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, zero, 0, 0, 0);
+            if (TYPE == Q4_K) {
+                // sc = 8*sh + sl (3-bit halves): nibble*sh and nibble*sl <= 105 stay int8, and a
+                // packed 16-bit multiply scales two bytes per half without carries, so the
+                // per-sub-block scale rides in the MFMA operand and both sums accumulate
+                // across sub-blocks in the matrix core (exact int32).
+                const u16x2 lh = {(uint16_t)(sc_lo >> 3), (uint16_t)(sc_lo >> 3)};
+                const u16x2 ll = {(uint16_t)(sc_lo & 7), (uint16_t)(sc_lo & 7)};
+                const u16x2 hh = {(uint16_t)(sc_hi >> 3), (uint16_t)(sc_hi >> 3)};
+                const u16x2 hl = {(uint16_t)(sc_hi & 7), (uint16_t)(sc_hi & 7)};
+                u32x4 b8lo, b1lo, b8hi, b1hi;
 #pragma unroll
-            for (int i = 0; i < 16; ++i) sumi[i] += sc_lo * c[i];
-            c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&hi, zero, 0, 0, 0);
+                for (int k = 0; k < 4; ++k) {
+                    b8lo[k] = as_u32(as_u16x2(lo[k]) * lh);
+                    b1lo[k] = as_u32(as_u16x2(lo[k]) * ll);
+                    b8hi[k] = as_u32(as_u16x2(hi[k]) * hh);
+                    b1hi[k] = as_u32(as_u16x2(hi[k]) * hl);
+                }
+                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b8lo, s8, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b1lo, s1, 0, 0, 0);
+                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b8hi, s8, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b1hi, s1, 0, 0, 0);
+            } else {  // Q5_K: 5-bit quants x 6-bit scale do not split into int8 halves
+                const i32x16 zero = {};
+                i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, zero, 0, 0, 0);
 #pragma unroll
-            for (int i = 0; i < 16; ++i) sumi[i] += sc_hi * c[i];
+                for (int i = 0; i < 16; ++i) sumi[i] += sc_lo * c[i];
+                c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&hi, zero, 0, 0, 0);
+#pragma unroll
+                for (int i = 0; i < 16; ++i) sumi[i] += sc_hi * c[i];
+            }
+        }
+        if (TYPE == Q4_K) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sumi[i] = 8 * s8[i] + s1[i];
         }
         // summins by f32 MFMA: A[m][k] = bsums[2k] + bsums[2k+1] (k = sub-block), B[k][n] = mn_k
         f32x16 mins;
