@@ -173,6 +173,43 @@ def large_gemv(dev, reps=20):
     return out
 
 
+def prefill_chain(chain, dev, M=512, reps=3):
+    """pp512-style prefill of the same weights: every matrix of the chain times an
+    M-column activation block (ne11 = M: Q8_K quantization + the int8-MFMA kq_mmq
+    GEMM, bit-exact with the per-column vec_dot chain). Eager launches, one CUDA
+    event pair around the whole chain; non-matmul ops excluded as in the tg chain."""
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(11)
+    xs, ys = {}, {}
+    for stage in chain.stages:
+        for _, _, K, N in stage:
+            if K not in xs:
+                xs[K] = torch.randn(M, K, device=dev, generator=gen)
+            if N not in ys:
+                ys[N] = torch.empty(M, N, device=dev)
+    ws_need = max(g.lib().mi355x_mul_mat_workspace_size(12, K, 1, M) for K in xs)
+    ws = torch.empty(ws_need, dtype=torch.uint8, device=dev)
+
+    def run():
+        for si, stage in enumerate(chain.stages):
+            for (name, typ, K, N), (_, w) in zip(stage, chain.w[si]):
+                g.mul_mat(typ, w, K, xs[K], out=ys[N], workspace=ws)
+
+    run()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        run()
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    macs = sum(N * K for stage in chain.stages for _, _, K, N in stage) * M
+    return {"M": M, "ms_per_batch": round(ms, 3), "tok_s": round(M / (ms * 1e-3), 1),
+            "int_TOPS": round(2 * macs / (ms * 1e-3) / 1e12, 1),
+            "note": "all chain matmuls at ne11=M (quantize + kq_mmq per matmul, eager)"}
+
+
 def cpu_baseline(chain, seconds):
     """The oracle's restated ggml mul_mat (NEON-order scalar C, pthreads) on the same
     chain, timed on this host's cores for a bounded number of tokens."""
@@ -212,6 +249,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--no-prefill", action="store_true")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -305,6 +343,7 @@ def main():
         kernels = {k: {"launches": v["launches"], "us_per_launch": round(v["ms"] * 1e3 / v["launches"], 2),
                        "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} for k, v in per.items()}
         large = None if args.no_large or world > 1 else large_gemv(dev)
+        prefill = None if args.no_prefill or world > 1 or not use_backend else prefill_chain(chain, dev)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(chain, args.cpu_seconds)
@@ -326,6 +365,7 @@ def main():
             "roofline": roof,
             "kernels": kernels,
             "gemv_large": large,
+            "prefill_pp512": prefill,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

@@ -486,8 +486,12 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     a.m_cols = (int)M;
     a.y = y;
     a.y_col_stride = y_col_stride;
-    const void *fn = type == Q5_K ? (const void *)kq_mmq<Q5_K> : (const void *)kq_mmq<Q4_K>;
-    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * block_bytes(type));
+    const void *fn = type == Q5_K ? (const void *)kq_mmq<Q5_K>
+                   : type == Q6_K ? (const void *)kq_mmq<Q6_K>
+                                  : (const void *)kq_mmq<Q4_K>;
+    // two superblock buffers: 64 Q8L columns + 64 weight rows (Q6_K: 224-B granule span), +16 B
+    // for the Q6_K realign reads past the last row
+    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16;
     allow_lds(fn, lds);
     const dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64), 1);
     hipEvent_t e0, e1;
@@ -496,7 +500,7 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     hipError_t e;
     if (timed) {
         e = hipExtLaunchKernel(fn, grid, dim3(256), args, lds, stream, e0, e1, 0);
-        timing_log(std::string("kq::kq_mmq<") + (type == Q5_K ? "13" : "12") + ">",
+        timing_log(std::string("kq::kq_mmq<") + std::to_string(type) + ">",
                    (double)N * a.nb * block_bytes(type) + (double)M * a.nb * Q8L_STRIDE + (double)M * N * 4.0, e0, e1);
     } else {
         e = hipLaunchKernel(fn, grid, dim3(256), args, lds, stream);
@@ -508,8 +512,10 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
 
 bool mmq_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M) {
     if (!rows_enabled() || M < kMmqMinCols || N <= 0) return false;
-    if (type != Q4_K && type != Q5_K) return false;
-    return ((uintptr_t)w & 15u) == 0 && (row_stride & 15u) == 0 && N < (1ll << 31) && M < (1ll << 31);
+    if (type != Q4_K && type != Q5_K && type != Q6_K) return false;
+    if (N >= (1ll << 31) || M >= (1ll << 31)) return false;
+    if (type == Q6_K) return true;  // any alignment: fetched from the 16-B boundary below each block
+    return ((uintptr_t)w & 15u) == 0 && (row_stride & 15u) == 0;
 }
 
 int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,

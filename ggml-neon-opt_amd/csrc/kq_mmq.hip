@@ -46,9 +46,70 @@ constexpr int MMQ_TILE = 64;                 // columns x rows per workgroup
 constexpr int MMQ_A_BYTES = MMQ_TILE * Q8L_STRIDE;  // 19456 B per superblock
 constexpr int MMQ_A_INSTR = MMQ_A_BYTES / 1024;     // 19 DMA instructions (exact)
 
-__host__ __device__ constexpr int mmq_b_instr(int type) { return MMQ_TILE * block_bytes(type) / 1024; }  // 9 / 11
+// Weight bytes per row in the LDS tile: the superblock itself (Q4_K 144, Q5_K 176,
+// 16-B aligned rows), or for Q6_K (210 B, any alignment) the 14 granules from the
+// 16-B boundary below it.
+__host__ __device__ constexpr int mmq_row_bytes(int type) { return type == Q6_K ? 224 : block_bytes(type); }
+__host__ __device__ constexpr int mmq_b_instr(int type) { return MMQ_TILE * mmq_row_bytes(type) / 1024; }  // 9 / 11 / 14
 __host__ __device__ constexpr int mmq_nw(int type) { return (MMQ_A_INSTR + mmq_b_instr(type) + 3) / 4; }
-__host__ __device__ constexpr int mmq_buf(int type) { return MMQ_A_BYTES + MMQ_TILE * block_bytes(type); }
+__host__ __device__ constexpr int mmq_buf(int type) { return MMQ_A_BYTES + MMQ_TILE * mmq_row_bytes(type); }
+
+// Q6_K superblock of one 32x32 tile: 8 chunks of 32 elements; a lane's 16 values
+// of a chunk are one 16-element scale group, so two MFMAs per chunk (the other
+// half's operand zeroed) give each group's dot, scaled by its int8 scale on VALU.
+// The weight operand is q - 32 (sign-extended 6-bit), so the sum is directly the
+// reference's isum - 32*isum_mins (README.md:369-394 / lane_q6K): no mins term.
+__device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *buf, const uint8_t *At, int n, int b,
+                                              int r, int h, int wm, int wn, f32x16 &sumf) {
+    const int nrow = n < a.n_rows ? n : a.n_rows - 1;  // the DMA clamped the same way
+    const uint32_t mis = (uint32_t)((uintptr_t)(a.w + (int64_t)nrow * a.row_stride + (int64_t)b * 210) & 15u);
+    const uint8_t *region = buf + MMQ_A_BYTES + (32 * wn + r) * 224 + mis;
+    const uint32_t s4 = (uint32_t)((uintptr_t)region & 3u);
+    const uint8_t *bb = region - s4;
+    const u32x4 SC = realign(*(const u32x4a *)(bb + 192), *(const uint32_t *)(bb + 208), s4);
+    const uint32_t dh = (*(const uint32_t *)(bb + 208) >> (8u * s4)) & 0xffffu;
+    i32x16 sumi;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) sumi[i] = 0;
+    const i32x16 zero = {};
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh) {
+        const u32x4 L0 = realign(*(const u32x4a *)(bb + 64 * nh + 16 * h), *(const uint32_t *)(bb + 64 * nh + 16 * h + 16), s4);
+        const u32x4 L1 = realign(*(const u32x4a *)(bb + 64 * nh + 32 + 16 * h),
+                                 *(const uint32_t *)(bb + 64 * nh + 48 + 16 * h), s4);
+        const u32x4 H = realign(*(const u32x4a *)(bb + 128 + 32 * nh + 16 * h),
+                                *(const uint32_t *)(bb + 144 + 32 * nh + 16 * h), s4);
+#pragma unroll
+        for (int cc = 0; cc < 4; ++cc) {
+            const int c = 4 * nh + cc;  // chunk: elements 32c .. 32c+31
+            const u32x4 L = (cc & 1) ? L1 : L0;
+            const uint32_t sh = (uint32_t)(cc >> 1) * 4u;
+            // x = q ^ 0x20 = (q - 32) in 6-bit two's complement; sign-extend bit 5 into bits 6-7
+            u32x4 q;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t x = ((L[k] >> sh) & 0x0f0f0f0fu) | ((((H[k] >> (2u * cc)) & 0x03030303u) ^ 0x02020202u) << 4);
+                const uint32_t sgn = x & 0x20202020u;
+                q[k] = x | (sgn << 1) | (sgn << 2);
+            }
+            const u32x4 act = *(const u32x4 *)(At + 16 + 32 * c + 16 * h);
+            const u32x4 q0 = h == 0 ? q : u32x4{0u, 0u, 0u, 0u};
+            const u32x4 q1 = h == 1 ? q : u32x4{0u, 0u, 0u, 0u};
+            const i32x16 d0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&q0, zero, 0, 0, 0);
+            const i32x16 d1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&q1, zero, 0, 0, 0);
+            const int g0 = sbyte(SC, 2 * c), g1 = sbyte(SC, 2 * c + 1);  // int8 group scales of row n
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sumi[i] += g0 * d0[i] + g1 * d1[i];
+        }
+    }
+    const float xd = h2f(dh);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
+        sumf[i] = fmaf(xd * yd, (float)sumi[i], sumf[i]);  // sum += d_all*y.d*(isum - 32*isum_mins)
+    }
+}
 
 template <int TYPE>
 __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
@@ -80,10 +141,12 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
                 src = a.xq + (int64_t)c * a.xq_col_stride + (int64_t)b * Q8L_STRIDE + 16 * piece;
                 dma16(src, (LDS void *)(buf + 1024 * t));
             } else {
-                int rw = g / (BSZ / 16);
-                const int piece = g - rw * (BSZ / 16);
+                constexpr int RG = mmq_row_bytes(TYPE) / 16;
+                int rw = g / RG;
+                const int piece = g - rw * RG;
                 rw = row0 + rw < a.n_rows ? row0 + rw : a.n_rows - 1;
-                src = a.w + (int64_t)rw * a.row_stride + (int64_t)b * BSZ + 16 * piece;
+                const uintptr_t blk = (uintptr_t)(a.w + (int64_t)rw * a.row_stride + (int64_t)b * BSZ);
+                src = (const uint8_t *)(blk & ~(uintptr_t)15) + 16 * piece;
                 dma16(src, (LDS void *)(buf + MMQ_A_BYTES + 1024 * (t - MMQ_A_INSTR)));
             }
         }
@@ -105,6 +168,11 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
         asm volatile("s_barrier" ::: "memory");  // every wave's part of superblock b
         const uint8_t *buf = smem + (b & 1) * BUF;
         const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;          // this lane's activation column
+        if (TYPE == Q6_K) {
+            q6_superblock(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            continue;
+        }
         const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;   // this lane's weight row
         const u32x4 hdr = *(const u32x4 *)Bt;
         // 6-bit scales / mins of the lane's row (get_scale_min_k4, README.md:732-739)
@@ -208,5 +276,6 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
 
 template __global__ void kq_mmq<Q4_K>(const MmqArgs a);
 template __global__ void kq_mmq<Q5_K>(const MmqArgs a);
+template __global__ void kq_mmq<Q6_K>(const MmqArgs a);
 
 }  // namespace kq

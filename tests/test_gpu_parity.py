@@ -291,9 +291,9 @@ def test_fused_ragged_partition(dev, oracle, npo, impl):
 
 
 # ---------------------------------------------------------------- batched (prefill) MFMA path
-@pytest.mark.parametrize("type_", [12, 13])
+@pytest.mark.parametrize("type_", [12, 13, 14])
 @pytest.mark.parametrize("K,N,M", [(256, 64, 16), (2048, 100, 33), (4096, 130, 64), (5632, 77, 100),
-                                   (768, 5, 70), (2048, 64, 512)])
+                                   (768, 5, 70), (1280, 33, 20), (2048, 64, 512)])
 def test_prefill_mfma_bit_exact(dev, oracle, npo, type_, K, N, M):
     """M >= 16 columns go through kq_mmq (int8 MFMA per 32-element sub-block, f32 MFMA
     for the mins, the reference's fp32 chain per element): identical to ggml's
