@@ -8,12 +8,16 @@ chain (every layer's attn_q/k/v, attn_output, ffn_gate/up, ffn_down, then the
 output head; 629.8 MB of K-quant weights, the Q4_K_M type mix of llama-quant.cpp
 [U]: attn_v/ffn_down Q6_K in the 10 use_more_bits layers, output Q6_K), each GEMV
 including its bit-exact Q8_K activation quantization. Weights are synthetic
-random blocks of the real shapes (no network for the GGUF); activations are
-synthetic f32 vectors per stage; non-matmul ops (norm, rope, attention, swiglu:
-1.5 % of the reference's CPU time, out.folded:122) are not part of the chain.
-The chain runs through the ggml-backend mirror (mi355x_backend_graph_compute):
-q/k/v and gate/up fuse into one launch each, and the 89 launches of a token are
-replayed from one hipGraph.
+random blocks of the real shapes (no network for the GGUF), their fp16 scales
+sized so activations keep an O(1) RMS down the chain. Every stage reads the
+previous stage's output (attn_q -> attn_output -> ffn_gate -> ffn_down -> next
+layer's q/k/v ... -> output), so each stage truly waits for the one before; the
+first stage reads a synthetic f32 vector. Non-matmul ops (norm, rope, attention,
+swiglu: 1.5 % of the reference's CPU time, out.folded:122) are not part of the
+chain. The chain runs through the ggml-backend mirror
+(mi355x_backend_graph_compute): q/k/v and gate/up fuse into one stage each and
+the 89 stage launches of a token are replayed from one hipGraph (--impl chain:
+ONE persistent kq_chain launch per token instead).
 
 Multi-GPU (--gpus N under torch.distributed.run): every rank decodes its own
 token stream with its own copy of the weights ("replicas", weak scaling); value
@@ -70,22 +74,35 @@ def q4km_chain(model):
     return stages
 
 
-def random_kquant(type_, N, K, gen, dev):
+# E[w^2] / d^2 of a random block (6-bit scales/mins uniform, quants uniform, dmin =
+# d * mean quant so a sub-block averages ~0): sum_j w_ij x_j keeps the RMS of x when
+# d = 1 / sqrt(K * W2).
+W2 = {12: 66727.0, 13: 277630.0, 14: 1.865e6}
+
+
+def random_kquant(type_, N, K, gen, dev, rms_keep=False):
     """Random valid K-quant rows generated on the device (every qs/scales byte is
-    legal; d/dmin fp16 in [2^-14, 2^-6], never NaN/Inf)."""
+    legal; d/dmin fp16, never NaN/Inf). Default d, dmin in [2^-14, 2^-6]; rms_keep:
+    d ~ U[0.75, 1.25] / sqrt(1.0208 K W2) and dmin = d * mean quant, so a chain of
+    GEMVs neither blows up nor vanishes."""
     nb = K // 256
     B = g.BLOCK_BYTES[type_]
     w = torch.randint(0, 256, (N, nb, B), dtype=torch.uint8, device=dev, generator=gen)
 
-    def f16():
-        r = torch.rand((N, nb), device=dev, generator=gen) * (2.0 ** -6 - 2.0 ** -14) + 2.0 ** -14
+    def f16(r):
         return r.to(torch.float16).view(torch.uint8).view(N, nb, 2)
 
-    if type_ in (g.TYPE_Q4_K, g.TYPE_Q5_K):
-        w[..., 0:2] = f16()
-        w[..., 2:4] = f16()
+    if rms_keep:
+        d = (torch.rand((N, nb), device=dev, generator=gen) * 0.5 + 0.75) / float(np.sqrt(1.0208 * K * W2[type_]))
+        dmin = d * (7.5 if type_ == g.TYPE_Q4_K else 15.5)
     else:
-        w[..., 208:210] = f16()
+        d = torch.rand((N, nb), device=dev, generator=gen) * (2.0 ** -6 - 2.0 ** -14) + 2.0 ** -14
+        dmin = torch.rand((N, nb), device=dev, generator=gen) * (2.0 ** -6 - 2.0 ** -14) + 2.0 ** -14
+    if type_ in (g.TYPE_Q4_K, g.TYPE_Q5_K):
+        w[..., 0:2] = f16(d)
+        w[..., 2:4] = f16(dmin)
+    else:
+        w[..., 208:210] = f16(d)
     return w.view(N, nb * B)
 
 
@@ -100,16 +117,23 @@ class Chain:
         self.w, self.x, self.y, self.nodes, self.keep = [], [], [], [], []
         self.bytes_per_token = 0
         self.row_shard = row_shard
-        for stage in self.stages:
+        # one decode stream: stage s+1 reads stage s's first output (row-split shards
+        # keep per-stage inputs: their exchange is the collective, see rowsplit.py)
+        self.dependent = row_shard is None
+        for si, stage in enumerate(self.stages):
             K = stage[0][2]
-            x = torch.randn(K, device=dev, generator=gen)
+            if self.dependent and si > 0:
+                x = self.y[si - 1][0][:K]
+                assert self.stages[si - 1][0][3] >= K
+            else:
+                x = torch.randn(K, device=dev, generator=gen)
             xt = g.make_tensor(g.TYPE_F32, K, 1, x.data_ptr())
             self.x.append(x)
             self.keep.append(xt)
             ws, ys = [], []
             for name, typ, K_, N in stage:
                 r0, r1 = (0, N) if row_shard is None else row_shard(N)
-                w = random_kquant(typ, r1 - r0, K_, gen, dev)
+                w = random_kquant(typ, r1 - r0, K_, gen, dev, rms_keep=self.dependent)
                 y = torch.empty(r1 - r0, device=dev)
                 wt = g.make_tensor(typ, K_, r1 - r0, w.data_ptr())
                 node = g.make_tensor(g.TYPE_F32, r1 - r0, 1, y.data_ptr(), op=g.OP_MUL_MAT, src0=wt, src1=xt)
@@ -225,14 +249,17 @@ def cpu_baseline(chain, seconds):
     tokens, t0 = 0, time.perf_counter()
     while True:
         for si, ws in enumerate(host):
-            for typ, w in ws:
-                O.mul_mat(typ, w, xs[si], n_threads=threads)
+            x = xs[si]
+            if chain.dependent and si > 0:
+                x = prev[:, :x.shape[1]]
+            outs = [O.mul_mat(typ, w, x, n_threads=threads) for typ, w in ws]
+            prev = outs[0]
         tokens += 1
         el = time.perf_counter() - t0
         if el >= seconds or tokens >= 50:
             break
     return {"value": tokens / el, "unit": "tok/s", "cores": threads, "kind": "port",
-            "sample": f"{tokens} token(s) of the full {chain.model} Q4_K_M matmul chain "
+            "sample": f"{tokens} token(s) of the full {chain.model} Q4_K_M matmul chain (dependent stages) "
                       f"({chain.bytes_per_token / 1e6:.1f} MB/token) through the oracle's restated "
                       f"ggml_compute_forward_mul_mat (quantize_row_q8_K_ref + NEON-order vec_dot, "
                       f"{threads} pthreads), {el:.1f} s"}
@@ -249,6 +276,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--impl", default="auto", choices=["auto", "rows", "chain", "tasks"],
+                    help="auto/rows: kq_rows per stage (hipGraph replay); chain: one persistent "
+                         "kq_chain launch per token; tasks: kq_gemv per stage")
     ap.add_argument("--no-prefill", action="store_true")
     args = ap.parse_args()
 
@@ -263,6 +293,7 @@ def main():
     torch.cuda.set_device(dev)
     if not g.device_available():
         raise SystemExit("bench: no gfx950 device or libggml_mi355x.so not loadable")
+    g.gemv_impl({"auto": g.GEMV_AUTO, "rows": g.GEMV_ROWS, "chain": g.GEMV_CHAIN, "tasks": g.GEMV_TASKS}[args.impl])
 
     def barrier():
         if world > 1:
@@ -348,6 +379,13 @@ def main():
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline(chain, args.cpu_seconds)
         wbytes = chain.bytes_per_token * (world if args.mode == "rowsplit" else 1)
+        if not use_backend:
+            executor = "rowsplit: gemv_fused per stage + RCCL all_gather"
+        elif args.impl == "chain":
+            executor = "kq_chain: 1 persistent launch per token (tagged write-through hand-off per stage)"
+        else:
+            executor = f"{'kq_gemv' if args.impl == 'tasks' else 'kq_rows'}: 1 launch per stage" + \
+                ("" if args.no_graph else ", hipGraph replay")
         result = {
             "metric": "tg128 tok/s + Q4_K GEMV achieved-HBM-GB/s, TinyLlama-1.1B Q4_K_M @1 GPU",
             "value": round(value, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
@@ -357,9 +395,10 @@ def main():
             "data": "synthetic (random valid K-quant blocks of the real shapes; random f32 activations)",
             "config": {"workload": f"{args.model} Q4_K_M decode matmul chain (tg, 1 token/step)",
                        "weights_MB_per_token": round(wbytes / 1e6, 1),
-                       "launches_per_token": chain.launches(),
+                       "stages_per_token": chain.launches(),
+                       "executor": executor,
                        "parallelism": (f"replicas x{world}" if args.mode == "replicas" else f"rowsplit{world}"),
-                       "hipgraph": use_backend and not args.no_graph},
+                       "hipgraph": use_backend and args.impl != "chain" and not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
             "effective_GBps": round(value * chain.bytes_per_token / 1e9 / (world if args.mode == "replicas" else 1), 1),
             "roofline": roof,

@@ -25,6 +25,7 @@ __global__ void kq_rows(const RowsArgs a);
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TYPE>
 __global__ void kq_mmq(const MmqArgs a);
+__global__ void kq_chain(const ChainArgs a);
 
 namespace {
 
@@ -297,14 +298,19 @@ std::atomic<int> g_impl{-1};
 bool rows_enabled() {
     int v = g_impl.load();
     if (v < 0) {
-        const char *e = getenv("MI355X_GEMV_IMPL");  // "tasks": force kq_gemv (A/B runs)
-        v = (e && strcmp(e, "tasks") == 0) ? MI355X_GEMV_TASKS : MI355X_GEMV_AUTO;
+        const char *e = getenv("MI355X_GEMV_IMPL");  // "tasks" / "rows": A/B runs
+        v = (e && strcmp(e, "tasks") == 0)  ? MI355X_GEMV_TASKS
+            : (e && strcmp(e, "rows") == 0)  ? MI355X_GEMV_ROWS
+            : (e && strcmp(e, "chain") == 0) ? MI355X_GEMV_CHAIN
+                                             : MI355X_GEMV_AUTO;
         int expect = -1;
         g_impl.compare_exchange_strong(expect, v);
         v = g_impl.load();
     }
-    return v == MI355X_GEMV_AUTO;
+    return v != MI355X_GEMV_TASKS;
 }
+
+bool chain_enabled() { return rows_enabled() && g_impl.load() == MI355X_GEMV_CHAIN; }
 
 template <int TM, bool FQ>
 rows_fn rows_inst() {
@@ -447,6 +453,71 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
         timing_log(rows_name(pl), rows_bytes(a, pl.fusedq), e0, e1);
     } else {
         hipLaunchKernelGGL(pl.fn, pl.grid, dim3(ROWS_WAVES * 64), pl.lds, stream, a);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+// ------------------------------------------------------------ persistent decode chain
+int plan_chain_stage(const mi355x_gemv_desc *d, int n, int64_t K, ChainStage &cs, ChainFit &fit) {
+    RowsPlan rp;
+    const int rc = plan_rows(d, n, K, true, rp);
+    if (rc) return rc;
+    const RowsArgs &a = rp.a;
+    memset(&cs, 0, sizeof(cs));
+    cs.n_desc = a.n_desc;
+    cs.nb = a.nb;
+    cs.bR = a.bR;
+    cs.waves_total = a.waves_total;
+    for (int i = 0; i <= MI355X_MAX_FUSED; ++i) cs.wave_prefix[i] = a.wave_prefix[i];
+    for (int i = 0; i < MI355X_MAX_FUSED; ++i) {
+        cs.rbase[i] = a.rbase[i];
+        cs.rrem[i] = a.rrem[i];
+        cs.type[i] = a.type[i];
+        cs.w[i] = a.w[i];
+        cs.y[i] = a.y[i];
+    }
+    fit.nb = fit.nb > a.nb ? fit.nb : a.nb;
+    fit.tmask |= rp.tmask;
+    fit.recs = fit.recs > a.bR * a.nb ? fit.recs : a.bR * a.nb;
+    fit.rpw = fit.rpw > a.rpw ? fit.rpw : a.rpw;
+    for (int i = 0; i < a.n_desc; ++i) {
+        const double rows = (double)a.rbase[i] * (a.wave_prefix[i + 1] - a.wave_prefix[i]) + a.rrem[i];
+        fit.bytes += rows * a.nb * block_bytes(a.type[i]) + rows * 4.0;
+    }
+    fit.bytes += (double)a.nb * QK * 4.0;
+    return MI355X_OK;
+}
+
+int chain_layout(const ChainFit &fit, ChainArgs &a, size_t &lds) {
+    a.act = 0;
+    a.ring = fit.nb * Q8L_STRIDE;
+    a.ring_stride = rows_ring(fit.tmask);
+    a.recs = a.ring + ROWS_WAVES * a.ring_stride;
+    a.recs_stride = fit.recs * 16;
+    a.outs = a.recs + ROWS_WAVES * a.recs_stride;
+    a.outs_stride = (fit.rpw * 4 + 15) & ~15;
+    const size_t total = (size_t)a.outs + (size_t)ROWS_WAVES * a.outs_stride;
+    if (total > kMaxLds) return MI355X_E_UNSUPPORTED;
+    // more than half a CU's LDS: one workgroup per CU, all of them resident
+    lds = total > kMaxLds / 2 + 1024 ? total : kMaxLds / 2 + 1024;
+    return MI355X_OK;
+}
+
+int launch_chain(const ChainArgs &a, size_t lds, double bytes, hipStream_t stream) {
+    if (a.n_stages <= 0) return MI355X_OK;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    allow_lds((const void *)kq_chain, lds);
+    const dim3 grid((unsigned)num_cus());
+    ChainArgs aa = a;
+    aa.stamps = g_stamps;
+    aa.stamps_cap = g_stamps_cap;
+    hipEvent_t e0, e1;
+    if (timing_slot(stream, e0, e1)) {
+        hipExtLaunchKernelGGL(kq_chain, grid, dim3(ROWS_WAVES * 64), (uint32_t)lds, stream, e0, e1, 0, aa);
+        timing_log("kq::kq_chain", bytes, e0, e1);
+    } else {
+        hipLaunchKernelGGL(kq_chain, grid, dim3(ROWS_WAVES * 64), lds, stream, aa);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
@@ -712,7 +783,7 @@ int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, i
 }
 
 int mi355x_gemv_impl(int impl) {
-    if (impl != MI355X_GEMV_AUTO && impl != MI355X_GEMV_TASKS) return MI355X_E_INVAL;
+    if (impl < MI355X_GEMV_AUTO || impl > MI355X_GEMV_CHAIN) return MI355X_E_INVAL;
     rows_enabled();  // resolve the environment default first
     return g_impl.exchange(impl);
 }

@@ -147,6 +147,36 @@ __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int
     return L;
 }
 
+// ---------------------------------------------------------------- persistent decode chain
+// kq_chain: one launch runs a whole sequence of decode MUL_MAT stages (a token's
+// graph). Each stage is planned exactly like one kq_rows launch (same wave split,
+// same per-row arithmetic); the grid is one ROWS_WAVES workgroup per CU for every
+// stage. A stage whose activation is an earlier node's output reads it from that
+// node's "bus": a copy of the output as {value, tag} pairs, stored write-through
+// (sc0 sc1) by the producer and polled by every consumer workgroup until each
+// pair carries this launch's tag — the activation fetch is the stage hand-off.
+struct ChainStage {
+    int n_desc, nb, bR, waves_total;
+    int wave_prefix[MI355X_MAX_FUSED + 1];
+    int rbase[MI355X_MAX_FUSED];
+    int rrem[MI355X_MAX_FUSED];
+    int type[MI355X_MAX_FUSED];
+    const uint8_t *w[MI355X_MAX_FUSED];
+    float *y[MI355X_MAX_FUSED];
+    uint32_t *bus[MI355X_MAX_FUSED];  // {value, tag} copy of y[d] when a later stage reads it, else null
+    const float *x;                   // activation written before the launch (xbus == null)
+    const uint32_t *xbus;             // or: the bus of the producing node
+};
+
+struct ChainArgs {
+    const ChainStage *st;
+    int n_stages;
+    int act, ring, ring_stride, recs, recs_stride, outs, outs_stride;  // LDS layout (max over stages)
+    uint32_t *sync;   // [0] epoch (tag of the last launch), [1] finished workgroups, [2] hand-off timeout flag
+    uint64_t *stamps; // diagnostics: per (workgroup, stage) x-ready / stage-done s_memrealtime
+    int64_t stamps_cap;
+};
+
 // ---------------------------------------------------------------- batched (prefill) MFMA GEMM
 // kq_mmq (M > 1): 64 x 64 output tiles, Q8L activations in a workspace.
 struct MmqArgs {

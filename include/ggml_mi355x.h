@@ -87,6 +87,7 @@ enum mi355x_status {
     MI355X_E_UNSUPPORTED = -2, /* combination not implemented on this device   */
     MI355X_E_WORKSPACE  = -3,  /* workspace missing or too small               */
     MI355X_E_NODEVICE   = -4,  /* no gfx950 device / HIP runtime unavailable   */
+    MI355X_E_TIMEOUT    = -5,  /* a persistent-chain stage hand-off timed out  */
 };
 
 /* Bytes of one row of `type` with `k` elements (ggml_row_size). k % 256 == 0. */
@@ -192,11 +193,16 @@ int mi355x_timing_read(mi355x_launch_timing *out, int max);
  * task lookup, after the prologue DMAs are issued and after their wait:
  * 8 x uint64 per wave, [(blockIdx.x * 4 + wave) * 8 + i]. NULL disables. */
 int mi355x_diag_stamps(void *buf, size_t bytes);
-/* Decode-GEMV implementation selector (A/B runs, parity of both paths):
- * MI355X_GEMV_AUTO (row-stream kq_rows when rows are contiguous, else kq_gemv) or
- * MI355X_GEMV_TASKS (always the 8-row-task kq_gemv). Returns the previous value. */
+/* Decode-GEMV implementation selector (A/B runs, parity of every path):
+ * MI355X_GEMV_AUTO (row-stream kq_rows when rows are contiguous, else kq_gemv),
+ * MI355X_GEMV_TASKS (always the 8-row-task kq_gemv), MI355X_GEMV_ROWS (kq_rows,
+ * one launch per stage; what AUTO does today) or MI355X_GEMV_CHAIN (as ROWS, but
+ * a backend graph of >= 2 decode stages runs as ONE persistent kq_chain launch).
+ * Returns the previous value, or MI355X_E_INVAL. */
 #define MI355X_GEMV_AUTO 0
 #define MI355X_GEMV_TASKS 1
+#define MI355X_GEMV_ROWS 2
+#define MI355X_GEMV_CHAIN 3
 int mi355x_gemv_impl(int impl);
 
 /* --------------------------------------------- ggml-backend mirror (C++) */
