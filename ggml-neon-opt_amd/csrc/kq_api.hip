@@ -326,7 +326,7 @@ rows_fn pick_rows(int tmask, bool fusedq) {
     }
 }
 
-int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, RowsPlan &pl) {
+int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, RowsPlan &pl, int waves_per_cu) {
     RowsArgs &a = pl.a;
     if (n_desc < 1 || n_desc > MI355X_MAX_FUSED) return MI355X_E_INVAL;
     if (K <= 0 || K % QK != 0) return MI355X_E_INVAL;
@@ -376,7 +376,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     a.stamps_cap = g_stamps_cap;
     // Waves: one workgroup of ROWS_WAVES per CU; each matrix gets waves in
     // proportion to its bytes (never more waves than rows), rows split evenly.
-    const int64_t cap = (int64_t)num_cus() * ROWS_WAVES;
+    const int64_t cap = (int64_t)num_cus() * waves_per_cu;
     int64_t wv[MI355X_MAX_FUSED] = {0, 0, 0, 0};
     int64_t waves = 0;
     for (int i = 0; i < n_desc; ++i) {
@@ -461,10 +461,15 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
 // ------------------------------------------------------------ persistent decode chain
 int plan_chain_stage(const mi355x_gemv_desc *d, int n, int64_t K, ChainStage &cs, ChainFit &fit) {
     RowsPlan rp;
-    const int rc = plan_rows(d, n, K, true, rp);
+    // the first `pollers` waves of every workgroup fetch and quantize the activation
+    // (no weight DMAs queued ahead of their polls); the others stream the rows
+    const int nb = (int)(K / QK);
+    const int pollers = chain_pollers(nb);
+    const int rc = plan_rows(d, n, K, true, rp, ROWS_WAVES - pollers);
     if (rc) return rc;
     const RowsArgs &a = rp.a;
     memset(&cs, 0, sizeof(cs));
+    cs.pollers = pollers;
     cs.n_desc = a.n_desc;
     cs.nb = a.nb;
     cs.bR = a.bR;
@@ -490,14 +495,20 @@ int plan_chain_stage(const mi355x_gemv_desc *d, int n, int64_t K, ChainStage &cs
 }
 
 int chain_layout(const ChainFit &fit, ChainArgs &a, size_t &lds) {
-    a.act = 0;
-    a.ring = fit.nb * Q8L_STRIDE;
+    a.act = 0;  // two activation buffers: stage s uses act + (s & 1) * act_stride
+    a.act_stride = fit.nb * Q8L_STRIDE;
+    a.ring = 2 * a.act_stride;
     a.ring_stride = rows_ring(fit.tmask);
     a.recs = a.ring + ROWS_WAVES * a.ring_stride;
     a.recs_stride = fit.recs * 16;
     a.outs = a.recs + ROWS_WAVES * a.recs_stride;
     a.outs_stride = (fit.rpw * 4 + 15) & ~15;
-    const size_t total = (size_t)a.outs + (size_t)ROWS_WAVES * a.outs_stride;
+    a.sig = a.outs + ROWS_WAVES * a.outs_stride;  // streaming waves done with their stage (counter)
+    {
+        const char *e = getenv("MI355X_CHAIN_PRE");  // experiment knob: prefetched steps per wave
+        a.pre = e ? atoi(e) : 2;
+    }
+    const size_t total = (size_t)a.sig + 16;
     if (total > kMaxLds) return MI355X_E_UNSUPPORTED;
     // more than half a CU's LDS: one workgroup per CU, all of them resident
     lds = total > kMaxLds / 2 + 1024 ? total : kMaxLds / 2 + 1024;

@@ -21,7 +21,7 @@
 struct ChainCache {
     std::vector<uint64_t> key;
     bool ok = false;  // key planned; false: not eligible, use per-stage launches
-    kq::ChainStage *d_stages = nullptr;
+    uint8_t *d_stages = nullptr;  // stage table, kq::kChainSlotBytes per stage
     uint32_t *sync = nullptr;  // epoch, finished workgroups, timeout flag
     std::vector<void *> bus;
     kq::ChainArgs args{};
@@ -210,10 +210,11 @@ int plan_chain(mi355x_backend *b, mi355x_tensor *const *nodes, int n_nodes, cons
         }
         st[li].xbus = ps.bus[k];
     }
-    if (hipMalloc(&c.d_stages, st.size() * sizeof(kq::ChainStage)) != hipSuccess) return MI355X_E_WORKSPACE;
+    std::vector<uint8_t> table(st.size() * kq::kChainSlotBytes, 0);
+    for (size_t i = 0; i < st.size(); ++i) memcpy(table.data() + i * kq::kChainSlotBytes, &st[i], sizeof(kq::ChainStage));
+    if (hipMalloc(&c.d_stages, table.size()) != hipSuccess) return MI355X_E_WORKSPACE;
     if (hipMalloc(&c.sync, 64) != hipSuccess) return MI355X_E_WORKSPACE;
-    if (hipMemcpyAsync(c.d_stages, st.data(), st.size() * sizeof(kq::ChainStage), hipMemcpyHostToDevice,
-                       b->stream) != hipSuccess ||
+    if (hipMemcpyAsync(c.d_stages, table.data(), table.size(), hipMemcpyHostToDevice, b->stream) != hipSuccess ||
         hipMemsetAsync(c.sync, 0, 64, b->stream) != hipSuccess || hipStreamSynchronize(b->stream) != hipSuccess)
         return MI355X_E_WORKSPACE;
     a.st = c.d_stages;
@@ -232,11 +233,13 @@ int chain_status(mi355x_backend *b) {
     if (b->chain.sync) syncs.push_back(b->chain.sync);
     int rc = MI355X_OK;
     for (uint32_t *s : syncs) {
-        uint32_t flag = 0;
-        if (hipMemcpy(&flag, s + 2, 4, hipMemcpyDeviceToHost) != hipSuccess) continue;
-        if (flag) {
+        uint32_t w[8] = {0};
+        if (hipMemcpy(w, s + 2, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) continue;
+        if (w[0]) {
+            fprintf(stderr, "ggml_mi355x: kq_chain hand-off timed out: stage %u, workgroup %u, superblock %u, tag seen %u, expected %u\n",
+                    w[1], w[2], w[3], w[4], w[5]);
             rc = MI355X_E_TIMEOUT;
-            hipMemset(s + 2, 0, 4);
+            hipMemset(s + 2, 0, sizeof(w));
         }
     }
     for (uint32_t *s : b->old_sync) hipFree(s);

@@ -18,6 +18,12 @@
 // split, same quad partials, same records and fp32 chain replay per row, so every
 // output is bit-identical to the per-launch path and to ggml_vec_dot_q4_K_q8_K.
 //
+// Roles: per stage the first `pollers` waves of a workgroup (1-6, by K) fetch and
+// quantize the activation and stream no weights, so their polls never queue behind
+// weight DMAs (vector-memory returns are in order); the other waves stream rows.
+// The stage table is read one dword per lane and fields come from v_readlane:
+// the next stage's descriptor is loaded a whole stage ahead.
+//
 // The grid is one workgroup per CU and every workgroup must be resident (they
 // wait on each other): the host launches exactly num_cus workgroups with more than
 // half the LDS of a CU. A hand-off that does not complete within ~20 ms sets
@@ -29,10 +35,6 @@ namespace kq {
 namespace {
 
 constexpr uint64_t kHandoffTicks = 2000000;  // s_memrealtime is 100 MHz: 20 ms
-
-// The stage table through the constant address space: uniform scalar loads (s_load)
-// into SGPRs instead of per-lane vector loads.
-typedef const ChainStage __attribute__((address_space(4))) *StagePtr;
 
 __device__ __forceinline__ u32x4 load_sys16(const uint32_t *p) {
     u32x4 r;
@@ -46,6 +48,61 @@ __device__ __forceinline__ void store_sys8(uint32_t *p, uint32_t v, uint32_t tag
     asm volatile("global_store_dwordx2 %0, %1, off sc0 sc1" ::"v"(p), "v"(w) : "memory");
 }
 
+// Stage descriptor, one dword per lane (lane i <- dword i of the 256-B table slot).
+// Loaded by inline asm (invisible to the compiler's waitcnt bookkeeping); the caller
+// guarantees completion (an s_waitcnt covering it) before desc_pin.
+__device__ __forceinline__ uint32_t desc_load(const uint8_t *table, int si, int lane) {
+    uint32_t v;
+    const uint32_t *p = (const uint32_t *)(table + (int64_t)si * kChainSlotBytes) + lane;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+    return v;
+}
+
+#define CH_OFF(f) ((int)(offsetof(ChainStage, f) / 4))
+
+__device__ __forceinline__ int rl(uint32_t v, int i) { return __builtin_amdgcn_readlane((int)v, i); }
+__device__ __forceinline__ uint64_t rl64(uint32_t v, int i) {
+    return (uint64_t)(uint32_t)rl(v, i) | ((uint64_t)(uint32_t)rl(v, i + 1) << 32);
+}
+
+// A wave's view of one stage: its role, rows and the resolved matrix.
+struct WaveStage {
+    int nb, bR, pollers, type;
+    WaveWork ww;
+    const uint8_t *w;
+    float *y;
+    uint32_t *bus;
+    const float *x;
+    const uint32_t *xbus;
+};
+
+__device__ __forceinline__ WaveStage resolve(uint32_t dv, int wave) {
+    WaveStage r;
+    r.nb = rl(dv, CH_OFF(nb));
+    r.bR = rl(dv, CH_OFF(bR));
+    r.pollers = rl(dv, CH_OFF(pollers));
+    const int n_desc = rl(dv, CH_OFF(n_desc));
+    const int waves_total = rl(dv, CH_OFF(waves_total));
+    // streaming waves: gw = (wave - pollers) * gridDim.x + blockIdx.x (spread over every CU)
+    const int gw = wave >= r.pollers ? (wave - r.pollers) * (int)gridDim.x + (int)blockIdx.x : 0x7fffffff;
+    int m = 0;
+#pragma unroll
+    for (int i = 1; i < MI355X_MAX_FUSED; ++i)
+        if (i < n_desc && gw >= rl(dv, CH_OFF(wave_prefix) + i)) m = i;
+    const int j = gw - rl(dv, CH_OFF(wave_prefix) + m);
+    const int base = rl(dv, CH_OFF(rbase) + m), rem = rl(dv, CH_OFF(rrem) + m);
+    r.ww.m = m;
+    r.ww.r0 = j * base + (j < rem ? j : rem);
+    r.ww.nrows = gw < waves_total ? base + (j < rem ? 1 : 0) : 0;
+    r.type = rl(dv, CH_OFF(type) + m);
+    r.w = (const uint8_t *)rl64(dv, CH_OFF(w) + 2 * m);
+    r.y = (float *)rl64(dv, CH_OFF(y) + 2 * m);
+    r.bus = (uint32_t *)rl64(dv, CH_OFF(bus) + 2 * m);
+    r.x = (const float *)rl64(dv, CH_OFF(x));
+    r.xbus = (const uint32_t *)rl64(dv, CH_OFF(xbus));
+    return r;
+}
+
 // Wave-uniform state of a wave's weight stream; survives a stage boundary so the
 // next stage's first ring is fetched before its activation is ready.
 struct Stream {
@@ -53,35 +110,6 @@ struct Stream {
     int T, it, islot;
     uint32_t mis;
 };
-
-__device__ __forceinline__ WaveWork stage_work(StagePtr st, int gw) {
-    WaveWork ww;
-    int m = 0;
-#pragma unroll
-    for (int i = 1; i < MI355X_MAX_FUSED; ++i)
-        if (i < st->n_desc && gw >= st->wave_prefix[i]) m = i;
-    ww.m = m;
-    const int j = gw - st->wave_prefix[m];
-    const int base = st->rbase[m], rem = st->rrem[m];
-    ww.r0 = j * base + (j < rem ? j : rem);
-    ww.nrows = gw < st->waves_total ? base + (j < rem ? 1 : 0) : 0;
-    return ww;
-}
-
-template <int TYPE>
-__device__ __forceinline__ Stream stream_open(StagePtr st, const WaveWork &ww) {
-    constexpr int BSZ = block_bytes(TYPE);
-    Stream S;
-    const int G = ww.nrows * st->nb;
-    S.T = (G + ROWS_SB - 1) / ROWS_SB;
-    const uint8_t *src = st->w[ww.m] + (int64_t)ww.r0 * st->nb * BSZ;
-    S.mis = (uint32_t)((uintptr_t)src & 15u);
-    S.s16 = src - S.mis;
-    S.last16 = G > 0 ? (const uint8_t *)((uintptr_t)(src + (int64_t)G * BSZ - 1) & ~(uintptr_t)15) : S.s16;
-    S.it = 0;
-    S.islot = 0;
-    return S;
-}
 
 template <int TYPE>
 __device__ __forceinline__ void stream_issue(Stream &S, uint8_t *ring, int lane) {
@@ -108,41 +136,53 @@ __device__ __forceinline__ void stream_issue(Stream &S, uint8_t *ring, int lane)
     ++S.it;
 }
 
-// Open the wave's stream of stage `st` and fill its ring (weights only).
+// Open the wave's stream of a stage and fill its ring (weights only).
 template <int TYPE>
-__device__ __forceinline__ void stream_prefetch(Stream &S, StagePtr st, const WaveWork &ww, uint8_t *ring,
-                                                int lane) {
-    S = stream_open<TYPE>(st, ww);
+__device__ __forceinline__ void stream_prefetch(Stream &S, const WaveStage &ws, uint8_t *ring, int lane, int pre) {
+    constexpr int BSZ = block_bytes(TYPE);
     constexpr int D = rows_depth(TYPE);
-    while (S.it < D && S.it < S.T) stream_issue<TYPE>(S, ring, lane);
+    const int G = ws.ww.nrows * ws.nb;
+    S.T = (G + ROWS_SB - 1) / ROWS_SB;
+    const uint8_t *src = ws.w + (int64_t)ws.ww.r0 * ws.nb * BSZ;
+    S.mis = (uint32_t)((uintptr_t)src & 15u);
+    S.s16 = src - S.mis;
+    S.last16 = G > 0 ? (const uint8_t *)((uintptr_t)(src + (int64_t)G * BSZ - 1) & ~(uintptr_t)15) : S.s16;
+    S.it = 0;
+    S.islot = 0;
+    while (S.it < D && S.it < pre && S.it < S.T) stream_issue<TYPE>(S, ring, lane);
 }
 
-// The stage's Q8_K activation into LDS (Q8L blocks), 16 lanes per superblock,
-// 4 superblocks per wave per pass. From the bus: poll until every pair of the
-// wave's blocks carries `tag`.
+__device__ __forceinline__ void prefetch(Stream &S, const WaveStage &ws, uint8_t *ring, int lane, int pre) {
+    if (ws.type == Q6_K) stream_prefetch<Q6_K>(S, ws, ring, lane, pre);
+    else if (ws.type == Q5_K) stream_prefetch<Q5_K>(S, ws, ring, lane, pre);
+    else stream_prefetch<Q4_K>(S, ws, ring, lane, pre);
+}
+
 struct Tm {  // diagnostics of one stage (wave 0): s_memrealtime stamps, poll count
     uint64_t poll0, ok, quant, comp, flush;
     int npoll;
 };
 
-__device__ __forceinline__ const uint32_t *poll_addr(StagePtr st, int wave, int lane, int i) {
-    const int nb = st->nb;
-    const int bi = 4 * ROWS_WAVES * i + 4 * wave + (lane >> 4);
-    const int b = bi < nb ? bi : nb - 1;
-    return st->xbus + 2 * ((int64_t)b * QK + 16 * (lane & 15));
-}
-
-__device__ __forceinline__ void stage_activation(StagePtr st, uint8_t *act, int wave, int lane, uint32_t tag,
-                                                 uint32_t *flag, Tm &tm) {
-    constexpr int PASS = 4 * ROWS_WAVES;
-    const int nb = st->nb;
+// The stage's Q8_K activation into LDS (Q8L blocks): poller wave p quantizes
+// superblocks 4*pollers*i + 4p + (lane >> 4), 16 lanes each. From the bus: poll
+// until every pair of the wave's blocks carries `tag`.
+__device__ __forceinline__ void stage_activation(const WaveStage &ws, uint8_t *act, int wave, int lane, uint32_t tag,
+                                                 uint32_t *flag, Tm &tm, int si, const uint32_t *sig,
+                                                 uint32_t sig_target) {
+    const int nb = ws.nb;
+    const int pass = 4 * ws.pollers;
+    if (wave >= ws.pollers) return;
+    if (ws.xbus) {  // no global polling before this workgroup's own streaming waves have flushed
+        while (__hip_atomic_load(sig, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) < sig_target)
+            __builtin_amdgcn_s_sleep(1);
+    }
 #pragma unroll 1
-    for (int i = 0; PASS * i + 4 * wave < nb; ++i) {
-        const int bi = PASS * i + 4 * wave + (lane >> 4);
+    for (int i = 0; pass * i + 4 * wave < nb; ++i) {
+        const int bi = pass * i + 4 * wave + (lane >> 4);
         const int b = bi < nb ? bi : nb - 1;
         u32x4 v[4];
-        if (st->xbus) {
-            const uint32_t *xp = poll_addr(st, wave, lane, i);
+        if (ws.xbus) {
+            const uint32_t *xp = ws.xbus + 2 * ((int64_t)b * QK + 16 * (lane & 15));
             const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
             if (i == 0) tm.poll0 = t0;
             u32x4 p[8];
@@ -151,6 +191,9 @@ __device__ __forceinline__ void stage_activation(StagePtr st, uint8_t *act, int 
 #pragma unroll
                 for (int k = 0; k < 8; ++k) p[k] = load_sys16(xp + 4 * k);
                 asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                // the loads are invisible to the compiler: pin their registers past the wait
+                asm volatile("" : "+v"(p[0]), "+v"(p[1]), "+v"(p[2]), "+v"(p[3]), "+v"(p[4]), "+v"(p[5]), "+v"(p[6]),
+                             "+v"(p[7]));
                 bool ok = true;
 #pragma unroll
                 for (int k = 0; k < 8; ++k) ok = ok && p[k].y == tag && p[k].w == tag;
@@ -159,7 +202,14 @@ __device__ __forceinline__ void stage_activation(StagePtr st, uint8_t *act, int 
                     break;
                 }
                 if (__builtin_amdgcn_s_memrealtime() - t0 > kHandoffTicks) {
-                    if (lane == 0) atomicOr(flag, 1u);
+                    if (lane == 0) {  // flag + what was still missing (host prints it)
+                        atomicOr(flag, 1u);
+                        flag[1] = (uint32_t)si;
+                        flag[2] = blockIdx.x;
+                        flag[3] = (uint32_t)b;
+                        flag[4] = p[0].y;
+                        flag[5] = tag;
+                    }
                     break;
                 }
                 __builtin_amdgcn_s_sleep(1);
@@ -167,7 +217,7 @@ __device__ __forceinline__ void stage_activation(StagePtr st, uint8_t *act, int 
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = u32x4{p[2 * k].x, p[2 * k].z, p[2 * k + 1].x, p[2 * k + 1].z};
         } else {
-            const float *xp = st->x + (int64_t)b * QK + 16 * (lane & 15);
+            const float *xp = ws.x + (int64_t)b * QK + 16 * (lane & 15);
 #pragma unroll
             for (int k = 0; k < 4; ++k) v[k] = *(const u32x4 *)(xp + 4 * k);
         }
@@ -176,26 +226,26 @@ __device__ __forceinline__ void stage_activation(StagePtr st, uint8_t *act, int 
     tm.quant = __builtin_amdgcn_s_memrealtime();
 }
 
-// Stage compute of one wave: kq_rows' main loop and flush (rows_body, kq_rows.hip),
-// continuing the stream whose first ring stream_prefetch issued.
+// Stage compute of one streaming wave: kq_rows' main loop and flush (rows_body,
+// kq_rows.hip), continuing the stream whose first ring `prefetch` issued.
 template <int TYPE>
-__device__ __forceinline__ void stage_rows(const ChainArgs &a, StagePtr st, const WaveWork &ww, Stream &S,
-                                           uint8_t *smem, int wave, int lane, uint32_t tag, Tm &tm) {
+__device__ __forceinline__ void stage_rows(const ChainArgs &a, const WaveStage &ws, Stream &S, uint8_t *smem,
+                                           const uint8_t *actq, int wave, int lane, uint32_t tag, Tm &tm) {
     constexpr int BSZ = block_bytes(TYPE);
     constexpr int NI = rows_ni(TYPE);
     constexpr int SLOT = rows_slot(TYPE);
     constexpr int D = rows_depth(TYPE);
-    const int nb = st->nb, bR = st->bR;
+    const int nb = ws.nb, bR = ws.bR;
+    const WaveWork &ww = ws.ww;
     const int q = lane >> 2, s = lane & 3;
     uint8_t *const ring = smem + a.ring + wave * a.ring_stride;
     uint8_t *const ring_end = ring + D * SLOT;
     Rec *const recs = (Rec *)(smem + a.recs + wave * a.recs_stride);
     float *const outs = (float *)(smem + a.outs + wave * a.outs_stride);
-    const uint8_t *const actq = smem + a.act;
     const int G = ww.nrows * nb;
     const int T = S.T;
+    while (S.it < D && S.it < T) stream_issue<TYPE>(S, ring, lane);  // the rest of the ring
 
-    while (S.it < D && S.it < T) stream_issue<TYPE>(S, ring, lane);  // (already full unless T < D)
     int io = q, rr = 0;
     while (io >= nb) {
         io -= nb;
@@ -206,8 +256,8 @@ __device__ __forceinline__ void stage_rows(const ChainArgs &a, StagePtr st, cons
     const uint8_t *cslot = ring;
 #pragma unroll 1
     for (int t = 0; t < T; ++t) {
-        // steps t .. S.it-1 are in flight and nothing else (the activation wait drained
-        // older loads); keep the younger ones going
+        // in flight: steps t .. S.it-1 plus possibly older/younger non-DMA loads, which
+        // only make these counted waits more conservative (returns are in order)
         if (T - t >= D) vm_wait<NI * (D - 1)>();
         else vm_wait_k<NI>(T - t - 1);
         if (ROWS_SB * t + q < G) {
@@ -266,22 +316,28 @@ __device__ __forceinline__ void stage_rows(const ChainArgs &a, StagePtr st, cons
     tm.comp = __builtin_amdgcn_s_memrealtime();
     if (ww.nrows > 0) {
         wave_lds_fence();
-        float *y = st->y[ww.m] + ww.r0;
-        uint32_t *bus = st->bus[ww.m];
-        if (bus) {  // the hand-off copy first: it is on the next stage's critical path
-            bus += 2 * (int64_t)ww.r0;
+        if (ws.bus) {  // the hand-off copy first: it is on the next stage's critical path
+            uint32_t *bus = ws.bus + 2 * (int64_t)ww.r0;
             for (int k = 0; k < ww.nrows; k += 64)
                 if (k + lane < ww.nrows) store_sys8(bus + 2 * (k + lane), __float_as_uint(outs[k + lane]), tag);
         }
+        float *y = ws.y + ww.r0;
         for (int k = 0; k < ww.nrows; k += 64)
             if (k + lane < ww.nrows) y[k + lane] = outs[k + lane];
     }
     tm.flush = __builtin_amdgcn_s_memrealtime();
 }
 
-template <int TYPE>
-__device__ __forceinline__ void prefetch_as(Stream &S, StagePtr st, const WaveWork &ww, uint8_t *ring, int lane) {
-    stream_prefetch<TYPE>(S, st, ww, ring, lane);
+// A streaming wave is done with its stage (outputs issued): count it in LDS.
+__device__ __forceinline__ void signal_done(uint32_t *sig, int lane) {
+    if (lane == 0) __hip_atomic_fetch_add(sig, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+}
+
+__device__ __forceinline__ void rows(const ChainArgs &a, const WaveStage &ws, Stream &S, uint8_t *smem,
+                                     const uint8_t *actq, int wave, int lane, uint32_t tag, Tm &tm) {
+    if (ws.type == Q6_K) stage_rows<Q6_K>(a, ws, S, smem, actq, wave, lane, tag, tm);
+    else if (ws.type == Q5_K) stage_rows<Q5_K>(a, ws, S, smem, actq, wave, lane, tag, tm);
+    else stage_rows<Q4_K>(a, ws, S, smem, actq, wave, lane, tag, tm);
 }
 
 }  // namespace
@@ -290,62 +346,68 @@ __global__ void __launch_bounds__(ROWS_WAVES * 64) kq_chain(const ChainArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int gw = wave * gridDim.x + blockIdx.x;
     uint8_t *const ring = smem + a.ring + wave * a.ring_stride;
-    // this launch's tag: one more than the last launch's (bumped by the last workgroup out)
-    uint32_t tag;
+    const bool stamps = a.stamps != nullptr;
+    // this launch's tag (one more than the last launch's, published by its last
+    // workgroup out) and stage 0's descriptor
+    uint32_t tag, dv;
     {
-        u32x4 e = load_sys16(a.sync);
+        const u32x4 e = load_sys16(a.sync);
+        dv = desc_load(a.st, 0, lane);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        asm volatile("" : "+v"(dv));
         tag = __builtin_amdgcn_readfirstlane(e.x) + 1u;
     }
-    const bool stamps = a.stamps != nullptr;
-
-    const StagePtr stages = (StagePtr)a.st;
+    uint32_t *const sig = (uint32_t *)(smem + a.sig);
+    if (threadIdx.x == 0) *sig = 0u;  // (ordered before any increment by the first barrier)
+    uint32_t sig_target = 0;          // streaming-wave completions of all earlier stages
+    WaveStage cur = resolve(dv, wave);
     Stream S;
-    int type;
-    WaveWork ww;
-    {
-        const StagePtr s0 = stages;
-        ww = stage_work(s0, gw);
-        type = s0->type[ww.m];
-        if (type == Q6_K) prefetch_as<Q6_K>(S, s0, ww, ring, lane);
-        else if (type == Q5_K) prefetch_as<Q5_K>(S, s0, ww, ring, lane);
-        else prefetch_as<Q4_K>(S, s0, ww, ring, lane);
-    }
+    S.T = 0;
+    prefetch(S, cur, ring, lane, a.pre);
+    uint32_t dn = a.n_stages > 1 ? desc_load(a.st, 1, lane) : 0u;  // one stage ahead
 
+    // One workgroup barrier per stage. The activation is double-buffered (stage s in
+    // act[s & 1]): pollers quantize stage s+1's activation while the streaming waves
+    // still compute stage s, and can never run two stages ahead (stage s+2's
+    // activation needs stage s+1's outputs, which needs every streaming wave past s).
 #pragma unroll 1
     for (int si = 0; si < a.n_stages; ++si) {
-        const StagePtr st = stages + si;
         Tm tm = {0, 0, 0, 0, 0, 0};
-        stage_activation(st, smem + a.act, wave, lane, tag, a.sync + 2, tm);
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // Q8_K row complete
+        uint8_t *const act = smem + a.act + (si & 1) * a.act_stride;
+        stage_activation(cur, act, wave, lane, tag, a.sync + 2, tm, si, sig, sig_target);  // pollers only
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");     // Q8_K row complete
         const uint64_t t_x = stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-        if (type == Q6_K) stage_rows<Q6_K>(a, st, ww, S, smem, wave, lane, tag, tm);
-        else if (type == Q5_K) stage_rows<Q5_K>(a, st, ww, S, smem, wave, lane, tag, tm);
-        else stage_rows<Q4_K>(a, st, ww, S, smem, wave, lane, tag, tm);
+        rows(a, cur, S, smem, act, wave, lane, tag, tm);                     // streaming waves only
+        if (wave >= cur.pollers) signal_done(sig, lane);
+        sig_target += ROWS_WAVES - cur.pollers;
         if (si + 1 < a.n_stages) {  // next stage's weights do not wait for its activation
-            const StagePtr nx = stages + si + 1;
-            ww = stage_work(nx, gw);
-            type = nx->type[ww.m];
-            if (type == Q6_K) prefetch_as<Q6_K>(S, nx, ww, ring, lane);
-            else if (type == Q5_K) prefetch_as<Q5_K>(S, nx, ww, ring, lane);
-            else prefetch_as<Q4_K>(S, nx, ww, ring, lane);
+            // dn is older than every DMA of this stage: the loop's last wait (T > 0) or
+            // the pollers' activation wait covered it; otherwise wait here
+            if (S.T == 0) vm_wait<0>();
+            asm volatile("" : "+v"(dn));
+            cur = resolve(dn, wave);
+            prefetch(S, cur, ring, lane, a.pre);
+            if (si + 2 < a.n_stages) dn = desc_load(a.st, si + 2, lane);
         }
-        if (stamps && wave == 0 && lane == 0) {
+        if (stamps && lane == 0 && (wave == 0 || wave == ROWS_WAVES - 1)) {
+            // wave 0 (a poller): first poll, poll success, quantized, polls;
+            // the last wave (streams rows): activation ready, computed, flushed, next ring issued
             const int64_t o = ((int64_t)blockIdx.x * a.n_stages + si) * 8;
             if (o + 7 < a.stamps_cap) {
-                a.stamps[o] = t_x;
-                a.stamps[o + 1] = tm.comp;
-                a.stamps[o + 2] = tm.flush;
-                a.stamps[o + 3] = __builtin_amdgcn_s_memrealtime();  // next stage's ring issued
-                a.stamps[o + 4] = tm.poll0;
-                a.stamps[o + 5] = tm.ok;
-                a.stamps[o + 6] = (uint64_t)tm.npoll;
-                a.stamps[o + 7] = tm.quant;
+                if (wave == 0) {
+                    a.stamps[o] = tm.poll0;
+                    a.stamps[o + 1] = tm.ok;
+                    a.stamps[o + 2] = tm.quant;
+                    a.stamps[o + 7] = (uint64_t)tm.npoll;
+                } else {
+                    a.stamps[o + 3] = t_x;
+                    a.stamps[o + 4] = tm.comp;
+                    a.stamps[o + 5] = tm.flush;
+                    a.stamps[o + 6] = __builtin_amdgcn_s_memrealtime();
+                }
             }
         }
-        asm volatile("s_barrier" ::: "memory");  // every wave is done with this stage's activation
     }
     // the last workgroup out publishes this launch's tag as the epoch
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");

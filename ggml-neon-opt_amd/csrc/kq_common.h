@@ -157,6 +157,7 @@ __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int
 // pair carries this launch's tag — the activation fetch is the stage hand-off.
 struct ChainStage {
     int n_desc, nb, bR, waves_total;
+    int pollers;  // waves 0..pollers-1 of each workgroup fetch + quantize the activation; the rest stream rows
     int wave_prefix[MI355X_MAX_FUSED + 1];
     int rbase[MI355X_MAX_FUSED];
     int rrem[MI355X_MAX_FUSED];
@@ -168,10 +169,19 @@ struct ChainStage {
     const uint32_t *xbus;             // or: the bus of the producing node
 };
 
+// Activation waves of a chain stage: 4 superblocks per wave per pass, at most 6 waves.
+__host__ __device__ constexpr int chain_pollers(int nb) { return nb <= 0 ? 1 : (nb + 3) / 4 < 6 ? (nb + 3) / 4 : 6; }
+// The device stage table holds one ChainStage per 256-B slot: lane i of a wave
+// loads dword i, fields are then read with v_readlane (no scalar-cache misses on
+// the stage hand-off path).
+constexpr int kChainSlotBytes = 256;
+static_assert(sizeof(ChainStage) <= kChainSlotBytes, "stage descriptor exceeds its table slot");
+
 struct ChainArgs {
-    const ChainStage *st;
+    const uint8_t *st;  // n_stages slots of kChainSlotBytes
     int n_stages;
-    int act, ring, ring_stride, recs, recs_stride, outs, outs_stride;  // LDS layout (max over stages)
+    int act, act_stride, ring, ring_stride, recs, recs_stride, outs, outs_stride, sig;  // LDS layout (max over stages)
+    int pre;          // weight steps per wave issued before the stage's activation is ready (<= ring depth)
     uint32_t *sync;   // [0] epoch (tag of the last launch), [1] finished workgroups, [2] hand-off timeout flag
     uint64_t *stamps; // diagnostics: per (workgroup, stage) x-ready / stage-done s_memrealtime
     int64_t stamps_cap;

@@ -32,7 +32,8 @@ struct RowsPlan {
 };
 // Row-stream decode GEMV (kq_rows): returns MI355X_E_UNSUPPORTED when the rows are
 // not contiguous or not aligned for it (callers then use kq_gemv).
-int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, RowsPlan &pl);
+int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, RowsPlan &pl,
+              int waves_per_cu = ROWS_WAVES);
 int launch_rows(const RowsPlan &pl, hipStream_t stream);
 bool rows_enabled();
 bool chain_enabled();  // MI355X_GEMV_CHAIN: backend graphs of decode stages run as one kq_chain launch

@@ -39,34 +39,34 @@ def main():
         be.synchronize()
         g.lib().mi355x_diag_stamps(None, 0)
         st = buf[:cus * S * 8].cpu().numpy().astype(np.int64).reshape(cus, S, 8)
-        npoll = st[:, :, 6].copy()
-        t0 = st[:, 0, 0].min()
+        npoll = st[:, :, 7].copy()
+        t0 = st[:, 0, 3].min()
         rel = (st - t0) * 10 / 1000.0  # 100 MHz ticks -> us
-        rel[:, :, 6] = npoll
+        rel[:, :, 7] = npoll
         runs.append(rel)
     R = np.median(np.stack(runs), axis=0)  # [wg, stage, 8]
-    # 0 x ready (after barrier), 1 compute done, 2 flush issued, 3 next ring issued,
-    # 4 first poll, 5 poll success, 6 polls, 7 quantized
+    # per (workgroup, stage): 0 first poll, 1 poll ok, 2 quantized (wave 0, a poller);
+    # 3 activation ready, 4 computed, 5 flushed, 6 next ring issued (last wave, streams rows); 7 polls
     med = lambda v: float(np.median(v))  # noqa: E731
-    print(f"{'st':>3} {'matrices':<22} {'poll0-prev':>10} {'polling':>8} {'npoll':>6} {'quant':>6} {'barrier':>7} "
-          f"{'compute':>8} {'flush':>6} {'pref':>6} {'vis':>6} {'span':>6}")
+    cols = ("gap", "poll", "npoll", "quant", "barrier", "compute", "flush", "pref", "vis", "span")
+    print(f"{'st':>3} {'matrices':<22} " + " ".join(f"{c:>7}" for c in cols))
     tot = {}
     for s, stage in enumerate(chain.stages):
-        prev3 = R[:, s - 1, 3] if s else R[:, 0, 4]
-        vis = (R[:, s, 5].min() - R[:, s - 1, 2].max()) if s else 0.0
-        span = R[:, s, 3].max() - (R[:, s - 1, 3].max() if s else 0.0)
-        row = dict(poll0=med(R[:, s, 4] - prev3), polling=med(R[:, s, 5] - R[:, s, 4]), npoll=med(R[:, s, 6]),
-                   quant=med(R[:, s, 7] - R[:, s, 5]), barrier=med(R[:, s, 0] - R[:, s, 7]),
-                   compute=med(R[:, s, 1] - R[:, s, 0]), flush=med(R[:, s, 2] - R[:, s, 1]),
-                   pref=med(R[:, s, 3] - R[:, s, 2]), vis=vis, span=span)
+        row = dict(
+            gap=med(R[:, s, 0] - R[:, s - 1, 6]) if s else 0.0,       # own streamers done -> first poll
+            poll=med(R[:, s, 1] - R[:, s, 0]) if s else 0.0, npoll=med(R[:, s, 7]),
+            quant=med(R[:, s, 2] - R[:, s, 1]) if s else 0.0,
+            barrier=med(R[:, s, 3] - R[:, s, 2]) if s else 0.0,
+            compute=med(R[:, s, 4] - R[:, s, 3]), flush=med(R[:, s, 5] - R[:, s, 4]),
+            pref=med(R[:, s, 6] - R[:, s, 5]),
+            vis=(R[:, s, 1].min() - R[:, s - 1, 5].max()) if s else 0.0,  # last flush anywhere -> first poll ok
+            span=R[:, s, 3].max() - (R[:, s - 1, 3].max() if s else 0.0))
         names = "+".join(n.split(".")[-1].replace("attn_", "").replace("ffn_", "") for n, *_ in stage)
         for k, v in row.items():
             tot.setdefault(names, {}).setdefault(k, []).append(v)
         if s < 6 or s >= S - 2:
-            print(f"{s:3d} {names:<22} " + " ".join(f"{row[k]:{w}.2f}" for k, w in
-                  (("poll0", 10), ("polling", 8), ("npoll", 6), ("quant", 6), ("barrier", 7), ("compute", 8),
-                   ("flush", 6), ("pref", 6), ("vis", 6), ("span", 6))))
-    print(f"token: {R[:, -1, 3].max():.1f} us")
+            print(f"{s:3d} {names:<22} " + " ".join(f"{row[c]:7.2f}" for c in cols))
+    print(f"token: {R[:, -1, 6].max():.1f} us (from the first workgroup's stage-0 activation)")
     for names, d in tot.items():
         print(f"  median {names:<22} " + " ".join(f"{k}={np.median(v):.2f}" for k, v in d.items()))
 
