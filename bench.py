@@ -74,6 +74,27 @@ def q4km_chain(model):
     return stages
 
 
+def gguf_chain(f):
+    """The same per-token chain read from a llama-architecture GGUF file (types and
+    shapes as stored; output.weight, or the tied token_embd.weight)."""
+    L = int(f.kv["llama.block_count"])
+    stages = []
+
+    def mat(name, tensor=None):
+        info = f.tensors[(tensor or name) + ".weight"]
+        assert len(info["ne"]) == 2 and info["type"] in (g.TYPE_Q4_K, g.TYPE_Q5_K, g.TYPE_Q6_K), name
+        return (name, info["type"], info["ne"][0], info["ne"][1])
+
+    for i in range(L):
+        b = f"blk.{i}."
+        stages.append([mat(b + "attn_q"), mat(b + "attn_k"), mat(b + "attn_v")])
+        stages.append([mat(b + "attn_output")])
+        stages.append([mat(b + "ffn_gate"), mat(b + "ffn_up")])
+        stages.append([mat(b + "ffn_down")])
+    stages.append([mat("output", "output" if "output.weight" in f.tensors else "token_embd")])
+    return stages
+
+
 # E[w^2] / d^2 of a random block (6-bit scales/mins uniform, quants uniform, dmin =
 # d * mean quant so a sub-block averages ~0): sum_j w_ij x_j keeps the RMS of x when
 # d = 1 / sqrt(K * W2).
@@ -109,9 +130,14 @@ def random_kquant(type_, N, K, gen, dev, rms_keep=False):
 class Chain:
     """Weights, inputs and ggml-style MUL_MAT nodes for one rank's token chain."""
 
-    def __init__(self, model, dev, seed, row_shard=None):
+    def __init__(self, model, dev, seed, row_shard=None, gguf=None):
         self.model = model
-        self.stages = q4km_chain(model)
+        self.gguf = gguf
+        if gguf is not None:  # real weights: a GGUFFile (ggml_mi355x.gguf)
+            self.stages = gguf_chain(gguf)
+            self.model = gguf.kv.get("general.name", os.path.basename(gguf.path))
+        else:
+            self.stages = q4km_chain(model)
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed)
         self.w, self.x, self.y, self.nodes, self.keep = [], [], [], [], []
@@ -133,7 +159,11 @@ class Chain:
             ws, ys = [], []
             for name, typ, K_, N in stage:
                 r0, r1 = (0, N) if row_shard is None else row_shard(N)
-                w = random_kquant(typ, r1 - r0, K_, gen, dev, rms_keep=self.dependent)
+                if gguf is not None:
+                    tname = name + ".weight" if name + ".weight" in gguf.tensors else "token_embd.weight"
+                    w = gguf.to_device(tname, dev)[r0:r1].contiguous()
+                else:
+                    w = random_kquant(typ, r1 - r0, K_, gen, dev, rms_keep=self.dependent)
                 y = torch.empty(r1 - r0, device=dev)
                 wt = g.make_tensor(typ, K_, r1 - r0, w.data_ptr())
                 node = g.make_tensor(g.TYPE_F32, r1 - r0, 1, y.data_ptr(), op=g.OP_MUL_MAT, src0=wt, src1=xt)
@@ -276,6 +306,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true")
     ap.add_argument("--no-graph", action="store_true")
+    ap.add_argument("--gguf", default=None,
+                    help="run the chain on a real llama-architecture GGUF file's weights (Q4_K/Q5_K/Q6_K)")
     ap.add_argument("--impl", default="auto", choices=["auto", "rows", "chain", "tasks"],
                     help="auto/rows: kq_rows per stage (hipGraph replay); chain: one persistent "
                          "kq_chain launch per token; tasks: kq_gemv per stage")
@@ -300,15 +332,20 @@ def main():
             import torch.distributed as dist
             dist.barrier()
 
+    gguf = None
+    if args.gguf:
+        from ggml_mi355x.gguf import GGUFFile
+        gguf = GGUFFile(args.gguf)
     use_backend = args.mode != "rowsplit"
     if not use_backend:  # world 1 runs the same path with one shard (exercises StageGather)
         from ggml_mi355x.rowsplit import RowSplitChain
-        runner = RowSplitChain(args.model, dev, rank, world, make_chain=Chain)
+        runner = RowSplitChain(args.model, dev, rank, world,
+                               make_chain=lambda *a, **k: Chain(*a, gguf=gguf, **k))
         chain = runner.chain
         step = runner.step
         stream = torch.cuda.current_stream()
     else:
-        chain = Chain(args.model, dev, seed=0x51A7 + rank)
+        chain = Chain(args.model, dev, seed=0x51A7 + rank, gguf=gguf)
         be = g.Backend(local)
         stream = torch.cuda.ExternalStream(be.stream)
         use_graph = not args.no_graph
@@ -392,8 +429,9 @@ def main():
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 4),
             "higher_is_better": True, "scaling": "weak" if args.mode == "replicas" else "strong",
             "vs_baseline": None, "dtype": "q4_K/q6_K x q8_K (u4/u6*i8 dot4 -> i32, f32 combine)",
-            "data": "synthetic (random valid K-quant blocks of the real shapes; random f32 activations)",
-            "config": {"workload": f"{args.model} Q4_K_M decode matmul chain (tg, 1 token/step)",
+            "data": (f"GGUF weights {os.path.basename(args.gguf)}; random f32 first activation" if args.gguf else
+                     "synthetic (random valid K-quant blocks of the real shapes; random f32 activations)"),
+            "config": {"workload": f"{chain.model} Q4_K_M decode matmul chain (tg, 1 token/step)",
                        "weights_MB_per_token": round(wbytes / 1e6, 1),
                        "stages_per_token": chain.launches(),
                        "executor": executor,

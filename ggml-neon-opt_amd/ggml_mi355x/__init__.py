@@ -35,6 +35,11 @@ EXPORTED_SYMBOLS = (
     "mi355x_backend_get_tensor", "mi355x_backend_synchronize", "mi355x_backend_supports_op",
     "mi355x_backend_graph_compute", "mi355x_timing_enable", "mi355x_timing_read", "mi355x_diag_stamps",
     "mi355x_gemv_fused_workspace_size", "mi355x_gemv_impl",
+    "mi355x_gguf_open", "mi355x_gguf_close", "mi355x_gguf_version", "mi355x_gguf_alignment",
+    "mi355x_gguf_data_offset", "mi355x_gguf_n_tensors", "mi355x_gguf_find_tensor", "mi355x_gguf_get_tensor",
+    "mi355x_gguf_tensor_data", "mi355x_gguf_upload", "mi355x_gguf_n_kv", "mi355x_gguf_find_key",
+    "mi355x_gguf_key", "mi355x_gguf_kv_type", "mi355x_gguf_get_int", "mi355x_gguf_get_float",
+    "mi355x_gguf_get_str", "mi355x_gguf_arr_n",
 )
 
 
@@ -119,6 +124,8 @@ def lib():
     L.mi355x_gemv_impl.restype = i32
     L.mi355x_diag_stamps.argtypes = [vp, sz]
     L.mi355x_diag_stamps.restype = i32
+    from . import gguf as _gguf
+    _gguf.bind(L)
     _lib = L
     return L
 

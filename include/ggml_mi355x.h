@@ -242,6 +242,52 @@ int mi355x_backend_supports_op(const mi355x_tensor *op); /* 1 / 0 */
 int mi355x_backend_graph_compute(mi355x_backend_t backend, mi355x_tensor *const *nodes,
                                  int n_nodes, int use_graph);
 
+/* ------------------------------------------------ GGUF model files (host) */
+/* Reader for GGUF v2/v3 files, the loader side of the path: llama-bench reads the
+ * model through ggml's gguf_reader (artifacts/perf/out.folded:2-3, 17-22) and
+ * llama_model_loader (out.folded:39-46); format restated in kq_gguf.cpp [U].
+ * The file is mapped read-only; tensor bytes (GGUF block layout, no repack) go to
+ * the device with mi355x_gguf_upload. Host-only except the upload: works without
+ * a GPU. */
+typedef struct mi355x_gguf *mi355x_gguf_t;
+
+typedef struct {
+    const char *name;  /* valid while the file is open */
+    int type;          /* ggml type number (enum mi355x_type for the K-quants / F32) */
+    int n_dims;
+    int64_t ne[4];     /* ne[0] = row length (K), ne[1] = rows (N), unused dims 1 */
+    uint64_t offset;   /* absolute byte offset of the data in the file */
+    uint64_t size;     /* bytes; 0 when the type's block size is unknown to the reader */
+} mi355x_gguf_tensor;
+
+/* GGUF metadata value types (gguf_type [U]) */
+enum mi355x_gguf_type {
+    MI355X_GGUF_U8 = 0, MI355X_GGUF_I8 = 1, MI355X_GGUF_U16 = 2, MI355X_GGUF_I16 = 3,
+    MI355X_GGUF_U32 = 4, MI355X_GGUF_I32 = 5, MI355X_GGUF_F32 = 6, MI355X_GGUF_BOOL = 7,
+    MI355X_GGUF_STRING = 8, MI355X_GGUF_ARRAY = 9, MI355X_GGUF_U64 = 10, MI355X_GGUF_I64 = 11,
+    MI355X_GGUF_F64 = 12,
+};
+
+mi355x_gguf_t mi355x_gguf_open(const char *path);  /* NULL on error (reason on stderr) */
+void mi355x_gguf_close(mi355x_gguf_t g);
+uint32_t mi355x_gguf_version(mi355x_gguf_t g);
+uint64_t mi355x_gguf_alignment(mi355x_gguf_t g);    /* general.alignment, default 32 */
+uint64_t mi355x_gguf_data_offset(mi355x_gguf_t g);  /* start of the tensor data section */
+int64_t mi355x_gguf_n_tensors(mi355x_gguf_t g);
+int64_t mi355x_gguf_find_tensor(mi355x_gguf_t g, const char *name); /* index or -1 */
+int mi355x_gguf_get_tensor(mi355x_gguf_t g, int64_t i, mi355x_gguf_tensor *out);
+const void *mi355x_gguf_tensor_data(mi355x_gguf_t g, int64_t i);    /* host pointer (mapped) */
+/* Async H2D copy of tensor i's bytes to device memory on `stream` (hipStream_t). */
+int mi355x_gguf_upload(mi355x_gguf_t g, int64_t i, void *dst_device, size_t dst_size, void *stream);
+int64_t mi355x_gguf_n_kv(mi355x_gguf_t g);
+int64_t mi355x_gguf_find_key(mi355x_gguf_t g, const char *key);     /* index or -1 */
+const char *mi355x_gguf_key(mi355x_gguf_t g, int64_t i);
+int mi355x_gguf_kv_type(mi355x_gguf_t g, int64_t i);                /* enum mi355x_gguf_type */
+int mi355x_gguf_get_int(mi355x_gguf_t g, int64_t i, int64_t *out);   /* integer / bool values */
+int mi355x_gguf_get_float(mi355x_gguf_t g, int64_t i, double *out);  /* any numeric value */
+const char *mi355x_gguf_get_str(mi355x_gguf_t g, int64_t i);        /* NULL unless a string */
+int64_t mi355x_gguf_arr_n(mi355x_gguf_t g, int64_t i);              /* array length, or -1 */
+
 #ifdef __cplusplus
 }
 #endif
