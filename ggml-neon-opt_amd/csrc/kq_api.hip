@@ -20,7 +20,7 @@ namespace kq {
 template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void kq_gemv(const GemvArgs a);
 __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
-template <int TMASK, bool FUSEDQ>
+template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void kq_rows(const RowsArgs a);
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TYPE>
@@ -94,6 +94,8 @@ int resident_wgs(const void *fn, size_t lds) {
     return n;
 }
 
+}  // namespace
+
 // ------------------------------------------------------------ launch timing
 struct TimedLaunch {
     std::string kernel;
@@ -135,6 +137,8 @@ void timing_log(const std::string &kernel, double bytes, hipEvent_t a, hipEvent_
     std::lock_guard<std::mutex> lk(g_tmu);
     g_tlog.push_back({kernel, bytes, a, b});
 }
+
+namespace {
 
 // Same spelling as rocprofv3's kernel names (kernel-trace "Kernel_Name").
 std::string gemv_name(const GemvPlan &pl) {
@@ -312,17 +316,24 @@ bool rows_enabled() {
 
 bool chain_enabled() { return rows_enabled() && g_impl.load() == MI355X_GEMV_CHAIN; }
 
-template <int TM, bool FQ>
+template <int TM, bool FQ, int PR>
 rows_fn rows_inst() {
-    return kq_rows<TM, FQ>;
+    return kq_rows<TM, FQ, PR>;
 }
 
-rows_fn pick_rows(int tmask, bool fusedq) {
+template <int TM>
+rows_fn rows_pick_pro(bool fusedq, int pro) {
+    if (!fusedq) return rows_inst<TM, false, 0>();
+    return pro == ROWS_PRO_NORM ? rows_inst<TM, true, 1>() : pro == ROWS_PRO_SWIGLU ? rows_inst<TM, true, 2>()
+                                                                                     : rows_inst<TM, true, 0>();
+}
+
+rows_fn pick_rows(int tmask, bool fusedq, int pro) {
     switch (tmask) {
-        case 1: return fusedq ? rows_inst<1, true>() : rows_inst<1, false>();
-        case 2: return fusedq ? rows_inst<2, true>() : rows_inst<2, false>();
-        case 4: return fusedq ? rows_inst<4, true>() : rows_inst<4, false>();
-        default: return fusedq ? rows_inst<7, true>() : rows_inst<7, false>();
+        case 1: return rows_pick_pro<1>(fusedq, pro);
+        case 2: return rows_pick_pro<2>(fusedq, pro);
+        case 4: return rows_pick_pro<4>(fusedq, pro);
+        default: return rows_pick_pro<7>(fusedq, pro);
     }
 }
 
@@ -353,7 +364,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     if (tmask != 1 && tmask != 2 && tmask != 4) tmask = 7;
     pl.tmask = tmask;
     pl.fusedq = fusedq;
-    pl.fn = pick_rows(tmask, fusedq);
+    pl.fn = pick_rows(tmask, fusedq, ROWS_PRO_NONE);
     a.n_desc = n_desc;
     a.nb = (int)nb;
     for (int i = 0; i < n_desc; ++i) {
@@ -430,7 +441,8 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
 }
 
 std::string rows_name(const RowsPlan &pl) {
-    return std::string("kq::kq_rows<") + std::to_string(pl.tmask) + ", " + (pl.fusedq ? "true" : "false") + ">";
+    return std::string("kq::kq_rows<") + std::to_string(pl.tmask) + ", " + (pl.fusedq ? "true" : "false") + ", " +
+           std::to_string(pl.a.pro) + ">";
 }
 
 double rows_bytes(const RowsArgs &a, bool fusedq) {
@@ -622,8 +634,66 @@ int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k,
 // One activation column (decode): kq_rows when the rows are contiguous (always for
 // GGUF tensors), kq_gemv otherwise. x is quantized inside the GEMV for K <= 8192
 // (x 16-B aligned), else into `ws` first.
+// With `ext` (fused prologue / residual epilogue): kq_rows applies them in-kernel
+// when it takes the shape with the fused quantizer; otherwise the prologue runs as its
+// own kernel into the front of the workspace and the residual adds follow the GEMV
+// (the same kernels as the separate nodes, so the bits do not depend on the path).
+size_t ext_x_bytes(int64_t k) { return ((size_t)k * 4 + 255) & ~(size_t)255; }
+
 int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *ws, size_t ws_size,
-            hipStream_t stream) {
+            hipStream_t stream, const mi355x_gemv_ext *ext) {
+    const bool has_ext = ext && (ext->prologue != MI355X_PRO_NONE || [&] {
+        for (int i = 0; i < n && i < MI355X_MAX_FUSED; ++i)
+            if (ext->residual[i]) return true;
+        return false;
+    }());
+    if (has_ext) {
+        if (ext->prologue != MI355X_PRO_NONE && !ext->x2) return MI355X_E_INVAL;
+        const bool x2_ok = ext->prologue == MI355X_PRO_NONE || ((uintptr_t)ext->x2 & 15u) == 0;
+        if (rows_enabled() && k / QK <= kRowsFusedMaxNb && ((uintptr_t)x & 15u) == 0 && x2_ok) {
+            RowsPlan rp;
+            const int rc = plan_rows(d, n, k, true, rp);
+            if (rc == MI355X_OK) {
+                rp.a.x = x;
+                rp.a.pro = ext->prologue == MI355X_PRO_RMS_NORM ? ROWS_PRO_NORM
+                           : ext->prologue == MI355X_PRO_SWIGLU ? ROWS_PRO_SWIGLU
+                                                                : ROWS_PRO_NONE;
+                rp.a.x2 = ext->x2;
+                rp.a.eps = ext->eps;
+                rp.fn = pick_rows(rp.tmask, true, rp.a.pro);
+                for (int i = 0; i < n; ++i) {
+                    rp.a.res[i] = ext->residual[i];
+                    rp.a.n_rows[i] = (int)d[i].n_rows;
+                }
+                if (!device_ok()) return MI355X_E_NODEVICE;
+                return launch_rows(rp, stream);
+            }
+            if (rc != MI355X_E_UNSUPPORTED) return rc;
+        }
+        // staged: prologue kernel -> GEMV -> residual adds
+        const float *xs = x;
+        uint8_t *w8 = (uint8_t *)ws;
+        size_t wsz = ws_size;
+        if (ext->prologue != MI355X_PRO_NONE) {
+            if (!ws || ws_size < ext_x_bytes(k) || ((uintptr_t)ws & 15u)) return MI355X_E_WORKSPACE;
+            if (!device_ok()) return MI355X_E_NODEVICE;
+            float *xt = (float *)ws;
+            const int rc = ext->prologue == MI355X_PRO_RMS_NORM ? launch_rms_norm(x, ext->x2, xt, k, 1, ext->eps, stream)
+                                                                : launch_swiglu(x, ext->x2, xt, k, stream);
+            if (rc) return rc;
+            xs = xt;
+            w8 += ext_x_bytes(k);
+            wsz -= ext_x_bytes(k);
+        }
+        int rc = gemv_m1(d, n, xs, k, w8, wsz, stream, nullptr);
+        if (rc) return rc;
+        for (int i = 0; i < n; ++i)
+            if (ext->residual[i] && d[i].n_rows > 0) {
+                rc = launch_binary(0, d[i].y, ext->residual[i], d[i].y, d[i].n_rows, stream);
+                if (rc) return rc;
+            }
+        return MI355X_OK;
+    }
     const bool fusedq = k / QK <= kFusedQMaxNb && ((uintptr_t)x & 15u) == 0;
     const size_t need = (size_t)(k / QK) * 292;
     if (rows_enabled()) {
@@ -773,6 +843,24 @@ int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x,
     for (int i = 0; i < n_desc && i < MI355X_MAX_FUSED; ++i)
         if (descs[i].y && ((uintptr_t)descs[i].y & 3u)) return MI355X_E_INVAL;
     return gemv_m1(descs, n_desc, x, k, workspace, workspace_size, (hipStream_t)stream);
+}
+
+size_t mi355x_gemv_ext_workspace_size(int64_t k) {
+    if (k <= 0 || k % QK) return 0;
+    return ext_x_bytes(k) + mi355x_gemv_fused_workspace_size(k);
+}
+
+int mi355x_gemv_fused_ext(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k,
+                          const mi355x_gemv_ext *ext, void *workspace, size_t workspace_size, void *stream) {
+    if (!descs || !x || ((uintptr_t)x & 3u)) return MI355X_E_INVAL;
+    if (k <= 0 || k % QK || n_desc < 1 || n_desc > MI355X_MAX_FUSED) return MI355X_E_INVAL;
+    if (ext && (ext->prologue < MI355X_PRO_NONE || ext->prologue > MI355X_PRO_SWIGLU)) return MI355X_E_INVAL;
+    if (ext && ext->prologue == MI355X_PRO_RMS_NORM && !(ext->eps >= 0.0f)) return MI355X_E_INVAL;
+    for (int i = 0; i < n_desc; ++i) {
+        if (descs[i].y && ((uintptr_t)descs[i].y & 3u)) return MI355X_E_INVAL;
+        if (ext && ext->residual[i] && ((uintptr_t)ext->residual[i] & 3u)) return MI355X_E_INVAL;
+    }
+    return gemv_m1(descs, n_desc, x, k, workspace, workspace_size, (hipStream_t)stream, ext);
 }
 
 int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,

@@ -40,6 +40,7 @@ struct mi355x_backend {
     hipGraphExec_t graph_exec = nullptr;
     ChainCache chain;
     std::vector<uint32_t *> old_sync;
+    bool fuse = true;
 };
 
 namespace {
@@ -54,53 +55,215 @@ void drop_graph(mi355x_backend *b) {
     b->graph_key.clear();
 }
 
-// One launch: a MUL_MAT node, or a run of ne11 == 1 MUL_MAT nodes sharing src1.
+// One launch: a MUL_MAT node, or a run of ne11 == 1 MUL_MAT nodes sharing src1
+// (kind GEMV, with its fused neighbours), or any other single node.
 struct Launch {
-    int first, count;
+    int first, count;  // nodes[first .. first+count): the MUL_MAT run, or the single node
+    int kind = 0;      // 0 single node, 1 MUL_MAT run
+    int pro = MI355X_PRO_NONE;
+    const float *x = nullptr, *x2 = nullptr;  // GEMV input (prologue source) and its second operand
+    float eps = 0.f;
+    float *y[MI355X_MAX_FUSED] = {};
+    const float *res[MI355X_MAX_FUSED] = {};
+    const float *norm_w = nullptr;  // single RMS_NORM with its MUL fused
+    float *norm_y = nullptr;
 };
 
-std::vector<Launch> plan_launches(mi355x_tensor *const *nodes, int n) {
+float f_of(int32_t bits) {
+    float f;
+    memcpy(&f, &bits, 4);
+    return f;
+}
+
+// readers[i]: number of node operands (over all nodes) that are node i's output.
+std::vector<int> count_readers(mi355x_tensor *const *nodes, int n) {
+    std::vector<int> r(n, 0);
+    for (int j = 0; j < n; ++j)
+        for (int s = 0; s < MI355X_MAX_SRC; ++s) {
+            const mi355x_tensor *u = nodes[j]->src[s];
+            if (!u) continue;
+            for (int i = 0; i < j; ++i)
+                if (nodes[i] == u || (nodes[i]->data && nodes[i]->data == u->data && nodes[i]->op != MI355X_OP_NONE)) {
+                    ++r[i];
+                    break;
+                }
+        }
+    return r;
+}
+
+bool elidable(const mi355x_tensor *t, int readers) {
+    return readers == 1 && !(t->flags & MI355X_TENSOR_FLAG_OUTPUT);
+}
+
+bool is_gemv_node(const mi355x_tensor *t) { return t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] == 1; }
+
+std::vector<Launch> plan_launches(mi355x_tensor *const *nodes, int n, bool fuse) {
     std::vector<Launch> out;
+    const std::vector<int> readers = fuse ? count_readers(nodes, n) : std::vector<int>(n, 0);
+    auto index_of = [&](const mi355x_tensor *u, int lo, int hi) {
+        for (int i = lo; i < hi; ++i)
+            if (nodes[i] == u) return i;
+        return -1;
+    };
     int i = 0;
     while (i < n) {
         const mi355x_tensor *t = nodes[i];
-        int cnt = 1;
-        if (t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] == 1) {
-            while (i + cnt < n && cnt < MI355X_MAX_FUSED) {
-                const mi355x_tensor *u = nodes[i + cnt];
-                if (u->op != MI355X_OP_MUL_MAT || u->src[1]->ne[1] != 1) break;
-                if (u->src[1]->data != t->src[1]->data || u->src[0]->ne[0] != t->src[0]->ne[0]) break;
+        Launch l;
+        l.first = i;
+        l.count = 1;
+        int head = i;  // first MUL_MAT of a run
+        // prologue fusion: RMS_NORM -> MUL -> MUL_MAT run, SWIGLU -> MUL_MAT run
+        if (fuse && t->op == MI355X_OP_RMS_NORM && i + 2 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
+            nodes[i + 1]->src[0] == t && elidable(t, readers[i]) && is_gemv_node(nodes[i + 2]) &&
+            nodes[i + 2]->src[1] == nodes[i + 1] && nodes[i + 1]->ne[0] == t->ne[0] && t->ne[1] == 1) {
+            int cnt = 0;
+            while (i + 2 + cnt < n && cnt < MI355X_MAX_FUSED && is_gemv_node(nodes[i + 2 + cnt]) &&
+                   nodes[i + 2 + cnt]->src[1] == nodes[i + 1])
+                ++cnt;
+            if (readers[i + 1] == cnt && !(nodes[i + 1]->flags & MI355X_TENSOR_FLAG_OUTPUT)) {
+                l.pro = MI355X_PRO_RMS_NORM;
+                l.x = (const float *)t->src[0]->data;
+                l.x2 = (const float *)nodes[i + 1]->src[1]->data;
+                l.eps = f_of(t->op_params[0]);
+                head = i + 2;
+            }
+        } else if (fuse && t->op == MI355X_OP_SWIGLU && i + 1 < n && is_gemv_node(nodes[i + 1]) &&
+                   nodes[i + 1]->src[1] == t && elidable(t, readers[i]) && t->ne[1] == 1) {
+            l.pro = MI355X_PRO_SWIGLU;
+            l.x = (const float *)t->src[0]->data;
+            l.x2 = (const float *)t->src[1]->data;
+            head = i + 1;
+        }
+        const mi355x_tensor *h = nodes[head];
+        if (h->op == MI355X_OP_MUL_MAT && h->src[1]->ne[1] == 1 && (l.pro != MI355X_PRO_NONE || head == i)) {
+            int cnt = 1;
+            while (head + cnt < n && cnt < MI355X_MAX_FUSED) {
+                const mi355x_tensor *u = nodes[head + cnt];
+                if (!is_gemv_node(u)) break;
+                if (u->src[1]->data != h->src[1]->data || u->src[0]->ne[0] != h->src[0]->ne[0]) break;
                 ++cnt;
             }
+            l.kind = 1;
+            l.first = head;
+            l.count = cnt;
+            if (l.pro == MI355X_PRO_NONE) l.x = (const float *)h->src[1]->data;
+            for (int k = 0; k < cnt; ++k) l.y[k] = (float *)nodes[head + k]->data;
+            int end = head + cnt;
+            // epilogue fusion: ADD(mul_mat, residual) right after the run (the last
+            // MUL_MAT's output, or any of the run's outputs, one ADD each)
+            while (fuse && end < n && nodes[end]->op == MI355X_OP_ADD) {
+                const mi355x_tensor *ad = nodes[end];
+                int k = -1, other = -1;
+                for (int s2 = 0; s2 < 2 && k < 0; ++s2) {
+                    const int j = index_of(ad->src[s2], head, head + cnt);
+                    if (j >= 0) {
+                        k = j - head;
+                        other = 1 - s2;
+                    }
+                }
+                if (k < 0 || l.res[k] || !elidable(nodes[head + k], readers[head + k])) break;
+                if (index_of(ad->src[other], i, end) >= 0) break;  // residual produced inside the fused range
+                if (ad->ne[0] != nodes[head + k]->ne[0] || ad->ne[1] != 1 || ad->type != MI355X_TYPE_F32) break;
+                l.res[k] = (const float *)ad->src[other]->data;
+                l.y[k] = (float *)ad->data;
+                ++end;
+            }
+            out.push_back(l);
+            i = end;
+            continue;
         }
-        out.push_back({i, cnt});
-        i += cnt;
+        // single node (with RMS_NORM -> MUL fused when the norm output is only read by the MUL)
+        if (fuse && t->op == MI355X_OP_RMS_NORM && i + 1 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
+            nodes[i + 1]->src[0] == t && elidable(t, readers[i]) && nodes[i + 1]->ne[0] == t->ne[0] &&
+            nodes[i + 1]->src[1]->ne[0] == t->ne[0] && nodes[i + 1]->src[1]->ne[1] == 1) {
+            l.norm_w = (const float *)nodes[i + 1]->src[1]->data;
+            l.norm_y = (float *)nodes[i + 1]->data;
+            l.count = 2;
+        }
+        out.push_back(l);
+        i += l.count;
     }
     return out;
+}
+
+int64_t nelem(const mi355x_tensor *t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
+
+int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
+    hipStream_t st = b->stream;
+    switch (t->op) {
+        case MI355X_OP_NONE:
+            return 0;
+        case MI355X_OP_MUL_MAT: {
+            const mi355x_tensor *w = t->src[0], *x = t->src[1];
+            return mi355x_mul_mat(w->type, w->data, w->ne[0], w->ne[1], w->nb[1], (const float *)x->data, x->ne[1],
+                                  x->nb[1], (float *)t->data, t->nb[1], b->workspace, b->workspace_size, st);
+        }
+        case MI355X_OP_GET_ROWS:
+            return mi355x_get_rows(t->src[0]->type, t->src[0]->data, t->src[0]->ne[0], t->src[0]->nb[1],
+                                   (const int32_t *)t->src[1]->data, t->src[1]->ne[0], (float *)t->data, st);
+        case MI355X_OP_RMS_NORM:
+            if (l.norm_w)
+                return mi355x_rms_norm((const float *)t->src[0]->data, l.norm_w, l.norm_y, t->ne[0], nelem(t) / t->ne[0],
+                                       f_of(t->op_params[0]), st);
+            return mi355x_rms_norm((const float *)t->src[0]->data, nullptr, (float *)t->data, t->ne[0],
+                                   nelem(t) / t->ne[0], f_of(t->op_params[0]), st);
+        case MI355X_OP_MUL:
+            return mi355x_mul((const float *)t->src[0]->data, (const float *)t->src[1]->data, (float *)t->data, nelem(t), st);
+        case MI355X_OP_ADD:
+            return mi355x_add((const float *)t->src[0]->data, (const float *)t->src[1]->data, (float *)t->data, nelem(t), st);
+        case MI355X_OP_SWIGLU:
+            return mi355x_swiglu((const float *)t->src[0]->data, (const float *)t->src[1]->data, (float *)t->data,
+                                 nelem(t), st);
+        case MI355X_OP_ROPE:
+            return mi355x_rope((const float *)t->src[0]->data, (float *)t->data, (int)t->ne[0], t->op_params[0],
+                               (int)(nelem(t) / t->ne[0]), (const int32_t *)t->src[1]->data,
+                               (const float *)t->src[2]->data, (int)t->src[2]->ne[1], st);
+        case MI355X_OP_ATTN_DECODE: {
+            mi355x_attn_desc a;
+            a.q = (const float *)t->src[0]->data;
+            a.k = (const float *)t->src[1]->data;
+            a.v = (const float *)t->src[2]->data;
+            a.pos = (const int32_t *)t->src[3]->data;
+            a.k_cache = (uint16_t *)t->src[4]->data;
+            a.v_cache = (uint16_t *)t->src[5]->data;
+            a.rope_table = (const float *)t->src[6]->data;
+            a.out = (float *)t->data;
+            a.n_head = t->op_params[0];
+            a.n_head_kv = t->op_params[1];
+            a.head_dim = t->op_params[2];
+            a.scale = f_of(t->op_params[3]);
+            a.n_ctx = (int)t->src[4]->ne[1];
+            return mi355x_attn_decode(&a, st);
+        }
+        default:
+            return MI355X_E_UNSUPPORTED;
+    }
 }
 
 int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<Launch> &launches) {
     for (const Launch &l : launches) {
         const mi355x_tensor *t = nodes[l.first];
-        if (t->op == MI355X_OP_NONE) continue;
-        const mi355x_tensor *w = t->src[0], *x = t->src[1];
         int rc;
-        if (l.count > 1 || x->ne[1] == 1) {
+        if (l.kind == 1) {
+            const mi355x_tensor *w = t->src[0];
             mi355x_gemv_desc d[MI355X_MAX_FUSED];
+            mi355x_gemv_ext ext;
+            memset(&ext, 0, sizeof(ext));
+            ext.prologue = l.pro;
+            ext.x2 = l.x2;
+            ext.eps = l.eps;
             for (int k = 0; k < l.count; ++k) {
                 const mi355x_tensor *n = nodes[l.first + k];
                 d[k].type = n->src[0]->type;
                 d[k].w = n->src[0]->data;
                 d[k].n_rows = n->src[0]->ne[1];
                 d[k].row_stride = n->src[0]->nb[1];
-                d[k].y = (float *)n->data;
+                d[k].y = l.y[k];
+                ext.residual[k] = l.res[k];
             }
-            rc = mi355x_gemv_fused(d, l.count, (const float *)x->data, w->ne[0], b->workspace, b->workspace_size,
-                                   b->stream);
+            rc = mi355x_gemv_fused_ext(d, l.count, l.x, w->ne[0], &ext, b->workspace, b->workspace_size, b->stream);
         } else {
-            rc = mi355x_mul_mat(w->type, w->data, w->ne[0], w->ne[1], w->nb[1], (const float *)x->data, x->ne[1],
-                                x->nb[1], (float *)t->data, t->nb[1], b->workspace, b->workspace_size,
-                                b->stream);
+            rc = enqueue_node(b, l, t);
         }
         if (rc) return rc;
     }
@@ -122,7 +285,10 @@ std::vector<uint64_t> graph_key_of(mi355x_tensor *const *nodes, int n_nodes) {
         const mi355x_tensor *t = nodes[i];
         key.push_back((uint64_t)(uintptr_t)t->data);
         key.push_back((uint64_t)t->op);
-        for (int s = 0; s < 2; ++s) {
+        key.push_back((uint64_t)t->flags);
+        for (int d = 0; d < 4; ++d) key.push_back((uint64_t)t->ne[d]);
+        for (int d = 0; d < 8; ++d) key.push_back((uint64_t)(uint32_t)t->op_params[d]);
+        for (int s = 0; s < MI355X_MAX_SRC; ++s) {
             const mi355x_tensor *u = t->src[s];
             if (!u) { key.push_back(0); continue; }
             key.push_back((uint64_t)(uintptr_t)u->data);
@@ -314,20 +480,69 @@ int mi355x_backend_synchronize(mi355x_backend_t b) {
 }
 
 // ggml_backend_device_i::supports_op for this device: MUL_MAT of a contiguous-row
-// K-quant src0 with an f32 src1, 2-D (no broadcast over ne2/ne3).
+// K-quant src0 with an f32 src1, 2-D (no broadcast over ne2/ne3), and the other
+// nodes of a llama decode token on contiguous f32 (the op table in the header).
+static bool contig_f32(const mi355x_tensor *t) { return t && t->type == MI355X_TYPE_F32 && t->nb[0] == 4 && t->data; }
+
 int mi355x_backend_supports_op(const mi355x_tensor *op) {
     if (!op) return 0;
-    if (op->op == MI355X_OP_NONE) return 1;
-    if (op->op != MI355X_OP_MUL_MAT) return 0;
-    const mi355x_tensor *w = op->src[0], *x = op->src[1];
-    if (!w || !x) return 0;
-    if (!is_kquant(w->type) || x->type != MI355X_TYPE_F32 || op->type != MI355X_TYPE_F32) return 0;
-    if (w->ne[0] % MI355X_QK_K || w->ne[0] != x->ne[0]) return 0;
-    if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1) return 0;
-    if (op->ne[0] != w->ne[1] || op->ne[1] != x->ne[1]) return 0;
-    if (x->nb[0] != 4 || op->nb[0] != 4) return 0;  // contiguous rows
-    if (w->nb[0] != mi355x_row_size(w->type, MI355X_QK_K)) return 0;
-    return 1;
+    switch (op->op) {
+        case MI355X_OP_NONE:
+            return 1;
+        case MI355X_OP_MUL_MAT: {
+            const mi355x_tensor *w = op->src[0], *x = op->src[1];
+            if (!w || !x) return 0;
+            if (!is_kquant(w->type) || x->type != MI355X_TYPE_F32 || op->type != MI355X_TYPE_F32) return 0;
+            if (w->ne[0] % MI355X_QK_K || w->ne[0] != x->ne[0]) return 0;
+            if (w->ne[2] != 1 || w->ne[3] != 1 || x->ne[2] != 1 || x->ne[3] != 1) return 0;
+            if (op->ne[0] != w->ne[1] || op->ne[1] != x->ne[1]) return 0;
+            if (x->nb[0] != 4 || op->nb[0] != 4) return 0;  // contiguous rows
+            if (w->nb[0] != mi355x_row_size(w->type, MI355X_QK_K)) return 0;
+            return 1;
+        }
+        case MI355X_OP_GET_ROWS: {
+            const mi355x_tensor *w = op->src[0], *ids = op->src[1];
+            if (!w || !ids || ids->type != MI355X_TYPE_I32 || !contig_f32(op)) return 0;
+            if (w->type != MI355X_TYPE_F32 && w->type != MI355X_TYPE_Q4_K && w->type != MI355X_TYPE_Q6_K) return 0;
+            return op->ne[0] == w->ne[0] && op->ne[1] == ids->ne[0] && w->ne[0] % MI355X_QK_K == 0;
+        }
+        case MI355X_OP_RMS_NORM:
+            return contig_f32(op) && contig_f32(op->src[0]) && op->ne[0] % MI355X_QK_K == 0 &&
+                   op->nb[1] == (size_t)op->ne[0] * 4;
+        case MI355X_OP_MUL:
+        case MI355X_OP_ADD:
+        case MI355X_OP_SWIGLU:
+            return contig_f32(op) && contig_f32(op->src[0]) && contig_f32(op->src[1]) &&
+                   nelem(op->src[0]) == nelem(op) && nelem(op->src[1]) == nelem(op);
+        case MI355X_OP_ROPE:
+            return contig_f32(op) && contig_f32(op->src[0]) && op->src[1] && op->src[1]->type == MI355X_TYPE_I32 &&
+                   contig_f32(op->src[2]) && op->op_params[0] > 0 && op->op_params[0] <= op->ne[0] &&
+                   op->src[2]->ne[0] == op->op_params[0];
+        case MI355X_OP_ATTN_DECODE: {
+            for (int s = 0; s < 7; ++s)
+                if (!op->src[s] || !op->src[s]->data) return 0;
+            const int nh = op->op_params[0], nkv = op->op_params[1], hd = op->op_params[2];
+            if ((hd != 64 && hd != 128) || nkv <= 0 || nh % nkv) return 0;
+            if (op->src[4]->type != MI355X_TYPE_F16 || op->src[5]->type != MI355X_TYPE_F16) return 0;
+            if (op->src[4]->ne[0] != (int64_t)nkv * hd || op->src[3]->type != MI355X_TYPE_I32) return 0;
+            if (op->src[5]->ne[0] != op->src[4]->ne[1] || op->src[6]->ne[1] < op->src[4]->ne[1]) return 0;
+            if (op->src[6]->ne[0] != hd) return 0;
+            return contig_f32(op) && op->ne[0] == (int64_t)nh * hd;
+        }
+        default:
+            return 0;
+    }
+}
+
+int mi355x_backend_set_fusion(mi355x_backend_t b, int enable) {
+    if (!b) return MI355X_E_INVAL;
+    const int prev = b->fuse ? 1 : 0;
+    if ((enable != 0) != b->fuse) {
+        hipStreamSynchronize(b->stream);
+        drop_graph(b);
+        b->fuse = enable != 0;
+    }
+    return prev;
 }
 
 int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes, int n_nodes, int use_graph) {
@@ -338,7 +553,7 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
         if (nodes[i]->op == MI355X_OP_MUL_MAT) {
             const mi355x_tensor *w = nodes[i]->src[0];
             size_t need = mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], nodes[i]->src[1]->ne[1]);
-            const size_t nf = mi355x_gemv_fused_workspace_size(w->ne[0]);
+            const size_t nf = mi355x_gemv_ext_workspace_size(w->ne[0]);
             need = need > nf ? need : nf;
             if (nodes[i]->src[1]->ne[1] == 1 && ((uintptr_t)nodes[i]->src[1]->data & 15u))
                 need = need > (size_t)(w->ne[0] / 256) * kq::Q8L_STRIDE ? need : (size_t)(w->ne[0] / 256) * kq::Q8L_STRIDE;
@@ -354,7 +569,7 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
         if (hipMalloc(&b->workspace, ws) != hipSuccess) return MI355X_E_WORKSPACE;
         b->workspace_size = ws;
     }
-    const std::vector<Launch> launches = plan_launches(nodes, n_nodes);
+    const std::vector<Launch> launches = plan_launches(nodes, n_nodes, b->fuse);
     const bool try_chain = kq::chain_enabled() && launches.size() >= 2;
     if (!use_graph && !try_chain) return enqueue(b, nodes, launches);
     std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);

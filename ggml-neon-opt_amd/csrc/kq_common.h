@@ -103,7 +103,14 @@ struct RowsArgs {
     const uint8_t *xq;    // Q8L activation row (!FUSEDQ), written by kq_quantize_q8L
     uint64_t *stamps;
     int64_t stamps_cap;
+    // fused neighbours of the MUL_MAT in the decode graph (FUSEDQ only):
+    int pro;              // ROWS_PRO_*: transform of x before its Q8_K quantization
+    float eps;            // ROWS_PRO_NORM: rms_norm epsilon
+    const float *x2;      // ROWS_PRO_NORM: norm weight (the MUL after RMS_NORM); ROWS_PRO_SWIGLU: up (x = gate)
+    const float *res[MI355X_MAX_FUSED];  // y[m] = mul_mat + res[m] (the ADD after the MUL_MAT), or null
+    int n_rows[MI355X_MAX_FUSED];
 };
+constexpr int ROWS_PRO_NONE = 0, ROWS_PRO_NORM = 1, ROWS_PRO_SWIGLU = 2;
 
 // One step = 16 consecutive superblocks of a wave's row stream (2304 / 2816 / 3360
 // B), fetched as 16-B granules from the 16-B boundary below them (+1 granule of
@@ -132,7 +139,7 @@ __host__ __device__ constexpr int rows_ring(int tmask) {
 //   recs: per wave bR*nb chain records (16 B), block-major [blk][row]
 //   outs: per wave rpw staged results
 struct RowsLayout {
-    int act, ring, ring_stride, recs, recs_stride, outs, outs_stride, total;
+    int act, ring, ring_stride, recs, recs_stride, outs, outs_stride, sums, total;
 };
 __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int rpw) {
     RowsLayout L;
@@ -143,11 +150,24 @@ __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int
     L.recs_stride = bR * nb * 16;
     L.outs = L.recs + ROWS_WAVES * L.recs_stride;
     L.outs_stride = (rpw * 4 + 15) & ~15;
-    L.total = L.outs + ROWS_WAVES * L.outs_stride;
+    L.sums = L.outs + ROWS_WAVES * L.outs_stride;  // ROWS_PRO_NORM: per-superblock sums of squares (double)
+    L.total = L.sums + nb * 8;
     return L;
 }
 
 // ---------------------------------------------------------------- persistent decode chain
+// Decode attention block (kq_ops.hip): one workgroup per query head.
+struct AttnArgs {
+    const float *q, *k, *v;       // projections of this token (before rope)
+    const int32_t *pos;           // device: the token's position (cache cell)
+    const float *rope_table;      // [n_ctx][head_dim/2][cos, sin]
+    uint16_t *k_cache;            // f16 [n_ctx][n_head_kv*head_dim]
+    uint16_t *v_cache;            // f16 [n_head_kv*head_dim][n_ctx] (transposed, non-FA layout)
+    float *out;                   // [n_head*head_dim]
+    int n_ctx, n_head, n_head_kv, head_dim;
+    float scale;
+};
+
 // kq_chain: one launch runs a whole sequence of decode MUL_MAT stages (a token's
 // graph). Each stage is planned exactly like one kq_rows launch (same wave split,
 // same per-row arithmetic); the grid is one ROWS_WAVES workgroup per CU for every

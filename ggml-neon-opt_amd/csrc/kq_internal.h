@@ -2,11 +2,15 @@
 // backend mirror (kq_backend.hip). Not part of the public ABI.
 #pragma once
 
+#include <string>
+
 #include "kq_common.h"
 
 namespace kq {
 
 int device_ok();
+bool timing_slot(hipStream_t s, hipEvent_t &a, hipEvent_t &b);
+void timing_log(const std::string &kernel, double bytes, hipEvent_t a, hipEvent_t b);
 int num_cus();
 int choose_ncol(int64_t M, int nb);
 typedef void (*gemv_fn)(const GemvArgs);
@@ -47,5 +51,11 @@ int chain_layout(const ChainFit &fit, ChainArgs &a, size_t &lds);
 int launch_chain(const ChainArgs &a, size_t lds, double bytes, hipStream_t stream);
 int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
                     hipStream_t stream);
+int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *ws, size_t ws_size,
+            hipStream_t stream, const mi355x_gemv_ext *ext = nullptr);
+// kq_ops.hip
+int launch_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t nrows, float eps, hipStream_t s);
+int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s);  // 0 add, 1 mul
+int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream_t s);
 
 }  // namespace kq

@@ -1,0 +1,488 @@
+// kq_ops.hip — the non-matmul ops of a llama decode token on gfx950 (SURVEY.md §8f
+// rank 4): get_rows, rms_norm (+ its weight MUL), add, mul, swiglu, rope and the
+// decode attention block (rope + f16 KV-cache write + KQ + soft_max + KQV).
+//
+// Reference functions (ggml-cpu @ a3cb0474 [U], as profiled in
+// artifacts/perf/out.folded; restated for the tests on the CPU side):
+//   get_rows  ggml_compute_forward_get_rows_q -> dequantize_row_q4_K   :103-104
+//   rms_norm  ggml_compute_forward_rms_norm_f32                        :189-193
+//   mul/add   binary_op<op_mul>/<op_add>                               :91-99, :115-121
+//   swiglu    ggml_vec_swiglu_f32 (ggml_v_silu)                        :107-113
+//   rope      ggml_compute_forward_rope_f32 (ggml_rope_cache_init, rope_yarn) :196-208
+//   attention set_rows (f32->f16), mul_mat(f16) -> ggml_vec_dot_f16, soft_max_f32
+//             (ggml_vec_soft_max_f32, ggml_v_expf), mul_mat(f16)       :140-144, :176, :209-234
+// Every kernel reproduces the reference's arithmetic op for op (see kq_ops_device.h);
+// these ops are HBM/latency-bound and tiny at decode, so the layout work is about
+// launch count (they fuse into the GEMVs where the graph allows, kq_rows.hip).
+#include <math.h>
+#include <string.h>
+
+#include <mutex>
+#include <vector>
+
+#include <hip/hip_ext.h>
+
+#include "kq_common.h"
+#include "kq_internal.h"
+#include "kq_device.h"
+#include "kq_ops_device.h"
+
+namespace kq {
+
+// ------------------------------------------------------------ get_rows
+// One workgroup per (id, 2048-element chunk); thread t dequantizes 8 consecutive
+// elements. Q4_K: y = fmaf(d*sc, q, -(dmin*m)) (gcc contracts `d1*q - m1` [U]);
+// Q6_K: y = (d*sc)*q; F32: copy.
+__global__ void __launch_bounds__(256) kq_get_rows(int type, const uint8_t *__restrict__ table, int64_t k,
+                                                   int64_t row_stride, const int32_t *__restrict__ ids,
+                                                   float *__restrict__ out) {
+    const int64_t r = blockIdx.y;
+    const int64_t e0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
+    if (e0 >= k) return;
+    const uint8_t *row = table + (int64_t)ids[r] * row_stride;
+    float *y = out + r * k + e0;
+    if (type == MI355X_TYPE_F32) {
+        const float *s = (const float *)row + e0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[i] = s[i];
+        return;
+    }
+    const int64_t b = e0 / QK;
+    const int e = (int)(e0 % QK);
+    if (type == MI355X_TYPE_Q4_K) {
+        const uint8_t *blk = row + b * 144;
+        const float d = h2f(*(const uint16_t *)blk), dmin = h2f(*(const uint16_t *)(blk + 2));
+        const uint8_t *sc = blk + 4;
+        const int j = e / 64, h = (e / 32) & 1, l0 = e % 32;
+        const int is = 2 * j + h;
+        int s, m;
+        if (is < 4) {
+            s = sc[is] & 63;
+            m = sc[is + 4] & 63;
+        } else {
+            s = (sc[is + 4] & 0xF) | ((sc[is - 4] >> 6) << 4);
+            m = (sc[is + 4] >> 4) | ((sc[is] >> 6) << 4);
+        }
+        const float d1 = d * (float)s, m1 = dmin * (float)m;
+        const uint8_t *q = blk + 16 + 32 * j + l0;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[i] = __builtin_fmaf(d1, (float)((q[i] >> (4 * h)) & 0xF), -m1);
+    } else {  // Q6_K
+        const uint8_t *blk = row + b * 210;
+        const float d = h2f((uint16_t)(blk[208] | (blk[209] << 8)));
+        const int half = e / 128, rr = e % 128, quarter = rr / 32, l0 = rr % 32;
+        const uint8_t *ql = blk + 64 * half, *qh = blk + 128 + 32 * half;
+        const int8_t *sc = (const int8_t *)(blk + 192) + 8 * half;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int l = l0 + i;
+            int q;
+            if (quarter == 0) q = (ql[l] & 0xF) | (((qh[l] >> 0) & 3) << 4);
+            else if (quarter == 1) q = (ql[l + 32] & 0xF) | (((qh[l] >> 2) & 3) << 4);
+            else if (quarter == 2) q = (ql[l] >> 4) | (((qh[l] >> 4) & 3) << 4);
+            else q = (ql[l + 32] >> 4) | (((qh[l] >> 6) & 3) << 4);
+            y[i] = d * (float)sc[l / 16 + 2 * quarter] * (float)(q - 32);
+        }
+    }
+}
+
+// ------------------------------------------------------------ rms_norm (+ mul)
+// One workgroup per row, 256 threads = 16 rows of 16 lanes; lane l of a row owns
+// elements [16l, 16l+16) of one superblock per pass. Sum order: kq_ops_device.h.
+__global__ void __launch_bounds__(256) kq_rms_norm(const float *__restrict__ x, const float *__restrict__ w,
+                                                   float *__restrict__ y, int64_t n, float eps) {
+    extern __shared__ double sb_sum[];
+    const int64_t row = blockIdx.x;
+    const float *xr = x + row * n;
+    float *yr = y + row * n;
+    const int nb = (int)(n / QK);
+    const int rid = threadIdx.x >> 4, l = threadIdx.x & 15;
+    for (int b0 = 0; b0 < nb; b0 += 16) {
+        const int b = b0 + rid;
+        double s = 0.0;
+        if (b < nb) {
+            float v[16];
+            const float4 *p = (const float4 *)(xr + (int64_t)b * QK + 16 * l);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 t = p[k];
+                v[4 * k] = t.x, v[4 * k + 1] = t.y, v[4 * k + 2] = t.z, v[4 * k + 3] = t.w;
+            }
+            s = sumsq16(v);
+        }
+        s = row16_sum(s);
+        if (b < nb && l == 0) sb_sum[b] = s;
+    }
+    __syncthreads();
+    double total = 0.0;
+    for (int b = 0; b < nb; ++b) total += sb_sum[b];
+    const float mean = (float)(total / (double)n);
+    const float scale = 1.0f / sqrtf(mean + eps);
+    for (int64_t i = threadIdx.x; i < n; i += 256) {
+        const float v = xr[i] * scale;
+        yr[i] = w ? v * w[i] : v;
+    }
+}
+
+// ------------------------------------------------------------ elementwise
+__global__ void __launch_bounds__(256) kq_binary(int op, const float *__restrict__ a, const float *__restrict__ b,
+                                                 float *__restrict__ y, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        y[i] = op == 0 ? a[i] + b[i] : a[i] * b[i];
+}
+
+// ggml_vec_swiglu_f32: NEON body for the first n & ~3 elements, libm tail otherwise.
+__global__ void __launch_bounds__(256) kq_swiglu(const float *__restrict__ g, const float *__restrict__ u,
+                                                 float *__restrict__ y, int64_t n) {
+    const int64_t n4 = n & ~(int64_t)3;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
+        y[i] = i < n4 ? v_silu(g[i]) * u[i] : (g[i] / (1.0f + expf(-g[i]))) * u[i];
+}
+
+// rotate_pairs (GGML_ROPE_TYPE_NORMAL) with the position's cos/sin row of the table;
+// x0*c - x1*s -> fmaf(x0, c, -(x1*s)), x0*s + x1*c -> fmaf(x0, s, x1*c) [U].
+__device__ __forceinline__ float2 rope_pair(float x0, float x1, float c, float s) {
+    return make_float2(__builtin_fmaf(x0, c, -(x1 * s)), __builtin_fmaf(x0, s, x1 * c));
+}
+
+__global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, float *__restrict__ y, int head_dim,
+                                               int n_dims, int n_heads, const int32_t *__restrict__ pos_p,
+                                               const float *__restrict__ table, int n_pos) {
+    const int pos = *pos_p;
+    const int per = head_dim / 2;
+    const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;  // pair index
+    if (i >= (int64_t)n_heads * per) return;
+    const int h = (int)(i / per), p = (int)(i % per);
+    const float *s = x + (int64_t)h * head_dim + 2 * p;
+    float *d = y + (int64_t)h * head_dim + 2 * p;
+    if (pos < 0 || pos >= n_pos) {  // outside the table: NaN, never a silent result
+        d[0] = d[1] = __builtin_nanf("");
+        return;
+    }
+    if (2 * p >= n_dims) {
+        d[0] = s[0];
+        d[1] = s[1];
+        return;
+    }
+    const float *cs = table + ((int64_t)pos * (n_dims / 2) + p) * 2;
+    const float2 r = rope_pair(s[0], s[1], cs[0], cs[1]);
+    d[0] = r.x;
+    d[1] = r.y;
+}
+
+// ------------------------------------------------------------ decode attention
+// One workgroup per query head h (kv head g = h / (n_head/n_head_kv)), 256 threads.
+//  1. rope(q_h), rope(k_g) at `pos` -> f16; v_g -> f16. The first query head of each
+//     kv group writes the new cell to the caches (K [cell][kvw], V transposed
+//     [ch][n_ctx]); every workgroup uses its own LDS copy of that cell, so no
+//     workgroup reads a cache cell written in this launch.
+//  2. kq[c] = vec_dot_f16(k_cache[c], q16) for c <= pos (NEON FP16 structure), * scale;
+//     cells pos < c < n_kv are masked (-INF) and contribute exact zeros below
+//     (the cache is zero-initialised, so their dot products are finite).
+//  3. soft_max: max; v_expf(w - max) per cell, group sums of 4 in the vaddvq order,
+//     the double sum over groups in order (one lane), p = e * (float)(1.0/sum) -> f16.
+//  4. kqv[d] = vec_dot_f16(v_cache[g*hd+d][0..n_kv), p16): thread (d, j) runs
+//     accumulator j (8 lanes) over cells 32it+8j+l, then the f16 reduce tree.
+template <int HD>
+__global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
+    static_assert(HD % 32 == 0 && HD <= 256, "head_dim");
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int h = blockIdx.x;
+    const int gsz = a.n_head / a.n_head_kv;
+    const int g = h / gsz;
+    const int kvw = a.n_head_kv * HD;
+    const int pos = *a.pos;
+    if (pos < 0 || pos >= a.n_ctx) {  // no cache cell for this position: fail loudly (NaN), touch nothing
+        for (int d = threadIdx.x; d < HD; d += 256) a.out[(int64_t)h * HD + d] = __builtin_nanf("");
+        return;
+    }
+    int n_kv = (pos + 1 + 31) / 32 * 32;
+    n_kv = n_kv < 32 ? 32 : n_kv;
+    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
+    const int t = threadIdx.x;
+    // LDS (attn_lds): q16 | k16 | v16 (HD f16 each) | w (n_ctx f32) | p16 (n_ctx f16) |
+    // red (HD*32 f16 accumulators) | scal (max, 1/sum); every piece 16-B aligned
+    uint16_t *q16 = (uint16_t *)smem;
+    uint16_t *k16 = q16 + HD;
+    uint16_t *v16 = k16 + HD;
+    float *w = (float *)(smem + 6 * HD);
+    uint16_t *p16 = (uint16_t *)(w + a.n_ctx);
+    h16 *red = (h16 *)(p16 + a.n_ctx);
+    float *scal = (float *)(red + HD * 32);
+
+    const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
+    const bool writer = (h % gsz) == 0;
+    if (t < HD / 2) {
+        const float c = tc[2 * t], s = tc[2 * t + 1];
+        const float *qp = a.q + (int64_t)h * HD + 2 * t;
+        const float2 rq = rope_pair(qp[0], qp[1], c, s);
+        q16[2 * t] = h2u(f2h_rne(rq.x));
+        q16[2 * t + 1] = h2u(f2h_rne(rq.y));
+        const float *kp = a.k + (int64_t)g * HD + 2 * t;
+        const float2 rk = rope_pair(kp[0], kp[1], c, s);
+        const uint16_t k0 = h2u(f2h_rne(rk.x)), k1 = h2u(f2h_rne(rk.y));
+        k16[2 * t] = k0;
+        k16[2 * t + 1] = k1;
+        if (writer) *(uint32_t *)(a.k_cache + (int64_t)pos * kvw + (int64_t)g * HD + 2 * t) = k0 | ((uint32_t)k1 << 16);
+    } else if (t < HD / 2 + HD) {
+        const int d = t - HD / 2;
+        const uint16_t vv = h2u(f2h_rne(a.v[(int64_t)g * HD + d]));
+        v16[d] = vv;
+        if (writer) a.v_cache[(int64_t)(g * HD + d) * a.n_ctx + pos] = vv;
+    }
+    __syncthreads();
+
+    // KQ + scale + mask
+    for (int c = t; c < n_kv; c += 256) {
+        float s = -INFINITY;
+        if (c <= pos) {
+            const uint4 *kr = c == pos ? (const uint4 *)k16 : (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+            uint4 kv[HD / 8];
+#pragma unroll
+            for (int i = 0; i < HD / 8; ++i) kv[i] = kr[i];
+            s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+        }
+        w[c] = s;
+    }
+    __syncthreads();
+    // max (order-free), then exp + group sums
+    if (t < 64) {
+        float m = -INFINITY;
+        for (int c = t; c < n_kv; c += 64) m = fmaxf(m, w[c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if (t == 0) scal[0] = m;
+    }
+    __syncthreads();
+    const float mx = scal[0];
+    for (int gi = t; gi < n_kv / 4; gi += 256) {
+        float e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float wv = w[4 * gi + k];
+            e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
+    }
+    __syncthreads();
+    if (t == 0) {
+        double sum = 0.0;
+        for (int gi = 0; gi < n_kv / 4; ++gi)
+            sum += (double)((w[4 * gi] + w[4 * gi + 1]) + (w[4 * gi + 2] + w[4 * gi + 3]));
+        sum = 1.0 / sum;
+        scal[1] = (float)sum;
+    }
+    __syncthreads();
+    const float inv = scal[1];
+    for (int c = t; c < n_kv; c += 256) p16[c] = h2u(f2h_rne(w[c] * inv));
+    __syncthreads();
+
+    // KQV: thread (d, j) -> accumulator j of output d
+    const int n_it = (pos + 32) / 32;  // iterations holding a cell <= pos; later ones add exact zeros
+    for (int item = t; item < HD * 4; item += 256) {
+        const int d = item >> 2, j = item & 3;
+        const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
+        h16 acc[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc[l] = (h16)0.0f;
+        for (int it = 0; it < n_it; ++it) {
+            const int c0 = 32 * it + 8 * j;
+            uint4 vv = *(const uint4 *)(vr + c0);
+            const uint4 pp = *(const uint4 *)(p16 + c0);
+            uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
+            const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+            if (pos >= c0 && pos < c0 + 8) {  // the new cell: LDS copy
+                const int l = pos - c0;
+                vw[l >> 1] = (vw[l >> 1] & (0xffff0000u >> (16 * (l & 1)))) | ((uint32_t)v16[d] << (16 * (l & 1)));
+            }
+#pragma unroll
+            for (int l = 0; l < 8; ++l)
+                acc[l] = hfma(u2h((uint16_t)(vw[l >> 1] >> (16 * (l & 1)))), u2h((uint16_t)(pw[l >> 1] >> (16 * (l & 1)))),
+                              acc[l]);
+        }
+#pragma unroll
+        for (int l = 0; l < 8; ++l) red[(d * 4 + j) * 8 + l] = acc[l];
+    }
+    __syncthreads();
+    for (int d = t; d < HD; d += 256) {
+        h16 s[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const h16 s0 = red[(d * 4 + 0) * 8 + l] + red[(d * 4 + 2) * 8 + l];
+            const h16 s1 = red[(d * 4 + 1) * 8 + l] + red[(d * 4 + 3) * 8 + l];
+            s[l] = s0 + s1;
+        }
+        a.out[(int64_t)h * HD + d] = f16x8_reduce(s);
+    }
+}
+
+size_t attn_lds(int hd, int n_ctx) { return (size_t)6 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16; }
+
+// ------------------------------------------------------------ launch helpers
+int check_launch() {
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+template <typename K, typename... Args>
+int timed_launch(const char *name, double bytes, K kern, dim3 grid, dim3 block, size_t lds, hipStream_t s,
+                 Args... args) {
+    hipEvent_t e0, e1;
+    if (timing_slot(s, e0, e1)) {
+        hipExtLaunchKernelGGL(kern, grid, block, (uint32_t)lds, s, e0, e1, 0, args...);
+        timing_log(name, bytes, e0, e1);
+    } else {
+        hipLaunchKernelGGL(kern, grid, block, lds, s, args...);
+    }
+    return check_launch();
+}
+
+int elem_grid(int64_t n) {
+    int64_t g = (n + 255) / 256;
+    return (int)(g < 4096 ? (g > 0 ? g : 1) : 4096);
+}
+
+int launch_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t nrows, float eps, hipStream_t s) {
+    if (nrows == 0) return MI355X_OK;
+    return timed_launch("kq::kq_rms_norm", (double)nrows * n * 8 + (w ? n * 4.0 : 0.0), kq_rms_norm,
+                        dim3((unsigned)nrows), dim3(256), (size_t)(n / QK) * 8 + 8, s, x, w, y, n, eps);
+}
+
+int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s) {
+    if (n == 0) return MI355X_OK;
+    return timed_launch(op == 0 ? "kq::kq_add" : "kq::kq_mul", n * 12.0, kq_binary, dim3(elem_grid(n)), dim3(256), 0,
+                        s, op, a, b, y, n);
+}
+
+int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream_t s) {
+    if (n == 0) return MI355X_OK;
+    return timed_launch("kq::kq_swiglu", n * 12.0, kq_swiglu, dim3(elem_grid(n)), dim3(256), 0, s, g, u, y, n);
+}
+
+int launch_attn(const AttnArgs &a, hipStream_t s) {
+    const size_t lds = attn_lds(a.head_dim, a.n_ctx);
+    const double bytes = 0;  // context-dependent; not a roofline kernel
+    if (a.head_dim == 64)
+        return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64>, dim3(a.n_head), dim3(256), lds, s, a);
+    return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128>, dim3(a.n_head), dim3(256), lds, s, a);
+}
+
+int check_attn(const AttnArgs &a) {
+    if (!a.q || !a.k || !a.v || !a.pos || !a.rope_table || !a.k_cache || !a.v_cache || !a.out) return MI355X_E_INVAL;
+    if (a.head_dim != 64 && a.head_dim != 128) return MI355X_E_UNSUPPORTED;
+    if (a.n_head <= 0 || a.n_head_kv <= 0 || a.n_head % a.n_head_kv) return MI355X_E_INVAL;
+    if (a.n_ctx < 32 || a.n_ctx % 32 || a.n_ctx > 8192) return MI355X_E_UNSUPPORTED;
+    if (((uintptr_t)a.k_cache & 15u) || ((uintptr_t)a.v_cache & 15u)) return MI355X_E_INVAL;
+    if (attn_lds(a.head_dim, a.n_ctx) > 64 * 1024) return MI355X_E_UNSUPPORTED;
+    return MI355X_OK;
+}
+
+}  // namespace kq
+
+using namespace kq;
+
+extern "C" {
+
+int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, const int32_t *ids, int64_t n_ids,
+                    float *dst, void *stream) {
+    if (!table || !ids || !dst || ne0 <= 0 || n_ids < 0) return MI355X_E_INVAL;
+    if (type != MI355X_TYPE_F32 && type != MI355X_TYPE_Q4_K && type != MI355X_TYPE_Q6_K) return MI355X_E_UNSUPPORTED;
+    if (ne0 % (type == MI355X_TYPE_F32 ? 8 : QK)) return MI355X_E_INVAL;
+    if (row_stride < mi355x_row_size(type, ne0) && type != MI355X_TYPE_F32) return MI355X_E_INVAL;
+    if (n_ids == 0) return MI355X_OK;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    const dim3 grid((unsigned)((ne0 / 8 + 255) / 256), (unsigned)n_ids);
+    return timed_launch("kq::kq_get_rows", (double)n_ids * (ne0 * 4.0 + (double)mi355x_row_size(type, ne0)),
+                        kq_get_rows, grid, dim3(256), 0, (hipStream_t)stream, type, (const uint8_t *)table, ne0,
+                        (int64_t)row_stride, ids, dst);
+}
+
+int mi355x_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t nrows, float eps, void *stream) {
+    if (!x || !y || n <= 0 || nrows < 0 || !(eps >= 0.0f)) return MI355X_E_INVAL;
+    if (n % QK || ((uintptr_t)x & 15u)) return MI355X_E_UNSUPPORTED;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_rms_norm(x, w, y, n, nrows, eps, (hipStream_t)stream);
+}
+
+int mi355x_add(const float *a, const float *b, float *y, int64_t n, void *stream) {
+    if (!a || !b || !y || n < 0) return MI355X_E_INVAL;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_binary(0, a, b, y, n, (hipStream_t)stream);
+}
+
+int mi355x_mul(const float *a, const float *b, float *y, int64_t n, void *stream) {
+    if (!a || !b || !y || n < 0) return MI355X_E_INVAL;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_binary(1, a, b, y, n, (hipStream_t)stream);
+}
+
+int mi355x_swiglu(const float *gate, const float *up, float *y, int64_t n, void *stream) {
+    if (!gate || !up || !y || n < 0) return MI355X_E_INVAL;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_swiglu(gate, up, y, n, (hipStream_t)stream);
+}
+
+size_t mi355x_rope_table_size(int n_pos, int n_dims) {
+    if (n_pos <= 0 || n_dims <= 0 || n_dims % 2) return 0;
+    return (size_t)n_pos * (size_t)(n_dims / 2) * 2 * sizeof(float);
+}
+
+// ggml_rope_cache_init / rope_yarn (ext_factor 0, attn_factor 1, no freq_factors) for
+// every position, built on the host with the C library's powf/cosf/sinf (the
+// functions the CPU path calls) and copied to the device table.
+int mi355x_rope_table(float *table, int n_pos, int n_dims, float freq_base, float freq_scale, void *stream) {
+    const size_t bytes = mi355x_rope_table_size(n_pos, n_dims);
+    if (!table || !bytes || !(freq_base > 0.0f)) return MI355X_E_INVAL;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    std::vector<float> host(bytes / sizeof(float));
+    const float theta_scale = powf(freq_base, -2.0f / (float)n_dims);
+    for (int p = 0; p < n_pos; ++p) {
+        float theta = (float)p;
+        for (int i = 0; i < n_dims / 2; ++i) {
+            const float th = freq_scale * theta;
+            host[((size_t)p * (n_dims / 2) + i) * 2 + 0] = cosf(th) * 1.0f;
+            host[((size_t)p * (n_dims / 2) + i) * 2 + 1] = sinf(th) * 1.0f;
+            theta *= theta_scale;
+        }
+    }
+    hipError_t e = hipMemcpyAsync(table, host.data(), bytes, hipMemcpyHostToDevice, (hipStream_t)stream);
+    if (e == hipSuccess) e = hipStreamSynchronize((hipStream_t)stream);
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+int mi355x_rope(const float *x, float *y, int head_dim, int n_dims, int n_heads, const int32_t *pos,
+                const float *table, int n_pos, void *stream) {
+    if (!x || !y || !pos || !table || head_dim <= 0 || head_dim % 2 || n_dims % 2 || n_dims > head_dim ||
+        n_heads < 0 || n_pos <= 0)
+        return MI355X_E_INVAL;
+    if (n_heads == 0) return MI355X_OK;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    const int64_t pairs = (int64_t)n_heads * (head_dim / 2);
+    return timed_launch("kq::kq_rope", pairs * 16.0, kq_rope, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
+                        (hipStream_t)stream, x, y, head_dim, n_dims, n_heads, pos, table, n_pos);
+}
+
+int mi355x_attn_decode(const mi355x_attn_desc *d, void *stream) {
+    if (!d) return MI355X_E_INVAL;
+    AttnArgs a;
+    a.q = d->q;
+    a.k = d->k;
+    a.v = d->v;
+    a.pos = d->pos;
+    a.rope_table = d->rope_table;
+    a.k_cache = d->k_cache;
+    a.v_cache = d->v_cache;
+    a.out = d->out;
+    a.n_ctx = d->n_ctx;
+    a.n_head = d->n_head;
+    a.n_head_kv = d->n_head_kv;
+    a.head_dim = d->head_dim;
+    a.scale = d->scale;
+    const int rc = check_attn(a);
+    if (rc) return rc;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_attn(a, (hipStream_t)stream);
+}
+
+}  // extern "C"

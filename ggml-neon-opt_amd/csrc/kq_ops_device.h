@@ -1,0 +1,116 @@
+// kq_ops_device.h — device arithmetic of the non-matmul decode ops, written to give
+// the same bits as ggml-cpu's aarch64 build (restated for the tests on the CPU side):
+//   * ggml_v_expf (NEON) lane by lane: same constants, same fused ops (vfmaq_f32 ->
+//     fmaf, vfmsq_f32 -> fmaf(-b, c, a)), same integer exponent tricks;
+//   * ggml_v_silu: x / (1 + v_expf(0 - x)) with a correctly rounded divide;
+//   * binary16 FMA / add (vfmaq_f16 / vaddq_f16) on the f16 ALU (v_fma_f16, v_add_f16:
+//     IEEE, one rounding, f16 denormals kept);
+//   * the RMS-norm sum of squares in a FIXED order shared by every kernel that
+//     computes it (kq_rms_norm and the kq_rows norm prologue): per 16 consecutive
+//     elements a sequential double sum, a balanced tree over the 16 groups of a
+//     256-element superblock, then superblocks in order. ggml sums sequentially in
+//     double (ggml_compute_forward_rms_norm_f32); the two orders can differ only in
+//     the last bits of the double, which reach the float mean only when it lies
+//     within ~2^-40 (relative) of a rounding boundary.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace kq {
+
+__device__ __forceinline__ float v_expf(float x) {
+    const float r = 0x1.8p23f;
+    const float z = __builtin_fmaf(x, 0x1.715476p+0f, r);
+    const float n = z - r;
+    const float b = __builtin_fmaf(-n, 0x1.7f7d1cp-20f, __builtin_fmaf(-n, 0x1.62e4p-1f, x));
+    const uint32_t e = __float_as_uint(z) << 23;
+    const float k = __uint_as_float(e + 0x3f800000u);
+    const float u = b * b;
+    const float j = __builtin_fmaf(
+        __builtin_fmaf(__builtin_fmaf(0x1.0e4020p-7f, b, 0x1.573e2ep-5f), u, __builtin_fmaf(0x1.555e66p-3f, b, 0x1.fffdb6p-2f)),
+        u, 0x1.ffffecp-1f * b);
+    const float an = __builtin_fabsf(n);
+    if (!(an > 126.0f)) return __builtin_fmaf(k, j, k);
+    const uint32_t d = n <= 0.0f ? 0x82000000u : 0u;
+    const float s1 = __uint_as_float(d + 0x7f000000u);
+    const float s2 = __uint_as_float(e - d);
+    if (an > 192.0f) return s1 * s1;
+    return __builtin_fmaf(s2, j, s2) * s1;
+}
+
+__device__ __forceinline__ float v_silu(float x) { return x / (1.0f + v_expf(0.0f - x)); }
+
+typedef _Float16 h16;
+
+__device__ __forceinline__ h16 hfma(h16 a, h16 b, h16 c) { return __builtin_fmaf16(a, b, c); }
+__device__ __forceinline__ h16 u2h(uint16_t u) { return __builtin_bit_cast(h16, u); }
+__device__ __forceinline__ uint16_t h2u(h16 h) { return __builtin_bit_cast(uint16_t, h); }
+// f32 -> f16 round-to-nearest-even (v_cvt_f16_f32) of an f32 VALUE: the asm pin keeps
+// the compiler from folding the producing f32 op into a mixed-precision instruction
+// (v_fma_mixlo_f16 rounds the exact result to f16 once; ggml rounds to f32 first).
+__device__ __forceinline__ h16 f2h_rne(float f) {
+    asm volatile("" : "+v"(f));
+    return (h16)f;
+}
+
+// GGML_F16_VEC_REDUCE tail: 8 f16 lanes (after sum[0]+=sum[2], sum[1]+=sum[3],
+// sum[0]+=sum[1]) -> vcvt halves, vaddq_f32, vaddvq_f32 = (t0+t1)+(t2+t3).
+__device__ __forceinline__ float f16x8_reduce(const h16 s[8]) {
+    float t[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) t[k] = (float)s[k] + (float)s[k + 4];
+    return (t[0] + t[1]) + (t[2] + t[3]);
+}
+
+// ggml_vec_dot_f16 (NEON FP16) of two f16 rows held as 8-element vectors of 16-B:
+// x[v], y[v] for v in [0, n/8); n % 32 == 0. Returns the f32 result.
+template <int N>
+__device__ __forceinline__ float vec_dot_f16_rows(const uint4 *x, const uint4 *y) {
+    static_assert(N % 32 == 0, "n % 32");
+    h16 acc[4][8];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc[j][l] = (h16)0.0f;
+#pragma unroll
+    for (int it = 0; it < N / 32; ++it)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const uint4 xv = x[4 * it + j], yv = y[4 * it + j];
+            const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
+#pragma unroll
+            for (int l = 0; l < 8; ++l) {
+                const uint16_t xb = (uint16_t)(xw[l >> 1] >> (16 * (l & 1)));
+                const uint16_t yb = (uint16_t)(yw[l >> 1] >> (16 * (l & 1)));
+                acc[j][l] = hfma(u2h(xb), u2h(yb), acc[j][l]);
+            }
+        }
+    h16 s[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) {
+        const h16 s0 = acc[0][l] + acc[2][l];
+        const h16 s1 = acc[1][l] + acc[3][l];
+        s[l] = s0 + s1;
+    }
+    return f16x8_reduce(s);
+}
+
+// Sum of squares of 16 consecutive floats, sequential in double (x*x rounded to float
+// first, as `(ggml_float)(x[i00] * x[i00])`).
+__device__ __forceinline__ double sumsq16(const float v[16]) {
+    double s = 0.0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s += (double)(v[k] * v[k]);
+    return s;
+}
+
+// Balanced tree over the 16 lanes of an aligned 16-lane row (xor 1, 2, 4, 8): every
+// lane of the row ends with the same value.
+__device__ __forceinline__ double row16_sum(double v) {
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
+    return v;
+}
+
+}  // namespace kq

@@ -21,6 +21,7 @@
 //    304-B "Q8L" blocks: d @0, qs @16, bsums @272): 16 lanes per superblock, x
 //    loaded by inline-asm global loads issued before the weight DMAs (K <= 8192);
 //    above that kq_quantize_q8L writes Q8L blocks to a workspace, copied by DMA.
+#include "kq_ops_device.h"
 #include "kq_rows_device.h"
 
 namespace kq {
@@ -40,7 +41,7 @@ __global__ void __launch_bounds__(WG_THREADS) kq_quantize_q8L(const float *__res
     quant16_store(v, lane & 15, y + bi * Q8L_STRIDE);
 }
 
-template <int TYPE, bool FUSEDQ>
+template <int TYPE, bool FUSEDQ, int PRO>
 __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww, uint8_t *smem, const RowsLayout &L,
                                           int wave, int lane, uint64_t st0) {
     constexpr int BSZ = block_bytes(TYPE);
@@ -86,6 +87,9 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         ++it_;
     };
 
+    const float *const res_p = a.res[ww.m];
+    uint32_t rv = 0;  // residual of the fused ADD for row r0 + lane (first 64 rows)
+
     // ---- prologue: activation loads, pre0 weight steps, quantize, then the rest of the ring
     const int pre_cap = a.pre0 < D ? a.pre0 : D;  // never more than the ring holds
     const int pre0 = T < pre_cap ? T : pre_cap;     // 0..3
@@ -93,7 +97,9 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     if (FUSEDQ) {
         constexpr int PASS = 4 * ROWS_WAVES;  // superblocks per workgroup pass
         u32x4 xv[ROWS_QPASS][4] = {};
+        u32x4 x2v[ROWS_QPASS][4] = {};  // norm weight / up, same elements as xv
         const int qiters = (nb + PASS - 1) / PASS;
+        constexpr int pro = PRO;
 #pragma unroll
         for (int i = 0; i < ROWS_QPASS; ++i) {
             if (i < qiters && PASS * i + 4 * wave < nb) {  // waves past the row load nothing
@@ -102,14 +108,64 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
                 const float *xp = a.x + (int64_t)b * QK + 16 * (lane & 15);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) xv[i][k] = gload16_asm(xp + 4 * k);
+                if (PRO != ROWS_PRO_NONE) {
+                    const float *x2p = a.x2 + (int64_t)b * QK + 16 * (lane & 15);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) x2v[i][k] = gload16_asm(x2p + 4 * k);
+                }
             }
         }
+        // residual of the fused ADD: one row per lane, fetched with the activation. Issued
+        // on every path (a dummy read of x without a residual) so that no branch joins a
+        // register whose asm load is still in flight.
+        rv = gload4_asm(res_p && ww.nrows > 0 ? res_p + ww.r0 + (lane < ww.nrows ? lane : 0) : a.x);
         for (int j = 0; j < pre0; ++j) issue();
         vm_wait_k<NI>(pre0);  // the activation loads are older than pre0 weight steps
         // the loads above are invisible to the compiler: pin their registers past the wait
         asm volatile("" : "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[1][0]),
                      "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]), "+v"(xv[2][0]), "+v"(xv[2][1]), "+v"(xv[2][2]),
                      "+v"(xv[2][3]));
+        if (pro != ROWS_PRO_NONE) {
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(x2v[i][k]));
+        }
+        if (pro == ROWS_PRO_SWIGLU) {  // ggml_vec_swiglu_f32: silu(gate) * up
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i)
+                if (i < qiters)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) xv[i][k] = swiglu4(xv[i][k], x2v[i][k]);
+        } else if (pro == ROWS_PRO_NORM) {  // rms_norm then MUL by the norm weight
+            double *sums = (double *)(smem + L.sums);
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i) {
+                const int b = PASS * i + 4 * wave + (lane >> 4);
+                double sq = 0.0;
+                if (i < qiters && b < nb) {
+                    float v[16];
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) {
+                        v[4 * k] = __uint_as_float(xv[i][k].x), v[4 * k + 1] = __uint_as_float(xv[i][k].y);
+                        v[4 * k + 2] = __uint_as_float(xv[i][k].z), v[4 * k + 3] = __uint_as_float(xv[i][k].w);
+                    }
+                    sq = sumsq16(v);
+                }
+                sq = row16_sum(sq);
+                if (i < qiters && b < nb && (lane & 15) == 0) sums[b] = sq;
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            double tot = 0.0;
+            for (int b = 0; b < nb; ++b) tot += sums[b];
+            const float mean = (float)(tot / (double)(nb * QK));
+            const float scale = 1.0f / sqrtf(mean + a.eps);
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i)
+                if (i < qiters)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) xv[i][k] = normmul4(xv[i][k], x2v[i][k], scale);
+        }
         if (a.stamps) sx = __builtin_amdgcn_s_memrealtime();
 #pragma unroll 1
         for (int i = 0; i < qiters; ++i) {  // one copy of the quantizer; pick the pass's registers
@@ -209,8 +265,16 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     if (ww.nrows > 0) {
         wave_lds_fence();
         float *y = a.y[ww.m] + ww.r0;
-        for (int k = 0; k < ww.nrows; k += 64)
-            if (k + lane < ww.nrows) y[k + lane] = outs[k + lane];
+        if (res_p) {  // ggml_add(mul_mat, residual): the same single f32 add per element
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            asm volatile("" : "+v"(rv));
+            for (int k = 0; k < ww.nrows; k += 64)
+                if (k + lane < ww.nrows)
+                    y[k + lane] = outs[k + lane] + (k == 0 ? __uint_as_float(rv) : res_p[ww.r0 + k + lane]);
+        } else {
+            for (int k = 0; k < ww.nrows; k += 64)
+                if (k + lane < ww.nrows) y[k + lane] = outs[k + lane];
+        }
     }
     if (a.stamps) {
         const int64_t o = ((int64_t)blockIdx.x * ROWS_WAVES + wave) * 8;
@@ -226,7 +290,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     }
 }
 
-template <int TMASK, bool FUSEDQ>
+template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void __launch_bounds__(ROWS_WAVES * 64) kq_rows(const RowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
@@ -247,27 +311,28 @@ __global__ void __launch_bounds__(ROWS_WAVES * 64) kq_rows(const RowsArgs a) {
     ww.nrows = gw < a.waves_total ? base + (j < rem ? 1 : 0) : 0;
 
     if (TMASK == 1) {
-        rows_body<Q4_K, FUSEDQ>(a, ww, smem, L, wave, lane, st0);
+        rows_body<Q4_K, FUSEDQ, PRO>(a, ww, smem, L, wave, lane, st0);
     } else if (TMASK == 2) {
-        rows_body<Q5_K, FUSEDQ>(a, ww, smem, L, wave, lane, st0);
+        rows_body<Q5_K, FUSEDQ, PRO>(a, ww, smem, L, wave, lane, st0);
     } else if (TMASK == 4) {
-        rows_body<Q6_K, FUSEDQ>(a, ww, smem, L, wave, lane, st0);
+        rows_body<Q6_K, FUSEDQ, PRO>(a, ww, smem, L, wave, lane, st0);
     } else {
         const int type = a.type[m];
-        if (type == Q6_K) rows_body<Q6_K, FUSEDQ>(a, ww, smem, L, wave, lane, st0);
-        else if (type == Q5_K) rows_body<Q5_K, FUSEDQ>(a, ww, smem, L, wave, lane, st0);
-        else rows_body<Q4_K, FUSEDQ>(a, ww, smem, L, wave, lane, st0);
+        if (type == Q6_K) rows_body<Q6_K, FUSEDQ, PRO>(a, ww, smem, L, wave, lane, st0);
+        else if (type == Q5_K) rows_body<Q5_K, FUSEDQ, PRO>(a, ww, smem, L, wave, lane, st0);
+        else rows_body<Q4_K, FUSEDQ, PRO>(a, ww, smem, L, wave, lane, st0);
     }
 }
 
-#define KQ_ROWS_INST(TM, FQ) template __global__ void kq_rows<TM, FQ>(const RowsArgs a);
-KQ_ROWS_INST(1, true)
-KQ_ROWS_INST(2, true)
-KQ_ROWS_INST(4, true)
-KQ_ROWS_INST(7, true)
-KQ_ROWS_INST(1, false)
-KQ_ROWS_INST(2, false)
-KQ_ROWS_INST(4, false)
-KQ_ROWS_INST(7, false)
+#define KQ_ROWS_INST(TM, FQ, PR) template __global__ void kq_rows<TM, FQ, PR>(const RowsArgs a);
+#define KQ_ROWS_INST_T(TM)        \
+    KQ_ROWS_INST(TM, true, 0)     \
+    KQ_ROWS_INST(TM, true, 1)     \
+    KQ_ROWS_INST(TM, true, 2)     \
+    KQ_ROWS_INST(TM, false, 0)
+KQ_ROWS_INST_T(1)
+KQ_ROWS_INST_T(2)
+KQ_ROWS_INST_T(4)
+KQ_ROWS_INST_T(7)
 
 }  // namespace kq

@@ -4,6 +4,7 @@
 #pragma once
 
 #include "kq_device.h"
+#include "kq_ops_device.h"
 
 namespace kq {
 
@@ -82,6 +83,32 @@ __device__ __forceinline__ void quant16_store(const u32x4 v[4], int l, uint8_t *
     *(u32x4 *)(qb + 16 + 16 * l) = q;
     *(int16_t *)(qb + 272 + 2 * l) = (int16_t)bsum;
     if (l == 0) *(float *)qb = d;
+}
+
+__device__ __forceinline__ uint32_t gload4_asm(const float *p) {
+    uint32_t r;
+    asm volatile("global_load_dword %0, %1, off" : "=v"(r) : "v"(p) : "memory");
+    return r;
+}
+
+// Fused-prologue transforms of 4 activation values held as f32 bits (kq_ops_device.h):
+// ggml_vec_swiglu_f32 (silu(g) * u) and rms_norm + MUL ((x * scale) * w).
+__device__ __forceinline__ u32x4 swiglu4(u32x4 g, u32x4 u) {
+    u32x4 r;
+    r.x = __float_as_uint(v_silu(__uint_as_float(g.x)) * __uint_as_float(u.x));
+    r.y = __float_as_uint(v_silu(__uint_as_float(g.y)) * __uint_as_float(u.y));
+    r.z = __float_as_uint(v_silu(__uint_as_float(g.z)) * __uint_as_float(u.z));
+    r.w = __float_as_uint(v_silu(__uint_as_float(g.w)) * __uint_as_float(u.w));
+    return r;
+}
+
+__device__ __forceinline__ u32x4 normmul4(u32x4 x, u32x4 w, float scale) {
+    u32x4 r;
+    r.x = __float_as_uint((__uint_as_float(x.x) * scale) * __uint_as_float(w.x));
+    r.y = __float_as_uint((__uint_as_float(x.y) * scale) * __uint_as_float(w.y));
+    r.z = __float_as_uint((__uint_as_float(x.z) * scale) * __uint_as_float(w.z));
+    r.w = __float_as_uint((__uint_as_float(x.w) * scale) * __uint_as_float(w.w));
+    return r;
 }
 
 __device__ __forceinline__ u32x4 gload16_asm(const float *p) {

@@ -17,12 +17,15 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 PKG_ROOT = os.path.dirname(HERE)
 LIB_PATH = os.environ.get("MI355X_LIB") or os.path.join(PKG_ROOT, "lib", "libggml_mi355x.so")
 
-TYPE_F32, TYPE_Q4_K, TYPE_Q5_K, TYPE_Q6_K, TYPE_Q8_K = 0, 12, 13, 14, 15
+TYPE_F32, TYPE_F16, TYPE_Q4_K, TYPE_Q5_K, TYPE_Q6_K, TYPE_Q8_K, TYPE_I32 = 0, 1, 12, 13, 14, 15, 26
 QK_K = 256
 BLOCK_BYTES = {TYPE_Q4_K: 144, TYPE_Q5_K: 176, TYPE_Q6_K: 210, TYPE_Q8_K: 292}
 TYPE_NAMES = {TYPE_Q4_K: "q4_K", TYPE_Q5_K: "q5_K", TYPE_Q6_K: "q6_K", TYPE_Q8_K: "q8_K", TYPE_F32: "f32"}
 MAX_FUSED = 4
-OP_NONE, OP_MUL_MAT = 0, 1
+OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROPE, OP_ATTN_DECODE = range(9)
+MAX_SRC = 8
+FLAG_OUTPUT = 1
+PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -40,6 +43,9 @@ EXPORTED_SYMBOLS = (
     "mi355x_gguf_tensor_data", "mi355x_gguf_upload", "mi355x_gguf_n_kv", "mi355x_gguf_find_key",
     "mi355x_gguf_key", "mi355x_gguf_kv_type", "mi355x_gguf_get_int", "mi355x_gguf_get_float",
     "mi355x_gguf_get_str", "mi355x_gguf_arr_n",
+    "mi355x_gemv_ext_workspace_size", "mi355x_gemv_fused_ext", "mi355x_backend_set_fusion",
+    "mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
+    "mi355x_rope_table_size", "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode",
 )
 
 
@@ -61,7 +67,20 @@ class Tensor(ctypes.Structure):
 
 
 Tensor._fields_ = [("type", ctypes.c_int), ("op", ctypes.c_int), ("ne", ctypes.c_int64 * 4),
-                   ("nb", ctypes.c_size_t * 4), ("src", ctypes.POINTER(Tensor) * 2), ("data", ctypes.c_void_p)]
+                   ("nb", ctypes.c_size_t * 4), ("src", ctypes.POINTER(Tensor) * MAX_SRC), ("data", ctypes.c_void_p),
+                   ("op_params", ctypes.c_int32 * 8), ("flags", ctypes.c_int32)]
+
+
+class GemvExt(ctypes.Structure):
+    _fields_ = [("prologue", ctypes.c_int), ("x2", ctypes.c_void_p), ("eps", ctypes.c_float),
+                ("residual", ctypes.c_void_p * MAX_FUSED)]
+
+
+class AttnDesc(ctypes.Structure):
+    _fields_ = [("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p), ("pos", ctypes.c_void_p),
+                ("rope_table", ctypes.c_void_p), ("k_cache", ctypes.c_void_p), ("v_cache", ctypes.c_void_p),
+                ("out", ctypes.c_void_p), ("n_ctx", ctypes.c_int), ("n_head", ctypes.c_int),
+                ("n_head_kv", ctypes.c_int), ("head_dim", ctypes.c_int), ("scale", ctypes.c_float)]
 
 _lib = None
 
@@ -124,6 +143,26 @@ def lib():
     L.mi355x_gemv_impl.restype = i32
     L.mi355x_diag_stamps.argtypes = [vp, sz]
     L.mi355x_diag_stamps.restype = i32
+    f32 = ctypes.c_float
+    L.mi355x_gemv_ext_workspace_size.argtypes = [i64]
+    L.mi355x_gemv_ext_workspace_size.restype = sz
+    L.mi355x_gemv_fused_ext.argtypes = [ctypes.POINTER(GemvDesc), i32, vp, i64, ctypes.POINTER(GemvExt), vp, sz, vp]
+    L.mi355x_gemv_fused_ext.restype = i32
+    L.mi355x_backend_set_fusion.argtypes = [vp, i32]
+    L.mi355x_backend_set_fusion.restype = i32
+    L.mi355x_get_rows.argtypes = [i32, vp, i64, sz, vp, i64, vp, vp]
+    L.mi355x_rms_norm.argtypes = [vp, vp, vp, i64, i64, f32, vp]
+    L.mi355x_add.argtypes = [vp, vp, vp, i64, vp]
+    L.mi355x_mul.argtypes = [vp, vp, vp, i64, vp]
+    L.mi355x_swiglu.argtypes = [vp, vp, vp, i64, vp]
+    L.mi355x_rope_table_size.argtypes = [i32, i32]
+    L.mi355x_rope_table_size.restype = sz
+    L.mi355x_rope_table.argtypes = [vp, i32, i32, f32, f32, vp]
+    L.mi355x_rope.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, vp]
+    L.mi355x_attn_decode.argtypes = [ctypes.POINTER(AttnDesc), vp]
+    for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
+              "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode"):
+        getattr(L, n).restype = i32
     from . import gguf as _gguf
     _gguf.bind(L)
     _lib = L
@@ -272,6 +311,98 @@ def gemv_fused(mats, x, stream=None, workspace=None):
                                    _stream(stream)), "mi355x_gemv_fused")
 
 
+def gemv_fused_ext(mats, x, prologue=PRO_NONE, x2=None, eps=0.0, residual=None, stream=None):
+    """gemv_fused with the decode graph's neighbours fused (mi355x_gemv_fused_ext):
+    prologue PRO_RMS_NORM (x2 = norm weight) / PRO_SWIGLU (x = gate, x2 = up), and
+    y_i = mul_mat_i + residual[i]."""
+    _require_device()
+    n = len(mats)
+    descs = (GemvDesc * n)()
+    for i, (t, w, y) in enumerate(mats):
+        descs[i] = GemvDesc(t, w.data_ptr(), w.shape[0], w.stride(0), y.data_ptr())
+    ext = GemvExt()
+    ext.prologue = prologue
+    ext.x2 = x2.data_ptr() if x2 is not None else None
+    ext.eps = eps
+    for i in range(MAX_FUSED):
+        r = residual[i] if residual is not None and i < len(residual) else None
+        ext.residual[i] = r.data_ptr() if r is not None else None
+    K = x.shape[-1]
+    need = int(lib().mi355x_gemv_ext_workspace_size(K))
+    ws = _workspace(need, x.device)
+    _check(lib().mi355x_gemv_fused_ext(descs, n, x.data_ptr(), K, ctypes.byref(ext), ws.data_ptr(), need,
+                                       _stream(stream)), "mi355x_gemv_fused_ext")
+
+
+# ------------------------------------------- decode ops (mi355x_get_rows ... attn)
+def get_rows(type_, table, K, ids, out=None, stream=None):
+    """table: (rows, rowbytes) uint8 (or (rows, K) f32); ids: int32 cuda -> (n, K) f32."""
+    torch = _torch()
+    _require_device()
+    n = ids.numel()
+    if out is None:
+        out = torch.empty((n, K), dtype=torch.float32, device=ids.device)
+    _check(lib().mi355x_get_rows(type_, table.data_ptr(), K, table.stride(0) * table.element_size(), ids.data_ptr(),
+                                 n, out.data_ptr(), _stream(stream)), "mi355x_get_rows")
+    return out
+
+
+def rms_norm(x, eps, w=None, out=None, stream=None):
+    torch = _torch()
+    _require_device()
+    x2 = x if x.dim() == 2 else x[None]
+    if out is None:
+        out = torch.empty_like(x)
+    _check(lib().mi355x_rms_norm(x.data_ptr(), w.data_ptr() if w is not None else None, out.data_ptr(),
+                                 x2.shape[1], x2.shape[0], eps, _stream(stream)), "mi355x_rms_norm")
+    return out
+
+
+def add(a, b, out=None, stream=None):
+    out = _torch().empty_like(a) if out is None else out
+    _check(lib().mi355x_add(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), _stream(stream)), "mi355x_add")
+    return out
+
+
+def mul(a, b, out=None, stream=None):
+    out = _torch().empty_like(a) if out is None else out
+    _check(lib().mi355x_mul(a.data_ptr(), b.data_ptr(), out.data_ptr(), a.numel(), _stream(stream)), "mi355x_mul")
+    return out
+
+
+def swiglu(g, u, out=None, stream=None):
+    out = _torch().empty_like(g) if out is None else out
+    _check(lib().mi355x_swiglu(g.data_ptr(), u.data_ptr(), out.data_ptr(), g.numel(), _stream(stream)),
+           "mi355x_swiglu")
+    return out
+
+
+def rope_table(n_pos, n_dims, freq_base=10000.0, freq_scale=1.0, device="cuda", stream=None):
+    torch = _torch()
+    _require_device()
+    t = torch.empty((n_pos, n_dims // 2, 2), dtype=torch.float32, device=device)
+    _check(lib().mi355x_rope_table(t.data_ptr(), n_pos, n_dims, freq_base, freq_scale, _stream(stream)),
+           "mi355x_rope_table")
+    return t
+
+
+def rope(x, head_dim, n_dims, pos, table, out=None, stream=None):
+    """x: (n_heads*head_dim,) f32; pos: int32 cuda tensor (1,)."""
+    out = _torch().empty_like(x) if out is None else out
+    _check(lib().mi355x_rope(x.data_ptr(), out.data_ptr(), head_dim, n_dims, x.numel() // head_dim, pos.data_ptr(),
+                             table.data_ptr(), table.shape[0], _stream(stream)), "mi355x_rope")
+    return out
+
+
+def attn_decode(q, k, v, pos, table, k_cache, v_cache, n_head, n_head_kv, head_dim, scale, out=None, stream=None):
+    """k_cache: (n_ctx, n_head_kv*hd) int16/uint16 view of f16; v_cache: (n_head_kv*hd, n_ctx)."""
+    out = _torch().empty(n_head * head_dim, dtype=_torch().float32, device=q.device) if out is None else out
+    a = AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(), table.data_ptr(), k_cache.data_ptr(),
+                 v_cache.data_ptr(), out.data_ptr(), k_cache.shape[0], n_head, n_head_kv, head_dim, scale)
+    _check(lib().mi355x_attn_decode(ctypes.byref(a), _stream(stream)), "mi355x_attn_decode")
+    return out
+
+
 def block_partials(type_, w, K, q8_row, stream=None):
     """Per-superblock integer partials -> (N, nb, 2) int32 cuda tensor."""
     torch = _torch()
@@ -342,6 +473,9 @@ class Backend:
         _check(lib().mi355x_backend_synchronize(self.h), "synchronize")
         self._keep.clear()
 
+    def set_fusion(self, enable):
+        return int(lib().mi355x_backend_set_fusion(self.h, 1 if enable else 0))
+
     def graph_compute(self, nodes, use_graph=True):
         arr = (ctypes.POINTER(Tensor) * len(nodes))(*[ctypes.pointer(n) for n in nodes])
         return int(lib().mi355x_backend_graph_compute(self.h, arr, len(nodes), 1 if use_graph else 0))
@@ -362,16 +496,28 @@ def supports_op(t: Tensor) -> bool:
     return bool(lib().mi355x_backend_supports_op(ctypes.byref(t)))
 
 
-def make_tensor(type_, ne0, ne1, data, row_stride=None, op=OP_NONE, src0=None, src1=None) -> Tensor:
-    """2-D ggml-style tensor descriptor: ne0 elements per row, ne1 rows, row stride nb1 bytes."""
+def make_tensor(type_, ne0, ne1, data, row_stride=None, op=OP_NONE, src0=None, src1=None, srcs=None,
+                op_params=None, flags=0) -> Tensor:
+    """2-D ggml-style tensor descriptor: ne0 elements per row, ne1 rows, row stride nb1 bytes.
+    `srcs` (list) overrides src0/src1; op_params: up to 8 int32 (use f32_bits for floats)."""
     t = Tensor()
     t.type = type_
     t.op = op
-    nb0 = BLOCK_BYTES.get(type_, 4)
-    nb1 = row_stride if row_stride is not None else (ne0 // QK_K * nb0 if type_ in BLOCK_BYTES else ne0 * 4)
+    nb0 = BLOCK_BYTES.get(type_, 2 if type_ == TYPE_F16 else 4)
+    nb1 = row_stride if row_stride is not None else (ne0 // QK_K * nb0 if type_ in BLOCK_BYTES else ne0 * nb0)
     t.ne[0], t.ne[1], t.ne[2], t.ne[3] = ne0, ne1, 1, 1
     t.nb[0], t.nb[1], t.nb[2], t.nb[3] = nb0, nb1, nb1 * ne1, nb1 * ne1
-    t.src[0] = ctypes.pointer(src0) if src0 is not None else ctypes.POINTER(Tensor)()
-    t.src[1] = ctypes.pointer(src1) if src1 is not None else ctypes.POINTER(Tensor)()
+    srcs = list(srcs) if srcs is not None else [src0, src1]
+    for i in range(MAX_SRC):
+        s = srcs[i] if i < len(srcs) else None
+        t.src[i] = ctypes.pointer(s) if s is not None else ctypes.POINTER(Tensor)()
     t.data = data
+    for i, v in enumerate(op_params or []):
+        t.op_params[i] = v
+    t.flags = flags
     return t
+
+
+def f32_bits(v: float) -> int:
+    import struct
+    return struct.unpack("<i", struct.pack("<f", v))[0]

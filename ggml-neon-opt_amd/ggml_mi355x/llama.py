@@ -1,0 +1,154 @@
+"""The llama decode graph (llm_build_llama, one token, non-flash attention) as
+ggml-mirror nodes on the MI355X backend.
+
+The reference builds this graph in llama.cpp (llama_model::build_graph ->
+llm_build_llama, artifacts/perf/out.folded:249-251) and ggml-cpu computes it node by
+node (ggml_graph_compute_thread -> ggml_compute_forward, out.folded:91-234). Here the
+same nodes go to mi355x_backend_graph_compute, which fuses RMS_NORM -> MUL -> MUL_MAT,
+SWIGLU -> MUL_MAT and MUL_MAT -> ADD into the GEMV launches, and replays the token's
+launches from a hipGraph (the node list is identical for every token; the token id
+and position are device inputs written before each step, as ggml's inp_tokens /
+inp_pos are).
+
+Per layer:
+  rms_norm(x)*attn_norm -> q, k, v (MUL_MAT) -> ATTN_DECODE (rope, f16 KV cache,
+  KQ, soft_max, KQV) -> attn_output (MUL_MAT) -> +x -> rms_norm*ffn_norm ->
+  gate, up (MUL_MAT) -> swiglu -> down (MUL_MAT) -> +ffn_inp
+then rms_norm*output_norm -> output (MUL_MAT) -> logits.
+"""
+from __future__ import annotations
+
+import ctypes
+
+from . import (FLAG_OUTPUT, OP_ADD, OP_ATTN_DECODE, OP_GET_ROWS, OP_MUL, OP_MUL_MAT, OP_RMS_NORM, OP_SWIGLU,
+               TYPE_F16, TYPE_F32, TYPE_I32, Backend, Mi355xError, f32_bits, make_tensor, rope_table)
+
+LAYER_MATS = ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down")
+
+
+def hparams(n_embd, n_layer, n_head, n_head_kv, n_ff, n_vocab, eps=1e-5, freq_base=10000.0):
+    return dict(n_embd=n_embd, n_layer=n_layer, n_head=n_head, n_head_kv=n_head_kv, head_dim=n_embd // n_head,
+                n_ff=n_ff, n_vocab=n_vocab, eps=eps, freq_base=freq_base)
+
+
+TINYLLAMA = hparams(2048, 22, 32, 4, 5632, 32000)
+LLAMA3_8B = hparams(4096, 32, 32, 8, 14336, 128256, eps=1e-5, freq_base=500000.0)
+
+
+class LlamaDecoder:
+    """Device state and node list of one decode token.
+
+    weights: dict with "token_embd", "output", "output_norm" and per layer i
+    "blk.{i}.<name>" for name in LAYER_MATS + ("attn_norm", "ffn_norm"); a K-quant
+    matrix is (type, uint8 cuda tensor [rows, rowbytes]), a norm is an f32 cuda tensor.
+    """
+
+    HOST_SLOTS = 1024
+
+    def __init__(self, backend: Backend, hp: dict, weights: dict, n_ctx: int, fuse: bool = True):
+        import torch
+        self.b, self.hp, self.w, self.n_ctx = backend, hp, weights, n_ctx
+        dev = weights["output_norm"].device
+        E, F, V = hp["n_embd"], hp["n_ff"], hp["n_vocab"]
+        hd, nh, nkv = hp["head_dim"], hp["n_head"], hp["n_head_kv"]
+        kvw = nkv * hd
+        f32 = torch.float32
+
+        def buf(n, dtype=f32):
+            return torch.zeros(n, dtype=dtype, device=dev)
+
+        self.token = buf(1, torch.int32)
+        self.pos = buf(1, torch.int32)
+        self.table = rope_table(n_ctx, hd, hp["freq_base"], 1.0, device=dev, stream=backend.stream)
+        self.k_cache = [torch.zeros((n_ctx, kvw), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
+        self.v_cache = [torch.zeros((kvw, n_ctx), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
+        self._bufs = []
+        self.nodes = []
+        T = []  # keeps every Tensor alive
+
+        def leaf(t, type_, ne0, ne1=1, row_stride=None):
+            x = make_tensor(type_, ne0, ne1, t.data_ptr(), row_stride=row_stride)
+            T.append(x)
+            return x
+
+        def node(op, n, srcs, params=None, flags=0, ne1=1):
+            b = buf(n)
+            self._bufs.append(b)
+            x = make_tensor(TYPE_F32, n, ne1, b.data_ptr(), op=op, srcs=srcs, op_params=params, flags=flags)
+            T.append(x)
+            self.nodes.append(x)
+            return x, b
+
+        def mat(name):
+            t, w = weights[name]
+            return leaf(w, t, w.shape[1] * 256 // {12: 144, 13: 176, 14: 210}[t], w.shape[0], row_stride=w.stride(0))
+
+        def mm(name, x):
+            wt = mat(name)
+            return node(OP_MUL_MAT, wt.ne[1], [wt, x])[0]
+
+        eps_bits = [f32_bits(hp["eps"])]
+        tok = leaf(self.token, TYPE_I32, 1)
+        pos = leaf(self.pos, TYPE_I32, 1)
+        tab = leaf(self.table, TYPE_F32, hd, n_ctx)
+        et, ew = weights["token_embd"]
+        emb_t = leaf(ew, et, E, ew.shape[0], row_stride=ew.stride(0) * ew.element_size())
+        x, _ = node(OP_GET_ROWS, E, [emb_t, tok])
+        scale = f32_bits(float(torch.tensor(1.0) / torch.sqrt(torch.tensor(float(hd)))))
+        for i in range(hp["n_layer"]):
+            p = f"blk.{i}."
+            n1, _ = node(OP_RMS_NORM, E, [x], eps_bits)
+            m1, _ = node(OP_MUL, E, [n1, leaf(weights[p + "attn_norm"], TYPE_F32, E)])
+            q = mm(p + "attn_q", m1)
+            k = mm(p + "attn_k", m1)
+            v = mm(p + "attn_v", m1)
+            kc = leaf(self.k_cache[i], TYPE_F16, kvw, n_ctx)
+            vc = leaf(self.v_cache[i], TYPE_F16, n_ctx, kvw)
+            att, _ = node(OP_ATTN_DECODE, nh * hd, [q, k, v, pos, kc, vc, tab], [nh, nkv, hd, scale])
+            o = mm(p + "attn_output", att)
+            ffn_inp, _ = node(OP_ADD, E, [o, x])
+            n2, _ = node(OP_RMS_NORM, E, [ffn_inp], eps_bits)
+            m2, _ = node(OP_MUL, E, [n2, leaf(weights[p + "ffn_norm"], TYPE_F32, E)])
+            gt = mm(p + "ffn_gate", m2)
+            up = mm(p + "ffn_up", m2)
+            glu, _ = node(OP_SWIGLU, F, [gt, up])
+            dn = mm(p + "ffn_down", glu)
+            x, self.last_hidden = node(OP_ADD, E, [dn, ffn_inp])
+        n3, _ = node(OP_RMS_NORM, E, [x], eps_bits)
+        m3, _ = node(OP_MUL, E, [n3, leaf(weights["output_norm"], TYPE_F32, E)])
+        wt = mat("output")
+        _, self.logits = node(OP_MUL_MAT, V, [wt, m3], flags=FLAG_OUTPUT)
+        self._tensors = T
+        self._arr = (ctypes.POINTER(type(T[0])) * len(self.nodes))(*[ctypes.pointer(n) for n in self.nodes])
+        # pinned staging slots for (token, pos): a slot is reused only after the stream
+        # has been synchronized (the H2D copies are asynchronous)
+        self._host = torch.zeros((self.HOST_SLOTS, 2), dtype=torch.int32).pin_memory()
+        self._slot = 0
+        backend.set_fusion(fuse)
+        torch.cuda.synchronize()  # weights / zeroed caches (torch's stream) before the backend stream runs
+
+    def reset(self):
+        for c in self.k_cache + self.v_cache:
+            c.zero_()
+
+    def step(self, token: int, pos: int, use_graph: bool = True):
+        """Enqueue one token (no synchronization); returns the device logits tensor."""
+        if not 0 <= pos < self.n_ctx:
+            raise Mi355xError(f"position {pos} outside the KV cache (n_ctx {self.n_ctx})")
+        from . import lib
+        if self._slot == self.HOST_SLOTS:
+            self.b.synchronize()
+            self._slot = 0
+        self._host[self._slot, 0] = token
+        self._host[self._slot, 1] = pos
+        L = lib()
+        hp = self._host.data_ptr() + 8 * self._slot
+        self._slot += 1
+        rc = L.mi355x_backend_set_tensor(self.b.h, self.token.data_ptr(), hp, 4)
+        rc = rc or L.mi355x_backend_set_tensor(self.b.h, self.pos.data_ptr(), hp + 4, 4)
+        if rc:
+            raise Mi355xError(f"set_tensor failed ({rc})")
+        rc = L.mi355x_backend_graph_compute(self.b.h, self._arr, len(self.nodes), 1 if use_graph else 0)
+        if rc:
+            raise Mi355xError(f"graph_compute failed ({rc})")
+        return self.logits

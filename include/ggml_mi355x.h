@@ -75,10 +75,12 @@ typedef struct {
 /* ggml_type values (ggml.h enum ggml_type) for the types this path handles. */
 enum mi355x_type {
     MI355X_TYPE_F32  = 0,
+    MI355X_TYPE_F16  = 1,
     MI355X_TYPE_Q4_K = 12,
     MI355X_TYPE_Q5_K = 13,
     MI355X_TYPE_Q6_K = 14,
     MI355X_TYPE_Q8_K = 15,
+    MI355X_TYPE_I32  = 26,
 };
 
 enum mi355x_status {
@@ -165,6 +167,26 @@ size_t mi355x_gemv_fused_workspace_size(int64_t k);
 int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k,
                       void *workspace, size_t workspace_size, void *stream);
 
+/* mi355x_gemv_fused with the decode graph's neighbours of the MUL_MATs fused in
+ * (the backend's node fusion uses this): `prologue` transforms x before its Q8_K
+ * quantization exactly as the separate node would (MI355X_PRO_RMS_NORM: ggml_rms_norm
+ * then ggml_mul by x2 = the norm weight; MI355X_PRO_SWIGLU: x = gate, x2 = up), and
+ * descs[i].y receives mul_mat + residual[i] when residual[i] != NULL (ggml_add).
+ * Bit-identical to the separate ops. Workspace: mi355x_gemv_ext_workspace_size(k)
+ * (used only when the kernel cannot fuse, e.g. rows not contiguous). */
+#define MI355X_PRO_NONE 0
+#define MI355X_PRO_RMS_NORM 1
+#define MI355X_PRO_SWIGLU 2
+typedef struct {
+    int prologue;
+    const float *x2;
+    float eps;
+    const float *residual[MI355X_MAX_FUSED];
+} mi355x_gemv_ext;
+size_t mi355x_gemv_ext_workspace_size(int64_t k);
+int mi355x_gemv_fused_ext(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k,
+                          const mi355x_gemv_ext *ext, void *workspace, size_t workspace_size, void *stream);
+
 /* Debug/parity hook: per-superblock integer partials of a Q4_K/Q5_K/Q6_K x Q8_K
  * dot, as the GEMV kernel computes them. For each row r and superblock b:
  * out[2*(r*nb+b)+0] = sumi (sum_j sc_j * dot_j), out[...+1] = summins
@@ -205,19 +227,91 @@ int mi355x_diag_stamps(void *buf, size_t bytes);
 #define MI355X_GEMV_CHAIN 3
 int mi355x_gemv_impl(int impl);
 
+/* --------------------------------------- decode ops of the llama graph (§8f) */
+/* The non-matmul nodes of one llama decode token (llm_build_llama, out.folded:249),
+ * each bit-compatible with the ggml-cpu function the reference profile shows
+ * (artifacts/perf/out.folded; restatement and [U] notes: the CPU checker under the tests).
+ * Device pointers, async on `stream`, 0 / MI355X_E* / hipError_t like the GEMVs. */
+
+/* GGML_OP_GET_ROWS (ggml_compute_forward_get_rows_q -> dequantize_row_q4_K,
+ * out.folded:103-104): dst[r][0..ne0) = row ids[r] of `table` as f32. type F32 /
+ * Q4_K / Q6_K; rows of `row_stride` bytes; ids: device int32[n_ids]. */
+int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, const int32_t *ids,
+                    int64_t n_ids, float *dst, void *stream);
+/* GGML_OP_RMS_NORM (ggml_compute_forward_rms_norm_f32, out.folded:189-193) over
+ * `nrows` rows of n floats, y = x * (1/sqrtf(mean(x^2) + eps)); when w != NULL the
+ * following GGML_OP_MUL by the norm weight is fused: y = (x*scale) * w (two roundings,
+ * as the two ops). n % 256 == 0. */
+int mi355x_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t nrows, float eps, void *stream);
+/* GGML_OP_ADD / GGML_OP_MUL on contiguous f32 (binary_op<op_add/op_mul>, out.folded:91-99, 115-121). */
+int mi355x_add(const float *a, const float *b, float *y, int64_t n, void *stream);
+int mi355x_mul(const float *a, const float *b, float *y, int64_t n, void *stream);
+/* GGML_OP_GLU / GLU_OP_SWIGLU split form (ggml_vec_swiglu_f32, out.folded:107-113):
+ * y = silu(gate) * up with ggml_v_silu/ggml_v_expf arithmetic. */
+int mi355x_swiglu(const float *gate, const float *up, float *y, int64_t n, void *stream);
+/* GGML_OP_ROPE, mode NORMAL, ext_factor 0, attn_factor 1 (ggml_compute_forward_rope_f32,
+ * ggml_rope_cache_init, rope_yarn; out.folded:196-208). The per-position cos/sin cache
+ * ggml builds on every call is built once for positions [0, n_pos) by the host C
+ * library (powf, cosf, sinf: the calls of the CPU path) into a device table of
+ * mi355x_rope_table_size() bytes. pos: device int32 (one token). */
+size_t mi355x_rope_table_size(int n_pos, int n_dims);
+int mi355x_rope_table(float *table, int n_pos, int n_dims, float freq_base, float freq_scale, void *stream);
+int mi355x_rope(const float *x, float *y, int head_dim, int n_dims, int n_heads, const int32_t *pos,
+                const float *table, int n_pos, void *stream);
+/* The non-flash attention block of a decode token, one launch: rope(q), rope(k) at
+ * *pos, f16 K/V cache cell write (set_rows, out.folded:209-215; V transposed),
+ * KQ = mul_mat(k_cache f16, q->f16) via ggml_vec_dot_f16 (NEON FP16 accumulation,
+ * out.folded:140-144), soft_max_ext(scale, causal mask) (out.folded:216-234), KQV =
+ * mul_mat(v_cache, kq->f16), permute + cont -> out[n_head*head_dim]. n_kv =
+ * min(n_ctx, max(32, pad32(pos+1))). head_dim 64 or 128; n_ctx % 32 == 0, <= 8192;
+ * caches zero-initialised by the caller, 16-B aligned. */
+typedef struct {
+    const float *q, *k, *v;    /* this token's projections, before rope */
+    const int32_t *pos;        /* device int32 */
+    const float *rope_table;   /* mi355x_rope_table(n_pos >= n_ctx, n_dims = head_dim) */
+    uint16_t *k_cache;         /* f16 [n_ctx][n_head_kv*head_dim] */
+    uint16_t *v_cache;         /* f16 [n_head_kv*head_dim][n_ctx] */
+    float *out;                /* [n_head*head_dim] */
+    int n_ctx, n_head, n_head_kv, head_dim;
+    float scale;               /* kq_scale = 1/sqrtf(head_dim) */
+} mi355x_attn_desc;
+int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
+
 /* --------------------------------------------- ggml-backend mirror (C++) */
 /* A minimal mirror of ggml-backend's device/buffer/graph interface
  * (ggml-backend-impl.h [U]; CPU sibling ggml-cpu.cpp:186, README.md:162),
  * enough for a ggml adapter to forward MUL_MAT nodes. */
-enum mi355x_op { MI355X_OP_NONE = 0, MI355X_OP_MUL_MAT = 1 };
+/* Node ops: MUL_MAT and the other nodes of a llama decode token (llm_build_llama).
+ * Operands (src[i]) and op_params per op:
+ *   MUL_MAT      src0 K-quant weights [K, N], src1 f32 [K, M]            -> f32 [N, M]
+ *   GET_ROWS     src0 table (F32/Q4_K/Q6_K) [K, rows], src1 I32 ids [n]  -> f32 [K, n]
+ *   RMS_NORM     src0 f32 [n, rows]; op_params[0] = eps (float bits)     -> f32
+ *   MUL, ADD     src0, src1 f32, same shape (contiguous)                 -> f32
+ *   SWIGLU       src0 gate, src1 up (GGML_OP_GLU, GLU_OP_SWIGLU, split)  -> f32
+ *   ROPE         src0 f32 [head_dim, n_heads], src1 I32 pos [1], src2 f32 rope table
+ *                [n_dims, n_pos] (mi355x_rope_table); op_params[0] = n_dims (mode NORMAL)
+ *   ATTN_DECODE  src0 q, src1 k, src2 v (f32, before rope), src3 I32 pos [1],
+ *                src4 F16 k_cache [kvw, n_ctx], src5 F16 v_cache [n_ctx, kvw] (transposed),
+ *                src6 rope table; op_params = {n_head, n_head_kv, head_dim, scale bits}
+ *                -> f32 [head_dim*n_head]: the non-flash attention block
+ *                (set_rows, mul_mat f16, soft_max_ext, mul_mat f16, permute, cont). */
+enum mi355x_op {
+    MI355X_OP_NONE = 0, MI355X_OP_MUL_MAT = 1, MI355X_OP_GET_ROWS = 2, MI355X_OP_RMS_NORM = 3,
+    MI355X_OP_MUL = 4, MI355X_OP_ADD = 5, MI355X_OP_SWIGLU = 6, MI355X_OP_ROPE = 7,
+    MI355X_OP_ATTN_DECODE = 8,
+};
+#define MI355X_MAX_SRC 8
+#define MI355X_TENSOR_FLAG_OUTPUT 1  /* read by the caller after graph_compute: never elided by fusion */
 
 typedef struct mi355x_tensor {
-    int type;                      /* enum mi355x_type                          */
+    int type;                      /* enum mi355x_type (+ F16 = 1, I32 = 26)    */
     int op;                        /* enum mi355x_op                            */
     int64_t ne[4];                 /* elements per dim (ggml order)            */
     size_t nb[4];                  /* bytes per dim                            */
-    struct mi355x_tensor *src[2];  /* MUL_MAT: src[0] weights, src[1] f32 input */
+    struct mi355x_tensor *src[MI355X_MAX_SRC];
     void *data;                    /* device pointer                            */
+    int32_t op_params[8];
+    int32_t flags;                 /* MI355X_TENSOR_FLAG_*                      */
 } mi355x_tensor;
 
 typedef struct mi355x_backend *mi355x_backend_t;
@@ -234,6 +328,13 @@ int mi355x_backend_get_tensor(mi355x_backend_t backend, void *host_dst, const vo
                               size_t size);              /* async D2H */
 int mi355x_backend_synchronize(mi355x_backend_t backend);
 int mi355x_backend_supports_op(const mi355x_tensor *op); /* 1 / 0 */
+/* Node fusion in graph_compute (default on): RMS_NORM -> MUL(norm weight) ->
+ * MUL_MAT(s) and SWIGLU -> MUL_MAT run as ONE GEMV launch whose prologue computes
+ * the norm / swiglu before the Q8_K quantization, and MUL_MAT -> ADD(residual)
+ * writes mul_mat + residual from the GEMV's epilogue; RMS_NORM -> MUL alone is one
+ * kernel. Fused intermediates (not flagged OUTPUT, read by no other node) are not
+ * written. Results are bit-identical with fusion off. Returns the previous value. */
+int mi355x_backend_set_fusion(mi355x_backend_t backend, int enable);
 /* Runs nodes in order on the backend stream. Consecutive MUL_MAT nodes with
  * ne11 == 1 that share src[1] are fused into one launch. When `use_graph` is
  * non-zero the launch sequence is captured once into a hipGraph and replayed

@@ -74,6 +74,27 @@ int kqo_mul_mat(int type, const void *src0, int64_t K, int64_t N, size_t nb01,
 int kqo_mul_mat_q8(int type, const void *src0, int64_t K, int64_t N, size_t nb01,
                    const void *src1_q8, int64_t M, float *dst, int n_threads, int variant);
 
+
+/* ---- non-matmul decode ops (kq_ops_oracle.c) ---- */
+uint16_t kqo_f16_fma(uint16_t a, uint16_t b, uint16_t c);
+uint16_t kqo_f16_add(uint16_t a, uint16_t b);
+void kqo_fp32_to_fp16_row(const float *x, uint16_t *y, int64_t n);
+float kqo_vec_dot_f16(int n, const uint16_t *x, const uint16_t *y);
+float kqo_v_expf(float x);
+void kqo_vec_swiglu_f32(int n, float *y, const float *x, const float *g);
+void kqo_soft_max_row(int n, float *dp, const float *sp, const float *mask, float scale);
+void kqo_rms_norm_f32(const float *x, float *y, int64_t n, float eps);
+void kqo_mul_f32(const float *a, const float *b, float *y, int64_t n);
+void kqo_add_f32(const float *a, const float *b, float *y, int64_t n);
+float kqo_rope_theta_scale(float freq_base, int n_dims);
+void kqo_rope_table(float *table, int n_pos, int n_dims, float freq_base, float freq_scale);
+void kqo_rope_norm(const float *x, float *y, int head_dim, int n_dims, int n_heads, int pos, const float *table);
+void kqo_get_rows(int type, const void *table, int64_t k, size_t row_stride, const int32_t *ids, int64_t n_ids,
+                  float *out);
+int kqo_attn_n_kv(int pos, int n_ctx);
+void kqo_attn_decode(const float *q, const float *k, const float *v, uint16_t *k_cache, uint16_t *v_cache, int pos,
+                     int n_ctx, int n_head, int n_head_kv, int head_dim, float scale, float *out);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,222 @@
+"""GPU parity of the non-matmul decode ops and of the full llama decode token
+ against the CPU oracle (oracle/kq_ops_oracle.c), through
+the C-ABI.
+
+Bar: bit-exact (every op restates ggml-cpu's arithmetic op for op). One stated
+exception by construction: RMS_NORM's double sum of squares runs in a fixed tree
+order on the GPU vs ggml's sequential order (kq_ops_device.h); the float results
+are compared bit-exactly here and a difference would be reported as the ≤ 1-ulp
+case of that note (none has been seen).
+"""
+import numpy as np
+import pytest
+
+from tests.test_gpu_parity import bits_equal, first_mismatch, t
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import kq_ops_oracle
+    kq_ops_oracle.lib()
+    return kq_ops_oracle
+
+
+# ---------------------------------------------------------------- elementwise
+@pytest.mark.parametrize("type_", [0, 12, 14])
+def test_get_rows(dev, O, npo, type_):
+    import torch
+    import ggml_mi355x as g
+    rng = np.random.default_rng(type_)
+    K, R = 2048, 50
+    if type_ == 0:
+        table = rng.standard_normal((R, K)).astype(np.float32)
+    else:
+        table = npo.random_blocks(rng, type_, R, K)
+    ids = np.array([0, 7, 49, 7, 13], np.int32)
+    got = g.get_rows(type_, t(table, dev), K, t(ids, dev)).cpu().numpy()
+    ref = O.get_rows(type_, table, K, ids)
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+    torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("n", [256, 2048, 5632, 8192])
+def test_rms_norm(dev, O, n):
+    import ggml_mi355x as g
+    rng = np.random.default_rng(n)
+    x = (rng.standard_normal((6, n)) * rng.uniform(1e-3, 1e3, (6, 1))).astype(np.float32)
+    x[1, : n // 2] *= 1e-5  # wide dynamic range inside one row
+    w = rng.uniform(0.5, 1.5, n).astype(np.float32)
+    for eps in (1e-5, 1e-6):
+        got = g.rms_norm(t(x, dev), eps).cpu().numpy()
+        ref = O.rms_norm(x, eps)
+        assert bits_equal(got, ref), first_mismatch(got, ref)
+        got = g.rms_norm(t(x, dev), eps, w=t(w, dev)).cpu().numpy()
+        ref = np.stack([O.mul(O.rms_norm(r, eps), w) for r in x])
+        assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
+def test_add_mul_swiglu(dev, O):
+    import ggml_mi355x as g
+    rng = np.random.default_rng(5)
+    n = 5632
+    a = (rng.standard_normal(n) * 4).astype(np.float32)
+    b = rng.standard_normal(n).astype(np.float32)
+    a[:8] = [0.0, -0.0, 1e-30, -1e-30, 88.0, -88.0, 100.0, -100.0]
+    a[8:16] = [-130.0, -150.0, -190.0, -200.0, 1e4, -1e4, 3.0e-39, -3.0e-39]  # v_expf slow path, denormals
+    assert bits_equal(g.add(t(a, dev), t(b, dev)).cpu().numpy(), O.add(a, b))
+    assert bits_equal(g.mul(t(a, dev), t(b, dev)).cpu().numpy(), O.mul(a, b))
+    got = g.swiglu(t(a, dev), t(b, dev)).cpu().numpy()
+    ref = O.swiglu(a, b)
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
+def test_v_expf_lanes(dev, O):
+    """The soft_max/silu exponential lane for lane over its whole range (fast and slow paths)."""
+    import ggml_mi355x as g
+    x = np.concatenate([np.linspace(-200, 90, 20001), -np.logspace(-30, 2.3, 3000)]).astype(np.float32)
+    # swiglu(x, 1) = x / (1 + v_expf(-x)): exercises v_expf at -x
+    got = g.swiglu(t(x, dev), t(np.ones_like(x), dev)).cpu().numpy()
+    ref = O.swiglu(x, np.ones_like(x))
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
+# ---------------------------------------------------------------- rope
+@pytest.mark.parametrize("hd,nh,base", [(64, 36, 10000.0), (128, 40, 500000.0)])
+def test_rope(dev, O, hd, nh, base):
+    import ggml_mi355x as g
+    import torch
+    n_ctx = 512
+    tab = g.rope_table(n_ctx, hd, base, 1.0, device=dev)
+    tref = O.rope_table(n_ctx, hd, base)
+    assert bits_equal(tab.cpu().numpy(), tref)  # the host C library builds both
+    rng = np.random.default_rng(hd)
+    x = rng.standard_normal(nh * hd).astype(np.float32) * 3
+    for p in (0, 1, 37, 511):
+        pos = torch.tensor([p], dtype=torch.int32, device=dev)
+        got = g.rope(t(x, dev), hd, hd, pos, tab).cpu().numpy()
+        ref = O.rope(x, hd, hd, p, tref)
+        assert bits_equal(got, ref), (p, first_mismatch(got, ref))
+
+
+# ---------------------------------------------------------------- attention
+@pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 256), (128, 32, 8, 128), (64, 8, 8, 64)])
+def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx):
+    """A growing KV cache: every position's output and both caches bit-exact."""
+    import torch
+    import ggml_mi355x as g
+    rng = np.random.default_rng(hd + nh)
+    kvw = nkv * hd
+    tab = g.rope_table(n_ctx, hd, 10000.0, 1.0, device=dev)
+    tref = O.rope_table(n_ctx, hd, 10000.0)
+    kc = torch.zeros((n_ctx, kvw), dtype=torch.int16, device=dev)
+    vc = torch.zeros((kvw, n_ctx), dtype=torch.int16, device=dev)
+    kc_ref = np.zeros((n_ctx, kvw), np.uint16)
+    vc_ref = np.zeros((kvw, n_ctx), np.uint16)
+    scale = float(np.float32(1.0) / np.sqrt(np.float32(hd)))
+    positions = list(range(0, 40)) + [n_ctx - 1]
+    for p in positions:
+        q = (rng.standard_normal(nh * hd) * 2).astype(np.float32)
+        k = (rng.standard_normal(kvw) * 2).astype(np.float32)
+        v = rng.standard_normal(kvw).astype(np.float32)
+        pos = torch.tensor([p], dtype=torch.int32, device=dev)
+        got = g.attn_decode(t(q, dev), t(k, dev), t(v, dev), pos, tab, kc, vc, nh, nkv, hd, scale).cpu().numpy()
+        ref = O.attn_decode(O.rope(q, hd, hd, p, tref), O.rope(k, hd, hd, p, tref), v, kc_ref, vc_ref, p, nh, nkv,
+                            hd, scale)
+        assert bits_equal(got, ref), (p, first_mismatch(got, ref))
+    assert (kc.cpu().numpy().view(np.uint16) == kc_ref).all()
+    assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
+
+
+def test_attn_decode_rejects_bad_position(dev):
+    """A position outside the cache never computes silently: NaN output, caches untouched."""
+    import torch
+    import ggml_mi355x as g
+    hd, nh, nkv, n_ctx = 64, 4, 2, 64
+    tab = g.rope_table(n_ctx, hd, device=dev)
+    kc = torch.zeros((n_ctx, nkv * hd), dtype=torch.int16, device=dev)
+    vc = torch.zeros((nkv * hd, n_ctx), dtype=torch.int16, device=dev)
+    x = torch.ones(nh * hd, device=dev)
+    out = g.attn_decode(x, x[: nkv * hd], x[: nkv * hd], torch.tensor([n_ctx], dtype=torch.int32, device=dev), tab,
+                        kc, vc, nh, nkv, hd, 0.125)
+    assert torch.isnan(out).all()
+    assert int(kc.abs().sum()) == 0 and int(vc.abs().sum()) == 0
+
+
+# ---------------------------------------------------------------- fused GEMV prologue / epilogue
+@pytest.mark.parametrize("pro", ["norm", "swiglu"])
+def test_gemv_fused_ext(dev, O, oracle, npo, impl, pro):
+    """RMS_NORM -> MUL -> MUL_MAT(s) -> ADD and SWIGLU -> MUL_MAT -> ADD in one launch
+    (kq_rows) or staged (kq_gemv): equal to the separate ops, bit for bit."""
+    import torch
+    import ggml_mi355x as g
+    rng = np.random.default_rng(11)
+    K = 2048 if pro == "norm" else 5632
+    mats = [(12, 384), (14, 128)] if pro == "norm" else [(14, 2048)]
+    x = (rng.standard_normal(K) * 3).astype(np.float32)
+    x2 = rng.uniform(0.5, 1.5, K).astype(np.float32) if pro == "norm" else rng.standard_normal(K).astype(np.float32)
+    ws = [npo.random_blocks(rng, ty, n, K) for ty, n in mats]
+    res = [rng.standard_normal(n).astype(np.float32) for _, n in mats]
+    ys = [torch.empty(n, device=dev) for _, n in mats]
+    g.gemv_fused_ext([(ty, t(w, dev), y) for (ty, _), w, y in zip(mats, ws, ys)], t(x, dev),
+                     prologue=g.PRO_RMS_NORM if pro == "norm" else g.PRO_SWIGLU, x2=t(x2, dev), eps=1e-5,
+                     residual=[t(r, dev) for r in res])
+    torch.cuda.synchronize()
+    xin = O.mul(O.rms_norm(x, 1e-5), x2) if pro == "norm" else O.swiglu(x, x2)
+    for (ty, _), w, r, y in zip(mats, ws, res, ys):
+        ref = O.add(oracle.mul_mat(ty, w, xin)[0], r)
+        got = y.cpu().numpy()
+        assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
+# ---------------------------------------------------------------- the whole token
+def _decoder(dev, hp, seed, n_ctx, fuse=True):
+    from tests import llama_model as LM
+    import ggml_mi355x as g
+    from ggml_mi355x.llama import LlamaDecoder
+    w = LM.build(hp, seed)
+    b = g.Backend()
+    dec = LlamaDecoder(b, hp, LM.to_device(w, dev), n_ctx, fuse=fuse)
+    return w, b, dec
+
+
+@pytest.mark.parametrize("fuse", [True, False], ids=["fused", "unfused"])
+def test_llama_decode_tokens(dev, O, fuse):
+    """Two TinyLlama-width layers (Q4_K_M mix) + a 4096-token vocabulary: the logits and
+    every layer's residual stream of 5 consecutive tokens (hipGraph replay across
+    tokens) bit-exact with the oracle's llm_build_llama restatement."""
+    import torch
+    from tests import llama_model as LM
+    from ggml_mi355x.llama import hparams
+    hp = hparams(2048, 2, 32, 4, 5632, 4096)
+    n_ctx = 64
+    w, b, dec = _decoder(dev, hp, 3, n_ctx, fuse)
+    model, cache = LM.oracle_model(hp, w, n_ctx)
+    tokens = [1, 4095, 17, 17, 300]
+    for p, tok in enumerate(tokens):
+        dec.step(tok, p)
+        b.synchronize()
+        got = dec.logits.cpu().numpy()
+        ref, trace = O.decode_token(model, tok, p, cache)
+        hid = dec.last_hidden.cpu().numpy()
+        assert bits_equal(hid, trace[-1]), (p, "hidden", first_mismatch(hid, trace[-1]))
+        assert bits_equal(got, ref), (p, first_mismatch(got, ref))
+    torch.cuda.synchronize()
+    b.close()
+
+
+def test_llama_fused_launch_count(dev):
+    """Fusion leaves 5 launches per layer + get_rows + the output GEMV."""
+    import ggml_mi355x as g
+    from ggml_mi355x.llama import hparams
+    hp = hparams(2048, 3, 32, 4, 5632, 1024)
+    _, b, dec = _decoder(dev, hp, 4, 64, True)
+    dec.step(5, 0, use_graph=False)
+    b.synchronize()
+    g.timing_enable(True)
+    dec.step(6, 1, use_graph=False)
+    rows = g.timing_read()
+    g.timing_enable(False)
+    assert len(rows) == 5 * hp["n_layer"] + 2, [r[0] for r in rows]
+    b.close()

@@ -1,0 +1,177 @@
+"""CPU checks of the decode-op oracle (oracle/kq_ops_oracle.c) and of the host side
+of the decode graph: the exact binary16 arithmetic against rational arithmetic,
+ggml_v_expf's accuracy, each op against a float64 statement of its math, a whole
+tiny llama token, and supports_op for the new node types."""
+import math
+from fractions import Fraction
+
+import numpy as np
+import pytest
+
+
+@pytest.fixture(scope="module")
+def O():
+    from oracle import kq_ops_oracle
+    kq_ops_oracle.lib()
+    return kq_ops_oracle
+
+
+def h2f(h):
+    return float(np.array([h], np.uint16).view(np.float16)[0])
+
+
+def nearest_f16(x: Fraction, neg_zero=False):
+    """Correctly rounded (RNE) binary16 of an exact rational, as bits."""
+    if x == 0:
+        return 0x8000 if neg_zero else 0
+    best = None
+    # candidates around float(x)
+    f = float(x)
+    c = int(np.array([f], np.float16).view(np.uint16)[0])
+    for d in range(-2, 3):
+        h = (c + d) & 0xFFFF
+        if (h & 0x7C00) == 0x7C00:
+            continue
+        if (h & 0x8000) != (0x8000 if x < 0 else 0) and (h & 0x7FFF):
+            continue
+        err = abs(Fraction(h2f(h)) - x)
+        key = (err, (h & 1))  # ties -> even mantissa
+        if best is None or key < best[0]:
+            best = (key, h)
+    return best[1]
+
+
+def test_f16_fma_add_exact(O):
+    rng = np.random.default_rng(0)
+    for _ in range(4000):
+        a, b, c = (int(v) for v in rng.integers(0, 0x7C00, 3))
+        a |= int(rng.integers(0, 2)) << 15
+        c |= int(rng.integers(0, 2)) << 15
+        ex = Fraction(h2f(a)) * Fraction(h2f(b)) + Fraction(h2f(c))
+        r = O.f16_fma(a, b, c)
+        if abs(ex) >= 65520:
+            assert (r & 0x7FFF) == 0x7C00
+            continue
+        if ex != 0:
+            assert r == nearest_f16(ex), (hex(a), hex(b), hex(c), hex(r))
+        s = Fraction(h2f(a)) + Fraction(h2f(c))
+        if s != 0 and abs(s) < 65520:
+            assert O.f16_add(a, c) == nearest_f16(s)
+    # signed zeros: (-0)+(-0) = -0, x + (-x) = +0, fma(-1, 0, -0) = -0
+    assert O.f16_add(0x8000, 0x8000) == 0x8000
+    assert O.f16_add(0x3C00, 0xBC00) == 0
+    assert O.f16_fma(0xBC00, 0x0000, 0x8000) == 0x8000
+    assert O.f16_fma(0x0001, 0x0001, 0x0000) == 0  # 2^-48 rounds to +0
+
+
+def test_v_expf_accuracy(O):
+    x = np.concatenate([np.linspace(-87, 88, 50001), np.array([0.0, -0.0, 1e-8, -1e-8])]).astype(np.float32)
+    e = O.v_expf(x)
+    ref = np.exp(x.astype(np.float64))
+    rel = np.abs(e - ref) / ref
+    assert rel.max() < 4 * 2.0 ** -24  # a few ulp (ggml's polynomial)
+    assert O.v_expf(np.array([-np.inf, -200.0], np.float32)).tolist() == [0.0, 0.0]
+
+
+def test_vec_dot_f16(O):
+    rng = np.random.default_rng(1)
+    for n in (32, 64, 96, 128, 256, 70):
+        x = O.fp32_to_fp16(rng.standard_normal(n))
+        y = O.fp32_to_fp16(rng.standard_normal(n))
+        ref = float(np.dot(x.view(np.float16).astype(np.float64), y.view(np.float16).astype(np.float64)))
+        got = float(O.vec_dot_f16(x, y))
+        assert abs(got - ref) <= 2e-3 * (1 + math.sqrt(n)), (n, got, ref)
+
+
+def test_soft_max_rms_swiglu_rope(O):
+    rng = np.random.default_rng(2)
+    s = (rng.standard_normal(96) * 5).astype(np.float32)
+    m = np.where(np.arange(96) < 70, 0.0, -np.inf).astype(np.float32)
+    p = O.soft_max_row(s, m, 0.125)
+    w = s.astype(np.float64) * 0.125 + m
+    ref = np.exp(w - w.max())
+    ref /= ref.sum()
+    assert np.abs(p - ref).max() < 1e-6 and (p[70:] == 0).all()
+    x = rng.standard_normal(2048).astype(np.float32)
+    assert np.allclose(O.rms_norm(x, 1e-5), x / np.sqrt((x.astype(np.float64) ** 2).mean() + 1e-5), rtol=1e-6)
+    g, u = rng.standard_normal(512).astype(np.float32), rng.standard_normal(512).astype(np.float32)
+    ref = g / (1 + np.exp(-g.astype(np.float64))) * u
+    assert np.allclose(O.swiglu(g, u), ref, rtol=1e-6, atol=1e-7)
+    tab = O.rope_table(64, 64)
+    q = rng.standard_normal(128).astype(np.float32)
+    th = 9 * 10000.0 ** (-np.arange(32) * 2 / 64)
+    q2 = q.reshape(2, 32, 2).astype(np.float64)
+    ref = np.stack([q2[..., 0] * np.cos(th) - q2[..., 1] * np.sin(th),
+                    q2[..., 0] * np.sin(th) + q2[..., 1] * np.cos(th)], -1).ravel()
+    assert np.abs(O.rope(q, 64, 64, 9, tab) - ref).max() < 1e-5
+
+
+def test_attn_decode_matches_float_attention(O):
+    rng = np.random.default_rng(3)
+    nh, nkv, hd, n_ctx = 8, 2, 64, 64
+    kc = np.zeros((n_ctx, nkv * hd), np.uint16)
+    vc = np.zeros((nkv * hd, n_ctx), np.uint16)
+    K, Vv = [], []
+    for p in range(10):
+        q = rng.standard_normal(nh * hd).astype(np.float32)
+        k = rng.standard_normal(nkv * hd).astype(np.float32)
+        v = rng.standard_normal(nkv * hd).astype(np.float32)
+        K.append(k)
+        Vv.append(v)
+        out = O.attn_decode(q, k, v, kc, vc, p, nh, nkv, hd, 0.125)
+        Ka, Va = np.stack(K).reshape(p + 1, nkv, hd), np.stack(Vv).reshape(p + 1, nkv, hd)
+        for h in range(nh):
+            gi = h // (nh // nkv)
+            sc = Ka[:, gi] @ q[h * hd:(h + 1) * hd].astype(np.float64) * 0.125
+            pr = np.exp(sc - sc.max())
+            pr /= pr.sum()
+            ref = pr @ Va[:, gi]
+            assert np.abs(out[h * hd:(h + 1) * hd] - ref).max() < 3e-2  # f16 K/V/q/p and f16 accumulation
+    assert O.attn_n_kv(0, 64) == 32 and O.attn_n_kv(31, 64) == 32 and O.attn_n_kv(32, 64) == 64
+
+
+def test_tiny_llama_token_oracle(O):
+    from tests import llama_model as LM
+    import ggml_mi355x.llama as LL
+    hp = LL.hparams(256, 2, 4, 2, 512, 300)
+    w = LM.build(hp, 0)
+    model, cache = LM.oracle_model(hp, w, 32)
+    for p, tok in enumerate([3, 299, 3]):
+        logits, trace = O.decode_token(model, tok, p, cache, n_threads=2)
+        assert logits.shape == (300,) and np.isfinite(logits).all() and len(trace) == 2
+        assert 0.05 < float(np.sqrt((trace[-1] ** 2).mean())) < 50
+
+
+def test_supports_decode_ops():
+    import ggml_mi355x as g
+    E, F = 2048, 5632
+    x = g.make_tensor(g.TYPE_F32, E, 1, 0x1000)
+    wn = g.make_tensor(g.TYPE_F32, E, 1, 0x2000)
+    assert g.supports_op(g.make_tensor(g.TYPE_F32, E, 1, 0x3000, op=g.OP_RMS_NORM, src0=x, op_params=[g.f32_bits(1e-5)]))
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, E + 8, 1, 0x3000, op=g.OP_RMS_NORM,
+                                           src0=g.make_tensor(g.TYPE_F32, E + 8, 1, 0x1000)))
+    assert g.supports_op(g.make_tensor(g.TYPE_F32, E, 1, 0x3000, op=g.OP_MUL, src0=x, src1=wn))
+    assert g.supports_op(g.make_tensor(g.TYPE_F32, E, 1, 0x3000, op=g.OP_ADD, src0=x, src1=wn))
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, E, 1, 0x3000, op=g.OP_ADD, src0=x,
+                                           src1=g.make_tensor(g.TYPE_F32, F, 1, 0x2000)))
+    gt = g.make_tensor(g.TYPE_F32, F, 1, 0x1000)
+    assert g.supports_op(g.make_tensor(g.TYPE_F32, F, 1, 0x3000, op=g.OP_SWIGLU, src0=gt, src1=gt))
+    emb = g.make_tensor(g.TYPE_Q4_K, E, 32000, 0x4000)
+    ids = g.make_tensor(g.TYPE_I32, 1, 1, 0x5000)
+    assert g.supports_op(g.make_tensor(g.TYPE_F32, E, 1, 0x3000, op=g.OP_GET_ROWS, src0=emb, src1=ids))
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, E, 1, 0x3000, op=g.OP_GET_ROWS, src0=emb, src1=x))
+    n_ctx, hd, nh, nkv = 256, 64, 32, 4
+    tab = g.make_tensor(g.TYPE_F32, hd, n_ctx, 0x6000)
+    kc = g.make_tensor(g.TYPE_F16, nkv * hd, n_ctx, 0x7000)
+    vc = g.make_tensor(g.TYPE_F16, n_ctx, nkv * hd, 0x8000)
+    q = g.make_tensor(g.TYPE_F32, nh * hd, 1, 0x9000)
+    kv = g.make_tensor(g.TYPE_F32, nkv * hd, 1, 0xa000)
+    att = g.make_tensor(g.TYPE_F32, nh * hd, 1, 0xb000, op=g.OP_ATTN_DECODE, srcs=[q, kv, kv, ids, kc, vc, tab],
+                        op_params=[nh, nkv, hd, g.f32_bits(0.125)])
+    assert g.supports_op(att)
+    bad = g.make_tensor(g.TYPE_F32, nh * hd, 1, 0xb000, op=g.OP_ATTN_DECODE, srcs=[q, kv, kv, ids, kc, vc, tab],
+                        op_params=[nh, 3, hd, g.f32_bits(0.125)])
+    assert not g.supports_op(bad)
+    rope = g.make_tensor(g.TYPE_F32, hd, nh, 0xc000, op=g.OP_ROPE, srcs=[g.make_tensor(g.TYPE_F32, hd, nh, 0x9000),
+                                                                         ids, tab], op_params=[hd])
+    assert g.supports_op(rope)
