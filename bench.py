@@ -1,6 +1,16 @@
 #!/usr/bin/env python3
-"""bench.py — tg (decode) tokens/s of the TinyLlama-1.1B Q4_K_M matmul chain on MI355X,
+"""bench.py — tg128 tokens/s of TinyLlama-1.1B Q4_K_M on MI355X (the full decode graph),
 plus the Q4_K x Q8_K GEMV's achieved HBM bandwidth against the roofline.
+
+Default workload ("token"): llama-bench's tg128 — token i decoded at position i of
+a fresh KV cache, i = 0 .. steps-1, each step the whole llm_build_llama graph
+(get_rows, per layer rms_norm -> q/k/v -> rope + f16 KV cache + attention -> o ->
+add -> rms_norm -> gate/up -> swiglu -> down -> add, then rms_norm -> output)
+through ggml_mi355x.llama.LlamaDecoder and mi355x_backend_graph_compute (node
+fusion: 5 launches per layer + 2, replayed from a hipGraph). The token id and
+position are written to the device before each step as ggml's inputs are. The
+per-token MUL_MAT chain alone ("chain" workload, described below) is reported
+beside it in "matmul_chain".
 
 Metric (BASELINE.json): "tg128 tok/s + Q4_K GEMV achieved-HBM-GB/s, TinyLlama-1.1B
 Q4_K_M @1 GPU". One step = one decoded token = the model's full per-token MUL_MAT
@@ -180,10 +190,55 @@ class Chain:
         return len(self.stages)
 
 
+HPARAMS = {"tinyllama-1.1b": dict(n_head=32, n_head_kv=4, freq_base=10000.0),
+           "llama-3-8b": dict(n_head=32, n_head_kv=8, freq_base=500000.0),
+           "llama-3-70b": dict(n_head=64, n_head_kv=8, freq_base=500000.0)}
+
+
+class Token:
+    """The full llama decode graph of one token (ggml_mi355x.llama.LlamaDecoder:
+    get_rows, 22 x [rms_norm, q/k/v, rope + KV cache + attention, o, add, rms_norm,
+    gate/up, swiglu, down, add], rms_norm, output) on synthetic Q4_K_M weights of the
+    real shapes (the chain's weights and type mix, plus token_embd Q4_K and f32 norms)."""
+
+    def __init__(self, model, dev, seed, be, n_ctx):
+        from ggml_mi355x.llama import LlamaDecoder, hparams
+        m = MODELS[model]
+        h = HPARAMS[model]
+        self.hp = hparams(m["E"], m["L"], h["n_head"], h["n_head_kv"], m["FF"], m["V"], freq_base=h["freq_base"])
+        self.model = model
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(seed)
+        self.stages = q4km_chain(model)
+        w = {}
+        self.bytes_per_token = 0
+        for stage in self.stages:
+            for name, typ, K, N in stage:
+                w[name] = (typ, random_kquant(typ, N, K, gen, dev, rms_keep=True))
+                self.bytes_per_token += w[name][1].numel()
+        w["token_embd"] = (g.TYPE_Q4_K, random_kquant(g.TYPE_Q4_K, m["V"], m["E"], gen, dev))
+        w["output_norm"] = torch.rand(m["E"], device=dev, generator=gen) * 0.4 + 0.8
+        for i in range(m["L"]):
+            for nm in ("attn_norm", "ffn_norm"):
+                w[f"blk.{i}.{nm}"] = torch.rand(m["E"], device=dev, generator=gen) * 0.4 + 0.8
+        self.w = w
+        self.wl = [[w[name] for name, _, _, _ in stage] for stage in self.stages]  # per stage, as Chain.w
+        self.n_ctx = n_ctx
+        self.dec = LlamaDecoder(be, self.hp, w, n_ctx)
+        rng = np.random.default_rng(seed)
+        self.tokens = rng.integers(0, m["V"], size=n_ctx).tolist()
+
+    def launches(self):
+        return 5 * self.hp["n_layer"] + 2
+
+
 def timed_kernel_stats(be, chain, tokens):
     """Per-launch kernel timing (hipExtLaunchKernelGGL events) over `tokens` eager chains."""
     g.timing_enable(True)
-    for _ in range(tokens):
+    for i in range(tokens):
+        if isinstance(chain, Token):
+            chain.dec.step(chain.tokens[i], i, use_graph=False)
+            continue
         rc = be.graph_compute(chain.nodes, use_graph=False)
         assert rc == 0, rc
     rows = g.timing_read()
@@ -246,7 +301,7 @@ def prefill_chain(chain, dev, M=512, reps=3):
 
     def run():
         for si, stage in enumerate(chain.stages):
-            for (name, typ, K, N), (_, w) in zip(stage, chain.w[si]):
+            for (name, typ, K, N), (_, w) in zip(stage, getattr(chain, "wl", chain.w)[si]):
                 g.mul_mat(typ, w, K, xs[K], out=ys[N], workspace=ws)
 
     run()
@@ -262,6 +317,68 @@ def prefill_chain(chain, dev, M=512, reps=3):
     return {"M": M, "ms_per_batch": round(ms, 3), "tok_s": round(M / (ms * 1e-3), 1),
             "int_TOPS": round(2 * macs / (ms * 1e-3) / 1e12, 1),
             "note": "all chain matmuls at ne11=M (quantize + kq_mmq per matmul, eager)"}
+
+
+def chain_side(model, dev, be, steps=64, warmup=8):
+    """The per-token MUL_MAT chain alone (no norm/rope/attention/swiglu), hipGraph replay:
+    the figure earlier rounds reported as the headline."""
+    chain = Chain(model, dev, seed=0x51A7)
+    for _ in range(warmup):
+        assert be.graph_compute(chain.nodes) == 0
+    be.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st = torch.cuda.ExternalStream(be.stream)
+    e0.record(st)
+    for _ in range(steps):
+        assert be.graph_compute(chain.nodes) == 0
+    e1.record(st)
+    be.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    out = {"tok_s": round(1e3 / ms, 1), "ms_per_token": round(ms, 4), "stages_per_token": chain.launches(),
+           "weights_MB_per_token": round(chain.bytes_per_token / 1e6, 1)}
+    del chain
+    torch.cuda.empty_cache()
+    return out
+
+
+def cpu_baseline_token(tk, seconds):
+    """The oracle's restated llm_build_llama token (ggml-cpu semantics op by op: the
+    matmuls through the restated ggml_compute_forward_mul_mat with pthreads, the other
+    ops scalar) on the same weights, positions 0, 1, 2, ... of a fresh KV cache, timed
+    on this host's cores for a bounded number of tokens."""
+    from oracle import kq_ops_oracle as OO
+    try:
+        ncores = len(os.sched_getaffinity(0))
+    except AttributeError:
+        ncores = os.cpu_count() or 1
+    threads = max(1, min(16, ncores))
+    hp = tk.hp
+    host = {k: ((v[0], v[1].cpu().numpy()) if isinstance(v, tuple) else v.cpu().numpy()) for k, v in tk.w.items()}
+    layers = []
+    for i in range(hp["n_layer"]):
+        p = f"blk.{i}."
+        layers.append({"attn_norm": host[p + "attn_norm"], "ffn_norm": host[p + "ffn_norm"],
+                       "wq": host[p + "attn_q"], "wk": host[p + "attn_k"], "wv": host[p + "attn_v"],
+                       "wo": host[p + "attn_output"], "w_gate": host[p + "ffn_gate"], "w_up": host[p + "ffn_up"],
+                       "w_down": host[p + "ffn_down"]})
+    model = {"hp": hp, "tok_embd": host["token_embd"], "output": host["output"], "output_norm": host["output_norm"],
+             "layers": layers, "rope_table": OO.rope_table(tk.n_ctx, hp["head_dim"], hp["freq_base"])}
+    kvw = hp["n_head_kv"] * hp["head_dim"]
+    cache = [(np.zeros((tk.n_ctx, kvw), np.uint16), np.zeros((kvw, tk.n_ctx), np.uint16))
+             for _ in range(hp["n_layer"])]
+    OO.lib()
+    tokens, t0 = 0, time.perf_counter()
+    while True:
+        OO.decode_token(model, tk.tokens[tokens], tokens, cache, n_threads=threads)
+        tokens += 1
+        el = time.perf_counter() - t0
+        if el >= seconds or tokens >= 50 or tokens >= tk.n_ctx:
+            break
+    return {"value": tokens / el, "unit": "tok/s", "cores": threads, "kind": "port",
+            "sample": f"{tokens} token(s) (positions 0..{tokens - 1}) of the full {tk.model} Q4_K_M decode graph "
+                      f"through the oracle's restated llm_build_llama / ggml-cpu ops (mul_mat: "
+                      f"quantize_row_q8_K_ref + NEON-order vec_dot, {threads} pthreads; f16 attention, "
+                      f"soft_max, rope, rms_norm, swiglu scalar), {el:.1f} s"}
 
 
 def cpu_baseline(chain, seconds):
@@ -312,7 +429,13 @@ def main():
                     help="auto/rows: kq_rows per stage (hipGraph replay); chain: one persistent "
                          "kq_chain launch per token; tasks: kq_gemv per stage")
     ap.add_argument("--no-prefill", action="store_true")
+    ap.add_argument("--workload", default="token", choices=["token", "chain"],
+                    help="token: the full decode graph (tg128: token i at position i of a fresh KV cache); "
+                         "chain: the per-token MUL_MAT chain only")
+    ap.add_argument("--no-chain", action="store_true", help="token workload: skip the matmul-chain side figure")
     args = ap.parse_args()
+    if args.workload == "token" and (args.mode == "rowsplit" or args.gguf or args.impl != "auto"):
+        args.workload = "chain"  # the row-split, GGUF-file and kernel-A/B runs are matmul-chain modes
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -344,6 +467,18 @@ def main():
         chain = runner.chain
         step = runner.step
         stream = torch.cuda.current_stream()
+    elif args.workload == "token":
+        be = g.Backend(local)
+        n_ctx = max(128, (max(args.steps, args.warmup) + 31) // 32 * 32)
+        chain = Token(args.model, dev, 0x51A7 + rank, be, n_ctx)
+        stream = torch.cuda.ExternalStream(be.stream)
+        use_graph = not args.no_graph
+        pos = [0]
+
+        def step():
+            i = pos[0]
+            chain.dec.step(chain.tokens[i], i, use_graph=use_graph)
+            pos[0] = i + 1
     else:
         chain = Chain(args.model, dev, seed=0x51A7 + rank, gguf=gguf)
         be = g.Backend(local)
@@ -360,6 +495,10 @@ def main():
     torch.cuda.synchronize()
     if use_backend:
         be.synchronize()
+    if isinstance(chain, Token):  # tg128: the timed tokens start from an empty KV cache
+        chain.dec.reset()
+        torch.cuda.synchronize()
+        pos[0] = 0
     barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
@@ -389,6 +528,9 @@ def main():
         roof = None
         per = {}
         if use_backend:
+            if isinstance(chain, Token):
+                chain.dec.reset()
+                torch.cuda.synchronize()
             per = timed_kernel_stats(be, chain, tokens=4)
             dom = max(per, key=lambda k: per[k]["ms"])
             d = per[dom]
@@ -410,13 +552,21 @@ def main():
                     roof["traffic_source"] = "profiles/r01_summary.json"
         kernels = {k: {"launches": v["launches"], "us_per_launch": round(v["ms"] * 1e3 / v["launches"], 2),
                        "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} for k, v in per.items()}
+        side = None
+        if isinstance(chain, Token) and not args.no_chain and world == 1:
+            side = chain_side(args.model, dev, be)
         large = None if args.no_large or world > 1 else large_gemv(dev)
         prefill = None if args.no_prefill or world > 1 or not use_backend else prefill_chain(chain, dev)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
-            cpu = cpu_baseline(chain, args.cpu_seconds)
+            cpu = cpu_baseline_token(chain, args.cpu_seconds) if isinstance(chain, Token) else \
+                cpu_baseline(chain, args.cpu_seconds)
         wbytes = chain.bytes_per_token * (world if args.mode == "rowsplit" else 1)
-        if not use_backend:
+        if isinstance(chain, Token):
+            executor = ("LlamaDecoder -> mi355x_backend_graph_compute: node fusion (norm/swiglu GEMV prologues, "
+                        "residual epilogues), kq_rows + kq_attn_decode, " +
+                        ("hipGraph replay" if not args.no_graph else "eager"))
+        elif not use_backend:
             executor = "rowsplit: gemv_fused per stage + RCCL all_gather"
         elif args.impl == "chain":
             executor = "kq_chain: 1 persistent launch per token (tagged write-through hand-off per stage)"
@@ -430,8 +580,12 @@ def main():
             "higher_is_better": True, "scaling": "weak" if args.mode == "replicas" else "strong",
             "vs_baseline": None, "dtype": "q4_K/q6_K x q8_K (u4/u6*i8 dot4 -> i32, f32 combine)",
             "data": (f"GGUF weights {os.path.basename(args.gguf)}; random f32 first activation" if args.gguf else
+                     "synthetic (random valid K-quant blocks of the real shapes, f32 norms, random token ids)"
+                     if isinstance(chain, Token) else
                      "synthetic (random valid K-quant blocks of the real shapes; random f32 activations)"),
-            "config": {"workload": f"{chain.model} Q4_K_M decode matmul chain (tg, 1 token/step)",
+            "config": {"workload": (f"{chain.model} Q4_K_M tg{args.steps}: full decode graph, token i at "
+                                    f"position i of a fresh f16 KV cache" if isinstance(chain, Token) else
+                                    f"{chain.model} Q4_K_M decode matmul chain (tg, 1 token/step)"),
                        "weights_MB_per_token": round(wbytes / 1e6, 1),
                        "stages_per_token": chain.launches(),
                        "executor": executor,
@@ -443,6 +597,7 @@ def main():
             "kernels": kernels,
             "gemv_large": large,
             "prefill_pp512": prefill,
+            "matmul_chain": side,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

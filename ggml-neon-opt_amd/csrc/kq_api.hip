@@ -381,6 +381,10 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
             pre_env = e ? atoi(e) : 1;
         }
         a.diag = diag;
+        // weight steps issued before the activation is quantized. One: a deeper early burst
+        // delays the activation loads queued behind it. Alone, K = 2048 GEMVs ran 5-9 %
+        // faster with the whole ring (tools/gemv_sweep.py pre0=3), but with the fused norm
+        // prologue (two vectors to fetch) the decode token was 1.6 % slower.
         a.pre0 = pre_env < 0 ? 0 : pre_env > 3 ? 3 : pre_env;
     }
     a.stamps = g_stamps;

@@ -166,6 +166,7 @@ struct AttnArgs {
     float *out;                   // [n_head*head_dim]
     int n_ctx, n_head, n_head_kv, head_dim;
     float scale;
+    int diag;  // diagnostics only (MI355X_ATTN_DIAG): 1/2/3 stop after loads/KQ/soft_max, 4 empty
 };
 
 // kq_chain: one launch runs a whole sequence of decode MUL_MAT stages (a token's

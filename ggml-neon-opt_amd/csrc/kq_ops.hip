@@ -15,6 +15,7 @@
 // these ops are HBM/latency-bound and tiny at decode, so the layout work is about
 // launch count (they fuse into the GEMVs where the graph allows, kq_rows.hip).
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -172,6 +173,12 @@ __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, floa
 
 // ------------------------------------------------------------ decode attention
 // One workgroup per query head h (kv head g = h / (n_head/n_head_kv)), 256 threads.
+//  0. Every load that does not depend on the position is issued together with the
+//     position itself: this token's q/k/v, K-cache row t (the cell thread t scores in
+//     the first pass) and the first VPF 8-cell groups of this thread's V-cache row(s).
+//     Only the rope-table row waits for the position, so a launch pays two memory
+//     latencies instead of four. Prefetched cells at or after pos are never used (the
+//     new cell comes from LDS, later cells are masked).
 //  1. rope(q_h), rope(k_g) at `pos` -> f16; v_g -> f16. The first query head of each
 //     kv group writes the new cell to the caches (K [cell][kvw], V transposed
 //     [ch][n_ctx]); every workgroup uses its own LDS copy of that cell, so no
@@ -183,23 +190,54 @@ __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, floa
 //     the double sum over groups in order (one lane), p = e * (float)(1.0/sum) -> f16.
 //  4. kqv[d] = vec_dot_f16(v_cache[g*hd+d][0..n_kv), p16): thread (d, j) runs
 //     accumulator j (8 lanes) over cells 32it+8j+l, then the f16 reduce tree.
+// A position outside the cache fails loudly: NaN output, caches untouched.
 template <int HD>
 __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
-    static_assert(HD % 32 == 0 && HD <= 256, "head_dim");
+    static_assert(HD == 64 || HD == 128, "head_dim");
+    constexpr int KV4 = HD / 8;          // 16-B pieces of one K-cache row
+    constexpr int ITEMS = HD * 4 / 256;  // KQV (d, j) items per thread
+    constexpr int VPF = 8 / ITEMS;       // prefetched 32-cell iterations per item
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int h = blockIdx.x;
     const int gsz = a.n_head / a.n_head_kv;
     const int g = h / gsz;
     const int kvw = a.n_head_kv * HD;
-    const int pos = *a.pos;
-    if (pos < 0 || pos >= a.n_ctx) {  // no cache cell for this position: fail loudly (NaN), touch nothing
-        for (int d = threadIdx.x; d < HD; d += 256) a.out[(int64_t)h * HD + d] = __builtin_nanf("");
-        return;
-    }
-    int n_kv = (pos + 1 + 31) / 32 * 32;
-    n_kv = n_kv < 32 ? 32 : n_kv;
-    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
     const int t = threadIdx.x;
+    if (a.diag == 4) return;  // diagnostics (MI355X_ATTN_DIAG): empty launch
+
+    // ---- 0. position-independent loads, issued with the position
+    const int pos_in = *a.pos;
+    float x0 = 0.f, x1 = 0.f, y0 = 0.f, y1 = 0.f;
+    if (t < HD / 2) {
+        const float *qp = a.q + (int64_t)h * HD + 2 * t;
+        const float *kp = a.k + (int64_t)g * HD + 2 * t;
+        x0 = qp[0];
+        x1 = qp[1];
+        y0 = kp[0];
+        y1 = kp[1];
+    } else if (t < HD / 2 + HD) {
+        x0 = a.v[(int64_t)g * HD + (t - HD / 2)];
+    }
+    uint4 kpre[KV4] = {};
+    if (t < a.n_ctx) {
+        const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)t * kvw + (int64_t)g * HD);
+#pragma unroll
+        for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
+    }
+    uint4 vpre[ITEMS][VPF] = {};
+#pragma unroll
+    for (int ii = 0; ii < ITEMS; ++ii) {
+        const int item = t + 256 * ii, d = item >> 2, j = item & 3;
+        const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx + 8 * j;
+#pragma unroll
+        for (int it = 0; it < VPF; ++it)
+            if (32 * it < a.n_ctx) vpre[ii][it] = *(const uint4 *)(vr + 32 * it);
+    }
+
+    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;  // no cache cell for this position
+    const int pos = bad ? 0 : pos_in;
+    int n_kv = (pos + 1 + 31) / 32 * 32;
+    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
     // LDS (attn_lds): q16 | k16 | v16 (HD f16 each) | w (n_ctx f32) | p16 (n_ctx f16) |
     // red (HD*32 f16 accumulators) | scal (max, 1/sum); every piece 16-B aligned
     uint16_t *q16 = (uint16_t *)smem;
@@ -211,40 +249,54 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     float *scal = (float *)(red + HD * 32);
 
     const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
-    const bool writer = (h % gsz) == 0;
+    const bool writer = !bad && (h % gsz) == 0;
     if (t < HD / 2) {
         const float c = tc[2 * t], s = tc[2 * t + 1];
-        const float *qp = a.q + (int64_t)h * HD + 2 * t;
-        const float2 rq = rope_pair(qp[0], qp[1], c, s);
+        const float2 rq = rope_pair(x0, x1, c, s);
         q16[2 * t] = h2u(f2h_rne(rq.x));
         q16[2 * t + 1] = h2u(f2h_rne(rq.y));
-        const float *kp = a.k + (int64_t)g * HD + 2 * t;
-        const float2 rk = rope_pair(kp[0], kp[1], c, s);
+        const float2 rk = rope_pair(y0, y1, c, s);
         const uint16_t k0 = h2u(f2h_rne(rk.x)), k1 = h2u(f2h_rne(rk.y));
         k16[2 * t] = k0;
         k16[2 * t + 1] = k1;
         if (writer) *(uint32_t *)(a.k_cache + (int64_t)pos * kvw + (int64_t)g * HD + 2 * t) = k0 | ((uint32_t)k1 << 16);
     } else if (t < HD / 2 + HD) {
         const int d = t - HD / 2;
-        const uint16_t vv = h2u(f2h_rne(a.v[(int64_t)g * HD + d]));
+        const uint16_t vv = h2u(f2h_rne(x0));
         v16[d] = vv;
         if (writer) a.v_cache[(int64_t)(g * HD + d) * a.n_ctx + pos] = vv;
     }
     __syncthreads();
+    if (a.diag == 1) {  // diagnostics: stop after the loads and rope
+        if (t < HD) a.out[(int64_t)h * HD + t] = x0 + __uint_as_float(kpre[0].x ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
+        return;
+    }
 
-    // KQ + scale + mask
+    // KQ + scale + mask; the first pass (c == t) scores the prefetched row
     for (int c = t; c < n_kv; c += 256) {
         float s = -INFINITY;
         if (c <= pos) {
-            const uint4 *kr = c == pos ? (const uint4 *)k16 : (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
-            uint4 kv[HD / 8];
+            uint4 kv[KV4];
+            if (c == pos) {
 #pragma unroll
-            for (int i = 0; i < HD / 8; ++i) kv[i] = kr[i];
+                for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+            } else if (c == t) {
+#pragma unroll
+                for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
+            } else {
+                const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+#pragma unroll
+                for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
+            }
             s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
         }
         w[c] = s;
     }
     __syncthreads();
+    if (a.diag == 2) {  // diagnostics: stop after KQ
+        if (t < HD) a.out[(int64_t)h * HD + t] = w[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+        return;
+    }
     // max (order-free), then exp + group sums
     if (t < 64) {
         float m = -INFINITY;
@@ -266,7 +318,8 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
     }
     __syncthreads();
-    if (t == 0) {
+    if (t == 0) {  // the sequential double sum is the pos-dependent part of this launch
+                   // (~40 ns per group, f64 issue-bound; tools/attn_phases.py)
         double sum = 0.0;
         for (int gi = 0; gi < n_kv / 4; ++gi)
             sum += (double)((w[4 * gi] + w[4 * gi + 1]) + (w[4 * gi + 2] + w[4 * gi + 3]));
@@ -277,18 +330,31 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     const float inv = scal[1];
     for (int c = t; c < n_kv; c += 256) p16[c] = h2u(f2h_rne(w[c] * inv));
     __syncthreads();
+    if (a.diag == 3) {  // diagnostics: stop after soft_max
+        if (t < HD) a.out[(int64_t)h * HD + t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+        return;
+    }
 
     // KQV: thread (d, j) -> accumulator j of output d
     const int n_it = (pos + 32) / 32;  // iterations holding a cell <= pos; later ones add exact zeros
-    for (int item = t; item < HD * 4; item += 256) {
+#pragma unroll
+    for (int ii = 0; ii < ITEMS; ++ii) {
+        const int item = t + 256 * ii;
         const int d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
         h16 acc[8];
 #pragma unroll
         for (int l = 0; l < 8; ++l) acc[l] = (h16)0.0f;
-        for (int it = 0; it < n_it; ++it) {
+        for (int it = 0; it < n_it; ++it) {  // VPF prefetched iterations, then global loads
             const int c0 = 32 * it + 8 * j;
-            uint4 vv = *(const uint4 *)(vr + c0);
+            uint4 vv;
+            if (it < VPF) {
+#pragma unroll
+                for (int k = 0; k < VPF; ++k)
+                    if (k == it) vv = vpre[ii][k];
+            } else {
+                vv = *(const uint4 *)(vr + c0);
+            }
             const uint4 pp = *(const uint4 *)(p16 + c0);
             uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
             const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
@@ -313,7 +379,8 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
             const h16 s1 = red[(d * 4 + 1) * 8 + l] + red[(d * 4 + 3) * 8 + l];
             s[l] = s0 + s1;
         }
-        a.out[(int64_t)h * HD + d] = f16x8_reduce(s);
+        const float o = f16x8_reduce(s);
+        a.out[(int64_t)h * HD + d] = bad ? __builtin_nanf("") : o;
     }
 }
 
@@ -479,6 +546,11 @@ int mi355x_attn_decode(const mi355x_attn_desc *d, void *stream) {
     a.n_head_kv = d->n_head_kv;
     a.head_dim = d->head_dim;
     a.scale = d->scale;
+    static const int diag = [] {
+        const char *e = getenv("MI355X_ATTN_DIAG");
+        return e ? atoi(e) : 0;
+    }();
+    a.diag = diag;
     const int rc = check_attn(a);
     if (rc) return rc;
     if (!device_ok()) return MI355X_E_NODEVICE;

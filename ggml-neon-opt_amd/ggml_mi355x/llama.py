@@ -57,8 +57,9 @@ class LlamaDecoder:
         def buf(n, dtype=f32):
             return torch.zeros(n, dtype=dtype, device=dev)
 
-        self.token = buf(1, torch.int32)
-        self.pos = buf(1, torch.int32)
+        # inp_tokens and inp_pos side by side: one 8-byte set_tensor per token
+        self.inp = buf(2, torch.int32)
+        self.token, self.pos = self.inp[0:1], self.inp[1:2]
         self.table = rope_table(n_ctx, hd, hp["freq_base"], 1.0, device=dev, stream=backend.stream)
         self.k_cache = [torch.zeros((n_ctx, kvw), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
         self.v_cache = [torch.zeros((kvw, n_ctx), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
@@ -144,8 +145,7 @@ class LlamaDecoder:
         L = lib()
         hp = self._host.data_ptr() + 8 * self._slot
         self._slot += 1
-        rc = L.mi355x_backend_set_tensor(self.b.h, self.token.data_ptr(), hp, 4)
-        rc = rc or L.mi355x_backend_set_tensor(self.b.h, self.pos.data_ptr(), hp + 4, 4)
+        rc = L.mi355x_backend_set_tensor(self.b.h, self.inp.data_ptr(), hp, 8)
         if rc:
             raise Mi355xError(f"set_tensor failed ({rc})")
         rc = L.mi355x_backend_graph_compute(self.b.h, self._arr, len(self.nodes), 1 if use_graph else 0)

@@ -101,9 +101,11 @@ def test_rope(dev, O, hd, nh, base):
 
 
 # ---------------------------------------------------------------- attention
-@pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 256), (128, 32, 8, 128), (64, 8, 8, 64)])
+@pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 256), (128, 32, 8, 128), (64, 8, 8, 64), (64, 8, 2, 512),
+                                             (128, 8, 4, 512)])
 def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx):
-    """A growing KV cache: every position's output and both caches bit-exact."""
+    """A growing KV cache: every position's output and both caches bit-exact (positions
+    past the kernel's prefetched cells — 256 K rows, 256/128 V cells — included)."""
     import torch
     import ggml_mi355x as g
     rng = np.random.default_rng(hd + nh)
@@ -115,7 +117,7 @@ def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx):
     kc_ref = np.zeros((n_ctx, kvw), np.uint16)
     vc_ref = np.zeros((kvw, n_ctx), np.uint16)
     scale = float(np.float32(1.0) / np.sqrt(np.float32(hd)))
-    positions = list(range(0, 40)) + [n_ctx - 1]
+    positions = list(range(0, 40)) + ([127, 128, 255, 256, 300] if n_ctx > 256 else []) + [n_ctx - 1]
     for p in positions:
         q = (rng.standard_normal(nh * hd) * 2).astype(np.float32)
         k = (rng.standard_normal(kvw) * 2).astype(np.float32)
