@@ -542,14 +542,16 @@ def main():
         if roof is not None:
             # HBM traffic of the same kernel from the committed rocprofv3 PMC pass of this
             # bench command (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), per launch
-            prof = os.path.join(ROOT, "profiles", "r01_summary.json")
+            pname = "r01_token_summary.json" if isinstance(chain, Token) else "r01_chain_summary.json"
+            prof = os.path.join(ROOT, "profiles", pname)
             if os.path.exists(prof):
                 with open(prof) as f:
                     pk = json.load(f).get("by_kernel", {}).get(roof["kernel"])
                 if pk and pk.get("hbm_read_per_launch"):
                     roof["traffic"] = round(pk["hbm_read_per_launch"], 0)
                     roof["traffic_unit"] = "bytes/launch (HBM read, rocprofv3 FETCH_SIZE x2)"
-                    roof["traffic_source"] = "profiles/r01_summary.json"
+                    roof["traffic_source"] = "profiles/" + pname
+                    roof["rocprof_us_per_launch"] = round(pk["us_per_launch"], 2)
         kernels = {k: {"launches": v["launches"], "us_per_launch": round(v["ms"] * 1e3 / v["launches"], 2),
                        "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} for k, v in per.items()}
         side = None

@@ -39,9 +39,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--steps", type=int, default=64)
     ap.add_argument("--launches", type=int, default=89)
+    ap.add_argument("--pmc-warmup", type=int, default=None, help="PMC passes: warmup tokens (default: --warmup)")
+    ap.add_argument("--pmc-steps", type=int, default=None, help="PMC passes: timed tokens (default: --steps)")
     ap.add_argument("--bench-json", default=None, help="bench JSON line (for the algorithmic bytes)")
     a = ap.parse_args()
     L, W, K = a.launches, a.warmup, a.steps
+    PW = a.warmup if a.pmc_warmup is None else a.pmc_warmup
+    PK = a.steps if a.pmc_steps is None else a.pmc_steps
     tr = kq_rows(os.path.join(a.src, "trace", "run_kernel_trace.csv"))
     timed = tr[W * L:(W + K) * L]
     assert len(timed) == K * L, (len(tr), len(timed))
@@ -49,9 +53,9 @@ def main():
     pf = os.path.join(a.src, "pmc_fetch", "run_counter_collection.csv")
     pw = os.path.join(a.src, "pmc_write", "run_counter_collection.csv")
     if os.path.exists(pf):
-        fetch = [float(r["Counter_Value"]) * 1024 * 2 for r in kq_rows(pf)][W * L:(W + K) * L]
+        fetch = [float(r["Counter_Value"]) * 1024 * 2 for r in kq_rows(pf)][PW * L:(PW + PK) * L]
     if os.path.exists(pw):
-        write = [float(r["Counter_Value"]) * 1024 for r in kq_rows(pw)][W * L:(W + K) * L]
+        write = [float(r["Counter_Value"]) * 1024 for r in kq_rows(pw)][PW * L:(PW + PK) * L]
 
     def dur(r):
         return (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3  # us
@@ -65,10 +69,11 @@ def main():
              "lds": int(timed[idx[0]]["LDS_Block_Size"]),
              "us_mean": statistics.mean(dur(timed[i]) for i in idx),
              "us_median": statistics.median(dur(timed[i]) for i in idx)}
+        pidx = [t * L + p for t in range(PK)]
         if fetch:
-            e["hbm_read_bytes"] = statistics.median(fetch[i] for i in idx)
+            e["hbm_read_bytes"] = statistics.median(fetch[i] for i in pidx)
         if write:
-            e["hbm_write_bytes"] = statistics.median(write[i] for i in idx)
+            e["hbm_write_bytes"] = statistics.median(write[i] for i in pidx)
         per_pos.append(e)
     by_kernel = {}
     for e in per_pos:
