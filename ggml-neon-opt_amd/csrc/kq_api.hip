@@ -391,6 +391,11 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     a.stamps_cap = g_stamps_cap;
     // Waves: one workgroup of ROWS_WAVES per CU; each matrix gets waves in
     // proportion to its bytes (never more waves than rows), rows split evenly.
+    static const int wpc_env = [] {  // experiment knob: cap on active waves per CU
+        const char *e = getenv("MI355X_GEMV_WPC");
+        return e ? atoi(e) : 0;
+    }();
+    if (wpc_env > 0 && wpc_env < waves_per_cu) waves_per_cu = wpc_env;
     const int64_t cap = (int64_t)num_cus() * waves_per_cu;
     int64_t wv[MI355X_MAX_FUSED] = {0, 0, 0, 0};
     int64_t waves = 0;
@@ -646,13 +651,17 @@ size_t ext_x_bytes(int64_t k) { return ((size_t)k * 4 + 255) & ~(size_t)255; }
 
 int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *ws, size_t ws_size,
             hipStream_t stream, const mi355x_gemv_ext *ext) {
-    const bool has_ext = ext && (ext->prologue != MI355X_PRO_NONE || [&] {
+    const bool has_ext = ext && (ext->prologue != MI355X_PRO_NONE || ext->epilogue != MI355X_EPI_NONE || [&] {
         for (int i = 0; i < n && i < MI355X_MAX_FUSED; ++i)
             if (ext->residual[i]) return true;
         return false;
     }());
     if (has_ext) {
         if (ext->prologue != MI355X_PRO_NONE && !ext->x2) return MI355X_E_INVAL;
+        const bool epi = ext->epilogue == MI355X_EPI_SWIGLU;
+        if (ext->epilogue != MI355X_EPI_NONE && !epi) return MI355X_E_INVAL;
+        if (epi && (n != 2 || !ext->epi_y || d[0].n_rows != d[1].n_rows || ext->residual[0] || ext->residual[1]))
+            return MI355X_E_INVAL;
         const bool x2_ok = ext->prologue == MI355X_PRO_NONE || ((uintptr_t)ext->x2 & 15u) == 0;
         if (rows_enabled() && k / QK <= kRowsFusedMaxNb && ((uintptr_t)x & 15u) == 0 && x2_ok) {
             RowsPlan rp;
@@ -669,10 +678,26 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
                     rp.a.res[i] = ext->residual[i];
                     rp.a.n_rows[i] = (int)d[i].n_rows;
                 }
-                if (!device_ok()) return MI355X_E_NODEVICE;
-                return launch_rows(rp, stream);
+                // SWIGLU epilogue in-kernel when gate wave j and up wave j land in the same
+                // workgroup with the same rows: equal wave counts, up's first wave on a
+                // workgroup boundary (gw = wave * grid + block)
+                const int g = (int)rp.grid.x;
+                const bool paired = epi && rp.a.wave_prefix[2] == 2 * rp.a.wave_prefix[1] &&
+                                    rp.a.wave_prefix[1] % g == 0 && rp.a.rbase[0] == rp.a.rbase[1] &&
+                                    rp.a.rrem[0] == rp.a.rrem[1];
+                if (!epi || paired) {
+                    if (paired) {
+                        rp.a.epi = 1;
+                        rp.a.epi_n = (int)d[0].n_rows;
+                        rp.a.epi_wave_off = rp.a.wave_prefix[1] / g;
+                        rp.a.epi_y = ext->epi_y;
+                    }
+                    if (!device_ok()) return MI355X_E_NODEVICE;
+                    return launch_rows(rp, stream);
+                }
+            } else if (rc != MI355X_E_UNSUPPORTED) {
+                return rc;
             }
-            if (rc != MI355X_E_UNSUPPORTED) return rc;
         }
         // staged: prologue kernel -> GEMV -> residual adds
         const float *xs = x;
@@ -696,6 +721,7 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
                 rc = launch_binary(0, d[i].y, ext->residual[i], d[i].y, d[i].n_rows, stream);
                 if (rc) return rc;
             }
+        if (epi && d[0].n_rows > 0) return launch_swiglu(d[0].y, d[1].y, ext->epi_y, d[0].n_rows, stream);
         return MI355X_OK;
     }
     const bool fusedq = k / QK <= kFusedQMaxNb && ((uintptr_t)x & 15u) == 0;
@@ -860,6 +886,7 @@ int mi355x_gemv_fused_ext(const mi355x_gemv_desc *descs, int n_desc, const float
     if (k <= 0 || k % QK || n_desc < 1 || n_desc > MI355X_MAX_FUSED) return MI355X_E_INVAL;
     if (ext && (ext->prologue < MI355X_PRO_NONE || ext->prologue > MI355X_PRO_SWIGLU)) return MI355X_E_INVAL;
     if (ext && ext->prologue == MI355X_PRO_RMS_NORM && !(ext->eps >= 0.0f)) return MI355X_E_INVAL;
+    if (ext && ext->epilogue == MI355X_EPI_SWIGLU && ((uintptr_t)ext->epi_y & 3u)) return MI355X_E_INVAL;
     for (int i = 0; i < n_desc; ++i) {
         if (descs[i].y && ((uintptr_t)descs[i].y & 3u)) return MI355X_E_INVAL;
         if (ext && ext->residual[i] && ((uintptr_t)ext->residual[i] & 3u)) return MI355X_E_INVAL;

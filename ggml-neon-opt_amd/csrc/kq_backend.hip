@@ -68,6 +68,7 @@ struct Launch {
     const float *res[MI355X_MAX_FUSED] = {};
     const float *norm_w = nullptr;  // single RMS_NORM with its MUL fused
     float *norm_y = nullptr;
+    float *epi_y = nullptr;  // GEMV run [gate, up] with the SWIGLU node fused as its epilogue
 };
 
 float f_of(int32_t bits) {
@@ -169,6 +170,16 @@ std::vector<Launch> plan_launches(mi355x_tensor *const *nodes, int n, bool fuse)
                 l.y[k] = (float *)ad->data;
                 ++end;
             }
+            // epilogue fusion: SWIGLU(gate, up) of a two-MUL_MAT run whose outputs only it reads
+            if (fuse && end < n && cnt == 2 && nodes[end]->op == MI355X_OP_SWIGLU && !l.res[0] && !l.res[1]) {
+                const mi355x_tensor *sg = nodes[end];
+                if (sg->src[0] == nodes[head] && sg->src[1] == nodes[head + 1] && elidable(nodes[head], readers[head]) &&
+                    elidable(nodes[head + 1], readers[head + 1]) && nodes[head]->ne[0] == nodes[head + 1]->ne[0] &&
+                    sg->ne[0] == nodes[head]->ne[0] && sg->ne[1] == 1 && sg->type == MI355X_TYPE_F32) {
+                    l.epi_y = (float *)sg->data;
+                    ++end;
+                }
+            }
             out.push_back(l);
             i = end;
             continue;
@@ -262,6 +273,8 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
                 d[k].y = l.y[k];
                 ext.residual[k] = l.res[k];
             }
+            ext.epilogue = l.epi_y ? MI355X_EPI_SWIGLU : MI355X_EPI_NONE;
+            ext.epi_y = l.epi_y;
             rc = mi355x_gemv_fused_ext(d, l.count, l.x, w->ne[0], &ext, b->workspace, b->workspace_size, b->stream);
         } else {
             rc = enqueue_node(b, l, t);

@@ -109,6 +109,11 @@ struct RowsArgs {
     const float *x2;      // ROWS_PRO_NORM: norm weight (the MUL after RMS_NORM); ROWS_PRO_SWIGLU: up (x = gate)
     const float *res[MI355X_MAX_FUSED];  // y[m] = mul_mat + res[m] (the ADD after the MUL_MAT), or null
     int n_rows[MI355X_MAX_FUSED];
+    // SWIGLU epilogue (epi != 0): y[0] = gate, y[1] = up with equal rows and wave counts,
+    // up wave `wave` pairs with gate wave `wave - epi_wave_off` of the same workgroup
+    // (identical row ranges); epi_y[r] = swiglu(gate[r], up[r]) for r < epi_n
+    int epi, epi_n, epi_wave_off;
+    float *epi_y;
 };
 constexpr int ROWS_PRO_NONE = 0, ROWS_PRO_NORM = 1, ROWS_PRO_SWIGLU = 2;
 

@@ -108,8 +108,8 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
                 const float *xp = a.x + (int64_t)b * QK + 16 * (lane & 15);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) xv[i][k] = gload16_asm(xp + 4 * k);
-                if (PRO != ROWS_PRO_NONE) {
-                    const float *x2p = a.x2 + (int64_t)b * QK + 16 * (lane & 15);
+                if (PRO != ROWS_PRO_NONE) {  // (diag bit 4: read x again instead of x2, timing only)
+                    const float *x2p = ((a.diag & 16) ? a.x : a.x2) + (int64_t)b * QK + 16 * (lane & 15);
 #pragma unroll
                     for (int k = 0; k < 4; ++k) x2v[i][k] = gload16_asm(x2p + 4 * k);
                 }
@@ -131,7 +131,8 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 #pragma unroll
                 for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(x2v[i][k]));
         }
-        if (pro == ROWS_PRO_SWIGLU) {  // ggml_vec_swiglu_f32: silu(gate) * up
+        if (a.diag & 32) {  // diagnostics (timing only): skip the transform
+        } else if (pro == ROWS_PRO_SWIGLU) {  // ggml_vec_swiglu_f32: silu(gate) * up
 #pragma unroll
             for (int i = 0; i < ROWS_QPASS; ++i)
                 if (i < qiters)
@@ -274,6 +275,22 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         } else {
             for (int k = 0; k < ww.nrows; k += 64)
                 if (k + lane < ww.nrows) y[k + lane] = outs[k + lane];
+        }
+    }
+    // ---- SWIGLU epilogue (the GLU node after the gate/up MUL_MATs): up wave and its
+    // gate partner own the same rows in this workgroup; both results are staged in LDS.
+    // Same arithmetic as kq_swiglu (ggml_vec_swiglu_f32: NEON body, libm tail).
+    if (a.epi) {  // uniform over the grid: every wave of the workgroup reaches the barrier
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        if (ww.m == 1 && ww.nrows > 0) {
+            const float *gouts = (const float *)(smem + L.outs + (wave - a.epi_wave_off) * L.outs_stride);
+            const int n4 = a.epi_n & ~3;
+            for (int k = 0; k < ww.nrows; k += 64)
+                if (k + lane < ww.nrows) {
+                    const int r = ww.r0 + k + lane;
+                    const float gv = gouts[k + lane], uv = outs[k + lane];
+                    a.epi_y[r] = r < n4 ? v_silu(gv) * uv : (gv / (1.0f + expf(-gv))) * uv;
+                }
         }
     }
     if (a.stamps) {

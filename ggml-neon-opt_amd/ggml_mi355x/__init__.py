@@ -26,6 +26,7 @@ OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROP
 MAX_SRC = 8
 FLAG_OUTPUT = 1
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
+EPI_NONE, EPI_SWIGLU = 0, 1
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -73,7 +74,7 @@ Tensor._fields_ = [("type", ctypes.c_int), ("op", ctypes.c_int), ("ne", ctypes.c
 
 class GemvExt(ctypes.Structure):
     _fields_ = [("prologue", ctypes.c_int), ("x2", ctypes.c_void_p), ("eps", ctypes.c_float),
-                ("residual", ctypes.c_void_p * MAX_FUSED)]
+                ("residual", ctypes.c_void_p * MAX_FUSED), ("epilogue", ctypes.c_int), ("epi_y", ctypes.c_void_p)]
 
 
 class AttnDesc(ctypes.Structure):
@@ -311,10 +312,11 @@ def gemv_fused(mats, x, stream=None, workspace=None):
                                    _stream(stream)), "mi355x_gemv_fused")
 
 
-def gemv_fused_ext(mats, x, prologue=PRO_NONE, x2=None, eps=0.0, residual=None, stream=None):
+def gemv_fused_ext(mats, x, prologue=PRO_NONE, x2=None, eps=0.0, residual=None, epi_y=None, stream=None):
     """gemv_fused with the decode graph's neighbours fused (mi355x_gemv_fused_ext):
-    prologue PRO_RMS_NORM (x2 = norm weight) / PRO_SWIGLU (x = gate, x2 = up), and
-    y_i = mul_mat_i + residual[i]."""
+    prologue PRO_RMS_NORM (x2 = norm weight) / PRO_SWIGLU (x = gate, x2 = up),
+    y_i = mul_mat_i + residual[i], and with epi_y (mats = [gate, up]) the SWIGLU
+    epilogue epi_y = swiglu(y_0, y_1)."""
     _require_device()
     n = len(mats)
     descs = (GemvDesc * n)()
@@ -327,6 +329,8 @@ def gemv_fused_ext(mats, x, prologue=PRO_NONE, x2=None, eps=0.0, residual=None, 
     for i in range(MAX_FUSED):
         r = residual[i] if residual is not None and i < len(residual) else None
         ext.residual[i] = r.data_ptr() if r is not None else None
+    ext.epilogue = EPI_SWIGLU if epi_y is not None else EPI_NONE
+    ext.epi_y = epi_y.data_ptr() if epi_y is not None else None
     K = x.shape[-1]
     need = int(lib().mi355x_gemv_ext_workspace_size(K))
     ws = _workspace(need, x.device)

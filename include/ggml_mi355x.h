@@ -177,11 +177,18 @@ int mi355x_gemv_fused(const mi355x_gemv_desc *descs, int n_desc, const float *x,
 #define MI355X_PRO_NONE 0
 #define MI355X_PRO_RMS_NORM 1
 #define MI355X_PRO_SWIGLU 2
+/* `epilogue` MI355X_EPI_SWIGLU: descs[0] = gate, descs[1] = up (n_desc == 2, equal
+ * n_rows, no residual); epi_y[r] = ggml_vec_swiglu_f32(gate, up)[r] is written besides
+ * descs[i].y — the GGML_GLU(SWIGLU) node that follows the gate/up MUL_MATs. */
+#define MI355X_EPI_NONE 0
+#define MI355X_EPI_SWIGLU 1
 typedef struct {
     int prologue;
     const float *x2;
     float eps;
     const float *residual[MI355X_MAX_FUSED];
+    int epilogue;
+    float *epi_y;
 } mi355x_gemv_ext;
 size_t mi355x_gemv_ext_workspace_size(int64_t k);
 int mi355x_gemv_fused_ext(const mi355x_gemv_desc *descs, int n_desc, const float *x, int64_t k,

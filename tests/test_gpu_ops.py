@@ -172,6 +172,31 @@ def test_gemv_fused_ext(dev, O, oracle, npo, impl, pro):
         assert bits_equal(got, ref), first_mismatch(got, ref)
 
 
+@pytest.mark.parametrize("n", [5632, 1000, 24])
+def test_gemv_swiglu_epilogue(dev, O, oracle, npo, impl, n):
+    """RMS_NORM -> MUL -> MUL_MAT(gate), MUL_MAT(up) -> SWIGLU in one launch: the gate
+    and up outputs and the SWIGLU output bit-exact with the separate ops (paired waves
+    in kq_rows at the real shape; the staged fallback where the waves cannot pair)."""
+    import torch
+    import ggml_mi355x as g
+    rng = np.random.default_rng(n)
+    K = 2048
+    x = (rng.standard_normal(K) * 3).astype(np.float32)
+    nw = rng.uniform(0.5, 1.5, K).astype(np.float32)
+    ws = [npo.random_blocks(rng, 12, n, K) for _ in range(2)]
+    ys = [torch.empty(n, device=dev) for _ in range(2)]
+    h = torch.empty(n, device=dev)
+    g.gemv_fused_ext([(12, t(w, dev), y) for w, y in zip(ws, ys)], t(x, dev), prologue=g.PRO_RMS_NORM,
+                     x2=t(nw, dev), eps=1e-5, epi_y=h)
+    torch.cuda.synchronize()
+    xin = O.mul(O.rms_norm(x, 1e-5), nw)
+    refs = [oracle.mul_mat(12, w, xin)[0] for w in ws]
+    for y, ref in zip(ys, refs):
+        assert bits_equal(y.cpu().numpy(), ref)
+    got, ref = h.cpu().numpy(), O.swiglu(refs[0], refs[1])
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+
+
 # ---------------------------------------------------------------- the whole token
 def _decoder(dev, hp, seed, n_ctx, fuse=True):
     from tests import llama_model as LM

@@ -59,6 +59,8 @@ if __name__ == "__main__":
         for kv in mode.split(":"):  # generic overrides: "pre0=0", "lib=path", combined with ':'
             if kv.startswith("pre0="):
                 env["MI355X_GEMV_PRE0"] = kv[5:]
+            elif kv.startswith("wpc="):
+                env["MI355X_GEMV_WPC"] = kv[4:]
             elif kv.startswith("lib="):
                 env["MI355X_LIB"] = os.path.join(ROOT, kv[4:])
         if mode == "prologue":
@@ -73,7 +75,7 @@ if __name__ == "__main__":
             env["MI355X_GEMV_IMPL"] = "tasks"
         elif mode.startswith("ring"):
             env["MI355X_GEMV_RING"] = mode[4:]
-        elif mode != "auto":
+        elif mode != "auto" and "=" not in mode:
             env["MI355X_GEMV_MODE"] = mode
         r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode != 0:

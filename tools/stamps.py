@@ -16,9 +16,13 @@ SHAPES = [("tl q", 12, 2048, 2048), ("tl 8rows", 12, 2048, 8), ("tl gate+up", 12
           ("70b down", 12, 28672, 8192)]
 
 
+PRO = os.environ.get("STAMPS_PRO", "none")  # none | norm | swiglu: fused prologue (kq_rows only)
+
+
 def main(impl):
     g.gemv_impl(impl)
-    tag = "rows " if impl == 0 else "tasks"
+    pro = {"none": g.PRO_NONE, "norm": g.PRO_RMS_NORM, "swiglu": g.PRO_SWIGLU}[PRO]
+    tag = ("rows " if impl == 0 else "tasks") + ("" if PRO == "none" else "/" + PRO)
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
     gen.manual_seed(3)
@@ -26,9 +30,16 @@ def main(impl):
     for label, typ, K, N in SHAPES:
         ws = [random_kquant(typ, N, K, gen, dev) for _ in range(max(2, int(600e6 // (N * K // 256 * 144))))]
         x = torch.randn(1, K, device=dev)
+        x2 = torch.rand(K, device=dev) + 0.5
         y = torch.empty(1, N, device=dev)
+
+        def mm(w):
+            if pro == g.PRO_NONE:
+                g.mul_mat(typ, w, K, x, out=y)
+            else:
+                g.gemv_fused_ext([(typ, w, y[0])], x[0], prologue=pro, x2=x2, eps=1e-5)
         for w in ws:
-            g.mul_mat(typ, w, K, x, out=y)
+            mm(w)
         res = []
         for r in range(5):
             buf.zero_()
@@ -37,7 +48,7 @@ def main(impl):
             for i in range(60):
                 if i == 59:
                     g.lib().mi355x_diag_stamps(buf.data_ptr(), buf.numel() * 8)
-                g.mul_mat(typ, ws[(r * 60 + i) % len(ws)], K, x, out=y)
+                mm(ws[(r * 60 + i) % len(ws)])
             torch.cuda.synchronize()
             g.lib().mi355x_diag_stamps(None, 0)
             st = buf.cpu().numpy().astype(np.int64).reshape(-1, 8)
@@ -68,5 +79,5 @@ def main(impl):
 
 
 if __name__ == "__main__":
-    for impl in (0, 1):
+    for impl in ((0,) if PRO != "none" or "rows" in sys.argv else (0, 1)):
         main(impl)
