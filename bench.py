@@ -13,21 +13,24 @@ per-token MUL_MAT chain alone ("chain" workload, described below) is reported
 beside it in "matmul_chain".
 
 Metric (BASELINE.json): "tg128 tok/s + Q4_K GEMV achieved-HBM-GB/s, TinyLlama-1.1B
-Q4_K_M @1 GPU". One step = one decoded token = the model's full per-token MUL_MAT
-chain (every layer's attn_q/k/v, attn_output, ffn_gate/up, ffn_down, then the
-output head; 629.8 MB of K-quant weights, the Q4_K_M type mix of llama-quant.cpp
-[U]: attn_v/ffn_down Q6_K in the 10 use_more_bits layers, output Q6_K), each GEMV
-including its bit-exact Q8_K activation quantization. Weights are synthetic
-random blocks of the real shapes (no network for the GGUF), their fp16 scales
-sized so activations keep an O(1) RMS down the chain. Every stage reads the
-previous stage's output (attn_q -> attn_output -> ffn_gate -> ffn_down -> next
-layer's q/k/v ... -> output), so each stage truly waits for the one before; the
-first stage reads a synthetic f32 vector. Non-matmul ops (norm, rope, attention,
-swiglu: 1.5 % of the reference's CPU time, out.folded:122) are not part of the
-chain. The chain runs through the ggml-backend mirror
-(mi355x_backend_graph_compute): q/k/v and gate/up fuse into one stage each and
-the 89 stage launches of a token are replayed from one hipGraph (--impl chain:
-ONE persistent kq_chain launch per token instead).
+Q4_K_M @1 GPU". One step = one decoded token of the whole graph; its matmuls carry
+629.8 MB of K-quant weights in the Q4_K_M type mix of llama-quant.cpp [U]
+(attn_v/ffn_down Q6_K in the 10 use_more_bits layers, output Q6_K, token_embd
+Q4_K), each GEMV including its bit-exact Q8_K activation quantization. Weights are
+synthetic random blocks of the real shapes (no network for the GGUF), their fp16
+scales sized so the residual stream keeps an O(1) RMS; norms f32 in [0.8, 1.2].
+
+"chain" workload (--workload chain; the row-split, GGUF-file and kernel A/B modes):
+the per-token MUL_MAT chain only, every stage reading the previous stage's output
+(attn_q -> attn_output -> ffn_gate -> ffn_down -> next layer's q/k/v ... -> output);
+q/k/v and gate/up fuse into one launch each, 89 launches per token from one hipGraph
+(--impl chain: ONE persistent kq_chain launch per token instead).
+
+"roofline": the dominant kernel's algorithmic bytes per launch over its event-timed
+launch duration; "traffic": its HBM read per launch from the committed rocprofv3
+PMC pass (profiles/). "gemv_large": single decode GEMVs of the Llama-3 configs.
+"prefill_pp512": every matmul of the token at ne11 = 512 (int8 MFMA). "cpu_baseline":
+the oracle's restated ggml-cpu token on this host's cores, a bounded sample.
 
 Multi-GPU (--gpus N under torch.distributed.run): every rank decodes its own
 token stream with its own copy of the weights ("replicas", weak scaling); value
@@ -253,30 +256,44 @@ def timed_kernel_stats(be, chain, tokens):
 
 
 def large_gemv(dev, reps=20):
-    """Q4_K decode GEMV at Llama-3 shapes, weight buffers rotated over > 512 MB so
-    the 256 MB Infinity Cache cannot serve them."""
+    """Decode GEMVs of the Llama-3 configs (BASELINE.json configs 3-4), one launch each,
+    weight buffers rotated over > 600 MB so the 256 MB Infinity Cache cannot serve them:
+    the 8B ffn_up, the 70B ffn_down, the 70B ffn_gate + ffn_up pair as the decode graph
+    fuses it (one launch, shared activation) and the 8B Q6_K output head."""
     out = {}
     gen = torch.Generator(device=dev)
     gen.manual_seed(7)
-    for label, K, N in (("llama3-8b ffn_up 4096x14336", 4096, 14336), ("llama3-70b ffn_down 28672x8192", 28672, 8192)):
-        nbytes = N * (K // 256) * 144
+    shapes = (("llama3-8b ffn_up 4096x14336", g.TYPE_Q4_K, 4096, (14336,)),
+              ("llama3-70b ffn_down 28672x8192", g.TYPE_Q4_K, 28672, (8192,)),
+              ("llama3-70b ffn_gate+ffn_up 8192x2x28672", g.TYPE_Q4_K, 8192, (28672, 28672)),
+              ("llama3-8b output q6_K 4096x128256", g.TYPE_Q6_K, 4096, (128256,)))
+    for label, typ, K, Ns in shapes:
+        nbytes = sum(N * (K // 256) * g.BLOCK_BYTES[typ] for N in Ns)
         nbuf = max(2, int(np.ceil(600e6 / nbytes)))
-        ws = [random_kquant(g.TYPE_Q4_K, N, K, gen, dev) for _ in range(nbuf)]
+        ws = [[random_kquant(typ, N, K, gen, dev) for N in Ns] for _ in range(nbuf)]
         x = torch.randn(1, K, device=dev, generator=gen)
-        y = torch.empty(1, N, device=dev)
-        for w in ws:
-            g.mul_mat(g.TYPE_Q4_K, w, K, x, out=y)
+        ys = [torch.empty(1, N, device=dev) for N in Ns]
+
+        def call(i):
+            if len(Ns) == 1:
+                g.mul_mat(typ, ws[i % nbuf][0], K, x, out=ys[0])
+            else:
+                g.gemv_fused([(typ, w, y[0]) for w, y in zip(ws[i % nbuf], ys)], x[0])
+
+        for i in range(nbuf):
+            call(i)
         g.timing_enable(True)
         for r in range(reps):
-            g.mul_mat(g.TYPE_Q4_K, ws[r % nbuf], K, x, out=y)
+            call(r)
         rows = g.timing_read()
         g.timing_enable(False)
         per_call = len(rows) // reps  # K > 8192: Q8_K quantize launch + GEMV launch
         ms = [sum(r[2] for r in rows[i * per_call:(i + 1) * per_call]) for i in range(reps)]
-        b = nbytes + K * 4 + N * 4
-        out[label] = {"bytes": b, "launches_per_call": per_call, "us_median": float(np.median(ms) * 1e3),
-                      "GBps_median": b / (np.median(ms) * 1e-3) / 1e9,
-                      "frac_median": b / (np.median(ms) * 1e-3) / 1e9 / HBM_PEAK_GBS}
+        b = nbytes + K * 4 + sum(Ns) * 4
+        out[label] = {"bytes": b, "launches_per_call": per_call, "kernel": rows[per_call - 1][0],
+                      "us_median": round(float(np.median(ms) * 1e3), 2),
+                      "GBps_median": round(b / (np.median(ms) * 1e-3) / 1e9, 1),
+                      "frac_median": round(b / (np.median(ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
         del ws
         torch.cuda.empty_cache()
     return out

@@ -131,7 +131,12 @@ __host__ __device__ constexpr int rows_ni(int type) { return (rows_gran(type) + 
 #ifndef KQ_ROWS_DQ4
 #define KQ_ROWS_DQ4 3
 #endif
-__host__ __device__ constexpr int rows_depth(int type) { return type == Q4_K ? KQ_ROWS_DQ4 : type == Q5_K ? 3 : 2; }
+#ifndef KQ_ROWS_DQ6
+#define KQ_ROWS_DQ6 2
+#endif
+__host__ __device__ constexpr int rows_depth(int type) {
+    return type == Q4_K ? KQ_ROWS_DQ4 : type == Q5_K ? 3 : KQ_ROWS_DQ6;
+}
 __host__ __device__ constexpr int rows_ring_bytes(int type) { return rows_depth(type) * rows_slot(type); }
 __host__ __device__ constexpr int cmax(int a, int b) { return a > b ? a : b; }
 __host__ __device__ constexpr int rows_ring(int tmask) {
