@@ -84,6 +84,14 @@ __host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg
 #endif
 constexpr int ROWS_WAVES = KQ_ROWS_WAVES;
 constexpr int ROWS_QPASS = 3;  // fused-quantization passes of 4*ROWS_WAVES superblocks
+// L2 prefetch issued with the first weight step (waves whose stream outlasts the
+// ring): while the activation is fetched and quantized, each wave touches the next
+// ROWS_PF x 4 KB of its stream past the ring (one dword per 64-B sector), so the HBM
+// keeps streaming and those steps later DMA from L2 / the Infinity Cache.
+#ifndef KQ_ROWS_PF
+#define KQ_ROWS_PF 2
+#endif
+constexpr int ROWS_PF = KQ_ROWS_PF;  // touches per wave when a.pf != 0
 
 struct RowsArgs {
     int n_desc;
@@ -91,6 +99,7 @@ struct RowsArgs {
     int rpw;          // max rows per wave (LDS sizing)
     int waves_total;
     int pre0;         // weight steps issued before the activation is quantized
+    int pf;           // L2 prefetch on/off (ROWS_PF 4-KB touches of the stream past the ring)
     int bR;           // rows per chain batch (bR*nb % 16 == 0 unless bR >= rpw)
     int diag;         // diagnostics: bit3 stream weights only
     int wave_prefix[MI355X_MAX_FUSED + 1];

@@ -67,6 +67,9 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     const uint8_t *last16 =
         G > 0 ? (const uint8_t *)((uintptr_t)(src + (int64_t)G * BSZ - 1) & ~(uintptr_t)15) : s16;
 
+    // L2 prefetch (uniform per wave): only streams longer than the ring, fused path
+    const bool pf_on = FUSEDQ && a.pf && T > D + 1;
+    uint32_t pf_sink = 0;
     uint8_t *islot = ring;
     int it_ = 0;  // next step to issue
     auto issue = [&]() {
@@ -120,7 +123,14 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         // register whose asm load is still in flight.
         rv = gload4_asm(res_p && ww.nrows > 0 ? res_p + ww.r0 + (lane < ww.nrows ? lane : 0) : a.x);
         for (int j = 0; j < pre0; ++j) issue();
-        vm_wait_k<NI>(pre0);  // the activation loads are older than pre0 weight steps
+        if (pf_on) {  // L2 prefetch of the stream just past the ring (younger than the pre0 steps)
+            const uint8_t *p = s16 + (int64_t)D * (ROWS_SB * BSZ) + 64 * lane;
+#pragma unroll
+            for (int i = 0; i < ROWS_PF; ++i) l2_touch(p + 4096 * i < last16 ? p + 4096 * i : last16, pf_sink);
+            vm_wait_kp<NI, ROWS_PF>(pre0);  // the activation loads are older than both
+        } else {
+            vm_wait_k<NI>(pre0);  // the activation loads are older than pre0 weight steps
+        }
         // the loads above are invisible to the compiler: pin their registers past the wait
         asm volatile("" : "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[1][0]),
                      "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]), "+v"(xv[2][0]), "+v"(xv[2][1]), "+v"(xv[2][2]),
@@ -204,8 +214,14 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     const uint8_t *cslot = ring;
 #pragma unroll 1
     for (int t = 0; t < T; ++t) {
-        if (T - t >= D) vm_wait<NI * (D - 1)>();  // steady state: D-1 younger steps in flight
-        else vm_wait_k<NI>(T - t - 1);
+        if (pf_on && t < pre0) {  // the prefetch touches sit between steps pre0-1 and pre0
+            if (T - t >= D) vm_wait<NI * (D - 1) + ROWS_PF>();
+            else vm_wait_kp<NI, ROWS_PF>(T - t - 1);
+        } else if (T - t >= D) {
+            vm_wait<NI * (D - 1)>();  // steady state: D-1 younger steps in flight
+        } else {
+            vm_wait_k<NI>(T - t - 1);
+        }
         if (!(a.diag & 8) && ROWS_SB * t + q < G) {
             const uint8_t *blk = cslot + mis + q * BSZ;
             const uint8_t *ab = actq + io * Q8L_STRIDE;
@@ -261,6 +277,9 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         }
     }
     const uint64_t st2 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (pf_on) {  // every touch has landed (they are older than step pre0): release the register
+        asm volatile("" ::"v"(pf_sink));
+    }
 
     // ---- flush staged results (coalesced)
     if (ww.nrows > 0) {

@@ -231,5 +231,20 @@ __device__ __forceinline__ void vm_wait_k(int k) {
     else if (k == 1) vm_wait<N>();
     else vm_wait<0>();
 }
+// s_waitcnt vmcnt(N * k + P): the same with P younger L2-prefetch loads still counted.
+template <int N, int P>
+__device__ __forceinline__ void vm_wait_kp(int k) {
+    if (k >= 3) vm_wait<3 * N + P>();
+    else if (k == 2) vm_wait<2 * N + P>();
+    else if (k == 1) vm_wait<N + P>();
+    else vm_wait<P>();
+}
+
+// One L2 prefetch touch: a dword load per lane into a register reserved for it
+// (tied in/out, so every touch reuses it and nothing else is allocated there while
+// the loads are in flight); the caller consumes `sink` after its covering wait.
+__device__ __forceinline__ void l2_touch(const void *p, uint32_t &sink) {
+    asm volatile("global_load_dword %0, %1, off" : "+v"(sink) : "v"(p) : "memory");
+}
 
 }  // namespace kq
