@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256) kq_get_rows(int type, const uint8_t *__re
 // elements [16l, 16l+16) of one superblock per pass. Sum order: kq_ops_device.h.
 __global__ void __launch_bounds__(256) kq_rms_norm(const float *__restrict__ x, const float *__restrict__ w,
                                                    float *__restrict__ y, int64_t n, float eps) {
-    extern __shared__ double sb_sum[];
+    extern __shared__ __attribute__((aligned(16))) double sb_sum[];
     const int64_t row = blockIdx.x;
     const float *xr = x + row * n;
     float *yr = y + row * n;
@@ -115,8 +115,7 @@ __global__ void __launch_bounds__(256) kq_rms_norm(const float *__restrict__ x, 
         if (b < nb && l == 0) sb_sum[b] = s;
     }
     __syncthreads();
-    double total = 0.0;
-    for (int b = 0; b < nb; ++b) total += sb_sum[b];
+    const double total = seq_sum_lds(sb_sum, nb);  // superblocks in order
     const float mean = (float)(total / (double)n);
     const float scale = 1.0f / sqrtf(mean + eps);
     for (int64_t i = threadIdx.x; i < n; i += 256) {
@@ -239,7 +238,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     int n_kv = (pos + 1 + 31) / 32 * 32;
     n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
     // LDS (attn_lds): q16 | k16 | v16 (HD f16 each) | w (n_ctx f32) | p16 (n_ctx f16) |
-    // red (HD*32 f16 accumulators) | scal (max, 1/sum); every piece 16-B aligned
+    // red (HD*32 f16 accumulators) | scal (max, 1/sum, 2 pad) [| gsum]; every piece 16-B aligned
     uint16_t *q16 = (uint16_t *)smem;
     uint16_t *k16 = q16 + HD;
     uint16_t *v16 = k16 + HD;
@@ -247,6 +246,9 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     uint16_t *p16 = (uint16_t *)(w + a.n_ctx);
     h16 *red = (h16 *)(p16 + a.n_ctx);
     float *scal = (float *)(red + HD * 32);
+    // per group of 4 cells: (double)((e0 + e1) + (e2 + e3)); lives in `red` (free until
+    // KQV) when it fits, past scal otherwise
+    double *gsum = (a.n_ctx / 4) * 8 <= HD * 64 ? (double *)red : (double *)(scal + 4);
 
     const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
     const bool writer = !bad && (h % gsz) == 0;
@@ -316,13 +318,12 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         }
 #pragma unroll
         for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
+        gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));  // the vaddvq group sum, in parallel
     }
     __syncthreads();
-    if (t == 0) {  // the sequential double sum is the pos-dependent part of this launch
-                   // (~40 ns per group, f64 issue-bound; tools/attn_phases.py)
-        double sum = 0.0;
-        for (int gi = 0; gi < n_kv / 4; ++gi)
-            sum += (double)((w[4 * gi] + w[4 * gi + 1]) + (w[4 * gi + 2] + w[4 * gi + 3]));
+    if (t == 0) {  // the sequential double sum over the groups, in order: only the
+                   // dependent f64 adds stay serial, fed by 16-B LDS reads 8 groups ahead
+        double sum = seq_sum_lds(gsum, n_kv / 4);
         sum = 1.0 / sum;
         scal[1] = (float)sum;
     }
@@ -384,7 +385,10 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     }
 }
 
-size_t attn_lds(int hd, int n_ctx) { return (size_t)6 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16; }
+size_t attn_lds(int hd, int n_ctx) {
+    const size_t gsum = (size_t)(n_ctx / 4) * 8 <= (size_t)hd * 64 ? 0 : (size_t)(n_ctx / 4) * 8;
+    return (size_t)6 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + gsum;
+}
 
 // ------------------------------------------------------------ launch helpers
 int check_launch() {

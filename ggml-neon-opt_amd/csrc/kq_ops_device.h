@@ -113,4 +113,34 @@ __device__ __forceinline__ double row16_sum(double v) {
     return v;
 }
 
+// In-order double sum of n LDS doubles (p 16-B aligned): sum = ((0 + p[0]) + p[1]) + ...,
+// the dependent adds fed by 16-B reads issued 8 values ahead instead of one LDS
+// round trip per value.
+__device__ __forceinline__ double seq_sum_lds(const double *p, int n) {
+    double sum = 0.0;
+    int i = 0;
+    if (n >= 8) {
+        const double2 *p2 = (const double2 *)p;
+        double2 c0 = p2[0], c1 = p2[1], c2 = p2[2], c3 = p2[3];
+        for (; i + 8 <= n; i += 8) {
+            double2 n0 = c0, n1 = c1, n2 = c2, n3 = c3;
+            if (i + 16 <= n) {
+                const int h = (i + 8) / 2;
+                n0 = p2[h], n1 = p2[h + 1], n2 = p2[h + 2], n3 = p2[h + 3];
+            }
+            sum += c0.x;
+            sum += c0.y;
+            sum += c1.x;
+            sum += c1.y;
+            sum += c2.x;
+            sum += c2.y;
+            sum += c3.x;
+            sum += c3.y;
+            c0 = n0, c1 = n1, c2 = n2, c3 = n3;
+        }
+    }
+    for (; i < n; ++i) sum += p[i];
+    return sum;
+}
+
 }  // namespace kq

@@ -102,7 +102,7 @@ def test_rope(dev, O, hd, nh, base):
 
 # ---------------------------------------------------------------- attention
 @pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 256), (128, 32, 8, 128), (64, 8, 8, 64), (64, 8, 2, 512),
-                                             (128, 8, 4, 512)])
+                                             (128, 8, 4, 512), (64, 4, 2, 4096)])
 def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx):
     """A growing KV cache: every position's output and both caches bit-exact (positions
     past the kernel's prefetched cells — 256 K rows, 256/128 V cells — included)."""
