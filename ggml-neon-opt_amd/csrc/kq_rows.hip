@@ -167,7 +167,8 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
                 if (i < qiters && b < nb && (lane & 15) == 0) sums[b] = sq;
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            const double tot = seq_sum_lds(sums, nb);  // superblocks in order
+            double tot = 0.0;  // superblocks in order (a batched read here spills the prologue registers)
+            for (int b = 0; b < nb; ++b) tot += sums[b];
             const float mean = (float)(tot / (double)(nb * QK));
             const float scale = 1.0f / sqrtf(mean + a.eps);
 #pragma unroll
