@@ -59,6 +59,10 @@ if __name__ == "__main__":
         for kv in mode.split(":"):  # generic overrides: "pre0=0", "lib=path", combined with ':'
             if kv.startswith("pre0="):
                 env["MI355X_GEMV_PRE0"] = kv[5:]
+            elif kv.startswith("bal="):
+                env["MI355X_GEMV_BAL"] = kv[4:]
+            elif kv.startswith("prio="):
+                env["MI355X_GEMV_PRIO"] = kv[5:]
             elif kv.startswith("pf="):
                 env["MI355X_GEMV_PF"] = kv[3:]
             elif kv.startswith("wpc="):

@@ -52,6 +52,8 @@ def main(impl):
             torch.cuda.synchronize()
             g.lib().mi355x_diag_stamps(None, 0)
             st = buf.cpu().numpy().astype(np.int64).reshape(-1, 8)
+            if os.environ.get("STAMPS_DUMP") and r == 4:  # raw per-(block, wave) rows for offline analysis
+                np.save(os.environ["STAMPS_DUMP"] + "_" + label.replace(" ", "_") + ".npy", st[:256 * 12])
             st = st[st[:, 0] != 0]
             t0 = st[:, 0].min()
             rel = (st - t0) * 10 / 1000.0  # 100 MHz ticks -> us
@@ -61,7 +63,7 @@ def main(impl):
                 res.append((len(st), rel[:, 0].max(), med(rel[ok, 4] - rel[ok, 0]), med(rel[ok, 5] - rel[ok, 4]),
                             med(rel[:, 1] - rel[:, 5]), med(rel[ok, 6] - rel[ok, 1]),
                             med(rel[:, 1] - rel[:, 0]), med(rel[:, 2] - rel[:, 1]), np.max(rel[:, 2] - rel[:, 1]),
-                            rel[:, 3].max()))
+                            rel[:, 3].max(), rel[:, 2].max(), med(rel[:, 2])))
                 continue
             res.append((len(st), rel[:, 0].max(), med(rel[:, 4] - rel[:, 0]), med(rel[:, 5] - rel[:, 4]),
                         med(rel[:, 6] - rel[:, 5]), med(rel[:, 1] - rel[:, 6]),
@@ -71,7 +73,7 @@ def main(impl):
         if impl == 0:
             print(f"{tag} {label:12s} waves={int(a[0]):5d} start_spread={a[1]:5.2f}us | x-wait {a[2]:4.2f} quant {a[3]:4.2f} "
                   f"barrier+fill {a[4]:4.2f} = prologue {a[6]:4.2f} | first step {a[5]:4.2f} loop med/max={a[7]:5.2f}/{a[8]:5.2f} "
-                  f"end={a[9]:6.2f}us")
+                  f"loop end med/max={a[11]:6.2f}/{a[10]:6.2f} end={a[9]:6.2f}us")
             continue
         print(f"{tag} {label:12s} waves={int(a[0]):5d} start_spread={a[1]:5.2f}us | lookup {a[2]:4.2f} issue {a[3]:4.2f} "
               f"wait {a[4]:4.2f} quant {a[5]:4.2f} = prologue {a[6]:4.2f} | loop med/max={a[7]:5.2f}/{a[8]:5.2f} "
