@@ -245,6 +245,7 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
             a.head_dim = t->op_params[2];
             a.scale = f_of(t->op_params[3]);
             a.n_ctx = (int)t->src[4]->ne[1];
+            a.rope_row = t->src[6]->ne[1] == 1 ? 1 : 0;  // the position's row, staged with pos
             return mi355x_attn_decode(&a, st);
         }
         default:
@@ -541,7 +542,8 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
             if ((hd != 64 && hd != 128) || nkv <= 0 || nh % nkv) return 0;
             if (op->src[4]->type != MI355X_TYPE_F16 || op->src[5]->type != MI355X_TYPE_F16) return 0;
             if (op->src[4]->ne[0] != (int64_t)nkv * hd || op->src[3]->type != MI355X_TYPE_I32) return 0;
-            if (op->src[5]->ne[0] != op->src[4]->ne[1] || op->src[6]->ne[1] < op->src[4]->ne[1]) return 0;
+            if (op->src[5]->ne[0] != op->src[4]->ne[1]) return 0;
+            if (op->src[6]->ne[1] != 1 && op->src[6]->ne[1] < op->src[4]->ne[1]) return 0;  // row or table
             if (op->src[6]->ne[0] != hd) return 0;
             return contig_f32(op) && op->ne[0] == (int64_t)nh * hd;
         }

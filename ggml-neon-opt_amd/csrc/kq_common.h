@@ -186,6 +186,7 @@ struct AttnArgs {
     int n_ctx, n_head, n_head_kv, head_dim;
     float scale;
     int diag;  // diagnostics only (MI355X_ATTN_DIAG): 1/2/3 stop after loads/KQ/soft_max, 4 empty
+    int rope_row;  // rope_table holds only the row of *pos (no position-dependent load)
 };
 
 // kq_chain: one launch runs a whole sequence of decode MUL_MAT stages (a token's

@@ -207,7 +207,12 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     // ---- 0. position-independent loads, issued with the position
     const int pos_in = *a.pos;
     float x0 = 0.f, x1 = 0.f, y0 = 0.f, y1 = 0.f;
+    float rc = 0.f, rs = 0.f;  // rope_row: cos/sin of the thread's pair, staged with the position
     if (t < HD / 2) {
+        if (a.rope_row) {
+            rc = a.rope_table[2 * t];
+            rs = a.rope_table[2 * t + 1];
+        }
         const float *qp = a.q + (int64_t)h * HD + 2 * t;
         const float *kp = a.k + (int64_t)g * HD + 2 * t;
         x0 = qp[0];
@@ -250,10 +255,10 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     // KQV) when it fits, past scal otherwise
     double *gsum = (a.n_ctx / 4) * 8 <= HD * 64 ? (double *)red : (double *)(scal + 4);
 
-    const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
+    const float *tc = a.rope_table + (a.rope_row ? 0 : (int64_t)pos * (HD / 2) * 2);
     const bool writer = !bad && (h % gsz) == 0;
     if (t < HD / 2) {
-        const float c = tc[2 * t], s = tc[2 * t + 1];
+        const float c = a.rope_row ? rc : tc[2 * t], s = a.rope_row ? rs : tc[2 * t + 1];
         const float2 rq = rope_pair(x0, x1, c, s);
         q16[2 * t] = h2u(f2h_rne(rq.x));
         q16[2 * t + 1] = h2u(f2h_rne(rq.y));
@@ -274,66 +279,106 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         return;
     }
 
-    // KQ + scale + mask; the first pass (c == t) scores the prefetched row
-    for (int c = t; c < n_kv; c += 256) {
-        float s = -INFINITY;
-        if (c <= pos) {
+    if (n_kv <= 256) {  // one cell per thread: score, max, exp and group sum stay in registers
+        const int c = t;
+        float sc = -INFINITY;
+        if (c < n_kv && c <= pos) {
             uint4 kv[KV4];
             if (c == pos) {
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
-            } else if (c == t) {
+            } else {
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
-            } else {
-                const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
-#pragma unroll
-                for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
             }
-            s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+            sc = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
         }
-        w[c] = s;
-    }
-    __syncthreads();
-    if (a.diag == 2) {  // diagnostics: stop after KQ
-        if (t < HD) a.out[(int64_t)h * HD + t] = w[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
-        return;
-    }
-    // max (order-free), then exp + group sums
-    if (t < 64) {
-        float m = -INFINITY;
-        for (int c = t; c < n_kv; c += 64) m = fmaxf(m, w[c]);
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        if (t == 0) scal[0] = m;
-    }
-    __syncthreads();
-    const float mx = scal[0];
-    for (int gi = t; gi < n_kv / 4; gi += 256) {
-        float e[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float wv = w[4 * gi + k];
-            e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+        const float wmx = wave_fmax(sc);  // max (order-free): per wave, then over the 4 waves
+        if ((t & 63) == 0) scal[t >> 6] = wmx;
+        __syncthreads();
+        if (a.diag == 2) {  // diagnostics: stop after KQ
+            if (t < HD) a.out[(int64_t)h * HD + t] = sc + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
         }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
-        gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));  // the vaddvq group sum, in parallel
-    }
-    __syncthreads();
-    if (t == 0) {  // the sequential double sum over the groups, in order: only the
-                   // dependent f64 adds stay serial, fed by 16-B LDS reads 8 groups ahead
-        double sum = seq_sum_lds(gsum, n_kv / 4);
-        sum = 1.0 / sum;
-        scal[1] = (float)sum;
-    }
-    __syncthreads();
-    const float inv = scal[1];
-    for (int c = t; c < n_kv; c += 256) p16[c] = h2u(f2h_rne(w[c] * inv));
-    __syncthreads();
-    if (a.diag == 3) {  // diagnostics: stop after soft_max
-        if (t < HD) a.out[(int64_t)h * HD + t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
-        return;
+        const float mx = fmaxf(fmaxf(scal[0], scal[1]), fmaxf(scal[2], scal[3]));
+        const float ec = c < n_kv && sc != -INFINITY ? v_expf(sc - mx) : 0.0f;
+        // group sum of cells 4g..4g+3 (lanes 4g..4g+3) in the vaddvq order (e0 + e1) + (e2 + e3)
+        const float s01 = ec + dpp_mov_f32<0xB1>(ec);   // lane 4g: e0 + e1, lane 4g+2: e2 + e3
+        const float g4 = s01 + dpp_mov_f32<0x4E>(s01);  // lane 4g: (e0 + e1) + (e2 + e3)
+        if ((t & 3) == 0 && c < n_kv) gsum[t >> 2] = (double)g4;
+        __syncthreads();
+        // every thread runs the same in-order double sum (no barrier to publish it)
+        const double sum = seq_sum_lds(gsum, n_kv / 4);
+        const float inv = (float)(1.0 / sum);
+        if (c < n_kv) p16[c] = h2u(f2h_rne(ec * inv));
+        __syncthreads();
+        if (a.diag == 3) {  // diagnostics: stop after soft_max
+            if (t < HD) a.out[(int64_t)h * HD + t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
+        }
+    } else {
+        // KQ + scale + mask; the first pass (c == t) scores the prefetched row
+        for (int c = t; c < n_kv; c += 256) {
+            float s = -INFINITY;
+            if (c <= pos) {
+                uint4 kv[KV4];
+                if (c == pos) {
+    #pragma unroll
+                    for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+                } else if (c == t) {
+    #pragma unroll
+                    for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
+                } else {
+                    const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+    #pragma unroll
+                    for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
+                }
+                s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+            }
+            w[c] = s;
+        }
+        __syncthreads();
+        if (a.diag == 2) {  // diagnostics: stop after KQ
+            if (t < HD) a.out[(int64_t)h * HD + t] = w[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
+        }
+        // max (order-free), then exp + group sums
+        if (t < 64) {
+            float m = -INFINITY;
+            for (int c = t; c < n_kv; c += 64) m = fmaxf(m, w[c]);
+    #pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            if (t == 0) scal[0] = m;
+        }
+        __syncthreads();
+        const float mx = scal[0];
+        for (int gi = t; gi < n_kv / 4; gi += 256) {
+            float e[4];
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float wv = w[4 * gi + k];
+                e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+            }
+    #pragma unroll
+            for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
+            gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));  // the vaddvq group sum, in parallel
+        }
+        __syncthreads();
+        if (t == 0) {  // the sequential double sum over the groups, in order: only the
+                       // dependent f64 adds stay serial, fed by 16-B LDS reads 8 groups ahead
+            double sum = seq_sum_lds(gsum, n_kv / 4);
+            sum = 1.0 / sum;
+            scal[1] = (float)sum;
+        }
+        __syncthreads();
+        const float inv = scal[1];
+        for (int c = t; c < n_kv; c += 256) p16[c] = h2u(f2h_rne(w[c] * inv));
+        __syncthreads();
+        if (a.diag == 3) {  // diagnostics: stop after soft_max
+            if (t < HD) a.out[(int64_t)h * HD + t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
+        }
+
     }
 
     // KQV: thread (d, j) -> accumulator j of output d
@@ -550,6 +595,7 @@ int mi355x_attn_decode(const mi355x_attn_desc *d, void *stream) {
     a.n_head_kv = d->n_head_kv;
     a.head_dim = d->head_dim;
     a.scale = d->scale;
+    a.rope_row = d->rope_row ? 1 : 0;
     static const int diag = [] {
         const char *e = getenv("MI355X_ATTN_DIAG");
         return e ? atoi(e) : 0;

@@ -113,6 +113,24 @@ __device__ __forceinline__ double row16_sum(double v) {
     return v;
 }
 
+// Max over a wave (order-free: fmaxf is exact): quad xor 1 / 2, half-row and row
+// mirrors by DPP, then the four rows by readlane. Every lane must be active.
+template <int CTRL>
+__device__ __forceinline__ float dpp_mov_f32(float v) {
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
+}
+__device__ __forceinline__ float wave_fmax(float v) {
+    v = fmaxf(v, dpp_mov_f32<0xB1>(v));   // quad_perm [1,0,3,2]
+    v = fmaxf(v, dpp_mov_f32<0x4E>(v));   // quad_perm [2,3,0,1]
+    v = fmaxf(v, dpp_mov_f32<0x141>(v));  // row_half_mirror
+    v = fmaxf(v, dpp_mov_f32<0x140>(v));  // row_mirror
+    const float r0 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 0));
+    const float r1 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 16));
+    const float r2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 32));
+    const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
+    return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
+}
+
 // In-order double sum of n LDS doubles (p 16-B aligned): sum = ((0 + p[0]) + p[1]) + ...,
 // the dependent adds fed by 16-B reads issued 8 values ahead instead of one LDS
 // round trip per value.

@@ -81,7 +81,8 @@ class AttnDesc(ctypes.Structure):
     _fields_ = [("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p), ("pos", ctypes.c_void_p),
                 ("rope_table", ctypes.c_void_p), ("k_cache", ctypes.c_void_p), ("v_cache", ctypes.c_void_p),
                 ("out", ctypes.c_void_p), ("n_ctx", ctypes.c_int), ("n_head", ctypes.c_int),
-                ("n_head_kv", ctypes.c_int), ("head_dim", ctypes.c_int), ("scale", ctypes.c_float)]
+                ("n_head_kv", ctypes.c_int), ("head_dim", ctypes.c_int), ("scale", ctypes.c_float),
+                ("rope_row", ctypes.c_int)]
 
 _lib = None
 
@@ -398,11 +399,14 @@ def rope(x, head_dim, n_dims, pos, table, out=None, stream=None):
     return out
 
 
-def attn_decode(q, k, v, pos, table, k_cache, v_cache, n_head, n_head_kv, head_dim, scale, out=None, stream=None):
-    """k_cache: (n_ctx, n_head_kv*hd) int16/uint16 view of f16; v_cache: (n_head_kv*hd, n_ctx)."""
+def attn_decode(q, k, v, pos, table, k_cache, v_cache, n_head, n_head_kv, head_dim, scale, out=None, stream=None,
+                rope_row=False):
+    """k_cache: (n_ctx, n_head_kv*hd) int16/uint16 view of f16; v_cache: (n_head_kv*hd, n_ctx).
+    rope_row: `table` is only the rope row of *pos (staged by the caller with the position)."""
     out = _torch().empty(n_head * head_dim, dtype=_torch().float32, device=q.device) if out is None else out
     a = AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(), table.data_ptr(), k_cache.data_ptr(),
-                 v_cache.data_ptr(), out.data_ptr(), k_cache.shape[0], n_head, n_head_kv, head_dim, scale)
+                 v_cache.data_ptr(), out.data_ptr(), k_cache.shape[0], n_head, n_head_kv, head_dim, scale,
+                 1 if rope_row else 0)
     _check(lib().mi355x_attn_decode(ctypes.byref(a), _stream(stream)), "mi355x_attn_decode")
     return out
 

@@ -57,10 +57,14 @@ class LlamaDecoder:
         def buf(n, dtype=f32):
             return torch.zeros(n, dtype=dtype, device=dev)
 
-        # inp_tokens and inp_pos side by side: one 8-byte set_tensor per token
-        self.inp = buf(2, torch.int32)
+        # inp_tokens, inp_pos and the rope row of that position side by side: one
+        # set_tensor of 8 + 4*head_dim bytes per token. The attention reads its cos/sin
+        # with q/k/v instead of after the position (one dependent round trip less);
+        # the row is the table's row, so the values are those of the device table.
+        self.inp = buf(2 + hd, torch.int32)
         self.token, self.pos = self.inp[0:1], self.inp[1:2]
         self.table = rope_table(n_ctx, hd, hp["freq_base"], 1.0, device=dev, stream=backend.stream)
+        self._table_host = self.table.cpu().reshape(n_ctx, hd).view(torch.int32)
         self.k_cache = [torch.zeros((n_ctx, kvw), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
         self.v_cache = [torch.zeros((kvw, n_ctx), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
         self._bufs = []
@@ -91,7 +95,7 @@ class LlamaDecoder:
         eps_bits = [f32_bits(hp["eps"])]
         tok = leaf(self.token, TYPE_I32, 1)
         pos = leaf(self.pos, TYPE_I32, 1)
-        tab = leaf(self.table, TYPE_F32, hd, n_ctx)
+        tab = leaf(self.inp[2:], TYPE_F32, hd, 1)  # the position's rope row (ne1 = 1)
         et, ew = weights["token_embd"]
         emb_t = leaf(ew, et, E, ew.shape[0], row_stride=ew.stride(0) * ew.element_size())
         x, _ = node(OP_GET_ROWS, E, [emb_t, tok])
@@ -123,7 +127,7 @@ class LlamaDecoder:
         self._arr = (ctypes.POINTER(type(T[0])) * len(self.nodes))(*[ctypes.pointer(n) for n in self.nodes])
         # pinned staging slots for (token, pos): a slot is reused only after the stream
         # has been synchronized (the H2D copies are asynchronous)
-        self._host = torch.zeros((self.HOST_SLOTS, 2), dtype=torch.int32).pin_memory()
+        self._host = torch.zeros((self.HOST_SLOTS, 2 + hd), dtype=torch.int32).pin_memory()
         self._slot = 0
         backend.set_fusion(fuse)
         torch.cuda.synchronize()  # weights / zeroed caches (torch's stream) before the backend stream runs
@@ -140,12 +144,14 @@ class LlamaDecoder:
         if self._slot == self.HOST_SLOTS:
             self.b.synchronize()
             self._slot = 0
-        self._host[self._slot, 0] = token
-        self._host[self._slot, 1] = pos
+        row = self._host[self._slot]
+        row[0] = token
+        row[1] = pos
+        row[2:] = self._table_host[pos]
         L = lib()
-        hp = self._host.data_ptr() + 8 * self._slot
+        hp = row.data_ptr()
         self._slot += 1
-        rc = L.mi355x_backend_set_tensor(self.b.h, self.inp.data_ptr(), hp, 8)
+        rc = L.mi355x_backend_set_tensor(self.b.h, self.inp.data_ptr(), hp, 4 * row.numel())
         if rc:
             raise Mi355xError(f"set_tensor failed ({rc})")
         rc = L.mi355x_backend_graph_compute(self.b.h, self._arr, len(self.nodes), 1 if use_graph else 0)

@@ -281,6 +281,9 @@ typedef struct {
     float *out;                /* [n_head*head_dim] */
     int n_ctx, n_head, n_head_kv, head_dim;
     float scale;               /* kq_scale = 1/sqrtf(head_dim) */
+    int rope_row;              /* 0: rope_table is the whole table, row *pos read on device;
+                                  1: rope_table is already the row of this token's position
+                                  (staged by the caller with *pos), read without waiting for pos */
 } mi355x_attn_desc;
 int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
 
@@ -299,7 +302,8 @@ int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
  *                [n_dims, n_pos] (mi355x_rope_table); op_params[0] = n_dims (mode NORMAL)
  *   ATTN_DECODE  src0 q, src1 k, src2 v (f32, before rope), src3 I32 pos [1],
  *                src4 F16 k_cache [kvw, n_ctx], src5 F16 v_cache [n_ctx, kvw] (transposed),
- *                src6 rope table; op_params = {n_head, n_head_kv, head_dim, scale bits}
+ *                src6 rope table [head_dim, >= n_ctx], or [head_dim, 1]: the row of this
+ *                token's position, staged with pos; op_params = {n_head, n_head_kv, head_dim, scale bits}
  *                -> f32 [head_dim*n_head]: the non-flash attention block
  *                (set_rows, mul_mat f16, soft_max_ext, mul_mat f16, permute, cont). */
 enum mi355x_op {

@@ -103,9 +103,11 @@ def test_rope(dev, O, hd, nh, base):
 # ---------------------------------------------------------------- attention
 @pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 256), (128, 32, 8, 128), (64, 8, 8, 64), (64, 8, 2, 512),
                                              (128, 8, 4, 512), (64, 4, 2, 4096)])
-def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx):
+@pytest.mark.parametrize("rope_row", [False, True])
+def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx, rope_row):
     """A growing KV cache: every position's output and both caches bit-exact (positions
-    past the kernel's prefetched cells — 256 K rows, 256/128 V cells — included)."""
+    past the kernel's prefetched cells — 256 K rows, 256/128 V cells — included); the
+    rope table whole (row *pos read on device) or only the position's row (rope_row)."""
     import torch
     import ggml_mi355x as g
     rng = np.random.default_rng(hd + nh)
@@ -123,7 +125,8 @@ def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx):
         k = (rng.standard_normal(kvw) * 2).astype(np.float32)
         v = rng.standard_normal(kvw).astype(np.float32)
         pos = torch.tensor([p], dtype=torch.int32, device=dev)
-        got = g.attn_decode(t(q, dev), t(k, dev), t(v, dev), pos, tab, kc, vc, nh, nkv, hd, scale).cpu().numpy()
+        got = g.attn_decode(t(q, dev), t(k, dev), t(v, dev), pos, tab[p].contiguous() if rope_row else tab, kc, vc,
+                            nh, nkv, hd, scale, rope_row=rope_row).cpu().numpy()
         ref = O.attn_decode(O.rope(q, hd, hd, p, tref), O.rope(k, hd, hd, p, tref), v, kc_ref, vc_ref, p, nh, nkv,
                             hd, scale)
         assert bits_equal(got, ref), (p, first_mismatch(got, ref))
