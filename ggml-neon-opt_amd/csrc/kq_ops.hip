@@ -223,7 +223,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         x0 = a.v[(int64_t)g * HD + (t - HD / 2)];
     }
     uint4 kpre[KV4] = {};
-    if (t < a.n_ctx) {
+    if (t < a.n_ctx && a.diag != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
         const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)t * kvw + (int64_t)g * HD);
 #pragma unroll
         for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
@@ -235,7 +235,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx + 8 * j;
 #pragma unroll
         for (int it = 0; it < VPF; ++it)
-            if (32 * it < a.n_ctx) vpre[ii][it] = *(const uint4 *)(vr + 32 * it);
+            if (32 * it < a.n_ctx && a.diag != 5) vpre[ii][it] = *(const uint4 *)(vr + 32 * it);
     }
 
     const bool bad = pos_in < 0 || pos_in >= a.n_ctx;  // no cache cell for this position
@@ -274,7 +274,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         if (writer) a.v_cache[(int64_t)(g * HD + d) * a.n_ctx + pos] = vv;
     }
     __syncthreads();
-    if (a.diag == 1) {  // diagnostics: stop after the loads and rope
+    if (a.diag == 1 || a.diag == 5) {  // diagnostics: stop after the loads and rope
         if (t < HD) a.out[(int64_t)h * HD + t] = x0 + __uint_as_float(kpre[0].x ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
         return;
     }
