@@ -106,11 +106,42 @@ __device__ __forceinline__ double sumsq16(const float v[16]) {
 }
 
 // Balanced tree over the 16 lanes of an aligned 16-lane row (xor 1, 2, 4, 8): every
-// lane of the row ends with the same value.
+// lane of the row ends with the same value. By DPP: quad permutes for xor 1 and 2;
+// after them every lane of a quad holds the quad's sum, so the half-row mirror
+// brings the other quad's sum (= the xor-4 partner's value) and the row mirror the
+// other half's (= xor 8); float addition is commutative, so every lane's sum has
+// the same bits as the xor tree. Every lane of the wave must be active.
+template <int CTRL>
+__device__ __forceinline__ double dpp_mov_f64(double v) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)b, CTRL, 0xF, 0xF, true);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(b >> 32), CTRL, 0xF, 0xF, true);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
 __device__ __forceinline__ double row16_sum(double v) {
-#pragma unroll
-    for (int m = 1; m < 16; m <<= 1) v += __shfl_xor(v, m, 64);
+    v += dpp_mov_f64<0xB1>(v);   // xor 1
+    v += dpp_mov_f64<0x4E>(v);   // xor 2
+    v += dpp_mov_f64<0x141>(v);  // the other quad of the half-row (xor 4)
+    v += dpp_mov_f64<0x140>(v);  // the other half of the row (xor 8)
     return v;
+}
+
+// In-order double sum of the first n values of sums[] (LDS), the same adds as
+// `for (b < n) tot += sums[b]`: lane i loads sums[c0 + i] for a chunk of 64 and the
+// dependent adds read the lanes in order (one LDS round trip per 64 values).
+__device__ __forceinline__ double seq_sum_lanes(const double *sums, int n, int lane) {
+    double tot = 0.0;
+    for (int c0 = 0; c0 < n; c0 += 64) {
+        const double v = c0 + lane < n ? sums[c0 + lane] : 0.0;
+        const uint64_t b = __builtin_bit_cast(uint64_t, v);
+        const int m = n - c0 < 64 ? n - c0 : 64;
+        for (int i = 0; i < m; ++i) {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, i);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), i);
+            tot += __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        }
+    }
+    return tot;
 }
 
 // Max over a wave (order-free: fmaxf is exact): quad xor 1 / 2, half-row and row

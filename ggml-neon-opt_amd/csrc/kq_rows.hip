@@ -152,23 +152,24 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             double *sums = (double *)(smem + L.sums);
 #pragma unroll
             for (int i = 0; i < ROWS_QPASS; ++i) {
-                const int b = PASS * i + 4 * wave + (lane >> 4);
-                double sq = 0.0;
-                if (i < qiters && b < nb) {
-                    float v[16];
+                if (i < qiters && PASS * i + 4 * wave < nb) {  // wave-uniform: this wave holds x of the pass
+                    const int b = PASS * i + 4 * wave + (lane >> 4);
+                    double sq = 0.0;
+                    if (b < nb) {
+                        float v[16];
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) {
-                        v[4 * k] = __uint_as_float(xv[i][k].x), v[4 * k + 1] = __uint_as_float(xv[i][k].y);
-                        v[4 * k + 2] = __uint_as_float(xv[i][k].z), v[4 * k + 3] = __uint_as_float(xv[i][k].w);
+                        for (int k = 0; k < 4; ++k) {
+                            v[4 * k] = __uint_as_float(xv[i][k].x), v[4 * k + 1] = __uint_as_float(xv[i][k].y);
+                            v[4 * k + 2] = __uint_as_float(xv[i][k].z), v[4 * k + 3] = __uint_as_float(xv[i][k].w);
+                        }
+                        sq = sumsq16(v);
                     }
-                    sq = sumsq16(v);
+                    sq = row16_sum(sq);  // DPP, every lane of the wave active
+                    if (b < nb && (lane & 15) == 0) sums[b] = sq;
                 }
-                sq = row16_sum(sq);
-                if (i < qiters && b < nb && (lane & 15) == 0) sums[b] = sq;
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            double tot = 0.0;  // superblocks in order (a batched read here spills the prologue registers)
-            for (int b = 0; b < nb; ++b) tot += sums[b];
+            const double tot = seq_sum_lanes(sums, nb, lane);  // superblocks in order
             const float mean = (float)(tot / (double)(nb * QK));
             const float scale = 1.0f / sqrtf(mean + a.eps);
 #pragma unroll
