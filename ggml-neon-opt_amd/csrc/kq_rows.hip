@@ -185,7 +185,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 #pragma unroll
             for (int k = 0; k < 4; ++k) cur[k] = i == 0 ? xv[0][k] : i == 1 ? xv[1][k] : xv[2][k];
             const int b = PASS * i + 4 * wave + (lane >> 4);
-            if (b < nb) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * b);
+            if (b < nb && !(a.diag & 64)) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * b);  // (diag 64: timing only)
         }
         if (a.stamps) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -300,7 +300,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     // ---- SWIGLU epilogue (the GLU node after the gate/up MUL_MATs): up wave and its
     // gate partner own the same rows in this workgroup; both results are staged in LDS.
     // Same arithmetic as kq_swiglu (ggml_vec_swiglu_f32: NEON body, libm tail).
-    if (a.epi) {  // uniform over the grid: every wave of the workgroup reaches the barrier
+    if (a.epi && !(a.diag & 128)) {  // uniform over the grid: every wave of the workgroup reaches the barrier (diag 128: timing only)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (ww.m == 1 && ww.nrows > 0) {
             const float *gouts = (const float *)(smem + L.outs + (wave - a.epi_wave_off) * L.outs_stride);
