@@ -116,7 +116,7 @@ __global__ void __launch_bounds__(256) kq_rms_norm(const float *__restrict__ x, 
     }
     __syncthreads();
     const double total = seq_sum_lds(sb_sum, nb);  // superblocks in order
-    const float mean = (float)(total / (double)n);
+    const float mean = (float)div_by_count(total, n);
     const float scale = 1.0f / sqrtf(mean + eps);
     for (int64_t i = threadIdx.x; i < n; i += 256) {
         const float v = xr[i] * scale;

@@ -162,6 +162,14 @@ __device__ __forceinline__ float wave_fmax(float v) {
     return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
 
+// sum / n in double, correctly rounded (ggml_float mean = sum/ne00): for n a power of
+// two the quotient is the exact product sum * 2^-k (both correctly rounded results of
+// the same real value), so the f64 divide sequence is skipped.
+__device__ __forceinline__ double div_by_count(double sum, int64_t n) {
+    if ((n & (n - 1)) == 0) return sum * (1.0 / (double)n);
+    return sum / (double)n;
+}
+
 // In-order double sum of n LDS doubles (p 16-B aligned): sum = ((0 + p[0]) + p[1]) + ...,
 // the dependent adds fed by 16-B reads issued 8 values ahead instead of one LDS
 // round trip per value.

@@ -170,7 +170,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             const double tot = seq_sum_lanes(sums, nb, lane);  // superblocks in order
-            const float mean = (float)(tot / (double)(nb * QK));
+            const float mean = (float)div_by_count(tot, (int64_t)nb * QK);
             const float scale = 1.0f / sqrtf(mean + a.eps);
 #pragma unroll
             for (int i = 0; i < ROWS_QPASS; ++i)
