@@ -323,14 +323,14 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
             if (c <= pos) {
                 uint4 kv[KV4];
                 if (c == pos) {
-    #pragma unroll
+#pragma unroll
                     for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
                 } else if (c == t) {
-    #pragma unroll
+#pragma unroll
                     for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
                 } else {
                     const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
-    #pragma unroll
+#pragma unroll
                     for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
                 }
                 s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
@@ -346,7 +346,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         if (t < 64) {
             float m = -INFINITY;
             for (int c = t; c < n_kv; c += 64) m = fmaxf(m, w[c]);
-    #pragma unroll
+#pragma unroll
             for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
             if (t == 0) scal[0] = m;
         }
@@ -354,12 +354,12 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         const float mx = scal[0];
         for (int gi = t; gi < n_kv / 4; gi += 256) {
             float e[4];
-    #pragma unroll
+#pragma unroll
             for (int k = 0; k < 4; ++k) {
                 const float wv = w[4 * gi + k];
                 e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
             }
-    #pragma unroll
+#pragma unroll
             for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
             gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));  // the vaddvq group sum, in parallel
         }
