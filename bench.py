@@ -358,6 +358,36 @@ def chain_side(model, dev, be, steps=64, warmup=8):
     return out
 
 
+def model_side(model, dev, steps=64, warmup=8):
+    """Another BASELINE config on the same executor: the full decode token of `model`
+    (tg<steps> from an empty KV cache, hipGraph replay) and its pp512 (every matmul
+    of the token at ne11 = 512, kq_mmq). Llama-3-8B covers configs 3 (pp512 + tg)
+    and 5 (Q6_K output / attn_v / ffn_down beside Q4_K, one kernel template)."""
+    be = g.Backend(torch.cuda.current_device())
+    n_ctx = max(128, (steps + 31) // 32 * 32)
+    tk = Token(model, dev, 0x51A7, be, n_ctx)
+    for i in range(warmup):
+        tk.dec.step(tk.tokens[i], i)
+    be.synchronize()
+    tk.dec.reset()
+    torch.cuda.synchronize()
+    st = torch.cuda.ExternalStream(be.stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for i in range(steps):
+        tk.dec.step(tk.tokens[i], i)
+    e1.record(st)
+    be.synchronize()
+    ms = e0.elapsed_time(e1) / steps
+    out = {"tg_tok_s": round(1e3 / ms, 1), "ms_per_token": round(ms, 4), "tg_steps": steps,
+           "weights_MB_per_token": round(tk.bytes_per_token / 1e6, 1),
+           "effective_GBps": round(tk.bytes_per_token / (ms * 1e-3) / 1e9, 1),
+           "launches_per_token": tk.launches(), "pp512": prefill_chain(tk, dev)}
+    del tk, be
+    torch.cuda.empty_cache()
+    return out
+
+
 def cpu_baseline_token(tk, seconds):
     """The oracle's restated llm_build_llama token (ggml-cpu semantics op by op: the
     matmuls through the restated ggml_compute_forward_mul_mat with pthreads, the other
@@ -450,6 +480,7 @@ def main():
                     help="token: the full decode graph (tg128: token i at position i of a fresh KV cache); "
                          "chain: the per-token MUL_MAT chain only")
     ap.add_argument("--no-chain", action="store_true", help="token workload: skip the matmul-chain side figure")
+    ap.add_argument("--no-8b", action="store_true", help="skip the Llama-3-8B side figure (configs 3 and 5)")
     args = ap.parse_args()
     if args.workload == "token" and (args.mode == "rowsplit" or args.gguf or args.impl != "auto"):
         args.workload = "chain"  # the row-split, GGUF-file and kernel-A/B runs are matmul-chain modes
@@ -575,6 +606,9 @@ def main():
         if isinstance(chain, Token) and not args.no_chain and world == 1:
             side = chain_side(args.model, dev, be)
         large = None if args.no_large or world > 1 else large_gemv(dev)
+        l3 = None
+        if isinstance(chain, Token) and not args.no_8b and world == 1 and args.model != "llama-3-8b":
+            l3 = model_side("llama-3-8b", dev)
         prefill = None if args.no_prefill or world > 1 or not use_backend else prefill_chain(chain, dev)
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
@@ -617,6 +651,7 @@ def main():
             "gemv_large": large,
             "prefill_pp512": prefill,
             "matmul_chain": side,
+            "llama3_8b": l3,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
