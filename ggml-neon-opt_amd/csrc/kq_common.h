@@ -101,7 +101,7 @@ struct RowsArgs {
     int pre0;         // weight steps issued before the activation is quantized
     int pf;           // L2 prefetch on/off (ROWS_PF 4-KB touches of the stream past the ring)
     int bR;           // rows per chain batch (bR*nb % 16 == 0 unless bR >= rpw)
-    int diag;         // diagnostics (timing only): bit3 stream weights only, 16/32 prologue, 64 no quantization, 128 no SWIGLU epilogue
+    int diag;         // diagnostics (timing only): bit3 stream weights only, 16/32 prologue, 64 no quantization, 128 no SWIGLU epilogue, 256 empty launch
     int wave_prefix[MI355X_MAX_FUSED + 1];
     int rbase[MI355X_MAX_FUSED];
     int rrem[MI355X_MAX_FUSED];

@@ -330,6 +330,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void __launch_bounds__(ROWS_WAVES * 64) kq_rows(const RowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    if (a.diag & 256) return;  // diagnostics (timing only): empty launch
     const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
