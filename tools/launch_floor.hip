@@ -37,7 +37,10 @@ int main() {
     struct Cfg {
         int mode, wgs, threads, lds;
     } cfgs[] = {{0, cus, 768, 0},      {0, cus, 768, 100 << 10}, {0, cus, 256, 0},  {0, cus / 4, 256, 0},
-                {1, cus, 768, 100 << 10}, {1, cus, 256, 0},      {1, cus / 4, 256, 0}, {1, 1, 64, 0}};
+                {1, cus, 768, 100 << 10}, {1, cus, 256, 0},      {1, cus / 4, 256, 0}, {1, 1, 64, 0},
+                // the GEMV's 3072 waves as 12-wave / 4-wave workgroups, with their LDS
+                {1, cus, 768, 0},         {1, 3 * cus, 256, 0},    {1, 3 * cus, 256, 32 << 10},
+                {1, 2 * cus, 384, 50 << 10}, {1, 2 * cus, 256, 0}};
     for (const Cfg &c : cfgs) {
         hipGraph_t g;
         hipGraphExec_t ge;
