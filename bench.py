@@ -646,6 +646,9 @@ def main():
                        "hipgraph": use_backend and args.impl != "chain" and not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
             "effective_GBps": round(value * chain.bytes_per_token / 1e9 / (world if args.mode == "replicas" else 1), 1),
+            # the whole token (every launch, gaps included) against the HBM roofline, per GPU
+            "token_hbm_frac": round(value * chain.bytes_per_token / 1e9 / (world if args.mode == "replicas" else 1)
+                                    / HBM_PEAK_GBS, 4),
             "roofline": roof,
             "kernels": kernels,
             "gemv_large": large,
