@@ -29,24 +29,39 @@ __global__ void kq_chain(const ChainArgs a);
 
 namespace {
 
-std::once_flag g_dev_once;
-int g_dev_ok = 0;
-int g_num_cus = 256;
+// Per-device probe (the caller's current device): 0 unknown, 1 gfx950, -1 not usable.
+// A process may drive several devices (one backend each), so nothing here is cached
+// for "the" device.
+constexpr int kMaxDevices = 64;
+std::mutex g_dev_mu;
+std::atomic<int> g_dev_state[kMaxDevices];
+int g_dev_cus[kMaxDevices] = {0};
 
-void probe_device() {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return;
+int current_device() {
     int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices) return -1;
+    return dev;
+}
+
+void probe_device(int dev) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0 || dev >= n) {
+        g_dev_state[dev].store(-1);
+        return;
+    }
     hipDeviceProp_t prop;
-    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) return;
+    if (hipGetDeviceProperties(&prop, dev) != hipSuccess) {
+        g_dev_state[dev].store(-1);
+        return;
+    }
     if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
         fprintf(stderr, "ggml_mi355x: device %d is %s, this library is built for gfx950 only\n", dev,
                 prop.gcnArchName);
+        g_dev_state[dev].store(-1);
         return;
     }
-    g_num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
-    g_dev_ok = 1;
+    g_dev_cus[dev] = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 256;
+    g_dev_state[dev].store(1, std::memory_order_release);
 }
 
 template <int NCOL, bool FUSEDQ, bool DEBUG>
@@ -79,18 +94,25 @@ constexpr int64_t kRowsFusedMaxNb = ROWS_QPASS * 4 * ROWS_WAVES;  // kq_rows: up
 uint64_t *g_stamps = nullptr;  // diagnostics (mi355x_diag_stamps)
 int64_t g_stamps_cap = 0;
 
-// Workgroups of one kernel resident per CU (registers / LDS), cached per (fn, lds).
+// Workgroups of one kernel resident per CU (registers / LDS), cached per
+// (device, fn, lds): function attributes are set per device.
+struct OccKey {
+    int dev;
+    const void *fn;
+    size_t lds;
+};
 int resident_wgs(const void *fn, size_t lds) {
     static std::mutex mu;
-    static std::vector<std::pair<std::pair<const void *, size_t>, int>> cache;
+    static std::vector<std::pair<OccKey, int>> cache;
+    const int dev = current_device();
     std::lock_guard<std::mutex> lk(mu);
     for (auto &e : cache)
-        if (e.first.first == fn && e.first.second == lds) return e.second;
+        if (e.first.dev == dev && e.first.fn == fn && e.first.lds == lds) return e.second;
     int n = 0;
     if (lds > 64 * 1024) hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, WG_THREADS, lds) != hipSuccess || n <= 0) n = 1;
     if (n > 8) n = 8;
-    cache.push_back({{fn, lds}, n});
+    cache.push_back({{dev, fn, lds}, n});
     return n;
 }
 
@@ -160,13 +182,18 @@ double gemv_bytes(const GemvArgs &a, bool fusedq) {
 }  // namespace
 
 int device_ok() {
-    std::call_once(g_dev_once, probe_device);
-    return g_dev_ok;
+    const int dev = current_device();
+    if (dev < 0) return 0;
+    const int st = g_dev_state[dev].load(std::memory_order_acquire);
+    if (st) return st > 0;
+    std::lock_guard<std::mutex> lk(g_dev_mu);
+    if (g_dev_state[dev].load() == 0) probe_device(dev);
+    return g_dev_state[dev].load() > 0;
 }
 
 int num_cus() {
-    device_ok();
-    return g_num_cus;
+    if (!device_ok()) return 256;
+    return g_dev_cus[current_device()];
 }
 
 int choose_ncol(int64_t M, int nb) {
@@ -274,12 +301,13 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
 void allow_lds(const void *fn, size_t lds) {
     if (lds <= 64 * 1024) return;
     static std::mutex mu;
-    static std::vector<std::pair<const void *, size_t>> done;
+    static std::vector<std::pair<int, const void *>> done;  // (device, fn): set per device
+    const int dev = current_device();
     std::lock_guard<std::mutex> lk(mu);
     for (auto &e : done)
-        if (e.first == fn && e.second >= lds) return;
+        if (e.first == dev && e.second == fn) return;
     hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)kMaxLds);
-    done.push_back({fn, kMaxLds});
+    done.push_back({dev, fn});
 }
 
 int launch_gemv(const GemvPlan &pl, hipStream_t stream) {

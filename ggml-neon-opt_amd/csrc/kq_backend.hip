@@ -46,6 +46,20 @@ struct mi355x_backend {
 
 namespace {
 
+// Every backend entry point runs on the backend's own device and restores the
+// caller's current device afterwards (ggml-cuda's ggml_cuda_set_device discipline):
+// one process may hold several backends (llama.cpp's layer split).
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && cur != dev && hipSetDevice(dev) == hipSuccess) prev = cur;
+    }
+    ~DeviceGuard() {
+        if (prev >= 0) hipSetDevice(prev);
+    }
+};
+
 bool is_kquant(int t) { return t == MI355X_TYPE_Q4_K || t == MI355X_TYPE_Q5_K || t == MI355X_TYPE_Q6_K; }
 
 void drop_graph(mi355x_backend *b) {
@@ -77,18 +91,50 @@ float f_of(int32_t bits) {
     return f;
 }
 
-// readers[i]: number of node operands (over all nodes) that are node i's output.
+// Byte range [lo, hi) a tensor's data spans (ggml_nbytes: the last element of every
+// dim; K-quant rows are whole blocks).
+struct Span {
+    uintptr_t lo = 0, hi = 0;
+};
+Span span_of(const mi355x_tensor *t) {
+    Span s;
+    if (!t || !t->data) return s;
+    const int64_t blck = is_kquant(t->type) ? MI355X_QK_K : 1;
+    uint64_t bytes = (uint64_t)(t->ne[0] / blck) * t->nb[0];
+    for (int d = 1; d < 4; ++d)
+        if (t->ne[d] > 1) bytes += (uint64_t)(t->ne[d] - 1) * t->nb[d];
+    s.lo = (uintptr_t)t->data;
+    s.hi = s.lo + (uintptr_t)bytes;
+    return s;
+}
+
+// readers[i]: number of node operands (over all nodes) that read node i's output.
+// A read is credited to the LATEST earlier node whose output overlaps the operand's
+// bytes (ggml-alloc reuses a dead node's buffer for a later node, so the latest
+// writer is the producer); reads through views at an offset count too. When the
+// latest overlapping writer does not cover the whole operand, older overlapping
+// writers are credited as well: over-counting only disables a fusion, it never
+// elides a live output.
 std::vector<int> count_readers(mi355x_tensor *const *nodes, int n) {
     std::vector<int> r(n, 0);
+    std::vector<Span> out(n);
+    for (int i = 0; i < n; ++i)
+        if (nodes[i]->op != MI355X_OP_NONE) out[i] = span_of(nodes[i]);
     for (int j = 0; j < n; ++j)
         for (int s = 0; s < MI355X_MAX_SRC; ++s) {
             const mi355x_tensor *u = nodes[j]->src[s];
             if (!u) continue;
-            for (int i = 0; i < j; ++i)
-                if (nodes[i] == u || (nodes[i]->data && nodes[i]->data == u->data && nodes[i]->op != MI355X_OP_NONE)) {
+            const Span us = span_of(u);
+            for (int i = j - 1; i >= 0; --i) {
+                if (nodes[i] == u) {  // the operand IS node i (whatever its buffer)
                     ++r[i];
                     break;
                 }
+                const Span &o = out[i];
+                if (o.hi <= o.lo || us.hi <= us.lo || !(o.lo < us.hi && us.lo < o.hi)) continue;
+                ++r[i];
+                if (o.lo <= us.lo && us.hi <= o.hi) break;  // fully produced by node i
+            }
         }
     return r;
 }
@@ -212,7 +258,8 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
         }
         case MI355X_OP_GET_ROWS:
             return mi355x_get_rows(t->src[0]->type, t->src[0]->data, t->src[0]->ne[0], t->src[0]->nb[1],
-                                   (const int32_t *)t->src[1]->data, t->src[1]->ne[0], (float *)t->data, st);
+                                   t->src[0]->ne[1], (const int32_t *)t->src[1]->data, t->src[1]->ne[0],
+                                   (float *)t->data, st);
         case MI355X_OP_RMS_NORM:
             if (l.norm_w)
                 return mi355x_rms_norm((const float *)t->src[0]->data, l.norm_w, l.norm_y, t->ne[0], nelem(t) / t->ne[0],
@@ -433,8 +480,10 @@ int chain_status(mi355x_backend *b) {
 extern "C" {
 
 mi355x_backend_t mi355x_backend_init(int device) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
+    DeviceGuard dg(device);
     if (!kq::device_ok()) return nullptr;
-    if (hipSetDevice(device) != hipSuccess) return nullptr;
     mi355x_backend *b = new mi355x_backend();
     b->device = device;
     if (hipStreamCreateWithFlags(&b->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -447,12 +496,15 @@ mi355x_backend_t mi355x_backend_init(int device) {
 
 void mi355x_backend_free(mi355x_backend_t b) {
     if (!b) return;
+    {
+    DeviceGuard dg(b->device);
     hipStreamSynchronize(b->stream);
     drop_graph(b);
     drop_chain(b);
     for (uint32_t *s : b->old_sync) hipFree(s);
     if (b->workspace) hipFree(b->workspace);
     hipStreamDestroy(b->stream);
+    }
     delete b;
 }
 
@@ -462,6 +514,7 @@ void *mi355x_backend_stream(mi355x_backend_t b) { return b ? (void *)b->stream :
 
 void *mi355x_backend_alloc(mi355x_backend_t b, size_t size) {
     if (!b) return nullptr;
+    DeviceGuard dg(b->device);
     void *p = nullptr;
     if (hipMalloc(&p, size ? size : 1) != hipSuccess) return nullptr;
     return p;
@@ -469,6 +522,7 @@ void *mi355x_backend_alloc(mi355x_backend_t b, size_t size) {
 
 void mi355x_backend_free_buffer(mi355x_backend_t b, void *ptr) {
     if (!b || !ptr) return;
+    DeviceGuard dg(b->device);
     hipStreamSynchronize(b->stream);
     drop_graph(b);  // a captured graph or a chain plan may reference the buffer
     drop_chain(b);
@@ -477,6 +531,7 @@ void mi355x_backend_free_buffer(mi355x_backend_t b, void *ptr) {
 
 int mi355x_backend_set_tensor(mi355x_backend_t b, void *dst, const void *host_src, size_t size) {
     if (!b || (!dst && size)) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
     // (hipStreamWriteValue32 per word for tiny inputs was measured 10 us/token slower
     // than this one copy of inp_tokens + inp_pos)
     const hipError_t e = hipMemcpyAsync(dst, host_src, size, hipMemcpyHostToDevice, b->stream);
@@ -485,12 +540,14 @@ int mi355x_backend_set_tensor(mi355x_backend_t b, void *dst, const void *host_sr
 
 int mi355x_backend_get_tensor(mi355x_backend_t b, void *host_dst, const void *src, size_t size) {
     if (!b || (!src && size)) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
     const hipError_t e = hipMemcpyAsync(host_dst, src, size, hipMemcpyDeviceToHost, b->stream);
     return e == hipSuccess ? 0 : (int)e;
 }
 
 int mi355x_backend_synchronize(mi355x_backend_t b) {
     if (!b) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
     const hipError_t e = hipStreamSynchronize(b->stream);
     if (e != hipSuccess) return (int)e;
     return chain_status(b);
@@ -519,13 +576,17 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
         }
         case MI355X_OP_GET_ROWS: {
             const mi355x_tensor *w = op->src[0], *ids = op->src[1];
-            if (!w || !ids || ids->type != MI355X_TYPE_I32 || !contig_f32(op)) return 0;
+            if (!w || !ids || ids->type != MI355X_TYPE_I32 || !ids->data || ids->nb[0] != 4 || !contig_f32(op))
+                return 0;
             if (w->type != MI355X_TYPE_F32 && w->type != MI355X_TYPE_Q4_K && w->type != MI355X_TYPE_Q6_K) return 0;
+            if (op->ne[1] > 1 && op->nb[1] != (size_t)op->ne[0] * 4) return 0;  // dst rows packed (kernel: out + r*k)
             return op->ne[0] == w->ne[0] && op->ne[1] == ids->ne[0] && w->ne[0] % MI355X_QK_K == 0;
         }
         case MI355X_OP_RMS_NORM:
+            // the kernel reads x + row*n with 16-B loads: src0 and dst packed rows, 16-B aligned
             return contig_f32(op) && contig_f32(op->src[0]) && op->ne[0] % MI355X_QK_K == 0 &&
-                   op->nb[1] == (size_t)op->ne[0] * 4;
+                   op->nb[1] == (size_t)op->ne[0] * 4 && op->src[0]->nb[1] == (size_t)op->ne[0] * 4 &&
+                   nelem(op->src[0]) == nelem(op) && ((uintptr_t)op->src[0]->data & 15u) == 0;
         case MI355X_OP_MUL:
         case MI355X_OP_ADD:
         case MI355X_OP_SWIGLU:
@@ -542,7 +603,18 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
             if ((hd != 64 && hd != 128) || nkv <= 0 || nh % nkv) return 0;
             if (op->src[4]->type != MI355X_TYPE_F16 || op->src[5]->type != MI355X_TYPE_F16) return 0;
             if (op->src[4]->ne[0] != (int64_t)nkv * hd || op->src[3]->type != MI355X_TYPE_I32) return 0;
-            if (op->src[5]->ne[0] != op->src[4]->ne[1]) return 0;
+            if (op->src[5]->ne[0] != op->src[4]->ne[1] || op->src[5]->ne[1] != op->src[4]->ne[0]) return 0;
+            // caches exactly [n_ctx][kvw] and [kvw][n_ctx] f16, 16-B aligned (the kernel's addressing)
+            if (op->src[4]->nb[0] != 2 || op->src[4]->nb[1] != (size_t)op->src[4]->ne[0] * 2) return 0;
+            if (op->src[5]->nb[0] != 2 || op->src[5]->nb[1] != (size_t)op->src[5]->ne[0] * 2) return 0;
+            if (((uintptr_t)op->src[4]->data & 15u) || ((uintptr_t)op->src[5]->data & 15u)) return 0;
+            const int64_t n_ctx = op->src[4]->ne[1];
+            if (n_ctx < 32 || n_ctx % 32 || n_ctx > 8192) return 0;
+            for (int s = 0; s < 3; ++s)
+                if (!contig_f32(op->src[s])) return 0;
+            if (nelem(op->src[0]) != (int64_t)nh * hd || nelem(op->src[1]) != (int64_t)nkv * hd ||
+                nelem(op->src[2]) != (int64_t)nkv * hd)
+                return 0;
             if (op->src[6]->ne[1] != 1 && op->src[6]->ne[1] < op->src[4]->ne[1]) return 0;  // row or table
             if (op->src[6]->ne[0] != hd) return 0;
             return contig_f32(op) && op->ne[0] == (int64_t)nh * hd;
@@ -554,6 +626,7 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
 
 int mi355x_backend_set_fusion(mi355x_backend_t b, int enable) {
     if (!b) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
     const int prev = b->fuse ? 1 : 0;
     if ((enable != 0) != b->fuse) {
         hipStreamSynchronize(b->stream);
@@ -565,6 +638,7 @@ int mi355x_backend_set_fusion(mi355x_backend_t b, int enable) {
 
 int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes, int n_nodes, int use_graph) {
     if (!b || (n_nodes > 0 && !nodes) || n_nodes < 0) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
     // replay fast path: the node list of the captured graph (every decode step after
     // the first) was validated, planned and captured under this key already
     if (use_graph && b->graph_exec && !kq::chain_enabled()) {

@@ -271,12 +271,21 @@ mi355x_gguf_t mi355x_gguf_open(const char *path) {
     for (Tensor &t : g->tensors) {
         const TypeSize ts = ggml_type_size(t.type);
         if (t.offset % g->alignment) return fail(g, path, "tensor '" + t.name + "': misaligned offset");
-        if (ts.blck) {
-            if (t.ne[0] % ts.blck) return fail(g, path, "tensor '" + t.name + "': row not a whole number of blocks");
-            uint64_t rows = 1;
-            for (int d = 1; d < 4; ++d) rows *= (uint64_t)t.ne[d];
-            t.size = (uint64_t)(t.ne[0] / ts.blck) * (uint64_t)ts.bytes * rows;
+        // unknown types are rejected: a caller sizing its reads from ne could not be
+        // bounded by t.size otherwise (upstream gguf.cpp rejects them too [U])
+        if (!ts.blck) return fail(g, path, "tensor '" + t.name + "': unknown ggml type " + std::to_string(t.type));
+        if (t.ne[0] % ts.blck) return fail(g, path, "tensor '" + t.name + "': row not a whole number of blocks");
+        // every product checked before it is formed (upstream: INT64_MAX / ne checks)
+        uint64_t size = (uint64_t)(t.ne[0] / ts.blck);
+        bool ovf = size > UINT64_MAX / (uint64_t)ts.bytes;
+        size *= ovf ? 1 : (uint64_t)ts.bytes;
+        for (int d = 1; d < 4 && !ovf; ++d) {
+            const uint64_t ne = (uint64_t)t.ne[d];
+            if (ne && size > UINT64_MAX / ne) ovf = true;
+            else size *= ne;
         }
+        if (ovf || size > (uint64_t)INT64_MAX) return fail(g, path, "tensor '" + t.name + "': size overflows 64 bits");
+        t.size = size;
         t.offset += g->data_offset;
         if (t.offset > g->map_size || t.size > g->map_size - t.offset)
             return fail(g, path, "tensor '" + t.name + "': data beyond the end of the file");

@@ -35,13 +35,19 @@ namespace kq {
 // elements. Q4_K: y = fmaf(d*sc, q, -(dmin*m)) (gcc contracts `d1*q - m1` [U]);
 // Q6_K: y = (d*sc)*q; F32: copy.
 __global__ void __launch_bounds__(256) kq_get_rows(int type, const uint8_t *__restrict__ table, int64_t k,
-                                                   int64_t row_stride, const int32_t *__restrict__ ids,
-                                                   float *__restrict__ out) {
+                                                   int64_t row_stride, int64_t n_rows,
+                                                   const int32_t *__restrict__ ids, float *__restrict__ out) {
     const int64_t r = blockIdx.y;
     const int64_t e0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8;
     if (e0 >= k) return;
-    const uint8_t *row = table + (int64_t)ids[r] * row_stride;
+    const int64_t id = ids[r];
     float *y = out + r * k + e0;
+    if (id < 0 || id >= n_rows) {  // ggml asserts 0 <= i01 < ne01: never read outside the table
+#pragma unroll
+        for (int i = 0; i < 8; ++i) y[i] = __builtin_nanf("");
+        return;
+    }
+    const uint8_t *row = table + id * row_stride;
     if (type == MI355X_TYPE_F32) {
         const float *s = (const float *)row + e0;
 #pragma unroll
@@ -115,7 +121,16 @@ __global__ void __launch_bounds__(256) kq_rms_norm(const float *__restrict__ x, 
         if (b < nb && l == 0) sb_sum[b] = s;
     }
     __syncthreads();
-    const double total = seq_sum_lds(sb_sum, nb);  // superblocks in order
+    double total = seq_sum_lds(sb_sum, nb);  // superblocks in order
+    if (rms_mean_ambiguous(div_by_count(total, n), n)) {  // block-uniform: every thread has the same total
+        __syncthreads();                                  // sb_sum[0] is reused below
+        if (threadIdx.x < 64) {
+            const double s = seq_sumsq_wave(xr, n, threadIdx.x);  // ggml's sequential order
+            if (threadIdx.x == 0) sb_sum[0] = s;
+        }
+        __syncthreads();
+        total = sb_sum[0];
+    }
     const float mean = (float)div_by_count(total, n);
     const float scale = 1.0f / sqrtf(mean + eps);
     for (int64_t i = threadIdx.x; i < n; i += 256) {
@@ -500,9 +515,9 @@ using namespace kq;
 
 extern "C" {
 
-int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, const int32_t *ids, int64_t n_ids,
-                    float *dst, void *stream) {
-    if (!table || !ids || !dst || ne0 <= 0 || n_ids < 0) return MI355X_E_INVAL;
+int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, int64_t n_rows, const int32_t *ids,
+                    int64_t n_ids, float *dst, void *stream) {
+    if (!table || !ids || !dst || ne0 <= 0 || n_ids < 0 || n_rows < 0) return MI355X_E_INVAL;
     if (type != MI355X_TYPE_F32 && type != MI355X_TYPE_Q4_K && type != MI355X_TYPE_Q6_K) return MI355X_E_UNSUPPORTED;
     if (ne0 % (type == MI355X_TYPE_F32 ? 8 : QK)) return MI355X_E_INVAL;
     if (row_stride < mi355x_row_size(type, ne0) && type != MI355X_TYPE_F32) return MI355X_E_INVAL;
@@ -511,7 +526,7 @@ int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride,
     const dim3 grid((unsigned)((ne0 / 8 + 255) / 256), (unsigned)n_ids);
     return timed_launch("kq::kq_get_rows", (double)n_ids * (ne0 * 4.0 + (double)mi355x_row_size(type, ne0)),
                         kq_get_rows, grid, dim3(256), 0, (hipStream_t)stream, type, (const uint8_t *)table, ne0,
-                        (int64_t)row_stride, ids, dst);
+                        (int64_t)row_stride, n_rows, ids, dst);
 }
 
 int mi355x_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t nrows, float eps, void *stream) {

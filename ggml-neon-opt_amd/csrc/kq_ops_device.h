@@ -5,13 +5,15 @@
 //   * ggml_v_silu: x / (1 + v_expf(0 - x)) with a correctly rounded divide;
 //   * binary16 FMA / add (vfmaq_f16 / vaddq_f16) on the f16 ALU (v_fma_f16, v_add_f16:
 //     IEEE, one rounding, f16 denormals kept);
-//   * the RMS-norm sum of squares in a FIXED order shared by every kernel that
+//   * the RMS-norm sum of squares: a fast FIXED order shared by every kernel that
 //     computes it (kq_rms_norm and the kq_rows norm prologue): per 16 consecutive
 //     elements a sequential double sum, a balanced tree over the 16 groups of a
 //     256-element superblock, then superblocks in order. ggml sums sequentially in
 //     double (ggml_compute_forward_rms_norm_f32); the two orders can differ only in
 //     the last bits of the double, which reach the float mean only when it lies
-//     within ~2^-40 (relative) of a rounding boundary.
+//     within ~2^-40 (relative) of a rounding boundary — detected exactly
+//     (rms_mean_ambiguous), and then the sum is redone in ggml's sequential order,
+//     so the float mean is the reference's in every case.
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -168,6 +170,49 @@ __device__ __forceinline__ float wave_fmax(float v) {
 __device__ __forceinline__ double div_by_count(double sum, int64_t n) {
     if ((n & (n - 1)) == 0) return sum * (1.0 / (double)n);
     return sum / (double)n;
+}
+
+// ---------------------------------------------------------------- rms_norm exactness guard
+// The fast sum of squares above runs in a fixed tree order; ggml sums
+// (ggml_float)(x*x) sequentially (ggml_compute_forward_rms_norm_f32). Both are sums of
+// non-negative terms with one rounding per add, so each is within (n + 32) * 2^-53 * S
+// of the exact S (partial sums never exceed S), and after the correctly rounded
+// division by n the two doubles md_tree, md_seq differ by less than
+// delta = (2n + 64) * 2^-53 * md. The float mean (float)md can therefore differ only
+// when md_tree lies within delta of a float rounding midpoint (the ones next to
+// f = (float)md_tree: delta is ~2^-39 relative even at n = 8192, a float ulp 2^-23).
+// Then, and for inf/NaN, the caller recomputes the sum in ggml's sequential order:
+// the mean is bit-exact by construction, and the slow path runs for about one row in
+// 10^4-10^5 of random data (tests/test_gpu_ops.py builds inputs that take it).
+__device__ __forceinline__ bool rms_mean_ambiguous(double md, int64_t n) {
+    const float f = (float)md;
+    if (!(f >= 0.0f && f <= 3.402823466e+38f)) return true;  // a sum of squares: >= 0, else inf/NaN
+    const double delta = (double)(2 * n + 64) * 0x1p-53 * md;
+    const uint32_t fb = __float_as_uint(f);                  // neighbours of f >= 0 by its bits
+    const double fu = (double)__uint_as_float(fb + 1u);
+    const double fd = fb ? (double)__uint_as_float(fb - 1u) : -(double)__uint_as_float(1u);
+    const double mid_up = ((double)f + fu) * 0.5, mid_dn = ((double)f + fd) * 0.5;  // exact in double
+    return __builtin_fabs(md - mid_up) <= delta || __builtin_fabs(md - mid_dn) <= delta;
+}
+
+// ggml's order, one wave: sum += (ggml_float)(x[i] * x[i]) for i = 0 .. n-1. Lane l
+// squares x[c0 + l] (a float product, as in C), then the dependent double adds read
+// the lanes in order. Every lane of the wave returns the same sum.
+__device__ __forceinline__ double seq_sumsq_wave(const float *x, int64_t n, int lane) {
+    double tot = 0.0;
+    for (int64_t c0 = 0; c0 < n; c0 += 64) {
+        const float v = c0 + lane < n ? x[c0 + lane] : 0.0f;
+        const float p = v * v;
+        const double sq = (double)p;
+        const uint64_t b = __builtin_bit_cast(uint64_t, sq);
+        const int m = n - c0 < 64 ? (int)(n - c0) : 64;
+        for (int i = 0; i < m; ++i) {
+            const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)b, i);
+            const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(b >> 32), i);
+            tot += __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+        }
+    }
+    return tot;
 }
 
 // In-order double sum of n LDS doubles (p 16-B aligned): sum = ((0 + p[0]) + p[1]) + ...,

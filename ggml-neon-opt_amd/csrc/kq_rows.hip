@@ -169,7 +169,11 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
                 }
             }
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            const double tot = seq_sum_lanes(sums, nb, lane);  // superblocks in order
+            double tot = seq_sum_lanes(sums, nb, lane);  // superblocks in order
+            // workgroup-uniform (every wave sums the same LDS values): the rare rows whose
+            // float mean could depend on the order are summed in ggml's order (each wave)
+            if (rms_mean_ambiguous(div_by_count(tot, (int64_t)nb * QK), (int64_t)nb * QK))
+                tot = seq_sumsq_wave(a.x, (int64_t)nb * QK, lane);
             const float mean = (float)div_by_count(tot, (int64_t)nb * QK);
             const float scale = 1.0f / sqrtf(mean + a.eps);
 #pragma unroll

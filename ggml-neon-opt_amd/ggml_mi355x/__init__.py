@@ -152,7 +152,7 @@ def lib():
     L.mi355x_gemv_fused_ext.restype = i32
     L.mi355x_backend_set_fusion.argtypes = [vp, i32]
     L.mi355x_backend_set_fusion.restype = i32
-    L.mi355x_get_rows.argtypes = [i32, vp, i64, sz, vp, i64, vp, vp]
+    L.mi355x_get_rows.argtypes = [i32, vp, i64, sz, i64, vp, i64, vp, vp]
     L.mi355x_rms_norm.argtypes = [vp, vp, vp, i64, i64, f32, vp]
     L.mi355x_add.argtypes = [vp, vp, vp, i64, vp]
     L.mi355x_mul.argtypes = [vp, vp, vp, i64, vp]
@@ -347,8 +347,8 @@ def get_rows(type_, table, K, ids, out=None, stream=None):
     n = ids.numel()
     if out is None:
         out = torch.empty((n, K), dtype=torch.float32, device=ids.device)
-    _check(lib().mi355x_get_rows(type_, table.data_ptr(), K, table.stride(0) * table.element_size(), ids.data_ptr(),
-                                 n, out.data_ptr(), _stream(stream)), "mi355x_get_rows")
+    _check(lib().mi355x_get_rows(type_, table.data_ptr(), K, table.stride(0) * table.element_size(), table.shape[0],
+                                 ids.data_ptr(), n, out.data_ptr(), _stream(stream)), "mi355x_get_rows")
     return out
 
 

@@ -140,6 +140,8 @@ class LlamaDecoder:
         """Enqueue one token (no synchronization); returns the device logits tensor."""
         if not 0 <= pos < self.n_ctx:
             raise Mi355xError(f"position {pos} outside the KV cache (n_ctx {self.n_ctx})")
+        if not 0 <= token < self.hp["n_vocab"]:
+            raise Mi355xError(f"token {token} outside the vocabulary (n_vocab {self.hp['n_vocab']})")
         from . import lib
         if self._slot == self.HOST_SLOTS:
             self.b.synchronize()

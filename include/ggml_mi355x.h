@@ -242,9 +242,11 @@ int mi355x_gemv_impl(int impl);
 
 /* GGML_OP_GET_ROWS (ggml_compute_forward_get_rows_q -> dequantize_row_q4_K,
  * out.folded:103-104): dst[r][0..ne0) = row ids[r] of `table` as f32. type F32 /
- * Q4_K / Q6_K; rows of `row_stride` bytes; ids: device int32[n_ids]. */
-int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, const int32_t *ids,
-                    int64_t n_ids, float *dst, void *stream);
+ * Q4_K / Q6_K; `n_rows` rows (ne01) of `row_stride` bytes; ids: device int32[n_ids].
+ * An id outside [0, n_rows) (ggml: GGML_ASSERT(i01 >= 0 && i01 < ne01)) reads nothing
+ * and writes a NaN row. */
+int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, int64_t n_rows,
+                    const int32_t *ids, int64_t n_ids, float *dst, void *stream);
 /* GGML_OP_RMS_NORM (ggml_compute_forward_rms_norm_f32, out.folded:189-193) over
  * `nrows` rows of n floats, y = x * (1/sqrtf(mean(x^2) + eps)); when w != NULL the
  * following GGML_OP_MUL by the norm weight is fused: y = (x*scale) * w (two roundings,

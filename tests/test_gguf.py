@@ -126,6 +126,15 @@ def test_bad_tensor_infos_rejected(tmp_path, npo):
     pos_ne0 = blob.index(name) + len(name) + 4
     with pytest.raises(ValueError):
         G.GGUFFile(_patched(tmp_path, blob, pos_ne0, "<Q", 500))
+    # ne = {2^40, 2^40}: (ne0/256)*144*ne1 wraps past 64 bits -- a wrapped small size
+    # must not pass the end-of-file check (checked products)
+    assert len(t[2]) == 2
+    p2 = _patched(tmp_path, blob, pos_ne0, "<Q", 2 ** 40)
+    with pytest.raises(ValueError):
+        G.GGUFFile(_patched(tmp_path, p2.read_bytes(), pos_ne0 + 8, "<Q", 2 ** 40))
+    # an unknown ggml type (its size cannot be bounded)
+    with pytest.raises(ValueError):
+        G.GGUFFile(_patched(tmp_path, blob, pos - 4, "<I", 99))
 
 
 def test_missing_file():

@@ -250,3 +250,106 @@ def test_llama_fused_launch_count(dev):
     g.timing_enable(False)
     assert len(rows) == 5 * hp["n_layer"] + 2, [r[0] for r in rows]
     b.close()
+
+
+# ---------------------------------------------------------------- review fixes (r2)
+@pytest.mark.parametrize("n", [2048, 4096, 8192])
+def test_rms_norm_order_split_rows(dev, O, oracle, npo, n):
+    """Rows whose float mean differs between ggml's sequential double sum and the GPU's
+    fast tree order (tests/adversarial.py): kq_rms_norm and the kq_rows norm prologue
+    both detect the ambiguity and re-sum in ggml's order, so the bits are the oracle's."""
+    import torch
+    import ggml_mi355x as g
+    from tests.adversarial import order_split_rows
+    rows, ms, mt = order_split_rows(n, count=4, seed=n)
+    assert (ms != mt).all()
+    w = np.random.default_rng(n).uniform(0.5, 1.5, n).astype(np.float32)
+    got = g.rms_norm(t(rows, dev), 1e-5).cpu().numpy()
+    ref = O.rms_norm(rows, 1e-5)
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+    got = g.rms_norm(t(rows, dev), 1e-5, w=t(w, dev)).cpu().numpy()
+    ref = np.stack([O.mul(O.rms_norm(r, 1e-5), w) for r in rows])
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+    # the fused prologue: the normalized row goes straight into the Q8_K quantizer
+    rng = np.random.default_rng(n + 1)
+    wq = npo.random_blocks(rng, 12, 512, n)
+    for r in rows:
+        y = torch.empty(512, device=dev)
+        g.gemv_fused_ext([(12, t(wq, dev), y)], t(r, dev), prologue=g.PRO_RMS_NORM, x2=t(w, dev), eps=1e-5)
+        torch.cuda.synchronize()
+        refy = oracle.mul_mat(12, wq, O.mul(O.rms_norm(r, 1e-5), w))[0]
+        assert bits_equal(y.cpu().numpy(), refy), first_mismatch(y.cpu().numpy(), refy)
+
+
+def test_get_rows_out_of_range_id(dev, npo):
+    """An id outside [0, n_rows) reads nothing and yields a NaN row (ggml asserts)."""
+    import ggml_mi355x as g
+    rng = np.random.default_rng(1)
+    K, R = 512, 10
+    table = npo.random_blocks(rng, 12, R, K)
+    ids = np.array([0, R, -1, 3, 1 << 30], np.int32)
+    got = g.get_rows(12, t(table, dev), K, t(ids, dev)).cpu().numpy()
+    assert np.isfinite(got[[0, 3]]).all()
+    assert np.isnan(got[[1, 2, 4]]).all()
+
+
+def _gemv_graph(be, K, N, rng, npo):
+    """Helper: device buffers for a 1-column MUL_MAT graph."""
+    import ggml_mi355x as g
+    w = npo.random_blocks(rng, 12, N, K)
+    p = be.alloc(w.nbytes)
+    be.set_tensor(p, w)
+    return w, g.make_tensor(12, K, N, p)
+
+
+@pytest.mark.parametrize("view_offset", [0, 64])
+def test_fusion_respects_reused_buffers_and_views(dev, O, oracle, npo, view_offset):
+    """ggml-alloc reuses a dead node's buffer: node 2's MUL_MAT output lands in the buffer
+    node 0 wrote, and node 4 reads it through a separate view (at offset 0 or 64 floats).
+    The MUL_MAT -> ADD epilogue fusion may not elide the MUL_MAT output then
+    (readers are credited to the LATEST overlapping writer)."""
+    import ggml_mi355x as g
+    K, N = 1024, 512
+    rng = np.random.default_rng(view_offset)
+    be = g.Backend()
+    w, wt = _gemv_graph(be, K, N, rng, npo)
+    x = rng.standard_normal(K).astype(np.float32)
+    w0 = rng.uniform(0.5, 1.5, K).astype(np.float32)
+    res = rng.standard_normal(N).astype(np.float32)
+    res2 = rng.standard_normal(N).astype(np.float32)
+    keep = []
+
+    def buf(a=None, n=None):
+        n = a.size if a is not None else n
+        p = be.alloc(n * 4)
+        if a is not None:
+            be.set_tensor(p, a)
+        return p
+
+    P = buf(n=max(K, N))  # shared by node 0 (dead after node 1) and node 2
+    xt = g.make_tensor(g.TYPE_F32, K, 1, buf(x))
+    w0t = g.make_tensor(g.TYPE_F32, K, 1, buf(w0))
+    n0 = g.make_tensor(g.TYPE_F32, K, 1, P, op=g.OP_MUL, src0=xt, src1=w0t)
+    n1 = g.make_tensor(g.TYPE_F32, K, 1, buf(n=K), op=g.OP_ADD, src0=n0, src1=xt)
+    n2 = g.make_tensor(g.TYPE_F32, N, 1, P, op=g.OP_MUL_MAT, src0=wt, src1=n1)
+    rt = g.make_tensor(g.TYPE_F32, N, 1, buf(res))
+    n3 = g.make_tensor(g.TYPE_F32, N, 1, buf(n=N), op=g.OP_ADD, src0=n2, src1=rt)
+    nv = N - view_offset
+    view = g.make_tensor(g.TYPE_F32, nv, 1, P + 4 * view_offset)  # a view of n2's output (op NONE)
+    r2t = g.make_tensor(g.TYPE_F32, nv, 1, buf(res2[view_offset:].copy()))
+    n4 = g.make_tensor(g.TYPE_F32, nv, 1, buf(n=nv), op=g.OP_ADD, src0=view, src1=r2t)
+    keep += [xt, w0t, view, rt, r2t, wt]
+    nodes = [n0, n1, n2, n3, n4]
+    for use_graph in (0, 1):
+        assert be.graph_compute(nodes, use_graph=use_graph) == 0
+        be.synchronize()
+        mm = oracle.mul_mat(12, w, O.add(O.mul(x, w0), x))[0]
+        h3 = np.zeros(N, np.float32)
+        h4 = np.zeros(nv, np.float32)
+        be.get_tensor(h3, n3.data)
+        be.get_tensor(h4, n4.data)
+        be.synchronize()
+        assert bits_equal(h3, O.add(mm, res))
+        assert bits_equal(h4, O.add(mm[view_offset:], res2[view_offset:])), first_mismatch(
+            h4, O.add(mm[view_offset:], res2[view_offset:]))
+    be.close()

@@ -175,3 +175,34 @@ def test_supports_decode_ops():
     rope = g.make_tensor(g.TYPE_F32, hd, nh, 0xc000, op=g.OP_ROPE, srcs=[g.make_tensor(g.TYPE_F32, hd, nh, 0x9000),
                                                                          ids, tab], op_params=[hd])
     assert g.supports_op(rope)
+    # layout the kernels assume: an unaligned or strided RMS_NORM source, a
+    # strided GET_ROWS destination and a padded KV cache are declined up front
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, E, 1, 0x3000, op=g.OP_RMS_NORM,
+                                           src0=g.make_tensor(g.TYPE_F32, E, 1, 0x1004)))
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, E, 2, 0x3000, op=g.OP_RMS_NORM,
+                                           src0=g.make_tensor(g.TYPE_F32, E, 2, 0x1000, row_stride=E * 4 + 64)))
+    ids2 = g.make_tensor(g.TYPE_I32, 2, 1, 0x5000)
+    assert g.supports_op(g.make_tensor(g.TYPE_F32, E, 2, 0x3000, op=g.OP_GET_ROWS, src0=emb, src1=ids2))
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, E, 2, 0x3000, row_stride=E * 4 + 16, op=g.OP_GET_ROWS,
+                                           src0=emb, src1=ids2))
+    kc_pad = g.make_tensor(g.TYPE_F16, nkv * hd, n_ctx, 0x7000, row_stride=nkv * hd * 2 + 32)
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, nh * hd, 1, 0xb000, op=g.OP_ATTN_DECODE,
+                                           srcs=[q, kv, kv, ids, kc_pad, vc, tab], op_params=[nh, nkv, hd, 0]))
+    kc_mis = g.make_tensor(g.TYPE_F16, nkv * hd, n_ctx, 0x7008)
+    assert not g.supports_op(g.make_tensor(g.TYPE_F32, nh * hd, 1, 0xb000, op=g.OP_ATTN_DECODE,
+                                           srcs=[q, kv, kv, ids, kc_mis, vc, tab], op_params=[nh, nkv, hd, 0]))
+
+
+@pytest.mark.parametrize("n", [1024, 2048, 4096, 8192])
+def test_rms_norm_order_split_inputs(O, n):
+    """The adversarial rows really separate the orders: the oracle (ggml's sequential
+    double sum) gives the sequential mean, and the GPU's fast tree order would round the
+    float mean the other way (tests/adversarial.py). The GPU tests feed these rows."""
+    from tests.adversarial import order_split_rows
+    rows, ms, mt = order_split_rows(n)
+    assert (ms != mt).all()
+    eps = np.float32(1e-5)
+    for r, m in zip(rows, ms):
+        y = O.rms_norm(r, float(eps))
+        scale = np.float32(1.0) / np.sqrt(np.float32(m + eps))
+        assert (y.view(np.uint32) == (r * scale).astype(np.float32).view(np.uint32)).all()
