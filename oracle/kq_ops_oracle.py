@@ -157,13 +157,15 @@ def attn_decode(q, k, v, k_cache, v_cache, pos, n_head, n_head_kv, head_dim, sca
 
 
 # ------------------------------------------------------------ one decode token
-def decode_token(model, token, pos, cache, n_threads=8):
+def decode_token(model, token, pos, cache, n_threads=8, variant="neon"):
     """The llama graph for one token (llm_build_llama, non-flash attention), ggml-cpu
     semantics op by op: get_rows -> [rms_norm*attn_norm -> q/k/v mul_mat -> rope ->
     attention -> wo mul_mat -> add -> rms_norm*ffn_norm -> gate/up mul_mat -> swiglu ->
     down mul_mat -> add] x n_layer -> rms_norm*output_norm -> output mul_mat.
     `model`: dict as built by tests/llama_model.py; `cache`: list of (k_cache, v_cache)
-    per layer, updated in place. Returns (logits, per-layer residual outputs)."""
+    per layer, updated in place. `variant`: the vec_dot form of the matmuls ("neon"
+    scalar, or "simd": AVX2 integer parts, bit-identical). Returns (logits,
+    per-layer residual outputs)."""
     hp = model["hp"]
     E, hd = hp["n_embd"], hp["head_dim"]
     eps = hp["eps"]
@@ -175,22 +177,22 @@ def decode_token(model, token, pos, cache, n_threads=8):
     for li, L in enumerate(model["layers"]):
         inp = x
         cur = mul(rms_norm(x, eps), L["attn_norm"])
-        q = KO.mul_mat(L["wq"][0], L["wq"][1], cur, n_threads)[0]
-        k = KO.mul_mat(L["wk"][0], L["wk"][1], cur, n_threads)[0]
-        v = KO.mul_mat(L["wv"][0], L["wv"][1], cur, n_threads)[0]
+        q = KO.mul_mat(L["wq"][0], L["wq"][1], cur, n_threads, variant)[0]
+        k = KO.mul_mat(L["wk"][0], L["wk"][1], cur, n_threads, variant)[0]
+        v = KO.mul_mat(L["wv"][0], L["wv"][1], cur, n_threads, variant)[0]
         q = rope(q, hd, hd, pos, table)
         k = rope(k, hd, hd, pos, table)
         kc, vc = cache[li]
         att = attn_decode(q, k, v, kc, vc, pos, hp["n_head"], hp["n_head_kv"], hd, float(scale))
-        cur = KO.mul_mat(L["wo"][0], L["wo"][1], att, n_threads)[0]
+        cur = KO.mul_mat(L["wo"][0], L["wo"][1], att, n_threads, variant)[0]
         ffn_inp = add(cur, inp)
         cur = mul(rms_norm(ffn_inp, eps), L["ffn_norm"])
-        g = KO.mul_mat(L["w_gate"][0], L["w_gate"][1], cur, n_threads)[0]
-        u = KO.mul_mat(L["w_up"][0], L["w_up"][1], cur, n_threads)[0]
+        g = KO.mul_mat(L["w_gate"][0], L["w_gate"][1], cur, n_threads, variant)[0]
+        u = KO.mul_mat(L["w_up"][0], L["w_up"][1], cur, n_threads, variant)[0]
         cur = swiglu(g, u)
-        cur = KO.mul_mat(L["w_down"][0], L["w_down"][1], cur, n_threads)[0]
+        cur = KO.mul_mat(L["w_down"][0], L["w_down"][1], cur, n_threads, variant)[0]
         x = add(cur, ffn_inp)
         trace.append(x)
     cur = mul(rms_norm(x, eps), model["output_norm"])
-    logits = KO.mul_mat(model["output"][0], model["output"][1], cur, n_threads)[0]
+    logits = KO.mul_mat(model["output"][0], model["output"][1], cur, n_threads, variant)[0]
     return logits, trace

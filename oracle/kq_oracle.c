@@ -31,6 +31,7 @@
 
 #include <math.h>
 #include <pthread.h>
+#include <sched.h>
 #include <stdatomic.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -518,7 +519,15 @@ static size_t type_size(int type) {
          : type == 14 ? sizeof(kqo_block_q6_K) : 0;
 }
 
+/* variant: 0 = NEON order (scalar), 1 = generic, 2 = NEON order with AVX2 integer
+ * parts (kq_cpu_simd.c; bit-identical to 0). */
 static vec_dot_fn pick_vec_dot(int type, int variant) {
+    if (variant == 2) {
+        if (type == 12) return kqo_vec_dot_q4_K_q8_K_simd;
+        if (type == 13) return kqo_vec_dot_q5_K_q8_K_simd;
+        if (type == 14) return kqo_vec_dot_q6_K_q8_K_simd;
+        return NULL;
+    }
     if (type == 12) return variant ? kqo_vec_dot_q4_K_q8_K_generic : kqo_vec_dot_q4_K_q8_K_neon;
     if (type == 13) return kqo_vec_dot_q5_K_q8_K_neon;
     if (type == 14) return variant ? kqo_vec_dot_q6_K_q8_K_generic : kqo_vec_dot_q6_K_q8_K_neon;
@@ -531,7 +540,7 @@ typedef struct {
     kqo_block_q8_K *wdata; int quantize;
     float *dst; vec_dot_fn vec_dot;
     int nth; atomic_int current_chunk;
-    pthread_barrier_t barrier;
+    atomic_int arrived; /* ggml_barrier: threads past the quantization */
 } mm_plan;
 
 typedef struct { mm_plan *p; int ith; } mm_arg;
@@ -572,7 +581,11 @@ static void *mm_thread(void *arg) {
         }
     }
     if (ith == 0) atomic_store(&p->current_chunk, nth);
-    pthread_barrier_wait(&p->barrier);
+    /* ggml_barrier (spin): every src1 slice quantized before any chunk runs */
+    atomic_fetch_add(&p->arrived, 1);
+    for (int spins = 0; atomic_load(&p->arrived) < nth;)
+        if (++spins < (1 << 16)) __builtin_ia32_pause();
+        else sched_yield(); /* oversubscribed host: let the straggler run */
 
     const int64_t nr0 = p->N, nr1 = p->M;
     int64_t chunk_size = (nr0 == 1 || nr1 == 1) ? 64 : 16;
@@ -596,23 +609,71 @@ static void *mm_thread(void *arg) {
     return NULL;
 }
 
+/* Persistent worker pool, as ggml's threadpool: workers are created once per
+ * thread count and spin (then yield) on a generation counter between graph nodes,
+ * so a mul_mat call costs no thread creation. The caller is ith 0. */
+static struct {
+    int nth;
+    pthread_t th[256];
+    mm_arg args[256];
+    atomic_int gen, done, quit;
+    mm_plan *volatile plan;
+} g_pool;
+static pthread_mutex_t g_pool_mu = PTHREAD_MUTEX_INITIALIZER;
+
+static void *pool_worker(void *arg) {
+    mm_arg *a = (mm_arg *)arg;
+    int seen = 0;
+    for (;;) {
+        int spins = 0, g;
+        while ((g = atomic_load(&g_pool.gen)) == seen && !atomic_load(&g_pool.quit)) {
+            if (++spins < 20000) __builtin_ia32_pause();
+            else sched_yield();
+        }
+        if (atomic_load(&g_pool.quit)) return NULL;
+        seen = g;
+        a->p = g_pool.plan;
+        mm_thread(a);
+        atomic_fetch_add(&g_pool.done, 1);
+    }
+}
+
+static void pool_resize(int nth) {
+    if (g_pool.nth == nth) return;
+    if (g_pool.nth > 1) {
+        atomic_store(&g_pool.quit, 1);
+        for (int t = 1; t < g_pool.nth; ++t) pthread_join(g_pool.th[t], NULL);
+    }
+    atomic_store(&g_pool.quit, 0);
+    atomic_store(&g_pool.gen, 0);
+    g_pool.nth = nth;
+    for (int t = 1; t < nth; ++t) {
+        g_pool.args[t].ith = t;
+        pthread_create(&g_pool.th[t], NULL, pool_worker, &g_pool.args[t]);
+    }
+}
+
 static int mm_run(mm_plan *p, int n_threads) {
     if (n_threads < 1) n_threads = 1;
+    if (n_threads > 256) n_threads = 256;
     p->nth = n_threads;
     atomic_init(&p->current_chunk, 0);
-    pthread_barrier_init(&p->barrier, NULL, (unsigned)n_threads);
-    pthread_t *th = (pthread_t *)calloc((size_t)n_threads, sizeof(pthread_t));
-    mm_arg *args = (mm_arg *)calloc((size_t)n_threads, sizeof(mm_arg));
-    for (int t = 0; t < n_threads; ++t) {
-        args[t].p = p;
-        args[t].ith = t;
-        if (t > 0) pthread_create(&th[t], NULL, mm_thread, &args[t]);
+    atomic_init(&p->arrived, 0);
+    mm_arg a0 = {p, 0};
+    if (n_threads == 1) {
+        mm_thread(&a0);
+        return 0;
     }
-    mm_thread(&args[0]); /* main thread is ith 0, as in ggml_graph_compute */
-    for (int t = 1; t < n_threads; ++t) pthread_join(th[t], NULL);
-    pthread_barrier_destroy(&p->barrier);
-    free(th);
-    free(args);
+    pthread_mutex_lock(&g_pool_mu); /* one graph node at a time per process */
+    pool_resize(n_threads);
+    g_pool.plan = p;
+    atomic_store(&g_pool.done, 0);
+    atomic_fetch_add(&g_pool.gen, 1);
+    mm_thread(&a0); /* main thread is ith 0, as in ggml_graph_compute */
+    for (int spins = 0; atomic_load(&g_pool.done) < n_threads - 1;)
+        if (++spins < (1 << 16)) __builtin_ia32_pause();
+        else sched_yield();
+    pthread_mutex_unlock(&g_pool_mu);
     return 0;
 }
 

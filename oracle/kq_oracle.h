@@ -57,6 +57,14 @@ void kqo_vec_dot_q6_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size
 void kqo_vec_dot_q6_K_q8_K_generic(int n, float *s, size_t bs, const void *vx, size_t bx,
                                    const void *vy, size_t by, int nrc);
 
+/* AVX2 forms (kq_cpu_simd.c): same integers, same fp32 chain -> bit-identical. */
+void kqo_vec_dot_q4_K_q8_K_simd(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                const void *vy, size_t by, int nrc);
+void kqo_vec_dot_q5_K_q8_K_simd(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                const void *vy, size_t by, int nrc);
+void kqo_vec_dot_q6_K_q8_K_simd(int n, float *s, size_t bs, const void *vx, size_t bx,
+                                const void *vy, size_t by, int nrc);
+
 /* Per-superblock integer partials (sumi, summins) of row . col, out[2*b+{0,1}].
  * Q6_K: (isum with unsigned 0..63 quants, isum_mins = sum bsums_g*sc_g). */
 void kqo_block_partials(int type, int n, const void *vx, const void *vy, int32_t *out);
@@ -65,7 +73,8 @@ void kqo_block_partials(int type, int n, const void *vx, const void *vy, int32_t
  * src1 f32: quantize src1 (per-thread slices), barrier, 64/16-row chunks handed
  * out by an atomic counter, one_chunk 16x16 blocking calling vec_dot per
  * (row, col). pthreads, n_threads >= 1. dst[j*N + i] (dst column j contiguous).
- * variant: 0 = NEON-order dot, 1 = generic dot. Returns 0 on success. */
+ * variant: 0 = NEON-order dot, 1 = generic dot, 2 = NEON order with AVX2 integer
+ * parts (bit-identical to 0). Worker threads persist between calls. Returns 0 on success. */
 int kqo_mul_mat(int type, const void *src0, int64_t K, int64_t N, size_t nb01,
                 const float *src1, int64_t M, size_t nb11, float *dst,
                 int n_threads, int variant);

@@ -17,6 +17,7 @@ Q4_K, Q5_K, Q6_K, Q8_K = 12, 13, 14, 15
 BLOCK_BYTES = {Q4_K: 144, Q5_K: 176, Q6_K: 210, Q8_K: 292}
 
 _lib = None
+VARIANTS = {"neon": 0, "generic": 1, "simd": 2}  # simd: AVX2 integer parts, bit-identical to neon
 
 
 def build():
@@ -32,7 +33,8 @@ def lib():
         vp, sz, i64, i32 = ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int64, ctypes.c_int
         L.kqo_quantize_row_q8_K.argtypes = [vp, vp, i64, i32]
         for name in ("kqo_vec_dot_q4_K_q8_K_neon", "kqo_vec_dot_q4_K_q8_K_generic", "kqo_vec_dot_q5_K_q8_K_neon",
-                     "kqo_vec_dot_q6_K_q8_K_neon", "kqo_vec_dot_q6_K_q8_K_generic"):
+                     "kqo_vec_dot_q6_K_q8_K_neon", "kqo_vec_dot_q6_K_q8_K_generic", "kqo_vec_dot_q4_K_q8_K_simd",
+                     "kqo_vec_dot_q5_K_q8_K_simd", "kqo_vec_dot_q6_K_q8_K_simd"):
             getattr(L, name).argtypes = [i32, vp, sz, vp, sz, vp, sz, i32]
         L.kqo_block_partials.argtypes = [i32, i32, vp, vp, vp]
         L.kqo_mul_mat.argtypes = [i32, vp, i64, i64, sz, vp, i64, sz, vp, i32, i32]
@@ -72,7 +74,8 @@ def vec_dot(type_, w_row, q8_row, K, variant="neon"):
     s = np.zeros(1, np.float32)
     name = {(Q4_K, "neon"): "kqo_vec_dot_q4_K_q8_K_neon", (Q4_K, "generic"): "kqo_vec_dot_q4_K_q8_K_generic",
             (Q5_K, "neon"): "kqo_vec_dot_q5_K_q8_K_neon", (Q6_K, "neon"): "kqo_vec_dot_q6_K_q8_K_neon",
-            (Q6_K, "generic"): "kqo_vec_dot_q6_K_q8_K_generic"}[(type_, variant)]
+            (Q6_K, "generic"): "kqo_vec_dot_q6_K_q8_K_generic", (Q4_K, "simd"): "kqo_vec_dot_q4_K_q8_K_simd",
+            (Q5_K, "simd"): "kqo_vec_dot_q5_K_q8_K_simd", (Q6_K, "simd"): "kqo_vec_dot_q6_K_q8_K_simd"}[(type_, variant)]
     getattr(lib(), name)(K, _p(s), 0, _p(w_row), 0, _p(q8_row), 0, 1)
     return s[0]
 
@@ -99,7 +102,7 @@ def mul_mat(type_, w, x, n_threads=1, variant="neon"):
     N = w.shape[0]
     out = np.zeros((M, N), np.float32)
     rc = lib().kqo_mul_mat(type_, _p(w), K, N, w.shape[1] if N else 0, _p(x), M, K * 4, _p(out), n_threads,
-                           0 if variant == "neon" else 1)
+                           VARIANTS[variant])
     assert rc == 0
     return out
 
@@ -113,7 +116,7 @@ def mul_mat_q8(type_, w, q8, K, n_threads=1, variant="neon"):
     N = w.shape[0]
     out = np.zeros((M, N), np.float32)
     rc = lib().kqo_mul_mat_q8(type_, _p(w), K, N, w.shape[1] if N else 0, _p(q8), M, _p(out), n_threads,
-                              0 if variant == "neon" else 1)
+                              VARIANTS[variant])
     assert rc == 0
     return out
 

@@ -130,3 +130,40 @@ def test_fp16_roundtrip(oracle):
         f = L.kqo_fp16_to_fp32(h)
         assert np.float32(f) == np.uint16(h).view(np.float16).astype(np.float32)
         assert L.kqo_fp32_to_fp16(f) == h
+
+
+@pytest.mark.parametrize("type_", TYPES)
+def test_simd_vec_dot_matches_scalar(oracle, npo, type_):
+    """The AVX2 vec_dot of the CPU baseline (oracle/kq_cpu_simd.c) is bit-identical to
+    the scalar NEON-order restatement: exact integer parts, the same fp32 chain —
+    including extreme blocks (max scales, nibble 15, q8 +-127, fp16 subnormal d)."""
+    rng = np.random.default_rng(21 + type_)
+    K = 4096
+    w = npo.random_blocks(rng, type_, 96, K)
+    w[:8] = 0xFF                                   # every quant / scale bit set
+    w[8:16, :] = rng.integers(0, 256, w[8:16].shape, dtype=np.uint8)  # any bytes, d/dmin included
+    x = rng.standard_normal((3, K)).astype(np.float32)
+    x[1, :256] = 0.0                               # all-zero activation block
+    x[2, ::7] *= 1e4                               # saturating outliers
+    a = oracle.mul_mat(type_, w, x, n_threads=1, variant="neon")
+    for nt in (1, 5):
+        b = oracle.mul_mat(type_, w, x, n_threads=nt, variant="simd")
+        same = (a.view(np.uint32) == b.view(np.uint32)) | (np.isnan(a) & np.isnan(b))
+        assert same.all()
+    q8 = oracle.quantize_q8_K(x[:1])[0]
+    for r in range(0, 96, 11):
+        assert np.float32(oracle.vec_dot(type_, w[r], q8, K, "simd")).view(np.uint32) == \
+            np.float32(oracle.vec_dot(type_, w[r], q8, K, "neon")).view(np.uint32) or \
+            np.isnan(oracle.vec_dot(type_, w[r], q8, K, "neon"))
+
+
+def test_thread_pool_reuse_and_resize(oracle, npo):
+    """The persistent worker pool gives the same bits across calls and thread counts."""
+    rng = np.random.default_rng(31)
+    K, N = 2048, 257
+    w = npo.random_blocks(rng, 12, N, K)
+    x = rng.standard_normal((2, K)).astype(np.float32)
+    ref = oracle.mul_mat(12, w, x, n_threads=1)
+    for nt in (4, 4, 7, 2, 7):
+        got = oracle.mul_mat(12, w, x, n_threads=nt, variant="simd")
+        assert (got.view(np.uint32) == ref.view(np.uint32)).all()
