@@ -62,6 +62,7 @@ MODELS = {
     "llama-3-70b": dict(E=8192, L=80, KV=1024, FF=28672, V=128256),
 }
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+I8_PEAK_TOPS = 5000.0  # dense int8 MFMA peak (2x the 2.5 PFLOP/s dense bf16; no sparsity)
 
 
 def use_more_bits(i, n):
@@ -143,7 +144,7 @@ def random_kquant(type_, N, K, gen, dev, rms_keep=False):
 class Chain:
     """Weights, inputs and ggml-style MUL_MAT nodes for one rank's token chain."""
 
-    def __init__(self, model, dev, seed, row_shard=None, gguf=None):
+    def __init__(self, model, dev, seed, gguf=None):
         self.model = model
         self.gguf = gguf
         if gguf is not None:  # real weights: a GGUFFile (ggml_mi355x.gguf)
@@ -155,10 +156,8 @@ class Chain:
         gen.manual_seed(seed)
         self.w, self.x, self.y, self.nodes, self.keep = [], [], [], [], []
         self.bytes_per_token = 0
-        self.row_shard = row_shard
-        # one decode stream: stage s+1 reads stage s's first output (row-split shards
-        # keep per-stage inputs: their exchange is the collective, see rowsplit.py)
-        self.dependent = row_shard is None
+        # one decode stream: stage s+1 reads stage s's first output
+        self.dependent = True
         for si, stage in enumerate(self.stages):
             K = stage[0][2]
             if self.dependent and si > 0:
@@ -171,7 +170,7 @@ class Chain:
             self.keep.append(xt)
             ws, ys = [], []
             for name, typ, K_, N in stage:
-                r0, r1 = (0, N) if row_shard is None else row_shard(N)
+                r0, r1 = 0, N
                 if gguf is not None:
                     tname = name + ".weight" if name + ".weight" in gguf.tensors else "token_embd.weight"
                     w = gguf.to_device(tname, dev)[r0:r1].contiguous()
@@ -204,20 +203,23 @@ class Token:
     gate/up, swiglu, down, add], rms_norm, output) on synthetic Q4_K_M weights of the
     real shapes (the chain's weights and type mix, plus token_embd Q4_K and f32 norms)."""
 
-    def __init__(self, model, dev, seed, be, n_ctx):
+    def __init__(self, model, dev, seed, be, n_ctx, split=None):
         from ggml_mi355x.llama import LlamaDecoder, hparams
+        from ggml_mi355x.rowsplit import TokenSplit
         m = MODELS[model]
         h = HPARAMS[model]
         self.hp = hparams(m["E"], m["L"], h["n_head"], h["n_head_kv"], m["FF"], m["V"], freq_base=h["freq_base"])
         self.model = model
+        self.split = TokenSplit(self.hp, *split) if split is not None else None  # (world, rank)
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed)
         self.stages = q4km_chain(model)
         w = {}
-        self.bytes_per_token = 0
+        self.bytes_per_token = 0  # this GPU's matmul weight bytes per token (its row slices)
         for stage in self.stages:
             for name, typ, K, N in stage:
-                w[name] = (typ, random_kquant(typ, N, K, gen, dev, rms_keep=True))
+                r0, r1 = self.split.rows_of(name) if self.split is not None else (0, N)
+                w[name] = (typ, random_kquant(typ, r1 - r0, K, gen, dev, rms_keep=True))
                 self.bytes_per_token += w[name][1].numel()
         w["token_embd"] = (g.TYPE_Q4_K, random_kquant(g.TYPE_Q4_K, m["V"], m["E"], gen, dev))
         w["output_norm"] = torch.rand(m["E"], device=dev, generator=gen) * 0.4 + 0.8
@@ -227,12 +229,13 @@ class Token:
         self.w = w
         self.wl = [[w[name] for name, _, _, _ in stage] for stage in self.stages]  # per stage, as Chain.w
         self.n_ctx = n_ctx
-        self.dec = LlamaDecoder(be, self.hp, w, n_ctx)
-        rng = np.random.default_rng(seed)
+        self.dec = LlamaDecoder(be, self.hp, w, n_ctx, split=self.split)
+        rng = np.random.default_rng(0x51A7)  # the same token stream on every rank
         self.tokens = rng.integers(0, m["V"], size=n_ctx).tolist()
 
     def launches(self):
-        return 5 * self.hp["n_layer"] + 2
+        n = 5 * self.hp["n_layer"] + 2
+        return n + (4 * self.hp["n_layer"] + 1 if self.split is not None else 0)
 
 
 def timed_kernel_stats(be, chain, tokens):
@@ -388,17 +391,36 @@ def model_side(model, dev, steps=64, warmup=8):
     return out
 
 
+def host_cpu():
+    """Host CPU model, logical CPUs of the machine and of this process's affinity."""
+    model = "unknown"
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    model = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    try:
+        aff = len(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = os.cpu_count() or 1
+    return model, os.cpu_count() or 1, aff
+
+
 def cpu_baseline_token(tk, seconds):
     """The oracle's restated llm_build_llama token (ggml-cpu semantics op by op: the
-    matmuls through the restated ggml_compute_forward_mul_mat with pthreads, the other
-    ops scalar) on the same weights, positions 0, 1, 2, ... of a fresh KV cache, timed
-    on this host's cores for a bounded number of tokens."""
+    matmuls through the restated ggml_compute_forward_mul_mat — quantize_row_q8_K_ref,
+    a persistent worker pool with 64-row chunks, the NEON-order vec_dot with AVX2
+    integer parts (bit-identical to the scalar restatement); f16 attention, soft_max,
+    rope, rms_norm, swiglu) on the same weights, tokens 0, 1, 2 ... from an empty cache.
+    Two legs as llama-bench runs them: -t 1 (BASELINE config 1) and -t N with N the
+    host threads available to this process (at most 16, the box's CPU share); each
+    leg gets about half of `seconds` after an untimed warm-up token."""
     from oracle import kq_ops_oracle as OO
-    try:
-        ncores = len(os.sched_getaffinity(0))
-    except AttributeError:
-        ncores = os.cpu_count() or 1
-    threads = max(1, min(16, ncores))
+    model_name, ncpu, aff = host_cpu()
+    threads_n = max(1, min(16, aff))
     hp = tk.hp
     host = {k: ((v[0], v[1].cpu().numpy()) if isinstance(v, tuple) else v.cpu().numpy()) for k, v in tk.w.items()}
     layers = []
@@ -411,21 +433,39 @@ def cpu_baseline_token(tk, seconds):
     model = {"hp": hp, "tok_embd": host["token_embd"], "output": host["output"], "output_norm": host["output_norm"],
              "layers": layers, "rope_table": OO.rope_table(tk.n_ctx, hp["head_dim"], hp["freq_base"])}
     kvw = hp["n_head_kv"] * hp["head_dim"]
-    cache = [(np.zeros((tk.n_ctx, kvw), np.uint16), np.zeros((kvw, tk.n_ctx), np.uint16))
-             for _ in range(hp["n_layer"])]
     OO.lib()
-    tokens, t0 = 0, time.perf_counter()
-    while True:
-        OO.decode_token(model, tk.tokens[tokens], tokens, cache, n_threads=threads)
-        tokens += 1
-        el = time.perf_counter() - t0
-        if el >= seconds or tokens >= 50 or tokens >= tk.n_ctx:
-            break
-    return {"value": tokens / el, "unit": "tok/s", "cores": threads, "kind": "port",
-            "sample": f"{tokens} token(s) (positions 0..{tokens - 1}) of the full {tk.model} Q4_K_M decode graph "
-                      f"through the oracle's restated llm_build_llama / ggml-cpu ops (mul_mat: "
-                      f"quantize_row_q8_K_ref + NEON-order vec_dot, {threads} pthreads; f16 attention, "
-                      f"soft_max, rope, rms_norm, swiglu scalar), {el:.1f} s"}
+
+    def leg(threads, budget):
+        cache = [(np.zeros((tk.n_ctx, kvw), np.uint16), np.zeros((kvw, tk.n_ctx), np.uint16))
+                 for _ in range(hp["n_layer"])]
+        t0 = time.perf_counter()  # warm-up: workers started, host threads at speed
+        while True:
+            OO.decode_token(model, tk.tokens[0], 0, cache, n_threads=threads, variant="simd")
+            if time.perf_counter() - t0 >= min(1.5, budget / 4):
+                break
+        for c in cache:
+            c[0][:] = 0
+            c[1][:] = 0
+        tokens, t0 = 0, time.perf_counter()
+        while True:
+            OO.decode_token(model, tk.tokens[tokens], tokens, cache, n_threads=threads, variant="simd")
+            tokens += 1
+            el = time.perf_counter() - t0
+            if el >= budget or tokens >= 128 or tokens >= tk.n_ctx:
+                break
+        return tokens, el
+
+    n1, e1 = leg(1, seconds / 2)
+    nn, en = leg(threads_n, seconds / 2)
+    return {"value": round(nn / en, 3), "unit": "tok/s", "cores": threads_n, "kind": "port",
+            "legs": {"t1": {"tok_s": round(n1 / e1, 3), "tokens": n1, "seconds": round(e1, 2)},
+                     f"t{threads_n}": {"tok_s": round(nn / en, 3), "tokens": nn, "seconds": round(en, 2)}},
+            "host_cpu": model_name, "host_logical_cpus": ncpu, "affinity_cpus": aff,
+            "sample": f"tokens 0..n-1 from an empty KV cache of the full {tk.model} Q4_K_M decode graph through "
+                      f"the oracle's restated llm_build_llama / ggml-cpu ops (mul_mat: quantize_row_q8_K_ref + "
+                      f"NEON-order vec_dot with AVX2 integer parts, bit-identical to the scalar restatement, "
+                      f"persistent pool); legs -t 1 ({n1} tokens, {e1:.1f} s) and -t {threads_n} ({nn} tokens, "
+                      f"{en:.1f} s); value is the -t {threads_n} leg"}
 
 
 def cpu_baseline(chain, seconds):
@@ -459,13 +499,57 @@ def cpu_baseline(chain, seconds):
                       f"{threads} pthreads), {el:.1f} s"}
 
 
+def spawn_ranks(n):
+    """`bench.py --gpus N` outside a launcher: start N rank processes (fresh
+    interpreters, before this process touches a GPU) with the torch.distributed.run
+    environment, wait for all of them and exit with the worst status."""
+    import socket
+    import subprocess
+    sock = socket.socket()
+    sock.bind(("127.0.0.1", 0))
+    port = sock.getsockname()[1]
+    sock.close()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
+    rcs = [p.wait() for p in procs]
+    bad = [rc for rc in rcs if rc != 0]
+    sys.exit(bad[0] if bad else 0)
+
+
+def tg_side(tk, steps, barrier):
+    """llama-bench's tg128 on the same decoder: `steps` tokens from an empty KV cache
+    (positions 0 .. steps-1), hipGraph replay, whatever --steps the headline used.
+    Every rank runs it (the row split's gathers are collective)."""
+    tk.dec.reset()
+    torch.cuda.synchronize()
+    st = torch.cuda.ExternalStream(tk.dec.b.stream)
+    barrier()
+    t0 = time.perf_counter()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for i in range(steps):
+        tk.dec.step(tk.tokens[i], i)
+    e1.record(st)
+    tk.dec.b.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    return {"tokens": steps, "tok_s": round(steps / el, 1), "ms_per_token": round(el / steps * 1e3, 4),
+            "gpu_ms_per_token": round(e0.elapsed_time(e1) / steps, 4)}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--model", default="tinyllama-1.1b", choices=sorted(MODELS))
-    ap.add_argument("--mode", default="replicas", choices=["replicas", "rowsplit"])
+    ap.add_argument("--mode", default=None, choices=["rowsplit", "replicas"],
+                    help="N > 1: rowsplit (default; the decode token's weight rows split over the GPUs, one "
+                         "RCCL all-gather per stage, one token stream: strong scaling) or replicas (an "
+                         "independent token stream per GPU: weak scaling)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true")
@@ -481,17 +565,24 @@ def main():
                          "chain: the per-token MUL_MAT chain only")
     ap.add_argument("--no-chain", action="store_true", help="token workload: skip the matmul-chain side figure")
     ap.add_argument("--no-8b", action="store_true", help="skip the Llama-3-8B side figure (configs 3 and 5)")
+    ap.add_argument("--tg", type=int, default=128, help="tokens of the tg side figure (0: skip)")
     args = ap.parse_args()
-    if args.workload == "token" and (args.mode == "rowsplit" or args.gguf or args.impl != "auto"):
-        args.workload = "chain"  # the row-split, GGUF-file and kernel-A/B runs are matmul-chain modes
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        spawn_ranks(args.gpus)  # exits
+    if args.workload == "token" and (args.gguf or args.impl != "auto"):
+        args.workload = "chain"  # the GGUF-file and kernel-A/B runs are matmul-chain modes
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    mode = args.mode or ("rowsplit" if world > 1 else "replicas")
+    if mode == "rowsplit" and args.workload != "token":
+        raise SystemExit("bench: the row split runs the decode token workload")
     if world > 1:
+        # control plane only (barriers, the RCCL id, the max over ranks): gloo on the host;
+        # the data path's collectives are the backend's own RCCL ALL_GATHER nodes
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl")
+        dist.init_process_group("gloo")
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     if not g.device_available():
@@ -507,18 +598,19 @@ def main():
     if args.gguf:
         from ggml_mi355x.gguf import GGUFFile
         gguf = GGUFFile(args.gguf)
-    use_backend = args.mode != "rowsplit"
-    if not use_backend:  # world 1 runs the same path with one shard (exercises StageGather)
-        from ggml_mi355x.rowsplit import RowSplitChain
-        runner = RowSplitChain(args.model, dev, rank, world,
-                               make_chain=lambda *a, **k: Chain(*a, gguf=gguf, **k))
-        chain = runner.chain
-        step = runner.step
-        stream = torch.cuda.current_stream()
-    elif args.workload == "token":
+    rowsplit = mode == "rowsplit"  # (--mode rowsplit at N = 1: the same graph, gathers over a 1-rank RCCL comm)
+    if args.workload == "token":
         be = g.Backend(local)
-        n_ctx = max(128, (max(args.steps, args.warmup) + 31) // 32 * 32)
-        chain = Token(args.model, dev, 0x51A7 + rank, be, n_ctx)
+        if rowsplit:
+            uid = torch.zeros(g.lib().mi355x_comm_id_size(), dtype=torch.uint8)
+            if rank == 0:
+                uid.copy_(torch.frombuffer(bytearray(g.comm_unique_id()), dtype=torch.uint8))
+            if world > 1:
+                import torch.distributed as dist
+                dist.broadcast(uid, 0)
+            be.set_comm(rank, world, bytes(uid.numpy().tobytes()))
+        n_ctx = max(128, (max(args.steps, args.warmup, args.tg) + 31) // 32 * 32)
+        chain = Token(args.model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank) if rowsplit else None)
         stream = torch.cuda.ExternalStream(be.stream)
         use_graph = not args.no_graph
         pos = [0]
@@ -541,8 +633,7 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
-    if use_backend:
-        be.synchronize()
+    be.synchronize()
     if isinstance(chain, Token):  # tg128: the timed tokens start from an empty KV cache
         chain.dec.reset()
         torch.cuda.synchronize()
@@ -556,42 +647,49 @@ def main():
         step()
     ev1.record(stream)
     torch.cuda.synchronize()
-    if use_backend:
-        be.synchronize()
+    be.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
     t_max = elapsed
     if world > 1:
         import torch.distributed as dist
-        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
-    tokens_total = args.steps * (world if args.mode == "replicas" else 1)
+    tokens_total = args.steps * (1 if rowsplit else world)
     value = tokens_total / t_max
+
+    # per-launch kernel timing (every rank: the row split's eager steps are collective)
+    per = {}
+    if isinstance(chain, Token):
+        chain.dec.reset()
+        torch.cuda.synchronize()
+        barrier()
+    per = timed_kernel_stats(be, chain, tokens=4)
+    tg = tg_side(chain, args.tg, barrier) if isinstance(chain, Token) and args.tg > 0 else None
 
     result = None
     if rank == 0:
-        # roofline of the dominant kernel, from per-launch kernel timestamps
+        # roofline of the dominant GEMV kernel, from per-launch kernel timestamps
         roof = None
-        per = {}
-        if use_backend:
-            if isinstance(chain, Token):
-                chain.dec.reset()
-                torch.cuda.synchronize()
-            per = timed_kernel_stats(be, chain, tokens=4)
-            dom = max(per, key=lambda k: per[k]["ms"])
+        gemv = {k: v for k, v in per.items() if "kq_rows" in k or "kq_gemv" in k or "kq_chain" in k}
+        if gemv:
+            dom = max(gemv, key=lambda k: gemv[k]["ms"])
             d = per[dom]
             ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                     "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
                     "launches": d["launches"], "bytes_per_launch": d["bytes"] / d["launches"],
                     "us_per_launch": d["ms"] * 1e3 / d["launches"]}
-        if roof is not None:
+        if roof is not None and not rowsplit:
             # HBM traffic of the same kernel from the committed rocprofv3 PMC pass of this
-            # bench command (FETCH_SIZE x2 gfx950 correction + WRITE_SIZE), per launch
-            pname = "r01_token_summary.json" if isinstance(chain, Token) else "r01_chain_summary.json"
+            # bench command (FETCH_SIZE x2 gfx950 correction), per launch
+            pname = "r02_token_summary.json" if isinstance(chain, Token) else "r01_chain_summary.json"
             prof = os.path.join(ROOT, "profiles", pname)
+            if not os.path.exists(prof) and isinstance(chain, Token):
+                pname = "r01_token_summary.json"
+                prof = os.path.join(ROOT, "profiles", pname)
             if os.path.exists(prof):
                 with open(prof) as f:
                     pk = json.load(f).get("by_kernel", {}).get(roof["kernel"])
@@ -609,28 +707,32 @@ def main():
         l3 = None
         if isinstance(chain, Token) and not args.no_8b and world == 1 and args.model != "llama-3-8b":
             l3 = model_side("llama-3-8b", dev)
-        prefill = None if args.no_prefill or world > 1 or not use_backend else prefill_chain(chain, dev)
+        prefill = None if args.no_prefill or world > 1 else prefill_chain(chain, dev)
+        if prefill is not None:
+            prefill["roofline"] = {"bound": "mfma", "achieved": prefill["int_TOPS"], "peak": I8_PEAK_TOPS,
+                                   "unit": "TOPS (int8 dense)", "frac": round(prefill["int_TOPS"] / I8_PEAK_TOPS, 4),
+                                   "mfma_pmc": "profiles/r02_prefill_mfma.md"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_token(chain, args.cpu_seconds) if isinstance(chain, Token) else \
                 cpu_baseline(chain, args.cpu_seconds)
-        wbytes = chain.bytes_per_token * (world if args.mode == "rowsplit" else 1)
+        local_bytes = chain.bytes_per_token  # weight bytes one GPU streams per token
         if isinstance(chain, Token):
             executor = ("LlamaDecoder -> mi355x_backend_graph_compute: node fusion (norm/swiglu GEMV prologues, "
-                        "residual epilogues), kq_rows + kq_attn_decode, " +
+                        "residual/swiglu epilogues), kq_rows + kq_attn_decode" +
+                        (", RCCL ncclAllGather per stage (row split)" if rowsplit else "") + ", " +
                         ("hipGraph replay" if not args.no_graph else "eager"))
-        elif not use_backend:
-            executor = "rowsplit: gemv_fused per stage + RCCL all_gather"
         elif args.impl == "chain":
             executor = "kq_chain: 1 persistent launch per token (tagged write-through hand-off per stage)"
         else:
             executor = f"{'kq_gemv' if args.impl == 'tasks' else 'kq_rows'}: 1 launch per stage" + \
                 ("" if args.no_graph else ", hipGraph replay")
+        per_gpu_rate = value / (world if not rowsplit else 1)  # tokens/s each GPU streams its weights for
         result = {
             "metric": "tg128 tok/s + Q4_K GEMV achieved-HBM-GB/s, TinyLlama-1.1B Q4_K_M @1 GPU",
             "value": round(value, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "weak" if args.mode == "replicas" else "strong",
+            "higher_is_better": True, "scaling": "strong" if rowsplit else "weak",
             "vs_baseline": None, "dtype": "q4_K/q6_K x q8_K (u4/u6*i8 dot4 -> i32, f32 combine)",
             "data": (f"GGUF weights {os.path.basename(args.gguf)}; random f32 first activation" if args.gguf else
                      "synthetic (random valid K-quant blocks of the real shapes, f32 norms, random token ids)"
@@ -639,18 +741,19 @@ def main():
             "config": {"workload": (f"{chain.model} Q4_K_M tg{args.steps}: full decode graph, token i at "
                                     f"position i of a fresh f16 KV cache" if isinstance(chain, Token) else
                                     f"{chain.model} Q4_K_M decode matmul chain (tg, 1 token/step)"),
-                       "weights_MB_per_token": round(wbytes / 1e6, 1),
+                       "weights_MB_per_token": round(local_bytes * (world if rowsplit else 1) / 1e6, 1),
+                       "weights_MB_per_token_per_gpu": round(local_bytes / 1e6, 1),
                        "stages_per_token": chain.launches(),
                        "executor": executor,
-                       "parallelism": (f"replicas x{world}" if args.mode == "replicas" else f"rowsplit{world}"),
-                       "hipgraph": use_backend and args.impl != "chain" and not args.no_graph},
+                       "parallelism": (f"rowsplit{world}" if rowsplit else f"replicas x{world}"),
+                       "hipgraph": args.impl != "chain" and not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
-            "effective_GBps": round(value * chain.bytes_per_token / 1e9 / (world if args.mode == "replicas" else 1), 1),
-            # the whole token (every launch, gaps included) against the HBM roofline, per GPU
-            "token_hbm_frac": round(value * chain.bytes_per_token / 1e9 / (world if args.mode == "replicas" else 1)
-                                    / HBM_PEAK_GBS, 4),
+            "effective_GBps": round(per_gpu_rate * local_bytes / 1e9, 1),
+            # the whole token (every launch, gap and gather included) against the HBM roofline, per GPU
+            "token_hbm_frac": round(per_gpu_rate * local_bytes / 1e9 / HBM_PEAK_GBS, 4),
             "roofline": roof,
             "kernels": kernels,
+            "tg128": tg,
             "gemv_large": large,
             "prefill_pp512": prefill,
             "matmul_chain": side,
@@ -660,6 +763,7 @@ def main():
         print(json.dumps(result), flush=True)
     if world > 1:
         import torch.distributed as dist
+        dist.barrier()
         dist.destroy_process_group()
     return result
 

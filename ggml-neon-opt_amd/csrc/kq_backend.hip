@@ -8,9 +8,12 @@
 // walks every node (ggml_graph_compute_thread, ggml-cpu.c:2883), this backend
 // enqueues one kernel per (fused) node on its HIP stream; repeated graphs
 // (decode steps) are replayed from a captured hipGraph.
+#include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+#include <rccl/rccl.h>
 
 #include <string>
 #include <vector>
@@ -42,6 +45,9 @@ struct mi355x_backend {
     ChainCache chain;
     std::vector<uint32_t *> old_sync;
     bool fuse = true;
+    ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
+    int rank = 0, world = 0;
+    int loop_rank = -1, loop_world = 0;  // single-GPU emulation of one rank (tests)
 };
 
 namespace {
@@ -59,6 +65,38 @@ struct DeviceGuard {
         if (prev >= 0) hipSetDevice(prev);
     }
 };
+
+// ---- RCCL, resolved at run time: the copy already loaded in the process (torch
+// bundles one) or /opt/rocm's. Only the entry points the row split uses.
+struct Rccl {
+    bool tried = false, ok = false;
+    ncclResult_t (*get_unique_id)(ncclUniqueId *) = nullptr;
+    ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
+    ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
+    ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    const char *(*error_string)(ncclResult_t) = nullptr;
+};
+
+Rccl &rccl() {
+    static Rccl r;
+    if (r.tried) return r;
+    r.tried = true;
+    void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_NOLOAD);
+    if (!h) h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) {
+        fprintf(stderr, "ggml_mi355x: librccl.so.1 not found (%s)\n", dlerror());
+        return r;
+    }
+    r.get_unique_id = (decltype(r.get_unique_id))dlsym(h, "ncclGetUniqueId");
+    r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
+    r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
+    r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.error_string;
+    return r;
+}
 
 bool is_kquant(int t) { return t == MI355X_TYPE_Q4_K || t == MI355X_TYPE_Q5_K || t == MI355X_TYPE_Q6_K; }
 
@@ -277,6 +315,23 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
             return mi355x_rope((const float *)t->src[0]->data, (float *)t->data, (int)t->ne[0], t->op_params[0],
                                (int)(nelem(t) / t->ne[0]), (const int32_t *)t->src[1]->data,
                                (const float *)t->src[2]->data, (int)t->src[2]->ne[1], st);
+        case MI355X_OP_ALL_GATHER: {
+            if (!b->comm && b->loop_world > 0) {  // emulated rank: own slice into place, the rest untouched
+                if (nelem(t) != nelem(t->src[0]) * b->loop_world) return MI355X_E_COMM;
+                const size_t n = (size_t)nelem(t->src[0]) * 4;
+                const hipError_t e = hipMemcpyAsync((char *)t->data + (size_t)b->loop_rank * n, t->src[0]->data, n,
+                                                    hipMemcpyDeviceToDevice, st);
+                return e == hipSuccess ? 0 : (int)e;
+            }
+            if (!b->comm || nelem(t) != nelem(t->src[0]) * b->world) return MI355X_E_COMM;
+            const ncclResult_t r = rccl().all_gather(t->src[0]->data, t->data, (size_t)nelem(t->src[0]), ncclFloat32,
+                                                     b->comm, st);
+            if (r != ncclSuccess) {
+                fprintf(stderr, "ggml_mi355x: ncclAllGather: %s\n", rccl().error_string(r));
+                return MI355X_E_COMM;
+            }
+            return 0;
+        }
         case MI355X_OP_ATTN_DECODE: {
             mi355x_attn_desc a;
             a.q = (const float *)t->src[0]->data;
@@ -503,6 +558,7 @@ void mi355x_backend_free(mi355x_backend_t b) {
     drop_chain(b);
     for (uint32_t *s : b->old_sync) hipFree(s);
     if (b->workspace) hipFree(b->workspace);
+    if (b->comm) rccl().comm_destroy(b->comm);
     hipStreamDestroy(b->stream);
     }
     delete b;
@@ -596,6 +652,10 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
             return contig_f32(op) && contig_f32(op->src[0]) && op->src[1] && op->src[1]->type == MI355X_TYPE_I32 &&
                    contig_f32(op->src[2]) && op->op_params[0] > 0 && op->op_params[0] <= op->ne[0] &&
                    op->src[2]->ne[0] == op->op_params[0];
+        case MI355X_OP_ALL_GATHER:
+            // a packed f32 slice gathered into a packed f32 vector (world known at compute time)
+            return contig_f32(op) && contig_f32(op->src[0]) && op->ne[1] == 1 && op->src[0]->ne[1] == 1 &&
+                   op->src[0]->ne[0] > 0 && op->ne[0] % op->src[0]->ne[0] == 0;
         case MI355X_OP_ATTN_DECODE: {
             for (int s = 0; s < 7; ++s)
                 if (!op->src[s] || !op->src[s]->data) return 0;
@@ -622,6 +682,62 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
         default:
             return 0;
     }
+}
+
+size_t mi355x_comm_id_size(void) { return sizeof(ncclUniqueId); }
+
+int mi355x_comm_get_unique_id(void *id_out) {
+    if (!id_out) return MI355X_E_INVAL;
+    Rccl &r = rccl();
+    if (!r.ok) return MI355X_E_COMM;
+    ncclUniqueId id;
+    const ncclResult_t e = r.get_unique_id(&id);
+    if (e != ncclSuccess) {
+        fprintf(stderr, "ggml_mi355x: ncclGetUniqueId: %s\n", r.error_string(e));
+        return MI355X_E_COMM;
+    }
+    memcpy(id_out, &id, sizeof(id));
+    return MI355X_OK;
+}
+
+int mi355x_backend_set_comm(mi355x_backend_t b, int rank, int world, const void *unique_id) {
+    if (!b || world < 1 || rank < 0 || rank >= world || !unique_id) return MI355X_E_INVAL;
+    Rccl &r = rccl();
+    if (!r.ok) return MI355X_E_COMM;
+    DeviceGuard dg(b->device);
+    hipStreamSynchronize(b->stream);
+    drop_graph(b);  // a captured graph holds the old communicator's collectives
+    if (b->comm) {
+        r.comm_destroy(b->comm);
+        b->comm = nullptr;
+        b->world = 0;
+    }
+    ncclUniqueId id;
+    memcpy(&id, unique_id, sizeof(id));
+    ncclComm_t c = nullptr;
+    const ncclResult_t e = r.comm_init_rank(&c, world, id, rank);
+    if (e != ncclSuccess) {
+        fprintf(stderr, "ggml_mi355x: ncclCommInitRank(rank %d of %d): %s\n", rank, world, r.error_string(e));
+        return MI355X_E_COMM;
+    }
+    b->comm = c;
+    b->rank = rank;
+    b->world = world;
+    return MI355X_OK;
+}
+
+int mi355x_backend_comm_world(mi355x_backend_t b) {
+    return b && b->comm ? b->world : (b && b->loop_world ? b->loop_world : 0);
+}
+
+int mi355x_backend_set_comm_loopback(mi355x_backend_t b, int rank, int world) {
+    if (!b || world < 0 || (world > 0 && (rank < 0 || rank >= world))) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
+    hipStreamSynchronize(b->stream);
+    drop_graph(b);
+    b->loop_rank = world > 0 ? rank : -1;
+    b->loop_world = world;
+    return MI355X_OK;
 }
 
 int mi355x_backend_set_fusion(mi355x_backend_t b, int enable) {

@@ -22,7 +22,7 @@ QK_K = 256
 BLOCK_BYTES = {TYPE_Q4_K: 144, TYPE_Q5_K: 176, TYPE_Q6_K: 210, TYPE_Q8_K: 292}
 TYPE_NAMES = {TYPE_Q4_K: "q4_K", TYPE_Q5_K: "q5_K", TYPE_Q6_K: "q6_K", TYPE_Q8_K: "q8_K", TYPE_F32: "f32"}
 MAX_FUSED = 4
-OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROPE, OP_ATTN_DECODE = range(9)
+OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROPE, OP_ATTN_DECODE, OP_ALL_GATHER = range(10)
 MAX_SRC = 8
 FLAG_OUTPUT = 1
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
@@ -47,6 +47,8 @@ EXPORTED_SYMBOLS = (
     "mi355x_gemv_ext_workspace_size", "mi355x_gemv_fused_ext", "mi355x_backend_set_fusion",
     "mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
     "mi355x_rope_table_size", "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode",
+    "mi355x_comm_id_size", "mi355x_comm_get_unique_id", "mi355x_backend_set_comm", "mi355x_backend_comm_world",
+    "mi355x_backend_set_comm_loopback",
 )
 
 
@@ -165,6 +167,16 @@ def lib():
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
               "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode"):
         getattr(L, n).restype = i32
+    L.mi355x_comm_id_size.argtypes = []
+    L.mi355x_comm_id_size.restype = sz
+    L.mi355x_comm_get_unique_id.argtypes = [vp]
+    L.mi355x_comm_get_unique_id.restype = i32
+    L.mi355x_backend_set_comm.argtypes = [vp, i32, i32, vp]
+    L.mi355x_backend_set_comm.restype = i32
+    L.mi355x_backend_comm_world.argtypes = [vp]
+    L.mi355x_backend_comm_world.restype = i32
+    L.mi355x_backend_set_comm_loopback.argtypes = [vp, i32, i32]
+    L.mi355x_backend_set_comm_loopback.restype = i32
     from . import gguf as _gguf
     _gguf.bind(L)
     _lib = L
@@ -484,6 +496,19 @@ class Backend:
     def set_fusion(self, enable):
         return int(lib().mi355x_backend_set_fusion(self.h, 1 if enable else 0))
 
+    def set_comm(self, rank, world, unique_id: bytes):
+        """Join the RCCL communicator of a row split (every rank, same id bytes)."""
+        buf = ctypes.create_string_buffer(bytes(unique_id), len(unique_id))
+        _check(lib().mi355x_backend_set_comm(self.h, rank, world, buf), "set_comm")
+
+    def set_comm_loopback(self, rank, world):
+        """Test emulation of one rank of a row split on this GPU (no communicator)."""
+        _check(lib().mi355x_backend_set_comm_loopback(self.h, rank, world), "set_comm_loopback")
+
+    @property
+    def comm_world(self):
+        return int(lib().mi355x_backend_comm_world(self.h))
+
     def graph_compute(self, nodes, use_graph=True):
         arr = (ctypes.POINTER(Tensor) * len(nodes))(*[ctypes.pointer(n) for n in nodes])
         return int(lib().mi355x_backend_graph_compute(self.h, arr, len(nodes), 1 if use_graph else 0))
@@ -498,6 +523,14 @@ class Backend:
             self.close()
         except Exception:
             pass
+
+
+def comm_unique_id() -> bytes:
+    """A fresh RCCL unique id (rank 0 of a row split creates it, the others receive it)."""
+    n = int(lib().mi355x_comm_id_size())
+    buf = ctypes.create_string_buffer(n)
+    _check(lib().mi355x_comm_get_unique_id(buf), "comm_get_unique_id")
+    return buf.raw
 
 
 def supports_op(t: Tensor) -> bool:

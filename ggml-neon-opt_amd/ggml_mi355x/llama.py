@@ -20,8 +20,8 @@ from __future__ import annotations
 
 import ctypes
 
-from . import (FLAG_OUTPUT, OP_ADD, OP_ATTN_DECODE, OP_GET_ROWS, OP_MUL, OP_MUL_MAT, OP_RMS_NORM, OP_SWIGLU,
-               TYPE_F16, TYPE_F32, TYPE_I32, Backend, Mi355xError, f32_bits, make_tensor, rope_table)
+from . import (FLAG_OUTPUT, OP_ADD, OP_ALL_GATHER, OP_ATTN_DECODE, OP_GET_ROWS, OP_MUL, OP_MUL_MAT, OP_RMS_NORM,
+               OP_SWIGLU, TYPE_F16, TYPE_F32, TYPE_I32, Backend, Mi355xError, f32_bits, make_tensor, rope_table)
 
 LAYER_MATS = ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down")
 
@@ -41,17 +41,27 @@ class LlamaDecoder:
     weights: dict with "token_embd", "output", "output_norm" and per layer i
     "blk.{i}.<name>" for name in LAYER_MATS + ("attn_norm", "ffn_norm"); a K-quant
     matrix is (type, uint8 cuda tensor [rows, rowbytes]), a norm is an f32 cuda tensor.
+
+    split: a rowsplit.TokenSplit — this process is one rank of a row split; the
+    matrices in `weights` are then the rank's row slices (TokenSplit.slice_weights),
+    the KV caches hold the rank's KV heads, and every stage's slice is ALL_GATHERed
+    (RCCL, the backend's communicator) before the next stage reads it. The logits
+    (and every gathered vector) are bit-identical to the single-GPU token.
     """
 
     HOST_SLOTS = 1024
 
-    def __init__(self, backend: Backend, hp: dict, weights: dict, n_ctx: int, fuse: bool = True):
+    def __init__(self, backend: Backend, hp: dict, weights: dict, n_ctx: int, fuse: bool = True, split=None):
         import torch
-        self.b, self.hp, self.w, self.n_ctx = backend, hp, weights, n_ctx
+        self.b, self.hp, self.w, self.n_ctx, self.split = backend, hp, weights, n_ctx, split
         dev = weights["output_norm"].device
         E, F, V = hp["n_embd"], hp["n_ff"], hp["n_vocab"]
         hd, nh, nkv = hp["head_dim"], hp["n_head"], hp["n_head_kv"]
+        world = split.world if split is not None else 1
+        if split is not None:
+            nh, nkv = split.n_head, split.n_head_kv  # this rank's heads
         kvw = nkv * hd
+        self.gathers = []  # (node output buffer) of every ALL_GATHER, in graph order
         f32 = torch.float32
 
         def buf(n, dtype=f32):
@@ -92,13 +102,29 @@ class LlamaDecoder:
             wt = mat(name)
             return node(OP_MUL_MAT, wt.ne[1], [wt, x])[0]
 
+        def gather(part, n_local, flags=0):
+            """ALL_GATHER of a row-split stage's slice (emitted for every split, a
+            world-1 split included: one RCCL copy; none without a split)."""
+            if split is None:
+                return part, None
+            full, b = node(OP_ALL_GATHER, n_local * world, [part], flags=flags)
+            self.gathers.append(b)
+            return full, b
+
+        def rows_view(t_buf, lo, n):
+            """The rows [lo, lo+n) of a full f32 vector (the residual of a local slice)."""
+            return leaf(t_buf[lo:lo + n], TYPE_F32, n)
+
+        El = E // world
+        r_e0 = split.rows["attn_output"][0] if split is not None else 0
+
         eps_bits = [f32_bits(hp["eps"])]
         tok = leaf(self.token, TYPE_I32, 1)
         pos = leaf(self.pos, TYPE_I32, 1)
         tab = leaf(self.inp[2:], TYPE_F32, hd, 1)  # the position's rope row (ne1 = 1)
         et, ew = weights["token_embd"]
         emb_t = leaf(ew, et, E, ew.shape[0], row_stride=ew.stride(0) * ew.element_size())
-        x, _ = node(OP_GET_ROWS, E, [emb_t, tok])
+        x, xb = node(OP_GET_ROWS, E, [emb_t, tok])
         scale = f32_bits(float(torch.tensor(1.0) / torch.sqrt(torch.tensor(float(hd)))))
         for i in range(hp["n_layer"]):
             p = f"blk.{i}."
@@ -110,19 +136,32 @@ class LlamaDecoder:
             kc = leaf(self.k_cache[i], TYPE_F16, kvw, n_ctx)
             vc = leaf(self.v_cache[i], TYPE_F16, n_ctx, kvw)
             att, _ = node(OP_ATTN_DECODE, nh * hd, [q, k, v, pos, kc, vc, tab], [nh, nkv, hd, scale])
+            att, _ = gather(att, nh * hd)
             o = mm(p + "attn_output", att)
-            ffn_inp, _ = node(OP_ADD, E, [o, x])
+            res = x if split is None else rows_view(xb, r_e0, El)
+            ffn_inp, fb = node(OP_ADD, El, [o, res])
+            ffn_inp, fbg = gather(ffn_inp, El)
+            fb = fbg if fbg is not None else fb
             n2, _ = node(OP_RMS_NORM, E, [ffn_inp], eps_bits)
             m2, _ = node(OP_MUL, E, [n2, leaf(weights[p + "ffn_norm"], TYPE_F32, E)])
             gt = mm(p + "ffn_gate", m2)
             up = mm(p + "ffn_up", m2)
-            glu, _ = node(OP_SWIGLU, F, [gt, up])
+            glu, _ = node(OP_SWIGLU, gt.ne[0], [gt, up])
+            glu, _ = gather(glu, F // world)
             dn = mm(p + "ffn_down", glu)
-            x, self.last_hidden = node(OP_ADD, E, [dn, ffn_inp])
+            res = ffn_inp if split is None else rows_view(fb, r_e0, El)
+            x, xb = node(OP_ADD, El, [dn, res])
+            x, xbg = gather(x, El)
+            xb = xbg if xbg is not None else xb
+            self.last_hidden = xb
         n3, _ = node(OP_RMS_NORM, E, [x], eps_bits)
         m3, _ = node(OP_MUL, E, [n3, leaf(weights["output_norm"], TYPE_F32, E)])
         wt = mat("output")
-        _, self.logits = node(OP_MUL_MAT, V, [wt, m3], flags=FLAG_OUTPUT)
+        if split is None:
+            _, self.logits = node(OP_MUL_MAT, V, [wt, m3], flags=FLAG_OUTPUT)
+        else:
+            lg, _ = node(OP_MUL_MAT, wt.ne[1], [wt, m3])
+            _, self.logits = gather(lg, V // world, flags=FLAG_OUTPUT)
         self._tensors = T
         self._arr = (ctypes.POINTER(type(T[0])) * len(self.nodes))(*[ctypes.pointer(n) for n in self.nodes])
         # pinned staging slots for (token, pos): a slot is reused only after the stream

@@ -1,95 +1,81 @@
-"""Row-split (tensor-parallel) GEMV over one process per GPU.
+"""Row split (tensor parallel) of the decode token over one process per GPU.
 
 Every weight row's dot product is independent, so rank r of a
-world of G owns a contiguous, 8-row-aligned slice of each matrix's rows (the
-GEMV kernel's task granularity), computes it with the unchanged single-GPU
-kernel (bit-identical per row) and the slices are combined with ONE collective
-per stage: all_gather of the padded slices (N/G floats per rank), or
-all_reduce(sum) over a zero-padded full-length vector (x + 0 = x, still exact).
-Over RCCL/xGMI these per-stage messages (1-112 KB) are latency-bound, which is
-why the row split only pays for large matrices (multi-GPU).
+world of G owns a contiguous slice of each matrix's rows, computes it with the
+unchanged single-GPU kernels (bit-identical per row) and the slices are combined
+by one ALL_GATHER node per stage (RCCL ncclAllGather on the backend stream, in the
+token's hipGraph; kq_backend.hip). An all_reduce(sum) over zero-padded slices
+would give the same bits (x + 0 = x) at G times the bytes. Over xGMI the per-stage
+messages (1-128 KB) are latency-bound: the split pays for large matrices
+(Llama-3-70B), not for TinyLlama.
 """
 from __future__ import annotations
 
 import math
 
 
-def shard_rows(n_rows: int, world: int, rank: int, align: int = 8):
-    """Contiguous row slice of `rank`: (r0, r1, per) with per = padded slice size."""
-    if world < 1 or not (0 <= rank < world):
-        raise ValueError("bad world/rank")
-    per = int(math.ceil(math.ceil(n_rows / world) / align) * align) if n_rows else 0
-    r0 = min(rank * per, n_rows)
-    r1 = min(r0 + per, n_rows)
-    return r0, r1, per
+class TokenSplit:
+    """Row split of one llama decode token over `world` GPUs (rank `rank`'s share).
 
+    The reference splits each MUL_MAT's weight rows over its threads, every thread
+    reading the same quantized activation (ggml_compute_forward_mul_mat's chunks,
+    README.md:125-131, 136/156); here the same rows go to different GPUs:
+      * attn_q rows of the rank's query heads [q0, q1) (nh / world heads each), attn_k
+        / attn_v rows of the KV heads those query heads read (GQA group h // (nh/nkv));
+        when world > n_head_kv, world/n_head_kv ranks hold the same KV head and each
+        keeps its own copy of that head's cache rows (identical bits);
+      * the attention of the rank's heads runs locally, on its KV-cache slice;
+      * attn_output, ffn_down: rows [r*E/world, (r+1)*E/world) with the residual ADD of
+        the same rows; ffn_gate / ffn_up: rows of F/world with the SWIGLU of those rows;
+        output: V/world rows;
+      * after every stage the slices are ALL_GATHERed (rank order = row order), so the
+        next stage reads the full activation: 4 gathers per layer + 1 for the logits.
+    Every row's dot product and every head's attention is the 1-GPU computation, so
+    the gathered vectors are bit-identical to the single-GPU token (and to the oracle).
+    """
 
-class StageGather:
-    """Packs the local slices of the matrices of one fused stage into one buffer and
-    reassembles the full outputs after one collective."""
+    def __init__(self, hp: dict, world: int, rank: int):
+        nh, nkv = hp["n_head"], hp["n_head_kv"]
+        E, F, V = hp["n_embd"], hp["n_ff"], hp["n_vocab"]
+        if world < 1 or not 0 <= rank < world:
+            raise ValueError("bad world/rank")
+        if nh % world:
+            raise ValueError(f"n_head {nh} not divisible by world {world}")
+        if nkv % world and world % nkv:
+            raise ValueError(f"n_head_kv {nkv} and world {world}: one must divide the other")
+        for n, what in ((E, "n_embd"), (F, "n_ff"), (V, "n_vocab")):
+            if n % world:
+                raise ValueError(f"{what} {n} not divisible by world {world}")
+        self.hp, self.world, self.rank = hp, world, rank
+        hd = hp["head_dim"]
+        group = nh // nkv
+        self.q0, self.q1 = rank * nh // world, (rank + 1) * nh // world
+        self.kv0, self.kv1 = self.q0 // group, (self.q1 - 1) // group + 1
+        self.n_head, self.n_head_kv = self.q1 - self.q0, self.kv1 - self.kv0
+        self.rows = {
+            "attn_q": (self.q0 * hd, self.q1 * hd),
+            "attn_k": (self.kv0 * hd, self.kv1 * hd),
+            "attn_v": (self.kv0 * hd, self.kv1 * hd),
+            "attn_output": (rank * E // world, (rank + 1) * E // world),
+            "ffn_gate": (rank * F // world, (rank + 1) * F // world),
+            "ffn_up": (rank * F // world, (rank + 1) * F // world),
+            "ffn_down": (rank * E // world, (rank + 1) * E // world),
+            "output": (rank * V // world, (rank + 1) * V // world),
+        }
 
-    def __init__(self, n_rows_list, world, rank, device, dtype=None, collective="all_gather", group=None):
-        import torch
-        self.world, self.rank, self.group = world, rank, group
-        self.collective = collective
-        self.n_rows = list(n_rows_list)
-        self.shards = [shard_rows(n, world, rank) for n in self.n_rows]
-        self.per = [s[2] for s in self.shards]
-        self.offs = [sum(self.per[:i]) for i in range(len(self.per))]
-        self.total = sum(self.per)
-        dtype = dtype or torch.float32
-        self.local = torch.zeros(self.total, device=device, dtype=dtype)
-        if collective == "all_gather":
-            self.gathered = torch.zeros(world * self.total, device=device, dtype=dtype)
-        elif collective == "all_reduce":
-            self.full = torch.zeros(world * self.total, device=device, dtype=dtype)
-        else:
-            raise ValueError(collective)
+    def rows_of(self, name: str):
+        """Row range of a weight by its GGUF name (blk.N.attn_q, output, ...)."""
+        return self.rows[name.split(".")[-1]]
 
-    def local_view(self, i):
-        """The slice of the packed local buffer that matrix i's GEMV writes."""
-        r0, r1, _ = self.shards[i]
-        return self.local[self.offs[i]:self.offs[i] + (r1 - r0)]
-
-    def exchange(self):
-        import torch.distributed as dist
-        if self.collective == "all_gather":
-            if self.world == 1:
-                self.gathered.copy_(self.local)
-            elif dist.get_backend(self.group) == "gloo":
-                parts = list(self.gathered.chunk(self.world))
-                dist.all_gather(parts, self.local, group=self.group)
+    def slice_weights(self, weights: dict) -> dict:
+        """The rank's share of a full weight dict (LlamaDecoder layout): K-quant
+        matrices sliced by rows, everything else (token_embd, norms) replicated."""
+        out = {}
+        for k, v in weights.items():
+            base = k.split(".")[-1]
+            if isinstance(v, tuple) and base in self.rows:
+                r0, r1 = self.rows[base]
+                out[k] = (v[0], v[1][r0:r1].contiguous() if hasattr(v[1], "contiguous") else v[1][r0:r1])
             else:
-                dist.all_gather_into_tensor(self.gathered, self.local, group=self.group)
-        else:
-            self.full.zero_()
-            self.full[self.rank * self.total:(self.rank + 1) * self.total].copy_(self.local)
-            if self.world > 1:
-                dist.all_reduce(self.full, group=self.group)
-
-    def output(self, i):
-        """Full output of matrix i (length n_rows[i]) after exchange()."""
-        buf = self.gathered if self.collective == "all_gather" else self.full
-        v = buf.view(self.world, self.total)[:, self.offs[i]:self.offs[i] + self.per[i]]
-        return v.reshape(-1)[:self.n_rows[i]]
-
-
-class RowSplitChain:
-    """A model's per-token GEMV chain with every matrix row-split over the ranks;
-    one collective per stage (bench.py --mode rowsplit)."""
-
-    def __init__(self, model, device, rank, world, make_chain, collective="all_gather"):
-        import ggml_mi355x as g
-        self.g = g
-        self.chain = make_chain(model, device, seed=0x51A7, row_shard=lambda n: shard_rows(n, world, rank)[:2])
-        self.gathers = []
-        for stage in self.chain.stages:
-            self.gathers.append(StageGather([n for _, _, _, n in stage], world, rank, device, collective=collective))
-
-    def step(self):
-        g = self.g
-        for si, stage in enumerate(self.chain.stages):
-            sg = self.gathers[si]
-            mats = [(typ, w, sg.local_view(i)) for i, (typ, w) in enumerate(self.chain.w[si])]
-            g.gemv_fused(mats, self.chain.x[si])
-            sg.exchange()
+                out[k] = v
+        return out

@@ -90,6 +90,7 @@ enum mi355x_status {
     MI355X_E_WORKSPACE  = -3,  /* workspace missing or too small               */
     MI355X_E_NODEVICE   = -4,  /* no gfx950 device / HIP runtime unavailable   */
     MI355X_E_TIMEOUT    = -5,  /* a persistent-chain stage hand-off timed out  */
+    MI355X_E_COMM       = -6,  /* RCCL missing / communicator error            */
 };
 
 /* Bytes of one row of `type` with `k` elements (ggml_row_size). k % 256 == 0. */
@@ -307,11 +308,17 @@ int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
  *                src6 rope table [head_dim, >= n_ctx], or [head_dim, 1]: the row of this
  *                token's position, staged with pos; op_params = {n_head, n_head_kv, head_dim, scale bits}
  *                -> f32 [head_dim*n_head]: the non-flash attention block
- *                (set_rows, mul_mat f16, soft_max_ext, mul_mat f16, permute, cont). */
+ *                (set_rows, mul_mat f16, soft_max_ext, mul_mat f16, permute, cont).
+ *   ALL_GATHER   src0 f32 [n] (this rank's contiguous row slice of a row-split MUL_MAT
+ *                chain stage) -> f32 [n * world]: the slices of every rank in rank order,
+ *                one RCCL ncclAllGather over xGMI on the backend stream (captured in the
+ *                hipGraph). Needs mi355x_backend_set_comm; the exchange step of the
+ *                row split (weight rows of one matrix across the GPUs,
+ *                the reference's per-thread row split README.md:125-131 across devices). */
 enum mi355x_op {
     MI355X_OP_NONE = 0, MI355X_OP_MUL_MAT = 1, MI355X_OP_GET_ROWS = 2, MI355X_OP_RMS_NORM = 3,
     MI355X_OP_MUL = 4, MI355X_OP_ADD = 5, MI355X_OP_SWIGLU = 6, MI355X_OP_ROPE = 7,
-    MI355X_OP_ATTN_DECODE = 8,
+    MI355X_OP_ATTN_DECODE = 8, MI355X_OP_ALL_GATHER = 9,
 };
 #define MI355X_MAX_SRC 8
 #define MI355X_TENSOR_FLAG_OUTPUT 1  /* read by the caller after graph_compute: never elided by fusion */
@@ -355,6 +362,21 @@ int mi355x_backend_set_fusion(mi355x_backend_t backend, int enable);
  * Returns 0 (GGML_STATUS_SUCCESS) or an error code. */
 int mi355x_backend_graph_compute(mi355x_backend_t backend, mi355x_tensor *const *nodes,
                                  int n_nodes, int use_graph);
+
+/* Row split over one process per GPU. RCCL is resolved at run time
+ * from the librccl.so.1 already loaded in the process, or /opt/rocm's (dlopen): the
+ * library has no link-time RCCL dependency. Rank 0 creates the id, the caller ships
+ * its bytes to the other ranks (any control channel: torch.distributed gloo, MPI,
+ * a file), then every rank joins. mi355x_comm_id_size() == 128 (ncclUniqueId). */
+size_t mi355x_comm_id_size(void);
+int mi355x_comm_get_unique_id(void *id_out);                      /* rank 0 */
+int mi355x_backend_set_comm(mi355x_backend_t backend, int rank, int world,
+                            const void *unique_id);               /* collective: every rank */
+int mi355x_backend_comm_world(mi355x_backend_t backend);         /* 0 if no communicator */
+/* Test emulation of ONE rank of a world on a single GPU, without a communicator:
+ * ALL_GATHER then copies this rank's slice to offset rank*n of its output and leaves
+ * the other ranks' parts as the caller put them. world = 0 turns it off. */
+int mi355x_backend_set_comm_loopback(mi355x_backend_t backend, int rank, int world);
 
 /* ------------------------------------------------ GGUF model files (host) */
 /* Reader for GGUF v2/v3 files, the loader side of the path: llama-bench reads the

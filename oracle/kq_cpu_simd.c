@@ -157,3 +157,128 @@ void kqo_vec_dot_q6_K_q8_K_simd(int n, float *s, size_t bs, const void *vx, size
     }
     *s = sum;
 }
+
+/* ------------------------------------------------------------ binary16 arithmetic */
+/* vfmaq_f16 lane c + a*b with one rounding (kq_ops_oracle.c kqo_f16_fma restates it
+ * on 128-bit integers). Here: p = a*b is exact in double (22 significant bits),
+ * s = p + c rounded to double with its exact error e (TwoSum); rounding s to binary16
+ * equals rounding p + c unless s sits exactly on a binary16 midpoint and e != 0 —
+ * then the tie is broken toward e. Finite inputs (the attention's values). */
+static inline uint16_t f16_from_double(double s, double err) {
+    uint64_t bits;
+    memcpy(&bits, &s, 8);
+    const uint16_t sign = (uint16_t)((bits >> 48) & 0x8000);
+    bits &= 0x7fffffffffffffffull;
+    if (bits == 0) return sign; /* signed zero: IEEE sum sign, as the restatement */
+    const int up = (err != 0.0) && ((err > 0) == (sign == 0)); /* exact value above |s| */
+    const int exp = (int)(bits >> 52) - 1023;                   /* finite, normal doubles here */
+    const uint64_t mant = (bits & 0xfffffffffffffull) | (1ull << 52);
+    int e = exp < -14 ? -14 : exp;
+    const int shift = 42 + (e - exp); /* low bits of the 53-bit significand below the quantum */
+    if (shift > 53) return sign;      /* < 2^-25: rounds to zero */
+    uint64_t q = mant >> shift;
+    const uint64_t rem = mant & ((1ull << shift) - 1), half = 1ull << (shift - 1);
+    if (rem > half || (rem == half && (err != 0.0 ? up : (int)(q & 1)))) q++;
+    if (q >= 2048) {
+        q >>= 1;
+        e++;
+    }
+    if (e > 15) return sign | 0x7c00;
+    if (q < 1024) return sign | (uint16_t)q; /* subnormal */
+    return sign | (uint16_t)(((e + 15) << 10) | (int)(q - 1024));
+}
+
+static inline double h2d(uint16_t h) { return (double)_cvtsh_ss(h); }
+
+uint16_t kqo_f16_fma_fast(uint16_t a, uint16_t b, uint16_t c) {
+    const double p = h2d(a) * h2d(b), cc = h2d(c);
+    const double s = p + cc;
+    const double bb = s - p;
+    const double err = (p - (s - bb)) + (cc - bb);
+    return f16_from_double(s, err);
+}
+
+uint16_t kqo_f16_add_fast(uint16_t a, uint16_t b) { return f16_from_double(h2d(a) + h2d(b), 0.0); /* exact */ }
+
+static inline uint64_t xs64(uint64_t *s) {
+    uint64_t x = *s;
+    x ^= x << 13;
+    x ^= x >> 7;
+    x ^= x << 17;
+    return *s = x;
+}
+
+long kqo_f16_fast_check(long n, uint64_t seed) {
+    uint64_t st = seed | 1;
+    long bad = 0;
+    for (long i = 0; i < n; ++i) {
+        const uint64_t r = xs64(&st);
+        uint16_t a = (uint16_t)r, b = (uint16_t)(r >> 16), c = (uint16_t)(r >> 32);
+        /* finite operands only; bias some toward nearby exponents and exact midpoints */
+        if (((a >> 10) & 0x1f) == 0x1f) a &= 0xbfff;
+        if (((b >> 10) & 0x1f) == 0x1f) b &= 0xbfff;
+        if (((c >> 10) & 0x1f) == 0x1f) c &= 0xbfff;
+        if ((r >> 48) % 4 == 0) c = (uint16_t)((c & 0x83ff) | (a & 0x7c00));
+        if (kqo_f16_fma_fast(a, b, c) != kqo_f16_fma(a, b, c)) ++bad;
+        if (kqo_f16_add_fast(a, c) != kqo_f16_add(a, c)) ++bad;
+    }
+    return bad;
+}
+
+/* kqo_vec_dot_f16 with the fast binary16 ops (same structure and order). */
+static float vec_dot_f16_fast(int n, const uint16_t *x, const uint16_t *y) {
+    const int np = n & ~31;
+    uint16_t sum[4][8];
+    memset(sum, 0, sizeof(sum));
+    for (int i = 0; i < np; i += 32)
+        for (int j = 0; j < 4; ++j)
+            for (int l = 0; l < 8; ++l)
+                sum[j][l] = kqo_f16_fma_fast(x[i + 8 * j + l], y[i + 8 * j + l], sum[j][l]);
+    for (int l = 0; l < 8; ++l) {
+        sum[0][l] = kqo_f16_add_fast(sum[0][l], sum[2][l]);
+        sum[1][l] = kqo_f16_add_fast(sum[1][l], sum[3][l]);
+    }
+    for (int l = 0; l < 8; ++l) sum[0][l] = kqo_f16_add_fast(sum[0][l], sum[1][l]);
+    float t[4];
+    for (int k = 0; k < 4; ++k) t[k] = kqo_fp16_to_fp32(sum[0][k]) + kqo_fp16_to_fp32(sum[0][k + 4]);
+    double sumf = (double)((t[0] + t[1]) + (t[2] + t[3]));
+    for (int i = np; i < n; ++i) sumf += (double)(kqo_fp16_to_fp32(x[i]) * kqo_fp16_to_fp32(y[i]));
+    return (float)sumf;
+}
+
+typedef struct {
+    const float *q;
+    const uint16_t *k_cache, *v_cache;
+    int pos, n_ctx, n_kv, gsz, kvw, head_dim;
+    float scale;
+    float *out;
+} attn_ctx;
+
+static void attn_head(void *vc, int h) {
+    const attn_ctx *a = (const attn_ctx *)vc;
+    const int g = h / a->gsz, hd = a->head_dim, n_kv = a->n_kv;
+    uint16_t q16[512];
+    float kq[8192], mask[8192];
+    uint16_t p16[8192];
+    for (int c = 0; c < n_kv; ++c) mask[c] = c <= a->pos ? 0.0f : -INFINITY;
+    kqo_fp32_to_fp16_row(a->q + (int64_t)h * hd, q16, hd);
+    for (int c = 0; c < n_kv; ++c)
+        kq[c] = vec_dot_f16_fast(hd, a->k_cache + (int64_t)c * a->kvw + (int64_t)g * hd, q16);
+    kqo_soft_max_row(n_kv, kq, kq, mask, a->scale);
+    kqo_fp32_to_fp16_row(kq, p16, n_kv);
+    for (int d = 0; d < hd; ++d)
+        a->out[(int64_t)h * hd + d] = vec_dot_f16_fast(n_kv, a->v_cache + (int64_t)(g * hd + d) * a->n_ctx, p16);
+}
+
+/* kqo_attn_decode (kq_ops_oracle.c) with the fast binary16 ops, heads spread over the
+ * worker pool as ggml-cpu spreads the attention's rows over its threads. */
+void kqo_attn_decode_fast(const float *q, const float *k, const float *v, uint16_t *k_cache, uint16_t *v_cache,
+                          int pos, int n_ctx, int n_head, int n_head_kv, int head_dim, float scale, float *out,
+                          int n_threads) {
+    const int kvw = n_head_kv * head_dim;
+    kqo_fp32_to_fp16_row(k, k_cache + (int64_t)pos * kvw, kvw);
+    for (int ch = 0; ch < kvw; ++ch) v_cache[(int64_t)ch * n_ctx + pos] = kqo_fp32_to_fp16(v[ch]);
+    attn_ctx a = {q, k_cache, v_cache, pos, n_ctx, kqo_attn_n_kv(pos, n_ctx), n_head / n_head_kv, kvw, head_dim,
+                  scale, out};
+    kqo_pool_run(n_threads, n_head, attn_head, &a);
+}

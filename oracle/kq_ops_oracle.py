@@ -43,6 +43,11 @@ def lib():
         L.kqo_attn_n_kv.argtypes = [i32, i32]
         L.kqo_attn_n_kv.restype = i32
         L.kqo_attn_decode.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp]
+        L.kqo_attn_decode_fast.argtypes = [vp, vp, vp, vp, vp, i32, i32, i32, i32, i32, f32, vp, i32]
+        L.kqo_f16_fma_fast.argtypes = [u16, u16, u16]
+        L.kqo_f16_fma_fast.restype = u16
+        L.kqo_f16_fast_check.argtypes = [ctypes.c_long, ctypes.c_uint64]
+        L.kqo_f16_fast_check.restype = ctypes.c_long
         _bound = True
     return L
 
@@ -145,19 +150,25 @@ def attn_n_kv(pos, n_ctx):
     return lib().kqo_attn_n_kv(pos, n_ctx)
 
 
-def attn_decode(q, k, v, k_cache, v_cache, pos, n_head, n_head_kv, head_dim, scale):
-    """Updates k_cache ([n_ctx, n_head_kv*hd] u16) and v_cache ([n_head_kv*hd, n_ctx] u16) in place."""
+def attn_decode(q, k, v, k_cache, v_cache, pos, n_head, n_head_kv, head_dim, scale, fast_threads=0):
+    """Updates k_cache ([n_ctx, n_head_kv*hd] u16) and v_cache ([n_head_kv*hd, n_ctx] u16) in place.
+    fast_threads > 0: the CPU-baseline form (kq_cpu_simd.c: double-based binary16 ops,
+    heads over the worker pool), bit-identical to the restatement."""
     q, k, v = _f32(q), _f32(k), _f32(v)
     assert k_cache.flags.c_contiguous and v_cache.flags.c_contiguous
     out = np.empty(n_head * head_dim, np.float32)
     n_ctx = k_cache.shape[0]
-    lib().kqo_attn_decode(_p(q), _p(k), _p(v), _p(k_cache), _p(v_cache), pos, n_ctx, n_head, n_head_kv, head_dim,
-                          scale, _p(out))
+    if fast_threads > 0:
+        lib().kqo_attn_decode_fast(_p(q), _p(k), _p(v), _p(k_cache), _p(v_cache), pos, n_ctx, n_head, n_head_kv,
+                                   head_dim, scale, _p(out), fast_threads)
+    else:
+        lib().kqo_attn_decode(_p(q), _p(k), _p(v), _p(k_cache), _p(v_cache), pos, n_ctx, n_head, n_head_kv,
+                              head_dim, scale, _p(out))
     return out
 
 
 # ------------------------------------------------------------ one decode token
-def decode_token(model, token, pos, cache, n_threads=8, variant="neon"):
+def decode_token(model, token, pos, cache, n_threads=8, variant="neon", full_trace=None):
     """The llama graph for one token (llm_build_llama, non-flash attention), ggml-cpu
     semantics op by op: get_rows -> [rms_norm*attn_norm -> q/k/v mul_mat -> rope ->
     attention -> wo mul_mat -> add -> rms_norm*ffn_norm -> gate/up mul_mat -> swiglu ->
@@ -165,7 +176,8 @@ def decode_token(model, token, pos, cache, n_threads=8, variant="neon"):
     `model`: dict as built by tests/llama_model.py; `cache`: list of (k_cache, v_cache)
     per layer, updated in place. `variant`: the vec_dot form of the matmuls ("neon"
     scalar, or "simd": AVX2 integer parts, bit-identical). Returns (logits,
-    per-layer residual outputs)."""
+    per-layer residual outputs). `full_trace` (a list) receives per layer a dict of
+    the attention output, ffn_inp, the swiglu output and the layer output."""
     hp = model["hp"]
     E, hd = hp["n_embd"], hp["head_dim"]
     eps = hp["eps"]
@@ -183,16 +195,19 @@ def decode_token(model, token, pos, cache, n_threads=8, variant="neon"):
         q = rope(q, hd, hd, pos, table)
         k = rope(k, hd, hd, pos, table)
         kc, vc = cache[li]
-        att = attn_decode(q, k, v, kc, vc, pos, hp["n_head"], hp["n_head_kv"], hd, float(scale))
+        att = attn_decode(q, k, v, kc, vc, pos, hp["n_head"], hp["n_head_kv"], hd, float(scale),
+                          fast_threads=n_threads if variant == "simd" else 0)
         cur = KO.mul_mat(L["wo"][0], L["wo"][1], att, n_threads, variant)[0]
         ffn_inp = add(cur, inp)
         cur = mul(rms_norm(ffn_inp, eps), L["ffn_norm"])
         g = KO.mul_mat(L["w_gate"][0], L["w_gate"][1], cur, n_threads, variant)[0]
         u = KO.mul_mat(L["w_up"][0], L["w_up"][1], cur, n_threads, variant)[0]
-        cur = swiglu(g, u)
-        cur = KO.mul_mat(L["w_down"][0], L["w_down"][1], cur, n_threads, variant)[0]
+        glu = swiglu(g, u)
+        cur = KO.mul_mat(L["w_down"][0], L["w_down"][1], glu, n_threads, variant)[0]
         x = add(cur, ffn_inp)
         trace.append(x)
+        if full_trace is not None:
+            full_trace.append({"att": att, "ffn_inp": ffn_inp, "glu": glu, "x": x})
     cur = mul(rms_norm(x, eps), model["output_norm"])
     logits = KO.mul_mat(model["output"][0], model["output"][1], cur, n_threads, variant)[0]
     return logits, trace

@@ -541,6 +541,8 @@ typedef struct {
     float *dst; vec_dot_fn vec_dot;
     int nth; atomic_int current_chunk;
     atomic_int arrived; /* ggml_barrier: threads past the quantization */
+    /* generic parallel-for (kqo_pool_run): tasks handed out by current_chunk */
+    void (*task_fn)(void *ctx, int task); void *task_ctx; int n_tasks;
 } mm_plan;
 
 typedef struct { mm_plan *p; int ith; } mm_arg;
@@ -571,6 +573,11 @@ static void *mm_thread(void *arg) {
     mm_arg *a = (mm_arg *)arg;
     mm_plan *p = a->p;
     const int ith = a->ith, nth = p->nth;
+    if (p->task_fn) { /* generic tasks: an atomic counter, no barrier */
+        for (int t = atomic_fetch_add(&p->current_chunk, 1); t < p->n_tasks; t = atomic_fetch_add(&p->current_chunk, 1))
+            p->task_fn(p->task_ctx, t);
+        return NULL;
+    }
     const int64_t nbq = p->K / QK_K;
     if (p->quantize) { /* every thread quantizes its block slice of every src1 row */
         for (int64_t i11 = 0; i11 < p->M; ++i11) {
@@ -675,6 +682,15 @@ static int mm_run(mm_plan *p, int n_threads) {
         else sched_yield();
     pthread_mutex_unlock(&g_pool_mu);
     return 0;
+}
+
+void kqo_pool_run(int n_threads, int n_tasks, void (*fn)(void *ctx, int task), void *ctx) {
+    mm_plan p;
+    memset(&p, 0, sizeof(p));
+    p.task_fn = fn;
+    p.task_ctx = ctx;
+    p.n_tasks = n_tasks;
+    mm_run(&p, n_threads < n_tasks ? n_threads : (n_tasks > 0 ? n_tasks : 1));
 }
 
 int kqo_mul_mat(int type, const void *src0, int64_t K, int64_t N, size_t nb01,

@@ -84,6 +84,9 @@ int kqo_mul_mat_q8(int type, const void *src0, int64_t K, int64_t N, size_t nb01
                    const void *src1_q8, int64_t M, float *dst, int n_threads, int variant);
 
 
+/* Run fn(ctx, task) for task in [0, n_tasks) on the persistent worker pool. */
+void kqo_pool_run(int n_threads, int n_tasks, void (*fn)(void *ctx, int task), void *ctx);
+
 /* ---- non-matmul decode ops (kq_ops_oracle.c) ---- */
 uint16_t kqo_f16_fma(uint16_t a, uint16_t b, uint16_t c);
 uint16_t kqo_f16_add(uint16_t a, uint16_t b);
@@ -103,6 +106,14 @@ void kqo_get_rows(int type, const void *table, int64_t k, size_t row_stride, con
 int kqo_attn_n_kv(int pos, int n_ctx);
 void kqo_attn_decode(const float *q, const float *k, const float *v, uint16_t *k_cache, uint16_t *v_cache, int pos,
                      int n_ctx, int n_head, int n_head_kv, int head_dim, float scale, float *out);
+
+/* ---- CPU-baseline forms (kq_cpu_simd.c), bit-identical to the restatements above ---- */
+uint16_t kqo_f16_fma_fast(uint16_t a, uint16_t b, uint16_t c);  /* double TwoSum + midpoint fix */
+uint16_t kqo_f16_add_fast(uint16_t a, uint16_t b);
+long kqo_f16_fast_check(long n, uint64_t seed);  /* mismatches vs kqo_f16_fma / _add on random triples */
+void kqo_attn_decode_fast(const float *q, const float *k, const float *v, uint16_t *k_cache, uint16_t *v_cache,
+                          int pos, int n_ctx, int n_head, int n_head_kv, int head_dim, float scale, float *out,
+                          int n_threads);
 
 #ifdef __cplusplus
 }

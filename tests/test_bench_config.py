@@ -34,3 +34,17 @@ def test_tinyllama_type_mix():
         assert types[f"blk.{i}.attn_q"] == (g.TYPE_Q4_K, 2048, 2048)
         assert types[f"blk.{i}.ffn_gate"] == (g.TYPE_Q4_K, 2048, 5632)
     assert types["output"] == (g.TYPE_Q6_K, 2048, 32000)
+
+
+def test_tinyllama_model_size_matches_published():
+    """llama-bench reports the TinyLlama-1.1B Q4_K_M model as 636.18 MiB (README.md:192,
+    the sum of ggml_nbytes over every tensor). The bench's mix — the matmul chain, the
+    Q4_K token_embd and the f32 norms (2 per layer + output_norm) — must reproduce it
+    within the print's rounding and a 6 KB residual (667,078,656 B = 636.174 MiB)."""
+    m = bench.MODELS["tinyllama-1.1b"]
+    E, L, V = m["E"], m["L"], m["V"]
+    total = _bytes("tinyllama-1.1b")                      # every MUL_MAT weight incl. output
+    total += V * (E // 256) * g.BLOCK_BYTES[g.TYPE_Q4_K]  # token_embd (Q4_K)
+    total += (2 * L + 1) * E * 4                          # attn_norm, ffn_norm, output_norm (f32)
+    mib = total / 2 ** 20
+    assert abs(mib - 636.18) <= 0.01, mib

@@ -1,7 +1,7 @@
-"""Multi-process (world_size 2, gloo, CPU) tests of the row-split path: shard layout,
-the packed per-stage gather / all-reduce, and that the reassembled outputs are
-bit-identical to the single-process result. The per-rank compute here is the
-oracle (CPU); on GPUs the same StageGather runs over RCCL with the HIP GEMV."""
+"""Multi-process (gloo, CPU) tests of the row-split decode token: the TokenSplit plan
+(ggml_mi355x/rowsplit.py) executed rank by rank with the oracle's ops and a gloo
+all_gather standing in for the backend's ALL_GATHER node (RCCL on GPUs), bit-identical
+to the single-process oracle token at world 2, 4 and 8."""
 import os
 import socket
 
@@ -17,61 +17,100 @@ def free_port():
     return p
 
 
-def test_shard_rows_cover_and_align():
-    from ggml_mi355x.rowsplit import shard_rows
-    for n in (0, 1, 7, 8, 255, 256, 2048, 5632, 32000, 128256):
-        for world in (1, 2, 3, 4, 8):
-            got = [shard_rows(n, world, r) for r in range(world)]
-            covered = []
-            for r0, r1, per in got:
-                assert per % 8 == 0 and r1 - r0 <= per
-                assert r0 % 8 == 0 or r0 == r1
-                covered.extend(range(r0, r1))
-            assert covered == list(range(n))
+# ------------------------------------------------ the dependent row-split decode token
+SPLIT_HP = dict(n_embd=512, n_layer=2, n_head=8, n_head_kv=2, head_dim=64, n_ff=768, n_vocab=1024, eps=1e-5,
+                freq_base=10000.0)
+SPLIT_CTX, SPLIT_TOKENS = 32, (5, 77, 1000)
 
 
-def _worker(rank, world, port, collective, results):
+def _split_token_worker(rank, world, port, results):
     import torch
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        from ggml_mi355x.rowsplit import StageGather
-        from oracle import kq_oracle as O
-        from oracle import kq_oracle_np as N
-        rng = np.random.default_rng(123)
-        K = 2048
-        specs = [(12, 2048), (12, 256), (14, 256)]  # q, k, v(Q6_K) of a TinyLlama layer
-        ws = [N.random_blocks(rng, t, n, K) for t, n in specs]
-        x = rng.standard_normal((1, K)).astype(np.float32)
-        sg = StageGather([n for _, n in specs], world, rank, torch.device("cpu"), collective=collective)
-        for i, ((t, n), w) in enumerate(zip(specs, ws)):
-            r0, r1, _ = sg.shards[i]
-            part = O.mul_mat(t, w[r0:r1], x)[0] if r1 > r0 else np.zeros(0, np.float32)
-            sg.local_view(i).copy_(torch.from_numpy(part))
-        sg.exchange()
-        ok = True
-        for i, ((t, n), w) in enumerate(zip(specs, ws)):
-            full = O.mul_mat(t, w, x)[0]
-            got = sg.output(i).numpy()
-            ok &= bool((got.view(np.uint32) == full.view(np.uint32)).all())
-        results[rank] = ok
+        from ggml_mi355x.rowsplit import TokenSplit
+        from tests import llama_model as LM
+        from tests.split_token import local_cache, local_model, split_decode_token
+        hp = SPLIT_HP
+        w = LM.build(hp, seed=4)
+        model, _ = LM.oracle_model(hp, w, SPLIT_CTX)
+        split = TokenSplit(hp, world, rank)
+        lm = local_model(model, split)
+        cache = local_cache(hp, split, SPLIT_CTX)
+
+        def gather(local):  # the ALL_GATHER node: rank-ordered concatenation
+            t = torch.from_numpy(np.ascontiguousarray(local, np.float32))
+            parts = [torch.empty_like(t) for _ in range(world)]
+            dist.all_gather(parts, t)
+            return torch.cat(parts).numpy()
+
+        out = []
+        for pos, tok in enumerate(SPLIT_TOKENS):
+            tr = []
+            logits = split_decode_token(lm, split, tok, pos, cache, gather, full_trace=tr)
+            out.append((logits.view(np.uint32).copy(), [{k: v.view(np.uint32).copy() for k, v in d.items()} for d in tr]))
+        results[rank] = out
     finally:
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("collective", ["all_gather", "all_reduce"])
-def test_rowsplit_gloo_world2_bit_exact(collective):
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_rowsplit_decode_token_gloo_bit_exact(world):
+    """Every rank of a row-split decode token (TokenSplit: q/k/v rows by head, attention
+    on the rank's KV heads, row slices of o / gate / up / down / output, ALL_GATHER after
+    each stage), run over gloo with the oracle's ops, reproduces the single-process
+    oracle token bit for bit: the logits and every gathered vector, at 3 dependent
+    positions of one KV cache. world 8 > n_head_kv 2: 4 ranks share each KV head."""
     import torch.multiprocessing as mp
+    from oracle import kq_ops_oracle as OO
+    from tests import llama_model as LM
+    hp = SPLIT_HP
+    w = LM.build(hp, seed=4)
+    model, cache = LM.oracle_model(hp, w, SPLIT_CTX)
+    ref = []
+    for pos, tok in enumerate(SPLIT_TOKENS):
+        tr = []
+        logits, _ = OO.decode_token(model, tok, pos, cache, n_threads=2, full_trace=tr)
+        ref.append((logits.view(np.uint32), tr))
     ctx = mp.get_context("spawn")
     mgr = ctx.Manager()
     results = mgr.dict()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, collective, results)) for r in range(2)]
+    procs = [ctx.Process(target=_split_token_worker, args=(r, world, port, results)) for r in range(world)]
     for p in procs:
         p.start()
     for p in procs:
-        p.join(timeout=240)
+        p.join(timeout=300)
         assert p.exitcode == 0
-    assert dict(results) == {0: True, 1: True}
+    assert sorted(results.keys()) == list(range(world))
+    for r in range(world):
+        for (lg, tr), (rlg, rtr) in zip(results[r], ref):
+            assert (lg == rlg).all()
+            for d, rd in zip(tr, rtr):
+                for k in ("att", "ffn_inp", "glu", "x"):
+                    assert (d[k] == rd[k].view(np.uint32)).all(), (r, k)
+
+
+def test_token_split_plan():
+    """TokenSplit row ranges: disjoint and covering for the row-split matrices, the KV
+    heads of the rank's query heads, and rejection of splits the plan cannot express."""
+    from ggml_mi355x.rowsplit import TokenSplit
+    for hp in (SPLIT_HP, dict(SPLIT_HP, n_embd=2048, n_head=32, n_head_kv=4, n_ff=5632, n_vocab=32000),
+               dict(SPLIT_HP, n_embd=8192, n_head=64, n_head_kv=8, n_ff=28672, n_vocab=128256, head_dim=128)):
+        group = hp["n_head"] // hp["n_head_kv"]
+        for world in (1, 2, 4, 8):
+            sp = [TokenSplit(hp, world, r) for r in range(world)]
+            for name, n in (("attn_q", hp["n_head"] * hp["head_dim"]), ("attn_output", hp["n_embd"]),
+                            ("ffn_gate", hp["n_ff"]), ("ffn_down", hp["n_embd"]), ("output", hp["n_vocab"])):
+                cov = [i for s in sp for i in range(*s.rows[name])]
+                assert cov == list(range(n)), (name, world)
+            for s in sp:
+                assert s.n_head == hp["n_head"] // world
+                assert s.kv0 == s.q0 // group and s.kv1 == (s.q1 - 1) // group + 1
+                assert s.rows["attn_k"] == (s.kv0 * hp["head_dim"], s.kv1 * hp["head_dim"])
+    with pytest.raises(ValueError):
+        TokenSplit(dict(SPLIT_HP, n_head=6), 4, 0)
+    with pytest.raises(ValueError):
+        TokenSplit(dict(SPLIT_HP, n_head_kv=3, n_head=24), 2, 0)

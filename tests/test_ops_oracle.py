@@ -206,3 +206,37 @@ def test_rms_norm_order_split_inputs(O, n):
         y = O.rms_norm(r, float(eps))
         scale = np.float32(1.0) / np.sqrt(np.float32(m + eps))
         assert (y.view(np.uint32) == (r * scale).astype(np.float32).view(np.uint32)).all()
+
+
+def test_fast_binary16_ops_match_restatement():
+    """The CPU baseline's binary16 FMA / add (double TwoSum with the midpoint fix,
+    oracle/kq_cpu_simd.c) equal the exact 128-bit restatement on 4M random finite
+    triples (subnormals, signed zeros, same-exponent operands included)."""
+    from oracle import kq_ops_oracle as O
+    L = O.lib()
+    assert L.kqo_f16_fast_check(4_000_000, 0x9E3779B97F4A7C15) == 0
+    # exact ties broken by a tiny addend: p = 1 + 2^-11 (a binary16 midpoint), c tiny
+    one_plus = 0x3C00 | 1  # 1 + 2^-10
+    half_ulp = 0x3800      # 0.5
+    for c in (0x0001, 0x8001, 0x0000, 0x8000):
+        assert L.kqo_f16_fma_fast(one_plus, half_ulp, c) == L.kqo_f16_fma(one_plus, half_ulp, c)
+
+
+@pytest.mark.parametrize("pos,n_threads", [(0, 1), (5, 3), (40, 4), (127, 8)])
+def test_fast_attention_matches_restatement(pos, n_threads):
+    """kqo_attn_decode_fast (heads over the pool) == kqo_attn_decode, output and caches."""
+    from oracle import kq_ops_oracle as O
+    rng = np.random.default_rng(pos)
+    nh, nkv, hd, n_ctx = 8, 2, 64, 128
+    kc = rng.integers(0, 0x4600, (n_ctx, nkv * hd)).astype(np.uint16)  # |x| < 6: finite sums
+    vc = rng.integers(0, 0x4600, (nkv * hd, n_ctx)).astype(np.uint16)
+    kc[:, ::3] |= 0x8000
+    vc[::5] |= 0x8000
+    q = rng.standard_normal(nh * hd).astype(np.float32)
+    k = rng.standard_normal(nkv * hd).astype(np.float32)
+    v = rng.standard_normal(nkv * hd).astype(np.float32)
+    kc2, vc2 = kc.copy(), vc.copy()
+    a = O.attn_decode(q, k, v, kc, vc, pos, nh, nkv, hd, 0.125)
+    b = O.attn_decode(q, k, v, kc2, vc2, pos, nh, nkv, hd, 0.125, fast_threads=n_threads)
+    assert (a.view(np.uint32) == b.view(np.uint32)).all()
+    assert (kc == kc2).all() and (vc == vc2).all()
