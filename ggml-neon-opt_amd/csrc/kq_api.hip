@@ -827,11 +827,79 @@ static void die(const char *fn, const char *msg) {
     abort();
 }
 
+// ---- the trait-table surface (ggml_vec_dot_t / ggml_from_float_t): called by
+// ggml-cpu's mul_mat from nth threads at once with HOST pointers into its own buffers
+// (src0 rows, params->wdata; README.md:121-137, :449), or with device pointers. Each
+// calling thread owns a non-blocking stream on its current device plus device staging;
+// host operands are copied in, results copied out, and only that stream is synchronized,
+// so concurrent callers never serialize on the default stream or share a buffer.
+namespace {
+struct ThreadCtx {
+    int dev = -1;
+    hipStream_t st = nullptr;
+    void *buf = nullptr;
+    size_t cap = 0;
+    ~ThreadCtx() {
+        if (buf) hipFree(buf);
+        if (st) hipStreamDestroy(st);
+    }
+};
+thread_local ThreadCtx t_ctx;
+
+ThreadCtx *thread_ctx(size_t need) {
+    ThreadCtx &c = t_ctx;
+    const int dev = current_device();
+    if (c.dev != dev) {  // the thread moved to another device: new stream and staging there
+        if (c.buf) hipFree(c.buf);
+        if (c.st) hipStreamDestroy(c.st);
+        c.buf = nullptr;
+        c.st = nullptr;
+        c.cap = 0;
+        c.dev = -1;
+        if (hipStreamCreateWithFlags(&c.st, hipStreamNonBlocking) != hipSuccess) return nullptr;
+        c.dev = dev;
+    }
+    if (need > c.cap) {
+        if (c.buf) hipFree(c.buf);
+        c.buf = nullptr;
+        c.cap = 0;
+        if (hipMalloc(&c.buf, need) != hipSuccess) return nullptr;
+        c.cap = need;
+    }
+    return &c;
+}
+
+// True when p is device-accessible memory of the current device (hipMalloc / managed).
+bool on_device(const void *p) {
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, p) != hipSuccess) {
+        (void)hipGetLastError();  // plain pageable host memory: not an error to keep
+        return false;
+    }
+    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+}
+}  // namespace
+
 void mi355x_quantize_row_q8_K(const float *x, void *y, int64_t k) {
     if (k % QK) die(__func__, "k % QK_K != 0");
-    const int rc = mi355x_quantize_q8_K(x, (size_t)k * 4, y, k, 1, nullptr);
-    if (rc) die(__func__, "launch failed");
-    if (hipStreamSynchronize(nullptr) != hipSuccess) die(__func__, "hipStreamSynchronize failed");
+    if (k == 0) return;
+    if (!device_ok()) die(__func__, "no gfx950 device");
+    const size_t xb = (size_t)k * 4, yb = (size_t)(k / QK) * 292;
+    const bool xd = on_device(x), yd = on_device(y);
+    ThreadCtx *c = thread_ctx(((xd ? 0 : xb + 16) + (yd ? 0 : yb) + 255) & ~(size_t)255);
+    if (!c) die(__func__, "stream / staging allocation failed");
+    const float *dx = x;
+    void *dy = y;
+    uint8_t *stage = (uint8_t *)c->buf;
+    if (!xd) {
+        if (hipMemcpyAsync(stage, x, xb, hipMemcpyHostToDevice, c->st) != hipSuccess) die(__func__, "copy in failed");
+        dx = (const float *)stage;
+        stage += (xb + 15) & ~(size_t)15;
+    }
+    if (!yd) dy = stage;
+    if (mi355x_quantize_q8_K(dx, xb, dy, k, 1, c->st)) die(__func__, "launch failed");
+    if (!yd && hipMemcpyAsync(y, dy, yb, hipMemcpyDeviceToHost, c->st) != hipSuccess) die(__func__, "copy out failed");
+    if (hipStreamSynchronize(c->st) != hipSuccess) die(__func__, "hipStreamSynchronize failed");
 }
 
 size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, int64_t ne11) {
@@ -982,10 +1050,28 @@ static void vec_dot_dev(int type, const char *fn, int n, float *s, const void *v
     if (nrc != 1) die(fn, "nrc != 1 unsupported (reference configuration: nrows == 1)");
     if (n <= 0 || n % QK) die(fn, "n % QK_K != 0");
     if (!device_ok()) die(fn, "no gfx950 device");
-    const int rc = mi355x_mul_mat_q8(type, vx, n, 1, mi355x_row_size(type, n), vy, 1,
-                                     mi355x_row_size(MI355X_TYPE_Q8_K, n), s, 4, nullptr);
+    const size_t wb = mi355x_row_size(type, n), qb = mi355x_row_size(MI355X_TYPE_Q8_K, n);
+    const bool xd = on_device(vx), yd = on_device(vy), sd = on_device(s);
+    const size_t need = (xd ? 0 : (wb + 15) & ~(size_t)15) + (yd ? 0 : (qb + 15) & ~(size_t)15) + 16;
+    ThreadCtx *c = thread_ctx(need);
+    if (!c) die(fn, "stream / staging allocation failed");
+    uint8_t *stage = (uint8_t *)c->buf;
+    const void *dx = vx, *dy = vy;
+    if (!xd) {
+        if (hipMemcpyAsync(stage, vx, wb, hipMemcpyHostToDevice, c->st) != hipSuccess) die(fn, "copy in failed");
+        dx = stage;
+        stage += (wb + 15) & ~(size_t)15;
+    }
+    if (!yd) {
+        if (hipMemcpyAsync(stage, vy, qb, hipMemcpyHostToDevice, c->st) != hipSuccess) die(fn, "copy in failed");
+        dy = stage;
+        stage += (qb + 15) & ~(size_t)15;
+    }
+    float *ds = sd ? s : (float *)stage;
+    const int rc = mi355x_mul_mat_q8(type, dx, n, 1, wb, dy, 1, qb, ds, 4, c->st);
     if (rc) die(fn, "launch failed");
-    if (hipStreamSynchronize(nullptr) != hipSuccess) die(fn, "hipStreamSynchronize failed");
+    if (!sd && hipMemcpyAsync(s, ds, 4, hipMemcpyDeviceToHost, c->st) != hipSuccess) die(fn, "copy out failed");
+    if (hipStreamSynchronize(c->st) != hipSuccess) die(fn, "hipStreamSynchronize failed");
 }
 
 void mi355x_vec_dot_q4_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx, const void *vy, size_t by,

@@ -25,6 +25,7 @@ MAX_FUSED = 4
 OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROPE, OP_ATTN_DECODE, OP_ALL_GATHER = range(10)
 MAX_SRC = 8
 FLAG_OUTPUT = 1
+E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_TIMEOUT, E_COMM = 0, -1, -2, -3, -4, -5, -6
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 
@@ -48,7 +49,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
     "mi355x_rope_table_size", "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode",
     "mi355x_comm_id_size", "mi355x_comm_get_unique_id", "mi355x_backend_set_comm", "mi355x_backend_comm_world",
-    "mi355x_backend_set_comm_loopback",
+    "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph",
 )
 
 
@@ -72,6 +73,27 @@ class Tensor(ctypes.Structure):
 Tensor._fields_ = [("type", ctypes.c_int), ("op", ctypes.c_int), ("ne", ctypes.c_int64 * 4),
                    ("nb", ctypes.c_size_t * 4), ("src", ctypes.POINTER(Tensor) * MAX_SRC), ("data", ctypes.c_void_p),
                    ("op_params", ctypes.c_int32 * 8), ("flags", ctypes.c_int32)]
+
+
+class GTensor(ctypes.Structure):
+    """mi355x_gtensor: the ggml_tensor-shaped mirror the lowering reads."""
+    pass
+
+
+GTensor._fields_ = [("type", ctypes.c_int), ("op", ctypes.c_int), ("ne", ctypes.c_int64 * 4),
+                    ("nb", ctypes.c_size_t * 4), ("op_params", ctypes.c_int32 * 16), ("flags", ctypes.c_int32),
+                    ("src", ctypes.POINTER(GTensor) * 10), ("view_src", ctypes.POINTER(GTensor)),
+                    ("view_offs", ctypes.c_size_t), ("data", ctypes.c_void_p), ("name", ctypes.c_char * 64)]
+
+
+class LowerOpts(ctypes.Structure):
+    _fields_ = [("rope_table", ctypes.c_void_p), ("rope_n_pos", ctypes.c_int), ("rope_freq_base", ctypes.c_float),
+                ("rope_freq_scale", ctypes.c_float)]
+
+
+(GOP_NONE, GOP_GET_ROWS, GOP_RMS_NORM, GOP_MUL, GOP_ADD, GOP_MUL_MAT, GOP_ROPE, GOP_SET_ROWS, GOP_SOFT_MAX, GOP_GLU,
+ GOP_RESHAPE, GOP_VIEW, GOP_PERMUTE, GOP_TRANSPOSE, GOP_CONT, GOP_CPY) = range(16)
+GLU_SWIGLU = 2
 
 
 class GemvExt(ctypes.Structure):
@@ -167,6 +189,10 @@ def lib():
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
               "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode"):
         getattr(L, n).restype = i32
+    L.mi355x_lower_ggml_graph.argtypes = [ctypes.POINTER(ctypes.POINTER(GTensor)), i32, ctypes.POINTER(LowerOpts),
+                                          ctypes.POINTER(Tensor), i32, ctypes.POINTER(ctypes.POINTER(Tensor)), i32,
+                                          ctypes.POINTER(i32)]
+    L.mi355x_lower_ggml_graph.restype = i32
     L.mi355x_comm_id_size.argtypes = []
     L.mi355x_comm_id_size.restype = sz
     L.mi355x_comm_get_unique_id.argtypes = [vp]
@@ -523,6 +549,20 @@ class Backend:
             self.close()
         except Exception:
             pass
+
+
+def lower_ggml_graph(gnodes, rope_table_ptr, rope_n_pos, freq_base, freq_scale=1.0, arena_cap=None):
+    """mi355x_lower_ggml_graph over a list of GTensor nodes (graph order). Returns
+    (status, [Tensor node list], arena) — the arena keeps the nodes alive."""
+    n = len(gnodes)
+    arr = (ctypes.POINTER(GTensor) * max(1, n))(*[ctypes.pointer(t) for t in gnodes])
+    cap = arena_cap or (4 * n + 64)
+    arena = (Tensor * cap)()
+    out = (ctypes.POINTER(Tensor) * cap)()
+    nn = ctypes.c_int(0)
+    opts = LowerOpts(rope_table_ptr, rope_n_pos, freq_base, freq_scale)
+    rc = int(lib().mi355x_lower_ggml_graph(arr, n, ctypes.byref(opts), arena, cap, out, cap, ctypes.byref(nn)))
+    return rc, [out[i].contents for i in range(nn.value)], (arena, out)
 
 
 def comm_unique_id() -> bytes:

@@ -51,7 +51,12 @@ class LlamaDecoder:
 
     HOST_SLOTS = 1024
 
-    def __init__(self, backend: Backend, hp: dict, weights: dict, n_ctx: int, fuse: bool = True, split=None):
+    def __init__(self, backend: Backend, hp: dict, weights: dict, n_ctx: int, fuse: bool = True, split=None,
+                 rope_src: str = "row"):
+        """backend None: describe only (host tensors, no device work) — the node list
+        the ggml lowering must reproduce (tests/test_lower.py). rope_src "row": the
+        attention reads the position's rope row staged with the inputs (the default);
+        "table": the whole table (what mi355x_lower_ggml_graph passes)."""
         import torch
         self.b, self.hp, self.w, self.n_ctx, self.split = backend, hp, weights, n_ctx, split
         dev = weights["output_norm"].device
@@ -73,8 +78,11 @@ class LlamaDecoder:
         # the row is the table's row, so the values are those of the device table.
         self.inp = buf(2 + hd, torch.int32)
         self.token, self.pos = self.inp[0:1], self.inp[1:2]
-        self.table = rope_table(n_ctx, hd, hp["freq_base"], 1.0, device=dev, stream=backend.stream)
-        self._table_host = self.table.cpu().reshape(n_ctx, hd).view(torch.int32)
+        if backend is not None:
+            self.table = rope_table(n_ctx, hd, hp["freq_base"], 1.0, device=dev, stream=backend.stream)
+            self._table_host = self.table.cpu().reshape(n_ctx, hd).view(torch.int32)
+        else:
+            self.table = torch.zeros(n_ctx * hd, dtype=f32, device=dev)
         self.k_cache = [torch.zeros((n_ctx, kvw), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
         self.v_cache = [torch.zeros((kvw, n_ctx), dtype=torch.int16, device=dev) for _ in range(hp["n_layer"])]
         self._bufs = []
@@ -121,7 +129,10 @@ class LlamaDecoder:
         eps_bits = [f32_bits(hp["eps"])]
         tok = leaf(self.token, TYPE_I32, 1)
         pos = leaf(self.pos, TYPE_I32, 1)
-        tab = leaf(self.inp[2:], TYPE_F32, hd, 1)  # the position's rope row (ne1 = 1)
+        if rope_src == "row":
+            tab = leaf(self.inp[2:], TYPE_F32, hd, 1)  # the position's rope row (ne1 = 1)
+        else:
+            tab = leaf(self.table, TYPE_F32, hd, n_ctx)
         et, ew = weights["token_embd"]
         emb_t = leaf(ew, et, E, ew.shape[0], row_stride=ew.stride(0) * ew.element_size())
         x, xb = node(OP_GET_ROWS, E, [emb_t, tok])
@@ -164,6 +175,8 @@ class LlamaDecoder:
             _, self.logits = gather(lg, V // world, flags=FLAG_OUTPUT)
         self._tensors = T
         self._arr = (ctypes.POINTER(type(T[0])) * len(self.nodes))(*[ctypes.pointer(n) for n in self.nodes])
+        if backend is None:
+            return
         # pinned staging slots for (token, pos): a slot is reused only after the stream
         # has been synchronized (the H2D copies are asynchronous)
         self._host = torch.zeros((self.HOST_SLOTS, 2 + hd), dtype=torch.int32).pin_memory()

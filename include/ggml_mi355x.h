@@ -105,17 +105,23 @@ int mi355x_device_available(void);
 /* Device mirror of ggml_from_float_t for GGML_TYPE_Q8_K
  * (type_traits_cpu[Q8_K].from_float = quantize_row_q8_K -> quantize_row_q8_K_ref).
  * x: k floats, y: k/256 block_q8_K. Bit-exact with the reference
- * (aarch64 build: iscale*x + 12582912.f contracted to one fma). Runs on the
- * default stream and returns after completion. Aborts if k % 256 != 0. */
+ * (aarch64 build: iscale*x + 12582912.f contracted to one fma). x and y may be host
+ * or device pointers (ggml-cpu passes src1 rows and params->wdata); runs on the
+ * calling thread's own stream and returns after it completes (reentrant, see the
+ * vec_dot entries below). Aborts if k % 256 != 0, as GGML_ASSERT does. */
 void mi355x_quantize_row_q8_K(const float *x, void *y, int64_t k);
 
 /* Device mirror of ggml_vec_dot_t for Q4_K x Q8_K / Q5_K x Q8_K / Q6_K x Q8_K
  * (README.md:449: void (int n, float *s, size_t bs, const void *vx, size_t bx,
  * const void *vy, size_t by, int nrc)). n % 256 == 0, nrc == 1 (the measured
  * reference configuration: no I8MM, README.md:677, so nrows == 1); bs/bx/by are
- * unused exactly as upstream. s, vx, vy are device pointers. Runs on the default
- * stream and returns after completion. The Q4_K result is bit-identical to the
- * reference NEON function's fp32 output (README.md:725-777, fmsub :551, fmadd :614). */
+ * unused exactly as upstream. s, vx, vy may be host pointers (ggml-cpu's src0 rows and
+ * params->wdata, as type_traits_cpu[type].vec_dot is called from mul_mat_one_chunk)
+ * or device pointers, in any mix. Reentrant: every calling thread uses its own HIP
+ * stream and staging buffer on its current device (ggml's nth threads call it at once,
+ * README.md:125-131), and the call returns after that stream completes (no default-
+ * stream synchronization). The Q4_K result is bit-identical to the reference NEON
+ * function's fp32 output (README.md:725-777, fmsub :551, fmadd :614). */
 void mi355x_vec_dot_q4_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx,
                               const void *vy, size_t by, int nrc);
 void mi355x_vec_dot_q5_K_q8_K(int n, float *s, size_t bs, const void *vx, size_t bx,
@@ -362,6 +368,56 @@ int mi355x_backend_set_fusion(mi355x_backend_t backend, int enable);
  * Returns 0 (GGML_STATUS_SUCCESS) or an error code. */
 int mi355x_backend_graph_compute(mi355x_backend_t backend, mi355x_tensor *const *nodes,
                                  int n_nodes, int use_graph);
+
+/* ------------------------------------------- ggml graph lowering (host only) */
+/* The adapter side of the drop-in: a ggml_tensor-shaped mirror
+ * that a ggml backend's graph_compute fills from the ggml_cgraph it is handed
+ * (ggml_backend_sched_compute_splits -> iface.graph_compute, README.md:162-163),
+ * one mirror per ggml node/leaf with the same fields (type, ne, nb, op, op_params,
+ * src, view_src/view_offs, data), and the lowering of llm_build_llama's decode
+ * node sequence onto this backend's node list:
+ *   GET_ROWS, RMS_NORM, MUL, ADD, MUL_MAT (K-quant x f32), GLU(SWIGLU, split) map 1:1;
+ *   RESHAPE / VIEW / PERMUTE / TRANSPOSE are aliases (no node);
+ *   the non-flash attention block — ROPE(Q), ROPE(K), SET_ROWS(K cache), SET_ROWS
+ *   (V cache), MUL_MAT(K cache, Q), SOFT_MAX(kq, mask, scale), MUL_MAT(V cache, kq),
+ *   PERMUTE, CONT — becomes ONE ATTN_DECODE node (rope table from the caller);
+ *   [up, gate] MUL_MAT pairs read by SWIGLU(gate, up) are emitted as [gate, up]
+ *   (independent nodes; the order the fused gate/up launch takes).
+ * The op numbering is this library's (the adapter maps GGML_OP_* by name). */
+enum mi355x_gop {
+    MI355X_GOP_NONE = 0, MI355X_GOP_GET_ROWS, MI355X_GOP_RMS_NORM, MI355X_GOP_MUL, MI355X_GOP_ADD,
+    MI355X_GOP_MUL_MAT, MI355X_GOP_ROPE, MI355X_GOP_SET_ROWS, MI355X_GOP_SOFT_MAX, MI355X_GOP_GLU,
+    MI355X_GOP_RESHAPE, MI355X_GOP_VIEW, MI355X_GOP_PERMUTE, MI355X_GOP_TRANSPOSE, MI355X_GOP_CONT,
+    MI355X_GOP_CPY,
+};
+#define MI355X_GLU_SWIGLU 2  /* op_params[0] of a GLU node (ggml_glu_op GGML_GLU_OP_SWIGLU) */
+typedef struct mi355x_gtensor {
+    int type;                       /* ggml_type numbering (F32 0, F16 1, Q4_K 12, ..., I32 26, I64 27) */
+    int op;                         /* enum mi355x_gop                           */
+    int64_t ne[4];
+    size_t nb[4];
+    int32_t op_params[16];          /* as ggml stores them (floats as bits)      */
+    int32_t flags;                  /* MI355X_TENSOR_FLAG_OUTPUT for graph outputs */
+    struct mi355x_gtensor *src[10];
+    struct mi355x_gtensor *view_src;
+    size_t view_offs;
+    void *data;                     /* device pointer (leaves, and nodes' outputs) */
+    char name[64];
+} mi355x_gtensor;
+typedef struct {
+    void *rope_table;               /* f32 [head_dim, n_pos] from mi355x_rope_table  */
+    int rope_n_pos;                 /* its rows (>= the KV cache size)           */
+    float rope_freq_base, rope_freq_scale; /* the table's parameters (checked against ROPE) */
+} mi355x_lower_opts;
+/* Lowers `n` ggml nodes (graph order) into backend nodes. Tensors are written into
+ * `arena` (cap entries: nodes and the leaf mirrors they reference); `nodes_out`
+ * (cap nodes_cap) receives the node list for mi355x_backend_graph_compute and
+ * *n_nodes its length. Returns 0, MI355X_E_UNSUPPORTED (a node or pattern this
+ * backend does not take: the caller leaves the graph to another backend) or
+ * MI355X_E_INVAL / MI355X_E_WORKSPACE (arena or output too small). */
+int mi355x_lower_ggml_graph(mi355x_gtensor *const *gnodes, int n, const mi355x_lower_opts *opts,
+                            mi355x_tensor *arena, int arena_cap, mi355x_tensor **nodes_out, int nodes_cap,
+                            int *n_nodes);
 
 /* Row split over one process per GPU. RCCL is resolved at run time
  * from the librccl.so.1 already loaded in the process, or /opt/rocm's (dlopen): the
