@@ -20,11 +20,10 @@ Q4_K), each GEMV including its bit-exact Q8_K activation quantization. Weights a
 synthetic random blocks of the real shapes (no network for the GGUF), their fp16
 scales sized so the residual stream keeps an O(1) RMS; norms f32 in [0.8, 1.2].
 
-"chain" workload (--workload chain; the row-split, GGUF-file and kernel A/B modes):
-the per-token MUL_MAT chain only, every stage reading the previous stage's output
+"chain" workload (--workload chain; the GGUF-file and kernel A/B modes): the
+per-token MUL_MAT chain only, every stage reading the previous stage's output
 (attn_q -> attn_output -> ffn_gate -> ffn_down -> next layer's q/k/v ... -> output);
-q/k/v and gate/up fuse into one launch each, 89 launches per token from one hipGraph
-(--impl chain: ONE persistent kq_chain launch per token instead).
+q/k/v and gate/up fuse into one launch each, 89 launches per token from one hipGraph.
 
 "roofline": the dominant kernel's algorithmic bytes per launch over its event-timed
 launch duration; "traffic": its HBM read per launch from the committed rocprofv3
@@ -556,9 +555,8 @@ def main():
     ap.add_argument("--no-graph", action="store_true")
     ap.add_argument("--gguf", default=None,
                     help="run the chain on a real llama-architecture GGUF file's weights (Q4_K/Q5_K/Q6_K)")
-    ap.add_argument("--impl", default="auto", choices=["auto", "rows", "chain", "tasks"],
-                    help="auto/rows: kq_rows per stage (hipGraph replay); chain: one persistent "
-                         "kq_chain launch per token; tasks: kq_gemv per stage")
+    ap.add_argument("--impl", default="auto", choices=["auto", "rows", "tasks"],
+                    help="auto/rows: kq_rows per stage (hipGraph replay); tasks: kq_gemv per stage")
     ap.add_argument("--no-prefill", action="store_true")
     ap.add_argument("--workload", default="token", choices=["token", "chain"],
                     help="token: the full decode graph (tg128: token i at position i of a fresh KV cache); "
@@ -587,7 +585,7 @@ def main():
     torch.cuda.set_device(dev)
     if not g.device_available():
         raise SystemExit("bench: no gfx950 device or libggml_mi355x.so not loadable")
-    g.gemv_impl({"auto": g.GEMV_AUTO, "rows": g.GEMV_ROWS, "chain": g.GEMV_CHAIN, "tasks": g.GEMV_TASKS}[args.impl])
+    g.gemv_impl({"auto": g.GEMV_AUTO, "rows": g.GEMV_ROWS, "tasks": g.GEMV_TASKS}[args.impl])
 
     def barrier():
         if world > 1:
@@ -673,7 +671,7 @@ def main():
     if rank == 0:
         # roofline of the dominant GEMV kernel, from per-launch kernel timestamps
         roof = None
-        gemv = {k: v for k, v in per.items() if "kq_rows" in k or "kq_gemv" in k or "kq_chain" in k}
+        gemv = {k: v for k, v in per.items() if "kq_rows" in k or "kq_gemv" in k}
         if gemv:
             dom = max(gemv, key=lambda k: gemv[k]["ms"])
             d = per[dom]
@@ -722,8 +720,6 @@ def main():
                         "residual/swiglu epilogues), kq_rows + kq_attn_decode" +
                         (", RCCL ncclAllGather per stage (row split)" if rowsplit else "") + ", " +
                         ("hipGraph replay" if not args.no_graph else "eager"))
-        elif args.impl == "chain":
-            executor = "kq_chain: 1 persistent launch per token (tagged write-through hand-off per stage)"
         else:
             executor = f"{'kq_gemv' if args.impl == 'tasks' else 'kq_rows'}: 1 launch per stage" + \
                 ("" if args.no_graph else ", hipGraph replay")
@@ -746,7 +742,7 @@ def main():
                        "stages_per_token": chain.launches(),
                        "executor": executor,
                        "parallelism": (f"rowsplit{world}" if rowsplit else f"replicas x{world}"),
-                       "hipgraph": args.impl != "chain" and not args.no_graph},
+                       "hipgraph": not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
             "effective_GBps": round(per_gpu_rate * local_bytes / 1e9, 1),
             # the whole token (every launch, gap and gather included) against the HBM roofline, per GPU

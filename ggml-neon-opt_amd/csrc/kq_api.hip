@@ -25,7 +25,6 @@ __global__ void kq_rows(const RowsArgs a);
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TYPE>
 __global__ void kq_mmq(const MmqArgs a);
-__global__ void kq_chain(const ChainArgs a);
 
 namespace {
 
@@ -333,7 +332,6 @@ bool rows_enabled() {
         const char *e = getenv("MI355X_GEMV_IMPL");  // "tasks" / "rows": A/B runs
         v = (e && strcmp(e, "tasks") == 0)  ? MI355X_GEMV_TASKS
             : (e && strcmp(e, "rows") == 0)  ? MI355X_GEMV_ROWS
-            : (e && strcmp(e, "chain") == 0) ? MI355X_GEMV_CHAIN
                                              : MI355X_GEMV_AUTO;
         int expect = -1;
         g_impl.compare_exchange_strong(expect, v);
@@ -342,7 +340,6 @@ bool rows_enabled() {
     return v != MI355X_GEMV_TASKS;
 }
 
-bool chain_enabled() { return rows_enabled() && g_impl.load() == MI355X_GEMV_CHAIN; }
 
 template <int TM, bool FQ, int PR>
 rows_fn rows_inst() {
@@ -505,82 +502,6 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
         timing_log(rows_name(pl), rows_bytes(a, pl.fusedq), e0, e1);
     } else {
         hipLaunchKernelGGL(pl.fn, pl.grid, dim3(ROWS_WAVES * 64), pl.lds, stream, a);
-    }
-    const hipError_t e = hipGetLastError();
-    return e == hipSuccess ? MI355X_OK : (int)e;
-}
-
-// ------------------------------------------------------------ persistent decode chain
-int plan_chain_stage(const mi355x_gemv_desc *d, int n, int64_t K, ChainStage &cs, ChainFit &fit) {
-    RowsPlan rp;
-    // the first `pollers` waves of every workgroup fetch and quantize the activation
-    // (no weight DMAs queued ahead of their polls); the others stream the rows
-    const int nb = (int)(K / QK);
-    const int pollers = chain_pollers(nb);
-    const int rc = plan_rows(d, n, K, true, rp, ROWS_WAVES - pollers);
-    if (rc) return rc;
-    const RowsArgs &a = rp.a;
-    memset(&cs, 0, sizeof(cs));
-    cs.pollers = pollers;
-    cs.n_desc = a.n_desc;
-    cs.nb = a.nb;
-    cs.bR = a.bR;
-    cs.waves_total = a.waves_total;
-    for (int i = 0; i <= MI355X_MAX_FUSED; ++i) cs.wave_prefix[i] = a.wave_prefix[i];
-    for (int i = 0; i < MI355X_MAX_FUSED; ++i) {
-        cs.rbase[i] = a.rbase[i];
-        cs.rrem[i] = a.rrem[i];
-        cs.type[i] = a.type[i];
-        cs.w[i] = a.w[i];
-        cs.y[i] = a.y[i];
-    }
-    fit.nb = fit.nb > a.nb ? fit.nb : a.nb;
-    fit.tmask |= rp.tmask;
-    fit.recs = fit.recs > a.bR * a.nb ? fit.recs : a.bR * a.nb;
-    fit.rpw = fit.rpw > a.rpw ? fit.rpw : a.rpw;
-    for (int i = 0; i < a.n_desc; ++i) {
-        const double rows = (double)a.rbase[i] * (a.wave_prefix[i + 1] - a.wave_prefix[i]) + a.rrem[i];
-        fit.bytes += rows * a.nb * block_bytes(a.type[i]) + rows * 4.0;
-    }
-    fit.bytes += (double)a.nb * QK * 4.0;
-    return MI355X_OK;
-}
-
-int chain_layout(const ChainFit &fit, ChainArgs &a, size_t &lds) {
-    a.act = 0;  // two activation buffers: stage s uses act + (s & 1) * act_stride
-    a.act_stride = fit.nb * Q8L_STRIDE;
-    a.ring = 2 * a.act_stride;
-    a.ring_stride = rows_ring(fit.tmask);
-    a.recs = a.ring + ROWS_WAVES * a.ring_stride;
-    a.recs_stride = fit.recs * 16;
-    a.outs = a.recs + ROWS_WAVES * a.recs_stride;
-    a.outs_stride = (fit.rpw * 4 + 15) & ~15;
-    a.sig = a.outs + ROWS_WAVES * a.outs_stride;  // streaming waves done with their stage (counter)
-    {
-        const char *e = getenv("MI355X_CHAIN_PRE");  // experiment knob: prefetched steps per wave
-        a.pre = e ? atoi(e) : 2;
-    }
-    const size_t total = (size_t)a.sig + 16;
-    if (total > kMaxLds) return MI355X_E_UNSUPPORTED;
-    // more than half a CU's LDS: one workgroup per CU, all of them resident
-    lds = total > kMaxLds / 2 + 1024 ? total : kMaxLds / 2 + 1024;
-    return MI355X_OK;
-}
-
-int launch_chain(const ChainArgs &a, size_t lds, double bytes, hipStream_t stream) {
-    if (a.n_stages <= 0) return MI355X_OK;
-    if (!device_ok()) return MI355X_E_NODEVICE;
-    allow_lds((const void *)kq_chain, lds);
-    const dim3 grid((unsigned)num_cus());
-    ChainArgs aa = a;
-    aa.stamps = g_stamps;
-    aa.stamps_cap = g_stamps_cap;
-    hipEvent_t e0, e1;
-    if (timing_slot(stream, e0, e1)) {
-        hipExtLaunchKernelGGL(kq_chain, grid, dim3(ROWS_WAVES * 64), (uint32_t)lds, stream, e0, e1, 0, aa);
-        timing_log("kq::kq_chain", bytes, e0, e1);
-    } else {
-        hipLaunchKernelGGL(kq_chain, grid, dim3(ROWS_WAVES * 64), lds, stream, aa);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
@@ -1012,7 +933,7 @@ int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, i
 }
 
 int mi355x_gemv_impl(int impl) {
-    if (impl < MI355X_GEMV_AUTO || impl > MI355X_GEMV_CHAIN) return MI355X_E_INVAL;
+    if (impl < MI355X_GEMV_AUTO || impl > MI355X_GEMV_ROWS) return MI355X_E_INVAL;
     rows_enabled();  // resolve the environment default first
     return g_impl.exchange(impl);
 }

@@ -21,18 +21,6 @@
 #include "kq_common.h"
 #include "kq_internal.h"
 
-// A node list planned as one persistent kq_chain launch (kq_chain.hip).
-struct ChainCache {
-    std::vector<uint64_t> key;
-    bool ok = false;  // key planned; false: not eligible, use per-stage launches
-    uint8_t *d_stages = nullptr;  // stage table, kq::kChainSlotBytes per stage
-    uint32_t *sync = nullptr;  // epoch, finished workgroups, timeout flag
-    std::vector<void *> bus;
-    kq::ChainArgs args{};
-    size_t lds = 0;
-    double bytes = 0;
-};
-
 struct mi355x_backend {
     int device = 0;
     hipStream_t stream = nullptr;
@@ -42,8 +30,6 @@ struct mi355x_backend {
     std::vector<uint64_t> graph_key;
     hipGraph_t graph = nullptr;
     hipGraphExec_t graph_exec = nullptr;
-    ChainCache chain;
-    std::vector<uint32_t *> old_sync;
     bool fuse = true;
     ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
     int rank = 0, world = 0;
@@ -387,14 +373,6 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
     return 0;
 }
 
-void drop_chain(mi355x_backend *b) {
-    ChainCache &c = b->chain;
-    if (c.d_stages) hipFree(c.d_stages);
-    for (void *p : c.bus) hipFree(p);
-    if (c.sync) b->old_sync.push_back(c.sync);  // its timeout flag is still reported once
-    c = ChainCache();
-}
-
 std::vector<uint64_t> graph_key_of(mi355x_tensor *const *nodes, int n_nodes) {
     std::vector<uint64_t> key;
     key.reserve((size_t)n_nodes * 16);
@@ -416,118 +394,6 @@ std::vector<uint64_t> graph_key_of(mi355x_tensor *const *nodes, int n_nodes) {
         for (int d = 0; d < 4; ++d) key.push_back((uint64_t)t->nb[d]);
     }
     return key;
-}
-
-bool overlaps(uintptr_t a0, uintptr_t a1, uintptr_t b0, uintptr_t b1) { return a0 < b1 && b0 < a1; }
-
-// Plan the node list as one kq_chain launch. Eligible: >= 2 launches, every one a
-// decode stage (ne11 == 1) that kq_rows takes with the fused quantizer; each
-// stage's activation is either exactly an earlier node's output (read from that
-// node's bus: a true RAW dependency, honoured by the hand-off) or memory that no
-// node of the list writes; outputs pairwise disjoint. Anything else keeps the
-// per-stage launches, which are stream-ordered.
-int plan_chain(mi355x_backend *b, mi355x_tensor *const *nodes, int n_nodes, const std::vector<Launch> &launches) {
-    ChainCache &c = b->chain;
-    if (launches.size() < 2) return MI355X_E_UNSUPPORTED;
-    struct Range {
-        uintptr_t a0, a1;
-    };
-    std::vector<Range> dst;
-    for (int i = 0; i < n_nodes; ++i) {
-        const mi355x_tensor *t = nodes[i];
-        if (t->op != MI355X_OP_MUL_MAT || t->src[1]->ne[1] != 1) return MI355X_E_UNSUPPORTED;
-        dst.push_back({(uintptr_t)t->data, (uintptr_t)t->data + (uintptr_t)t->ne[0] * 4});
-    }
-    for (size_t i = 0; i < dst.size(); ++i)
-        for (size_t j = i + 1; j < dst.size(); ++j)
-            if (overlaps(dst[i].a0, dst[i].a1, dst[j].a0, dst[j].a1)) return MI355X_E_UNSUPPORTED;
-    std::vector<kq::ChainStage> st(launches.size());
-    std::vector<int> node_stage(n_nodes, -1), node_desc(n_nodes, -1);
-    std::vector<int> producer(launches.size(), -1);
-    kq::ChainFit fit;
-    for (size_t li = 0; li < launches.size(); ++li) {
-        const Launch &l = launches[li];
-        const mi355x_tensor *t = nodes[l.first];
-        const mi355x_tensor *w = t->src[0], *x = t->src[1];
-        const int64_t K = w->ne[0];
-        mi355x_gemv_desc d[MI355X_MAX_FUSED];
-        for (int k = 0; k < l.count; ++k) {
-            const mi355x_tensor *n = nodes[l.first + k];
-            d[k].type = n->src[0]->type;
-            d[k].w = n->src[0]->data;
-            d[k].n_rows = n->src[0]->ne[1];
-            d[k].row_stride = n->src[0]->nb[1];
-            d[k].y = (float *)n->data;
-            node_stage[l.first + k] = (int)li;
-            node_desc[l.first + k] = k;
-        }
-        int rc = kq::plan_chain_stage(d, l.count, K, st[li], fit);
-        if (rc) return rc;
-        const uintptr_t x0 = (uintptr_t)x->data, x1 = x0 + (uintptr_t)K * 4;
-        for (int j = 0; j < l.first; ++j)
-            if ((uintptr_t)nodes[j]->data == x0 && nodes[j]->ne[0] >= K) producer[li] = j;
-        if (producer[li] < 0) {
-            if (x0 & 15u) return MI355X_E_UNSUPPORTED;
-            for (const Range &r : dst)
-                if (overlaps(x0, x1, r.a0, r.a1)) return MI355X_E_UNSUPPORTED;
-            st[li].x = (const float *)x->data;
-        }
-    }
-    size_t lds = 0;
-    kq::ChainArgs a{};
-    int rc = kq::chain_layout(fit, a, lds);
-    if (rc) return rc;
-    // buses of the nodes some stage reads
-    for (size_t li = 0; li < launches.size(); ++li) {
-        const int j = producer[li];
-        if (j < 0) continue;
-        kq::ChainStage &ps = st[node_stage[j]];
-        const int k = node_desc[j];
-        if (!ps.bus[k]) {
-            void *p = nullptr;
-            const size_t bytes = (size_t)nodes[j]->ne[0] * 8;
-            if (hipMalloc(&p, bytes) != hipSuccess) return MI355X_E_WORKSPACE;
-            c.bus.push_back(p);
-            if (hipMemsetAsync(p, 0, bytes, b->stream) != hipSuccess) return MI355X_E_WORKSPACE;  // tag 0 never matches
-            ps.bus[k] = (uint32_t *)p;
-        }
-        st[li].xbus = ps.bus[k];
-    }
-    std::vector<uint8_t> table(st.size() * kq::kChainSlotBytes, 0);
-    for (size_t i = 0; i < st.size(); ++i) memcpy(table.data() + i * kq::kChainSlotBytes, &st[i], sizeof(kq::ChainStage));
-    if (hipMalloc(&c.d_stages, table.size()) != hipSuccess) return MI355X_E_WORKSPACE;
-    if (hipMalloc(&c.sync, 64) != hipSuccess) return MI355X_E_WORKSPACE;
-    if (hipMemcpyAsync(c.d_stages, table.data(), table.size(), hipMemcpyHostToDevice, b->stream) != hipSuccess ||
-        hipMemsetAsync(c.sync, 0, 64, b->stream) != hipSuccess || hipStreamSynchronize(b->stream) != hipSuccess)
-        return MI355X_E_WORKSPACE;
-    a.st = c.d_stages;
-    a.n_stages = (int)st.size();
-    a.sync = c.sync;
-    c.args = a;
-    c.lds = lds;
-    c.bytes = fit.bytes;
-    c.ok = true;
-    return MI355X_OK;
-}
-
-// Report (once) a hand-off timeout of any chain launched on this backend.
-int chain_status(mi355x_backend *b) {
-    std::vector<uint32_t *> syncs = b->old_sync;
-    if (b->chain.sync) syncs.push_back(b->chain.sync);
-    int rc = MI355X_OK;
-    for (uint32_t *s : syncs) {
-        uint32_t w[8] = {0};
-        if (hipMemcpy(w, s + 2, sizeof(w), hipMemcpyDeviceToHost) != hipSuccess) continue;
-        if (w[0]) {
-            fprintf(stderr, "ggml_mi355x: kq_chain hand-off timed out: stage %u, workgroup %u, superblock %u, tag seen %u, expected %u\n",
-                    w[1], w[2], w[3], w[4], w[5]);
-            rc = MI355X_E_TIMEOUT;
-            hipMemset(s + 2, 0, sizeof(w));
-        }
-    }
-    for (uint32_t *s : b->old_sync) hipFree(s);
-    b->old_sync.clear();
-    return rc;
 }
 
 }  // namespace
@@ -555,8 +421,6 @@ void mi355x_backend_free(mi355x_backend_t b) {
     DeviceGuard dg(b->device);
     hipStreamSynchronize(b->stream);
     drop_graph(b);
-    drop_chain(b);
-    for (uint32_t *s : b->old_sync) hipFree(s);
     if (b->workspace) hipFree(b->workspace);
     if (b->comm) rccl().comm_destroy(b->comm);
     hipStreamDestroy(b->stream);
@@ -580,8 +444,7 @@ void mi355x_backend_free_buffer(mi355x_backend_t b, void *ptr) {
     if (!b || !ptr) return;
     DeviceGuard dg(b->device);
     hipStreamSynchronize(b->stream);
-    drop_graph(b);  // a captured graph or a chain plan may reference the buffer
-    drop_chain(b);
+    drop_graph(b);  // a captured graph may reference the buffer
     hipFree(ptr);
 }
 
@@ -605,8 +468,7 @@ int mi355x_backend_synchronize(mi355x_backend_t b) {
     if (!b) return MI355X_E_INVAL;
     DeviceGuard dg(b->device);
     const hipError_t e = hipStreamSynchronize(b->stream);
-    if (e != hipSuccess) return (int)e;
-    return chain_status(b);
+    return e == hipSuccess ? 0 : (int)e;
 }
 
 // ggml_backend_device_i::supports_op for this device: MUL_MAT of a contiguous-row
@@ -757,7 +619,7 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
     DeviceGuard dg(b->device);
     // replay fast path: the node list of the captured graph (every decode step after
     // the first) was validated, planned and captured under this key already
-    if (use_graph && b->graph_exec && !kq::chain_enabled()) {
+    if (use_graph && b->graph_exec) {
         const std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);
         if (key == b->graph_key) {
             const hipError_t e = hipGraphLaunch(b->graph_exec, b->stream);
@@ -787,22 +649,8 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
         b->workspace_size = ws;
     }
     const std::vector<Launch> launches = plan_launches(nodes, n_nodes, b->fuse);
-    const bool try_chain = kq::chain_enabled() && launches.size() >= 2;
-    if (!use_graph && !try_chain) return enqueue(b, nodes, launches);
+    if (!use_graph) return enqueue(b, nodes, launches);
     std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);
-    if (try_chain) {
-        if (b->chain.key != key) {
-            hipStreamSynchronize(b->stream);  // a running chain may still use the old plan
-            drop_chain(b);
-            b->chain.key = key;
-            if (plan_chain(b, nodes, n_nodes, launches) != MI355X_OK) {
-                drop_chain(b);
-                b->chain.key = key;  // remembered as not eligible
-            }
-        }
-        if (b->chain.ok) return kq::launch_chain(b->chain.args, b->chain.lds, b->chain.bytes, b->stream);
-        if (!use_graph) return enqueue(b, nodes, launches);
-    }
     if (!b->graph_exec || key != b->graph_key) {
         drop_graph(b);
         if (hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) != hipSuccess)

@@ -174,7 +174,6 @@ __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int
     return L;
 }
 
-// ---------------------------------------------------------------- persistent decode chain
 // Decode attention block (kq_ops.hip): one workgroup per query head.
 struct AttnArgs {
     const float *q, *k, *v;       // projections of this token (before rope)
@@ -187,45 +186,6 @@ struct AttnArgs {
     float scale;
     int diag;  // diagnostics only (MI355X_ATTN_DIAG): 1/2/3 stop after loads/KQ/soft_max, 4 empty
     int rope_row;  // rope_table holds only the row of *pos (no position-dependent load)
-};
-
-// kq_chain: one launch runs a whole sequence of decode MUL_MAT stages (a token's
-// graph). Each stage is planned exactly like one kq_rows launch (same wave split,
-// same per-row arithmetic); the grid is one ROWS_WAVES workgroup per CU for every
-// stage. A stage whose activation is an earlier node's output reads it from that
-// node's "bus": a copy of the output as {value, tag} pairs, stored write-through
-// (sc0 sc1) by the producer and polled by every consumer workgroup until each
-// pair carries this launch's tag — the activation fetch is the stage hand-off.
-struct ChainStage {
-    int n_desc, nb, bR, waves_total;
-    int pollers;  // waves 0..pollers-1 of each workgroup fetch + quantize the activation; the rest stream rows
-    int wave_prefix[MI355X_MAX_FUSED + 1];
-    int rbase[MI355X_MAX_FUSED];
-    int rrem[MI355X_MAX_FUSED];
-    int type[MI355X_MAX_FUSED];
-    const uint8_t *w[MI355X_MAX_FUSED];
-    float *y[MI355X_MAX_FUSED];
-    uint32_t *bus[MI355X_MAX_FUSED];  // {value, tag} copy of y[d] when a later stage reads it, else null
-    const float *x;                   // activation written before the launch (xbus == null)
-    const uint32_t *xbus;             // or: the bus of the producing node
-};
-
-// Activation waves of a chain stage: 4 superblocks per wave per pass, at most 6 waves.
-__host__ __device__ constexpr int chain_pollers(int nb) { return nb <= 0 ? 1 : (nb + 3) / 4 < 6 ? (nb + 3) / 4 : 6; }
-// The device stage table holds one ChainStage per 256-B slot: lane i of a wave
-// loads dword i, fields are then read with v_readlane (no scalar-cache misses on
-// the stage hand-off path).
-constexpr int kChainSlotBytes = 256;
-static_assert(sizeof(ChainStage) <= kChainSlotBytes, "stage descriptor exceeds its table slot");
-
-struct ChainArgs {
-    const uint8_t *st;  // n_stages slots of kChainSlotBytes
-    int n_stages;
-    int act, act_stride, ring, ring_stride, recs, recs_stride, outs, outs_stride, sig;  // LDS layout (max over stages)
-    int pre;          // weight steps per wave issued before the stage's activation is ready (<= ring depth)
-    uint32_t *sync;   // [0] epoch (tag of the last launch), [1] finished workgroups, [2] hand-off timeout flag
-    uint64_t *stamps; // diagnostics: per (workgroup, stage) x-ready / stage-done s_memrealtime
-    int64_t stamps_cap;
 };
 
 // ---------------------------------------------------------------- batched (prefill) MFMA GEMM

@@ -40,15 +40,6 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
               int waves_per_cu = ROWS_WAVES);
 int launch_rows(const RowsPlan &pl, hipStream_t stream);
 bool rows_enabled();
-bool chain_enabled();  // MI355X_GEMV_CHAIN: backend graphs of decode stages run as one kq_chain launch
-// Per-chain LDS fit (max over stages) and algorithmic bytes.
-struct ChainFit {
-    int nb = 0, tmask = 0, recs = 0, rpw = 0;
-    double bytes = 0;
-};
-int plan_chain_stage(const mi355x_gemv_desc *d, int n, int64_t K, ChainStage &cs, ChainFit &fit);
-int chain_layout(const ChainFit &fit, ChainArgs &a, size_t &lds);
-int launch_chain(const ChainArgs &a, size_t lds, double bytes, hipStream_t stream);
 int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
                     hipStream_t stream);
 int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *ws, size_t ws_size,

@@ -1,5 +1,5 @@
-// kq_rows_device.h — device helpers of the row-stream decode kernels (kq_rows.hip,
-// kq_chain.hip): fused Q8_K quantization into the aligned Q8L layout, the per-type
+// kq_rows_device.h — device helpers of the row-stream decode kernel (kq_rows.hip):
+// fused Q8_K quantization into the aligned Q8L layout, the per-type
 // quad partials and the counted-wait helpers.
 #pragma once
 

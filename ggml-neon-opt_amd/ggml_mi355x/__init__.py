@@ -209,13 +209,12 @@ def lib():
     return L
 
 
-GEMV_AUTO, GEMV_TASKS, GEMV_ROWS, GEMV_CHAIN = 0, 1, 2, 3
+GEMV_AUTO, GEMV_TASKS, GEMV_ROWS = 0, 1, 2
 
 
 def gemv_impl(impl):
     """Select the decode GEMV kernel (GEMV_AUTO / GEMV_ROWS: row-stream kq_rows, one
-    launch per stage; GEMV_TASKS: kq_gemv; GEMV_CHAIN: backend graphs of >= 2 decode
-    stages as one persistent kq_chain launch). Returns the previous selection."""
+    launch per stage; GEMV_TASKS: kq_gemv). Returns the previous selection."""
     prev = lib().mi355x_gemv_impl(impl)
     if prev < 0:
         raise Mi355xError(f"mi355x_gemv_impl failed with status {prev}")

@@ -89,7 +89,7 @@ enum mi355x_status {
     MI355X_E_UNSUPPORTED = -2, /* combination not implemented on this device   */
     MI355X_E_WORKSPACE  = -3,  /* workspace missing or too small               */
     MI355X_E_NODEVICE   = -4,  /* no gfx950 device / HIP runtime unavailable   */
-    MI355X_E_TIMEOUT    = -5,  /* a persistent-chain stage hand-off timed out  */
+    MI355X_E_TIMEOUT    = -5,  /* an overlapped launch's activation hand-off timed out */
     MI355X_E_COMM       = -6,  /* RCCL missing / communicator error            */
 };
 
@@ -231,14 +231,12 @@ int mi355x_timing_read(mi355x_launch_timing *out, int max);
 int mi355x_diag_stamps(void *buf, size_t bytes);
 /* Decode-GEMV implementation selector (A/B runs, parity of every path):
  * MI355X_GEMV_AUTO (row-stream kq_rows when rows are contiguous, else kq_gemv),
- * MI355X_GEMV_TASKS (always the 8-row-task kq_gemv), MI355X_GEMV_ROWS (kq_rows,
- * one launch per stage; what AUTO does today) or MI355X_GEMV_CHAIN (as ROWS, but
- * a backend graph of >= 2 decode stages runs as ONE persistent kq_chain launch).
- * Returns the previous value, or MI355X_E_INVAL. */
+ * MI355X_GEMV_TASKS (always the 8-row-task kq_gemv) or MI355X_GEMV_ROWS (kq_rows,
+ * one launch per stage; what AUTO does today). Returns the previous value, or
+ * MI355X_E_INVAL. */
 #define MI355X_GEMV_AUTO 0
 #define MI355X_GEMV_TASKS 1
 #define MI355X_GEMV_ROWS 2
-#define MI355X_GEMV_CHAIN 3
 int mi355x_gemv_impl(int impl);
 
 /* --------------------------------------- decode ops of the llama graph (§8f) */
