@@ -48,5 +48,11 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
 int launch_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t nrows, float eps, hipStream_t s);
 int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s);  // 0 add, 1 mul
 int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream_t s);
+int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a);  // + check_attn
+int launch_attn(const AttnArgs &a, hipStream_t s);
+bool attn_group_ok(const AttnArgs &a, int nwaves);      // the one-workgroup-per-kv-group path applies
+size_t attn_group_bytes(const AttnArgs &a, int nwaves);  // its LDS
+// kq_api.hip
+void allow_lds(const void *fn, size_t lds);
 
 }  // namespace kq

@@ -18,6 +18,7 @@
 #include <stdlib.h>
 #include <string.h>
 
+#include <atomic>
 #include <mutex>
 #include <vector>
 
@@ -25,6 +26,7 @@
 
 #include "kq_common.h"
 #include "kq_internal.h"
+#include "kq_attn_device.h"
 #include "kq_device.h"
 #include "kq_ops_device.h"
 
@@ -152,12 +154,6 @@ __global__ void __launch_bounds__(256) kq_swiglu(const float *__restrict__ g, co
     const int64_t n4 = n & ~(int64_t)3;
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
         y[i] = i < n4 ? v_silu(g[i]) * u[i] : (g[i] / (1.0f + expf(-g[i]))) * u[i];
-}
-
-// rotate_pairs (GGML_ROPE_TYPE_NORMAL) with the position's cos/sin row of the table;
-// x0*c - x1*s -> fmaf(x0, c, -(x1*s)), x0*s + x1*c -> fmaf(x0, s, x1*c) [U].
-__device__ __forceinline__ float2 rope_pair(float x0, float x1, float c, float s) {
-    return make_float2(__builtin_fmaf(x0, c, -(x1 * s)), __builtin_fmaf(x0, s, x1 * c));
 }
 
 __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, float *__restrict__ y, int head_dim,
@@ -445,6 +441,16 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     }
 }
 
+// One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read
+// once into LDS and serve its n_head/n_head_kv query heads, one wave each.
+template <int HD>
+__global__ void __launch_bounds__(1024) kq_attn_group(const AttnArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    attn_group<HD>(a, blockIdx.x, smem, wave, (int)(blockDim.x >> 6), lane);
+}
+
 size_t attn_lds(int hd, int n_ctx) {
     const size_t gsum = (size_t)(n_ctx / 4) * 8 <= (size_t)hd * 64 ? 0 : (size_t)(n_ctx / 4) * 8;
     return (size_t)6 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + gsum;
@@ -491,9 +497,50 @@ int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream
     return timed_launch("kq::kq_swiglu", n * 12.0, kq_swiglu, dim3(elem_grid(n)), dim3(256), 0, s, g, u, y, n);
 }
 
+int attn_group_waves(const AttnArgs &a) {
+    const int gsz = a.n_head / a.n_head_kv;
+    return gsz < 4 ? 4 : gsz > 16 ? 16 : gsz;
+}
+
+size_t attn_group_bytes(const AttnArgs &a, int nwaves) {
+    const int gsz = a.n_head / a.n_head_kv;
+    return (size_t)attn_group_lds(a.head_dim, a.n_ctx, gsz < nwaves ? gsz : nwaves).total;
+}
+
+bool attn_group_ok(const AttnArgs &a, int nwaves) {
+    const uintptr_t m = (uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v;  // 8-B pair loads
+    return (m & 7u) == 0 && a.diag == 0 && attn_group_bytes(a, nwaves) <= 160 * 1024;
+}
+
+// MI355X_ATTN_GROUP (one workgroup per kv group) or MI355X_ATTN_HEAD (per query head);
+// -1 until the first launch reads MI355X_ATTN_IMPL ("head": A/B and parity runs).
+std::atomic<int> g_attn_impl{-1};
+int attn_impl() {
+    int v = g_attn_impl.load();
+    if (v < 0) {
+        const char *e = getenv("MI355X_ATTN_IMPL");
+        int expect = -1;
+        g_attn_impl.compare_exchange_strong(expect, e && strcmp(e, "head") == 0 ? MI355X_ATTN_HEAD : MI355X_ATTN_GROUP);
+        v = g_attn_impl.load();
+    }
+    return v;
+}
+
 int launch_attn(const AttnArgs &a, hipStream_t s) {
-    const size_t lds = attn_lds(a.head_dim, a.n_ctx);
     const double bytes = 0;  // context-dependent; not a roofline kernel
+    const int nw = attn_group_waves(a);
+    if (attn_impl() == MI355X_ATTN_GROUP && attn_group_ok(a, nw)) {
+        const size_t glds = attn_group_bytes(a, nw);
+        if (a.head_dim == 64) {
+            allow_lds((const void *)kq_attn_group<64>, glds);
+            return timed_launch("kq::kq_attn_group<64>", bytes, kq_attn_group<64>, dim3(a.n_head_kv), dim3(64 * nw),
+                                glds, s, a);
+        }
+        allow_lds((const void *)kq_attn_group<128>, glds);
+        return timed_launch("kq::kq_attn_group<128>", bytes, kq_attn_group<128>, dim3(a.n_head_kv), dim3(64 * nw),
+                            glds, s, a);
+    }
+    const size_t lds = attn_lds(a.head_dim, a.n_ctx);
     if (a.head_dim == 64)
         return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64>, dim3(a.n_head), dim3(256), lds, s, a);
     return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128>, dim3(a.n_head), dim3(256), lds, s, a);
@@ -597,6 +644,25 @@ int mi355x_rope(const float *x, float *y, int head_dim, int n_dims, int n_heads,
 int mi355x_attn_decode(const mi355x_attn_desc *d, void *stream) {
     if (!d) return MI355X_E_INVAL;
     AttnArgs a;
+    const int rc = attn_args_from(d, a);
+    if (rc) return rc;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_attn(a, (hipStream_t)stream);
+}
+
+int mi355x_attn_impl(int impl) {
+    if (impl != MI355X_ATTN_GROUP && impl != MI355X_ATTN_HEAD) return MI355X_E_INVAL;
+    const int prev = attn_impl();
+    g_attn_impl.store(impl);
+    return prev;
+}
+
+}  // extern "C"
+
+namespace kq {
+
+int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a) {
+    if (!d) return MI355X_E_INVAL;
     a.q = d->q;
     a.k = d->k;
     a.v = d->v;
@@ -616,10 +682,7 @@ int mi355x_attn_decode(const mi355x_attn_desc *d, void *stream) {
         return e ? atoi(e) : 0;
     }();
     a.diag = diag;
-    const int rc = check_attn(a);
-    if (rc) return rc;
-    if (!device_ok()) return MI355X_E_NODEVICE;
-    return launch_attn(a, (hipStream_t)stream);
+    return check_attn(a);
 }
 
-}  // extern "C"
+}  // namespace kq

@@ -43,6 +43,12 @@ __device__ __forceinline__ float v_expf(float x) {
 
 __device__ __forceinline__ float v_silu(float x) { return x / (1.0f + v_expf(0.0f - x)); }
 
+// rotate_pairs (GGML_ROPE_TYPE_NORMAL) with the position's cos/sin row of the table;
+// x0*c - x1*s -> fmaf(x0, c, -(x1*s)), x0*s + x1*c -> fmaf(x0, s, x1*c) [U].
+__device__ __forceinline__ float2 rope_pair(float x0, float x1, float c, float s) {
+    return make_float2(__builtin_fmaf(x0, c, -(x1 * s)), __builtin_fmaf(x0, s, x1 * c));
+}
+
 typedef _Float16 h16;
 
 __device__ __forceinline__ h16 hfma(h16 a, h16 b, h16 c) { return __builtin_fmaf16(a, b, c); }

@@ -120,7 +120,10 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         }
         // residual of the fused ADD: one row per lane, fetched with the activation. Issued
         // on every path (a dummy read of x without a residual) so that no branch joins a
-        // register whose asm load is still in flight.
+        // register whose asm load is still in flight; rv stays live until the flush waits
+        // for it (the res_p branch is a run-time condition). An asm load whose register the
+        // compiler sees dead is reused while the load is in flight: a build with that branch
+        // compiled out faulted (profiles/r02_attn_epilogue_rejected.md).
         rv = gload4_asm(res_p && ww.nrows > 0 ? res_p + ww.r0 + (lane < ww.nrows ? lane : 0) : a.x);
         for (int j = 0; j < pre0; ++j) issue();
         if (pf_on) {  // L2 prefetch of the stream just past the ring (younger than the pre0 steps)

@@ -28,6 +28,7 @@ FLAG_OUTPUT = 1
 E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_TIMEOUT, E_COMM = 0, -1, -2, -3, -4, -5, -6
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
+ATTN_GROUP, ATTN_HEAD = 0, 1
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -49,7 +50,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
     "mi355x_rope_table_size", "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode",
     "mi355x_comm_id_size", "mi355x_comm_get_unique_id", "mi355x_backend_set_comm", "mi355x_backend_comm_world",
-    "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph",
+    "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph", "mi355x_attn_impl",
 )
 
 
@@ -96,17 +97,17 @@ class LowerOpts(ctypes.Structure):
 GLU_SWIGLU = 2
 
 
-class GemvExt(ctypes.Structure):
-    _fields_ = [("prologue", ctypes.c_int), ("x2", ctypes.c_void_p), ("eps", ctypes.c_float),
-                ("residual", ctypes.c_void_p * MAX_FUSED), ("epilogue", ctypes.c_int), ("epi_y", ctypes.c_void_p)]
-
-
 class AttnDesc(ctypes.Structure):
     _fields_ = [("q", ctypes.c_void_p), ("k", ctypes.c_void_p), ("v", ctypes.c_void_p), ("pos", ctypes.c_void_p),
                 ("rope_table", ctypes.c_void_p), ("k_cache", ctypes.c_void_p), ("v_cache", ctypes.c_void_p),
                 ("out", ctypes.c_void_p), ("n_ctx", ctypes.c_int), ("n_head", ctypes.c_int),
                 ("n_head_kv", ctypes.c_int), ("head_dim", ctypes.c_int), ("scale", ctypes.c_float),
                 ("rope_row", ctypes.c_int)]
+
+
+class GemvExt(ctypes.Structure):
+    _fields_ = [("prologue", ctypes.c_int), ("x2", ctypes.c_void_p), ("eps", ctypes.c_float),
+                ("residual", ctypes.c_void_p * MAX_FUSED), ("epilogue", ctypes.c_int), ("epi_y", ctypes.c_void_p)]
 
 _lib = None
 
@@ -186,6 +187,8 @@ def lib():
     L.mi355x_rope_table.argtypes = [vp, i32, i32, f32, f32, vp]
     L.mi355x_rope.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, vp]
     L.mi355x_attn_decode.argtypes = [ctypes.POINTER(AttnDesc), vp]
+    L.mi355x_attn_impl.argtypes = [i32]
+    L.mi355x_attn_impl.restype = i32
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
               "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode"):
         getattr(L, n).restype = i32
@@ -348,6 +351,11 @@ def gemv_fused(mats, x, stream=None, workspace=None):
         workspace = _workspace(need, x.device)
     _check(lib().mi355x_gemv_fused(descs, n, x.data_ptr(), K, workspace.data_ptr() if need else None, need,
                                    _stream(stream)), "mi355x_gemv_fused")
+
+
+def attn_impl(impl):
+    """ATTN_GROUP (one workgroup per kv group, default) / ATTN_HEAD; returns the previous."""
+    return int(lib().mi355x_attn_impl(impl))
 
 
 def gemv_fused_ext(mats, x, prologue=PRO_NONE, x2=None, eps=0.0, residual=None, epi_y=None, stream=None):

@@ -293,6 +293,13 @@ typedef struct {
                                   (staged by the caller with *pos), read without waiting for pos */
 } mi355x_attn_desc;
 int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
+/* Attention kernel selector (A/B runs, parity of both): MI355X_ATTN_GROUP (default where
+ * the group's cells fit in LDS: one workgroup per KV group, its cells [0, n_kv) read once
+ * and shared by the group's n_head/n_head_kv query heads) or MI355X_ATTN_HEAD (one
+ * workgroup per query head). Returns the previous value, or MI355X_E_INVAL. */
+#define MI355X_ATTN_GROUP 0
+#define MI355X_ATTN_HEAD 1
+int mi355x_attn_impl(int impl);
 
 /* --------------------------------------------- ggml-backend mirror (C++) */
 /* A minimal mirror of ggml-backend's device/buffer/graph interface

@@ -101,10 +101,20 @@ def test_rope(dev, O, hd, nh, base):
 
 
 # ---------------------------------------------------------------- attention
+@pytest.fixture(params=[0, 1], ids=["group", "head"])
+def attn_impl(request):
+    """Runs an attention test on both kernels: one workgroup per kv group (default; the
+    per-head kernel where the group's slice does not fit in LDS) and one per query head."""
+    import ggml_mi355x as g
+    prev = g.attn_impl(request.param)
+    yield request.param
+    g.attn_impl(prev)
+
+
 @pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 256), (128, 32, 8, 128), (64, 8, 8, 64), (64, 8, 2, 512),
-                                             (128, 8, 4, 512), (64, 4, 2, 4096)])
+                                             (128, 8, 4, 512), (64, 4, 2, 4096), (128, 64, 8, 96)])
 @pytest.mark.parametrize("rope_row", [False, True])
-def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx, rope_row):
+def test_attn_decode_sequence(dev, O, attn_impl, hd, nh, nkv, n_ctx, rope_row):
     """A growing KV cache: every position's output and both caches bit-exact (positions
     past the kernel's prefetched cells — 256 K rows, 256/128 V cells — included); the
     rope table whole (row *pos read on device) or only the position's row (rope_row)."""
@@ -134,7 +144,7 @@ def test_attn_decode_sequence(dev, O, hd, nh, nkv, n_ctx, rope_row):
     assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
 
 
-def test_attn_decode_rejects_bad_position(dev):
+def test_attn_decode_rejects_bad_position(dev, attn_impl):
     """A position outside the cache never computes silently: NaN output, caches untouched."""
     import torch
     import ggml_mi355x as g
