@@ -25,6 +25,8 @@ __global__ void kq_rows(const RowsArgs a);
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TYPE>
 __global__ void kq_mmq(const MmqArgs a);
+template <int NWV, int CT>
+__global__ void kq_mmq_k4(const MmqArgs a);
 
 namespace {
 
@@ -529,9 +531,30 @@ int launch_quantize_q8L(const float *x, int64_t x_stride_floats, void *y, int64_
 // ------------------------------------------------------------ batched MFMA path
 constexpr int64_t kMmqMinCols = 16;  // below this the NCOL GEMV streams the weights fewer times
 
+// Prefill kernel selector (mi355x_mmq_impl): -1 until first read from MI355X_MMQ_IMPL
+// (tile64 / k4: A/B runs and parity of every variant).
+std::atomic<int> g_mmq_impl{-1};
+int mmq_impl() {
+    int v = g_mmq_impl.load();
+    if (v < 0) {
+        const char *e = getenv("MI355X_MMQ_IMPL");
+        int x = MI355X_MMQ_AUTO;
+        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : strcmp(e, "k4") == 0 ? MI355X_MMQ_K4 : x;
+        int expect = -1;
+        g_mmq_impl.compare_exchange_strong(expect, x);
+        v = g_mmq_impl.load();
+    }
+    return v;
+}
+
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
                float *y, int64_t y_col_stride, hipStream_t stream) {
     MmqArgs a;
+    static const int mmq_diag = [] {
+        const char *e = getenv("MI355X_MMQ_DIAG");
+        return e ? atoi(e) : 0;
+    }();
+    a.diag = mmq_diag;
     a.w = (const uint8_t *)w;
     a.row_stride = (int64_t)row_stride;
     a.n_rows = (int)N;
@@ -546,19 +569,35 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
                                   : (const void *)kq_mmq<Q4_K>;
     // two superblock buffers: 64 Q8L columns + 64 weight rows (Q6_K: 224-B granule span), +16 B
     // for the Q6_K realign reads past the last row
-    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16;
+    size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16;
+    dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64), 1);
+    dim3 block(256);
+    std::string name = std::string("kq::kq_mmq<") + std::to_string(type) + ">";
+    if (type == Q4_K) {
+        // streamed Q4_K kernel (kq_mmq.hip kq_mmq_k4<8, 2>: 256 weight rows x 64 columns per
+        // workgroup) where its grid fills most of the chip; measured 8-12 % faster there and
+        // slower on half-empty grids (profiles/r02_prefill_ablation.md)
+        const int impl = mmq_impl();
+        const int64_t g82 = ((N + 255) / 256) * ((M + 63) / 64);
+        if (impl == MI355X_MMQ_K4 || (impl == MI355X_MMQ_AUTO && g82 >= 160)) {
+            fn = (const void *)kq_mmq_k4<8, 2>;
+            lds = (size_t)4 * 64 * Q8L_STRIDE;
+            grid = dim3((unsigned)((M + 63) / 64), (unsigned)((N + 255) / 256), 1);
+            block = dim3(512);
+            name = "kq::kq_mmq_k4<8, 2>";
+        }
+    }
     allow_lds(fn, lds);
-    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64), 1);
     hipEvent_t e0, e1;
     const bool timed = timing_slot(stream, e0, e1);
     void *args[] = {&a};
     hipError_t e;
     if (timed) {
-        e = hipExtLaunchKernel(fn, grid, dim3(256), args, lds, stream, e0, e1, 0);
-        timing_log(std::string("kq::kq_mmq<") + std::to_string(type) + ">",
-                   (double)N * a.nb * block_bytes(type) + (double)M * a.nb * Q8L_STRIDE + (double)M * N * 4.0, e0, e1);
+        e = hipExtLaunchKernel(fn, grid, block, args, lds, stream, e0, e1, 0);
+        timing_log(name, (double)N * a.nb * block_bytes(type) + (double)M * a.nb * Q8L_STRIDE + (double)M * N * 4.0,
+                   e0, e1);
     } else {
-        e = hipLaunchKernel(fn, grid, dim3(256), args, lds, stream);
+        e = hipLaunchKernel(fn, grid, block, args, lds, stream);
     }
     if (e != hipSuccess) return (int)e;
     e = hipGetLastError();
@@ -936,6 +975,13 @@ int mi355x_gemv_impl(int impl) {
     if (impl < MI355X_GEMV_AUTO || impl > MI355X_GEMV_ROWS) return MI355X_E_INVAL;
     rows_enabled();  // resolve the environment default first
     return g_impl.exchange(impl);
+}
+
+int mi355x_mmq_impl(int impl) {
+    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_K4) return MI355X_E_INVAL;
+    const int prev = mmq_impl();
+    g_mmq_impl.store(impl);
+    return prev;
 }
 
 int mi355x_diag_stamps(void *buf, size_t bytes) {

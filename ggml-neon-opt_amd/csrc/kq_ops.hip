@@ -512,15 +512,17 @@ bool attn_group_ok(const AttnArgs &a, int nwaves) {
     return (m & 7u) == 0 && a.diag == 0 && attn_group_bytes(a, nwaves) <= 160 * 1024;
 }
 
-// MI355X_ATTN_GROUP (one workgroup per kv group) or MI355X_ATTN_HEAD (per query head);
-// -1 until the first launch reads MI355X_ATTN_IMPL ("head": A/B and parity runs).
+// MI355X_ATTN_HEAD (one workgroup per query head: the default, the fastest launch) or
+// MI355X_ATTN_GROUP (one workgroup per kv group: each group's cells read once, 1/gsz of the
+// cache traffic, +2.3 us per launch on the TinyLlama token: profiles/r02_attention_ab.md);
+// -1 until the first launch reads MI355X_ATTN_IMPL ("group" / "head").
 std::atomic<int> g_attn_impl{-1};
 int attn_impl() {
     int v = g_attn_impl.load();
     if (v < 0) {
         const char *e = getenv("MI355X_ATTN_IMPL");
         int expect = -1;
-        g_attn_impl.compare_exchange_strong(expect, e && strcmp(e, "head") == 0 ? MI355X_ATTN_HEAD : MI355X_ATTN_GROUP);
+        g_attn_impl.compare_exchange_strong(expect, e && strcmp(e, "group") == 0 ? MI355X_ATTN_GROUP : MI355X_ATTN_HEAD);
         v = g_attn_impl.load();
     }
     return v;

@@ -29,6 +29,7 @@ E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_TIMEOUT, E_COMM = 0, -1
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 ATTN_GROUP, ATTN_HEAD = 0, 1
+MMQ_AUTO, MMQ_TILE64, MMQ_K4 = 0, 1, 2
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -51,6 +52,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_rope_table_size", "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode",
     "mi355x_comm_id_size", "mi355x_comm_get_unique_id", "mi355x_backend_set_comm", "mi355x_backend_comm_world",
     "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph", "mi355x_attn_impl",
+    "mi355x_mmq_impl",
 )
 
 
@@ -189,6 +191,8 @@ def lib():
     L.mi355x_attn_decode.argtypes = [ctypes.POINTER(AttnDesc), vp]
     L.mi355x_attn_impl.argtypes = [i32]
     L.mi355x_attn_impl.restype = i32
+    L.mi355x_mmq_impl.argtypes = [i32]
+    L.mi355x_mmq_impl.restype = i32
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
               "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode"):
         getattr(L, n).restype = i32
@@ -351,6 +355,11 @@ def gemv_fused(mats, x, stream=None, workspace=None):
         workspace = _workspace(need, x.device)
     _check(lib().mi355x_gemv_fused(descs, n, x.data_ptr(), K, workspace.data_ptr() if need else None, need,
                                    _stream(stream)), "mi355x_gemv_fused")
+
+
+def mmq_impl(impl):
+    """Prefill GEMM variant (MMQ_*); returns the previous."""
+    return int(lib().mi355x_mmq_impl(impl))
 
 
 def attn_impl(impl):

@@ -238,6 +238,15 @@ int mi355x_diag_stamps(void *buf, size_t bytes);
 #define MI355X_GEMV_TASKS 1
 #define MI355X_GEMV_ROWS 2
 int mi355x_gemv_impl(int impl);
+/* Prefill (ne11 >= 16) GEMM selector (A/B runs, parity of every variant): MI355X_MMQ_AUTO
+ * (Q4_K: the streamed 256 x 64 kernel where its grid fills the chip, else 64 x 64 tiles;
+ * Q5_K / Q6_K: 64 x 64 tiles), MI355X_MMQ_TILE64 (64 x 64 tiles for every type) or
+ * MI355X_MMQ_K4 (the streamed kernel for every Q4_K shape). Returns the previous value, or
+ * MI355X_E_INVAL. */
+#define MI355X_MMQ_AUTO 0
+#define MI355X_MMQ_TILE64 1
+#define MI355X_MMQ_K4 2
+int mi355x_mmq_impl(int impl);
 
 /* --------------------------------------- decode ops of the llama graph (§8f) */
 /* The non-matmul nodes of one llama decode token (llm_build_llama, out.folded:249),
@@ -293,10 +302,11 @@ typedef struct {
                                   (staged by the caller with *pos), read without waiting for pos */
 } mi355x_attn_desc;
 int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
-/* Attention kernel selector (A/B runs, parity of both): MI355X_ATTN_GROUP (default where
- * the group's cells fit in LDS: one workgroup per KV group, its cells [0, n_kv) read once
- * and shared by the group's n_head/n_head_kv query heads) or MI355X_ATTN_HEAD (one
- * workgroup per query head). Returns the previous value, or MI355X_E_INVAL. */
+/* Attention kernel selector (A/B runs, parity of both): MI355X_ATTN_HEAD (default: one
+ * workgroup per query head, the fastest launch) or MI355X_ATTN_GROUP (one workgroup per KV
+ * group where its cells fit in LDS: cells [0, n_kv) read once and shared by the group's
+ * n_head/n_head_kv query heads, 1/gsz of the cache reads). Returns the previous value, or
+ * MI355X_E_INVAL. */
 #define MI355X_ATTN_GROUP 0
 #define MI355X_ATTN_HEAD 1
 int mi355x_attn_impl(int impl);

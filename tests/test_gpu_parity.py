@@ -291,10 +291,21 @@ def test_fused_ragged_partition(dev, oracle, npo, impl):
 
 
 # ---------------------------------------------------------------- batched (prefill) MFMA path
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "tile64", "k4"])
+def mmq(request):
+    """Runs a prefill test on every GEMM variant (Q5_K / Q6_K: the 64 x 64 kernel in all)."""
+    import ggml_mi355x as g
+    prev = g.mmq_impl(request.param)
+    yield request.param
+    g.mmq_impl(prev)
+
+
 @pytest.mark.parametrize("type_", [12, 13, 14])
 @pytest.mark.parametrize("K,N,M", [(256, 64, 16), (2048, 100, 33), (4096, 130, 64), (5632, 77, 100),
                                    (768, 5, 70), (1280, 33, 20), (2048, 64, 512)])
-def test_prefill_mfma_bit_exact(dev, oracle, npo, type_, K, N, M):
+def test_prefill_mfma_bit_exact(dev, oracle, npo, mmq, type_, K, N, M):
+    if type_ != 12 and mmq > 1:
+        pytest.skip("the streamed kernels are Q4_K only")
     """M >= 16 columns go through kq_mmq (int8 MFMA per 32-element sub-block, f32 MFMA
     for the mins, the reference's fp32 chain per element): identical to ggml's
     per-(row, column) vec_dot loop."""
@@ -308,7 +319,7 @@ def test_prefill_mfma_bit_exact(dev, oracle, npo, type_, K, N, M):
     assert bits_equal(got, ref), first_mismatch(got, ref)
 
 
-def test_prefill_full_size_subset(dev, oracle, npo):
+def test_prefill_full_size_subset(dev, oracle, npo, mmq):
     """Llama-3-8B ffn_up at pp512: every output on the GPU, a column x row subset re-computed."""
     import ggml_mi355x as g
     K, N, M = 4096, 14336, 512

@@ -17,11 +17,13 @@ SHAPES = [("l3 q/o", 12, 4096, 4096), ("l3 up", 12, 4096, 14336), ("l3 down", 12
           ("l3 down q6", 14, 14336, 4096)]
 
 
-def main(M=512, reps=10):
+def main(M=512, reps=10, only=None):
     dev = torch.device("cuda:0")
     gen = torch.Generator(device=dev)
     gen.manual_seed(2)
     for label, typ, K, N in SHAPES:
+        if only and typ not in only:
+            continue
         w = random_kquant(typ, N, K, gen, dev)
         x = torch.randn(M, K, device=dev, generator=gen)
         y = torch.empty(M, N, device=dev)
@@ -42,4 +44,4 @@ def main(M=512, reps=10):
 
 
 if __name__ == "__main__":
-    main()
+    main(only=[int(t) for t in os.environ["PREFILL_TYPES"].split(",")] if os.environ.get("PREFILL_TYPES") else None)
