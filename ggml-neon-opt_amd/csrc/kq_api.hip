@@ -550,11 +550,6 @@ int mmq_impl() {
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
                float *y, int64_t y_col_stride, hipStream_t stream) {
     MmqArgs a;
-    static const int mmq_diag = [] {
-        const char *e = getenv("MI355X_MMQ_DIAG");
-        return e ? atoi(e) : 0;
-    }();
-    a.diag = mmq_diag;
     a.w = (const uint8_t *)w;
     a.row_stride = (int64_t)row_stride;
     a.n_rows = (int)N;
@@ -575,7 +570,7 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     std::string name = std::string("kq::kq_mmq<") + std::to_string(type) + ">";
     if (type == Q4_K) {
         // streamed Q4_K kernel (kq_mmq.hip kq_mmq_k4<8, 2>: 256 weight rows x 64 columns per
-        // workgroup) where its grid fills most of the chip; measured 8-12 % faster there and
+        // workgroup) where its grid fills most of the chip; measured ~7 % faster there and
         // slower on half-empty grids (profiles/r02_prefill_ablation.md)
         const int impl = mmq_impl();
         const int64_t g82 = ((N + 255) / 256) * ((M + 63) / 64);

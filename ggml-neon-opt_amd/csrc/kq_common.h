@@ -200,9 +200,6 @@ struct MmqArgs {
     float *y;                // dst column j at y + j * y_col_stride
     int64_t y_col_stride;    // floats
     int nb;
-    int diag;                // diagnostics (timing only, MI355X_MMQ_DIAG): 1 no chain epilogue,
-                             // 2 no scale split, 4 no integer MFMA, 8 no mins MFMA,
-                             // 16 launch-order tiles (no XCD-aware order); kq_mmq<Q4_K> only
 };
 
 }  // namespace kq

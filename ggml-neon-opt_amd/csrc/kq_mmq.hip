@@ -9,8 +9,8 @@
 //    (nibble*half <= 105 fits int8), so sumi = 8*S8 + S1 accumulates across all
 //    sub-blocks inside the matrix core; Q5_K: sumi += sc_j(row) * dot_j on VALU.
 //    Exact int32 either way (README.md:754-771);
-//  * summins = sum_j mn_j(row) * (bsums[2j] + bsums[2j+1]) by f32 MFMA 32x32x2:
-//    integers below 2^24, so exact (README.md:741-744);
+//  * summins = sum_j mn_j(row) * (bsums[2j] + bsums[2j+1]) on one f16 MFMA 32x32x16
+//    (bs = 64*hi + lo split, below): integers below 2^24, so exact (README.md:741-744);
 //  * the fp32 chain per output element runs superblock by superblock in order,
 //    sumf = fmaf(-(float)summins, dmin, sumf); sumf = fmaf((float)sumi, d, sumf)
 //    (fmsub/fmadd, README.md:551/:614) -- the same ops as the GEMV kernels, so
@@ -21,8 +21,24 @@
 // DMA instructions per wave and superblock so the wait is a constant vmcnt.
 // MFMA operand maps (verified with exact integer data, tools/mfma_layout_check.hip):
 //   i8 32x32x32: lane l (r = l&31, h = l>>5) holds A[r][16h+j], B[16h+j][r], j<16;
-//   f32 32x32x2: A[r][h], B[h][r]; C/D: col = r, row = (reg&3) + 8(reg>>2) + 4h.
+//   f16 32x32x16: A[r][8h+j], B[8h+j][r], j<8; C/D (every dtype): col = r,
+//   row = (reg&3) + 8(reg>>2) + 4h.
 #include "kq_device.h"
+
+// Timing-only ablations of kq_mmq<Q4_K>, compile time so the product kernel carries none of
+// them (as run-time branches they cost 40 VGPRs and a wave per SIMD): 1 no chain epilogue,
+// 2 no scale split, 4 no integer MFMA, 8 no mins MFMA, 16 launch-order tiles.
+// Experiment build: make variant-mmq NAME=d13 VFLAGS=-DKQ_MMQ_DIAG=13 (tools/mmq_diag.sh).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+#ifndef KQ_MMQ_DIAG
+#define KQ_MMQ_DIAG 0
+#endif
+// Experiment build: Q4_K with unsplit operands (one int8 MFMA per sub-block, the scale
+// applied on VALU as for Q5_K) instead of the scale split (two MFMAs per sub-block).
+#ifndef KQ_MMQ_Q4_VALU
+#define KQ_MMQ_Q4_VALU 0
+#endif
 
 namespace kq {
 
@@ -127,7 +143,7 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
     // L + 16, ... (one XCD): the weight tile is fetched into that XCD's L2 once and
     // served from it to the others; the activation tiles fit every XCD's L2.
     int tx = blockIdx.x, ty = blockIdx.y;
-    if (!(a.diag & 16)) {
+    if (!(KQ_MMQ_DIAG & 16)) {
         const int gx = gridDim.x, L = blockIdx.y * gx + blockIdx.x;
         const int span = 8 * gx;                  // blocks per group of 8 row tiles
         const int grp = L / span, in = L - grp * span;
@@ -213,15 +229,15 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
             const uint32_t sw = jp < 2 ? s03 : s47;
             const int sc_lo = (int)((sw >> (16u * (uint32_t)(jp & 1))) & 0xffu);
             const int sc_hi = (int)((sw >> (16u * (uint32_t)(jp & 1) + 8u)) & 0xffu);
-            if (TYPE == Q4_K && (a.diag & 6)) {  // diagnostics (timing only)
-                if (!(a.diag & 4)) {
+            if (TYPE == Q4_K && (KQ_MMQ_DIAG & 6)) {  // diagnostics (timing only)
+                if (!(KQ_MMQ_DIAG & 4)) {
                     s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, s8, 0, 0, 0);
                     s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&hi, s1, 0, 0, 0);
                 } else {
                     s8[jp] += (int)(lo.x ^ alo.y ^ (uint32_t)sc_lo);
                     s1[jp] += (int)(hi.y ^ ahi.x ^ (uint32_t)sc_hi);
                 }
-            } else if (TYPE == Q4_K) {
+            } else if (TYPE == Q4_K && !KQ_MMQ_Q4_VALU) {
                 // sc = 8*sh + sl (3-bit halves): nibble*sh and nibble*sl <= 105 stay int8, and a
                 // packed 16-bit multiply scales two bytes per half without carries, so the
                 // per-sub-block scale rides in the MFMA operand and both sums accumulate
@@ -243,6 +259,7 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
                 s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b8hi, s8, 0, 0, 0);
                 s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b1hi, s1, 0, 0, 0);
             } else {  // Q5_K: 5-bit quants x 6-bit scale do not split into int8 halves
+                      // (and Q4_K in the KQ_MMQ_Q4_VALU experiment build)
                 const i32x16 zero = {};
                 i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, zero, 0, 0, 0);
 #pragma unroll
@@ -252,23 +269,30 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
                 for (int i = 0; i < 16; ++i) sumi[i] += sc_hi * c[i];
             }
         }
-        if (TYPE == Q4_K) {
+        if (TYPE == Q4_K && !KQ_MMQ_Q4_VALU) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) sumi[i] = 8 * s8[i] + s1[i];
         }
-        // summins by f32 MFMA: A[m][k] = bsums[2k] + bsums[2k+1] (k = sub-block), B[k][n] = mn_k
+        // summins = sum_j mn_j * bs_j exactly on one f16 MFMA 32x32x16 (bs_j = bsums[2j] +
+        // bsums[2j+1] = 64*hi + lo, lo in 0..63): A = [lo_0..7 | hi_0..7] of the lane's
+        // activation column, B = [mn_0..7 | 64*mn_0..7] of its weight row; every product and
+        // partial sum is an integer below 2^24. (Four dependent f32 MFMAs 32x32x2 cost 256
+        // cycles per superblock against 32 for this one.)
         f32x16 mins;
+        {
+            const u32x4 b0 = *(const u32x4 *)(At + 272), b1 = *(const u32x4 *)(At + 288);
+            const uint32_t bw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            f16x8 am, bm;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) mins[i] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 4; ++s) {
-            if (a.diag & 8) break;  // diagnostics (timing only)
-            const int k = 2 * s + h;
-            const uint32_t bs2 = *(const uint32_t *)(At + 272 + 4 * k);
-            const float av = (float)((int)(int16_t)(bs2 & 0xffffu) + (int)(int16_t)(bs2 >> 16));
-            const uint32_t mw = k < 4 ? m03 : m47;
-            const float bv = (float)((mw >> (8u * (uint32_t)(k & 3))) & 0xffu);
-            mins = __builtin_amdgcn_mfma_f32_32x32x2f32(av, bv, mins, 0, 0, 0);
+            for (int j = 0; j < 8; ++j) {
+                const int bs = (int)(int16_t)(bw[j] & 0xffffu) + (int)(int16_t)(bw[j] >> 16);
+                am[j] = (_Float16)(h ? (bs >> 6) : (bs & 63));
+                const uint32_t mw = j < 4 ? m03 : m47;
+                const int mn = (int)((mw >> (8u * (uint32_t)(j & 3))) & 0xffu);
+                bm[j] = (_Float16)(h ? 64 * mn : mn);
+            }
+            const f32x16 zero = {};
+            mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
         }
         // the reference's fp32 update per element, superblock order
         const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16);
@@ -276,7 +300,7 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
         for (int i = 0; i < 16; ++i) {
             const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
             const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
-            if (a.diag & 1) {  // diagnostics (timing only)
+            if (KQ_MMQ_DIAG & 1) {  // diagnostics (timing only)
                 sumf[i] += (float)sumi[i] + mins[i] + yd;
             } else if (TYPE == Q5_K) {
                 const float t = fmaf(yd * xd, (float)sumi[i], -((yd * xdm) * mins[i]));
@@ -317,8 +341,6 @@ __global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
 //  * tile order: the column tiles of 8 consecutive row tiles go to one XCD (speed only).
 // Constant vmcnt: every wave issues NA DMA and 5 weight loads per superblock step
 // (indices past the last superblock re-fetch it into a free slot / register set).
-typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
-
 __device__ __forceinline__ u32x4 ld16_asm(const uint8_t *p) {
     u32x4 v;
     asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
