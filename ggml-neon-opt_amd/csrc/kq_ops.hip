@@ -208,7 +208,11 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     constexpr int ITEMS = HD * 4 / 256;  // KQV (d, j) items per thread
     constexpr int VPF = 8 / ITEMS;       // prefetched 32-cell iterations per item
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int h = blockIdx.x;
+    // XCD-aware head order (speed only): workgroup b runs on XCD b % 8, so XCD x takes the
+    // consecutive heads [x*n_head/8, (x+1)*n_head/8) and a KV group's cells are fetched into
+    // the L2 of 8*gsz/n_head XCDs (TinyLlama: 2, Llama-3: 1) instead of all 8.
+    int h = blockIdx.x;
+    if ((a.n_head & 7) == 0) h = (h & 7) * (a.n_head >> 3) + (h >> 3);
     const int gsz = a.n_head / a.n_head_kv;
     const int g = h / gsz;
     const int kvw = a.n_head_kv * HD;

@@ -162,3 +162,45 @@ def test_kernels_do_not_spill_to_scratch(tmp_path):
         assert not spilled, f"kernels using scratch: {spilled}"
         kernels += len(names)
     assert kernels >= 20
+
+
+# Register budgets of the hot kernels (VGPRs incl. AGPRs, from the code object). kq_rows
+# runs 12 waves per workgroup = 3 per SIMD (<= 168 registers); the prefill budgets sit a
+# little above today's counts: round 2 found timing diagnostics compiled in as run-time
+# branches (kq_mmq<Q4_K> 152 -> 192, kq_mmq<Q5_K> 244 -> 368 registers) costing 40 % of
+# the 8B ffn_up GEMM. Raising a budget needs a measurement.
+VGPR_BUDGET = [
+    (r"^_ZN2kq7kq_rows", 168),
+    (r"^_ZN2kq6kq_mmqILi12E", 160),
+    (r"^_ZN2kq6kq_mmqILi13E", 256),
+    (r"^_ZN2kq9kq_mmq_k4", 256),
+    (r"^_ZN2kq14kq_attn_decode", 256),
+]
+
+
+def test_hot_kernel_register_budgets(tmp_path):
+    import re
+    import shutil
+    import subprocess
+    import ggml_mi355x as g
+    readelf = "/opt/rocm/lib/llvm/bin/llvm-readelf"
+    if not os.path.exists(readelf):
+        readelf = shutil.which("llvm-readelf")
+    assert readelf, "llvm-readelf not found"
+    seen = {pat: 0 for pat, _ in VGPR_BUDGET}
+    over = []
+    for k, obj in enumerate(_gfx950_code_objects(g.LIB_PATH)):
+        p = tmp_path / f"co{k}.o"
+        p.write_bytes(obj)
+        notes = subprocess.run([readelf, "--notes", str(p)], capture_output=True, text=True, check=True).stdout
+        names = re.findall(r"\.name:\s+(\S+)", notes)
+        vgprs = [int(v) for v in re.findall(r"\.vgpr_count:\s+(\d+)", notes)]
+        assert len(names) == len(vgprs)
+        for n, v in zip(names, vgprs):
+            for pat, budget in VGPR_BUDGET:
+                if re.match(pat, n):
+                    seen[pat] += 1
+                    if v > budget:
+                        over.append((n, v, budget))
+    assert all(seen.values()), f"budgeted kernels missing: {[p for p, c in seen.items() if not c]}"
+    assert not over, f"kernels over their register budget: {over}"
