@@ -539,6 +539,52 @@ def tg_side(tk, steps, barrier):
             "gpu_ms_per_token": round(e0.elapsed_time(e1) / steps, 4)}
 
 
+def split_model_side(model, dev, world, rank, local, barrier, steps=16, warmup=4):
+    """BASELINE config 4 on the same executor: `model`'s full decode token row-split over
+    the job's ranks (every rank its rows and heads, one RCCL ALL_GATHER node per stage,
+    DESIGN.md section 6) or, at one rank, on one GPU without communicator — the scaling
+    run's reference point. `steps` tokens from an empty KV cache, hipGraph replay, the
+    wall time of the slowest rank. Collective: every rank calls it."""
+    be = g.Backend(local)
+    if world > 1:
+        uid = torch.zeros(g.lib().mi355x_comm_id_size(), dtype=torch.uint8)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(g.comm_unique_id()), dtype=torch.uint8))
+        import torch.distributed as dist
+        dist.broadcast(uid, 0)
+        be.set_comm(rank, world, bytes(uid.numpy().tobytes()))
+    n_ctx = max(128, (max(steps, warmup) + 31) // 32 * 32)
+    tk = Token(model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank) if world > 1 else None)
+    for i in range(warmup):
+        tk.dec.step(tk.tokens[i], i)
+    be.synchronize()
+    tk.dec.reset()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        tk.dec.step(tk.tokens[i], i)
+    be.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([el], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+    ms = el / steps * 1e3
+    local_bytes = tk.bytes_per_token
+    out = {"model": model, "parallelism": f"rowsplit{world}" if world > 1 else "1 GPU", "tg_steps": steps,
+           "tok_s": round(steps / el, 2), "ms_per_token": round(ms, 3),
+           "weights_MB_per_token": round(local_bytes * world / 1e6, 1) if world > 1 else round(local_bytes / 1e6, 1),
+           "weights_MB_per_token_per_gpu": round(local_bytes / 1e6, 1),
+           "token_hbm_frac": round(local_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+           "launches_per_token": tk.launches()}
+    del tk, be
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -564,6 +610,8 @@ def main():
     ap.add_argument("--no-chain", action="store_true", help="token workload: skip the matmul-chain side figure")
     ap.add_argument("--no-8b", action="store_true", help="skip the Llama-3-8B side figure (configs 3 and 5)")
     ap.add_argument("--tg", type=int, default=128, help="tokens of the tg side figure (0: skip)")
+    ap.add_argument("--no-70b", action="store_true",
+                    help="skip the Llama-3-70B side figure (config 4: row split over the job's GPUs, 1 GPU at N = 1)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args.gpus)  # exits
@@ -666,6 +714,9 @@ def main():
         barrier()
     per = timed_kernel_stats(be, chain, tokens=4)
     tg = tg_side(chain, args.tg, barrier) if isinstance(chain, Token) and args.tg > 0 else None
+    l70 = None
+    if isinstance(chain, Token) and not args.no_70b and args.model != "llama-3-70b":
+        l70 = split_model_side("llama-3-70b", dev, world, rank, local, barrier)
 
     result = None
     if rank == 0:
@@ -754,6 +805,7 @@ def main():
             "prefill_pp512": prefill,
             "matmul_chain": side,
             "llama3_8b": l3,
+            "llama3_70b": l70,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
