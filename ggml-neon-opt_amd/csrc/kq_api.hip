@@ -27,6 +27,9 @@ template <int TYPE>
 __global__ void kq_mmq(const MmqArgs a);
 template <int NWV, int CT>
 __global__ void kq_mmq_k4(const MmqArgs a);
+#ifndef KQ_K4_NWV
+#define KQ_K4_NWV 8  // waves of the kq_mmq_k4 instantiation (experiment builds: kq_mmq.hip)
+#endif
 
 namespace {
 
@@ -573,13 +576,14 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
         // workgroup) where its grid fills most of the chip; measured ~7 % faster there and
         // slower on half-empty grids (profiles/r02_prefill_ablation.md)
         const int impl = mmq_impl();
-        const int64_t g82 = ((N + 255) / 256) * ((M + 63) / 64);
+        constexpr int RT = 32 * KQ_K4_NWV;  // weight rows per workgroup
+        const int64_t g82 = ((N + RT - 1) / RT) * ((M + 63) / 64) * RT / 256;
         if (impl == MI355X_MMQ_K4 || (impl == MI355X_MMQ_AUTO && g82 >= 160)) {
-            fn = (const void *)kq_mmq_k4<8, 2>;
+            fn = (const void *)kq_mmq_k4<KQ_K4_NWV, 2>;
             lds = (size_t)4 * 64 * Q8L_STRIDE;
-            grid = dim3((unsigned)((M + 63) / 64), (unsigned)((N + 255) / 256), 1);
-            block = dim3(512);
-            name = "kq::kq_mmq_k4<8, 2>";
+            grid = dim3((unsigned)((M + 63) / 64), (unsigned)((N + RT - 1) / RT), 1);
+            block = dim3(64 * KQ_K4_NWV);
+            name = KQ_K4_NWV == 8 ? "kq::kq_mmq_k4<8, 2>" : "kq::kq_mmq_k4<NWV, 2>";
         }
     }
     allow_lds(fn, lds);

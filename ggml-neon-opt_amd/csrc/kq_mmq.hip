@@ -36,6 +36,14 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #endif
 // Experiment build: Q4_K with unsplit operands (one int8 MFMA per sub-block, the scale
 // applied on VALU as for Q5_K) instead of the scale split (two MFMAs per sub-block).
+// kq_mmq_k4 experiment builds: KQ_K4_DIAG 1 compute only (no loads), 2 data movement only;
+// KQ_K4_NWV waves per workgroup of the launched instantiation (32 weight rows each).
+#ifndef KQ_K4_DIAG
+#define KQ_K4_DIAG 0
+#endif
+#ifndef KQ_K4_NWV
+#define KQ_K4_NWV 8
+#endif
 #ifndef KQ_MMQ_Q4_VALU
 #define KQ_MMQ_Q4_VALU 0
 #endif
@@ -380,6 +388,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
     const uint8_t *wrow = a.w + (int64_t)(n < a.n_rows ? n : a.n_rows - 1) * a.row_stride;
 
     auto dma = [&](int b) {  // superblock min(b, nb-1) of the column tile into slot b % DEPTH
+        if (KQ_K4_DIAG & 1) return;  // timing only: no data movement
         const int bb = b < nb ? b : nb - 1;
         uint8_t *slot = smem + (b % C::DEPTH) * C::SLOT;
 #pragma unroll
@@ -397,6 +406,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
         }
     };
     auto wload = [&](int b, u32x4 (&W)[5]) {  // header + this lane's qs half of each sub-block pair
+        if (KQ_K4_DIAG & 1) return;
         const uint8_t *blk = wrow + (int64_t)(b < nb ? b : nb - 1) * 144;
         W[0] = ld16_asm(blk);
 #pragma unroll
@@ -419,6 +429,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
         asm volatile("s_barrier" ::: "memory");  // every wave's part of the slot; slot b-1 free
         dma(b + 3);
         wload(b + 2, Wn);
+        if (KQ_K4_DIAG & 2) return;  // timing only: data movement and barriers, no compute
         const uint8_t *slot = smem + (b % C::DEPTH) * C::SLOT;
         const u32x4 hdr = W[0];
         const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
@@ -519,7 +530,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
     }
 }
 
-template __global__ void kq_mmq_k4<8, 2>(const MmqArgs a);
+template __global__ void kq_mmq_k4<KQ_K4_NWV, 2>(const MmqArgs a);
 
 template __global__ void kq_mmq<Q4_K>(const MmqArgs a);
 template __global__ void kq_mmq<Q5_K>(const MmqArgs a);
