@@ -44,6 +44,20 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #ifndef KQ_K4_NWV
 #define KQ_K4_NWV 8
 #endif
+// Q6_K chunk loop unrolled by 2 and kq_mmq held to 2 waves per SIMD: fully unrolled, the
+// compiler kept every chunk's MFMA results live (376 VGPRs, one wave per SIMD); now 146
+// and Q6_K prefill 23-29 % faster, Q5_K 4 % (profiles/r02_prefill_ablation.md).
+#ifndef KQ_MMQ_Q6_UNROLL
+#define KQ_MMQ_Q6_UNROLL 2
+#endif
+#ifndef KQ_MMQ_WPE
+#define KQ_MMQ_WPE 2
+#endif
+#if KQ_MMQ_WPE > 0
+#define KQ_MMQ_WPE_ATTR __attribute__((amdgpu_waves_per_eu(KQ_MMQ_WPE)))
+#else
+#define KQ_MMQ_WPE_ATTR
+#endif
 #ifndef KQ_MMQ_Q4_VALU
 #define KQ_MMQ_Q4_VALU 0
 #endif
@@ -103,7 +117,7 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
                                  *(const uint32_t *)(bb + 64 * nh + 48 + 16 * h), s4);
         const u32x4 H = realign(*(const u32x4a *)(bb + 128 + 32 * nh + 16 * h),
                                 *(const uint32_t *)(bb + 144 + 32 * nh + 16 * h), s4);
-#pragma unroll
+#pragma unroll KQ_MMQ_Q6_UNROLL
         for (int cc = 0; cc < 4; ++cc) {
             const int c = 4 * nh + cc;  // chunk: elements 32c .. 32c+31
             const u32x4 L = (cc & 1) ? L1 : L0;
@@ -136,7 +150,7 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
 }
 
 template <int TYPE>
-__global__ void __launch_bounds__(256) kq_mmq(const MmqArgs a) {
+__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a) {
     constexpr int BSZ = block_bytes(TYPE);
     constexpr int NB_I = mmq_b_instr(TYPE);
     constexpr int NW = mmq_nw(TYPE);

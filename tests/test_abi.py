@@ -173,6 +173,7 @@ VGPR_BUDGET = [
     (r"^_ZN2kq7kq_rows", 168),
     (r"^_ZN2kq6kq_mmqILi12E", 160),
     (r"^_ZN2kq6kq_mmqILi13E", 256),
+    (r"^_ZN2kq6kq_mmqILi14E", 168),
     (r"^_ZN2kq9kq_mmq_k4", 256),
     (r"^_ZN2kq14kq_attn_decode", 256),
 ]
