@@ -539,6 +539,63 @@ def tg_side(tk, steps, barrier):
             "gpu_ms_per_token": round(e0.elapsed_time(e1) / steps, 4)}
 
 
+def connect(be, world, rank):
+    """RCCL communicator of the row split on backend `be`: the unique id from rank 0 over
+    the gloo control plane, then mi355x_backend_set_comm on every rank. Returns None, or
+    the error every rank agrees on (a failure on any rank fails all, so no rank waits in a
+    collective the others never enter)."""
+    err = None
+    try:
+        uid = torch.zeros(g.lib().mi355x_comm_id_size(), dtype=torch.uint8)
+        if rank == 0:
+            uid.copy_(torch.frombuffer(bytearray(g.comm_unique_id()), dtype=torch.uint8))
+        if world > 1:
+            import torch.distributed as dist
+            dist.broadcast(uid, 0)
+        be.set_comm(rank, world, bytes(uid.numpy().tobytes()))
+    except Exception as e:  # noqa: BLE001 - reported in the JSON line
+        err = f"{type(e).__name__}: {e}"
+    if world > 1:
+        import torch.distributed as dist
+        bad = torch.tensor([0 if err is None else 1], dtype=torch.int32)
+        dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        if bad.item() and err is None:
+            err = "communicator setup failed on another rank"
+    return err
+
+
+def replicas_side(model, dev, world, rank, local, barrier, steps=64, warmup=8):
+    """At N > 1 beside the row split: every rank decodes its own token stream with a full
+    copy of the weights (no communicator, weak scaling), tokens of all ranks / the
+    slowest rank's wall time. Collective: every rank calls it."""
+    be = g.Backend(local)
+    n_ctx = max(128, (max(steps, warmup) + 31) // 32 * 32)
+    tk = Token(model, dev, 0x51A7 + rank, be, n_ctx)
+    for i in range(warmup):
+        tk.dec.step(tk.tokens[i], i)
+    be.synchronize()
+    tk.dec.reset()
+    torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        tk.dec.step(tk.tokens[i], i)
+    be.synchronize()
+    barrier()
+    el = time.perf_counter() - t0
+    import torch.distributed as dist
+    t = torch.tensor([el], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    el = float(t.item())
+    out = {"model": model, "parallelism": f"replicas x{world}", "scaling": "weak", "tg_steps": steps,
+           "tok_s": round(world * steps / el, 1), "tok_s_per_gpu": round(steps / el, 1),
+           "ms_per_token": round(el / steps * 1e3, 4),
+           "token_hbm_frac": round(tk.bytes_per_token * steps / el / 1e9 / HBM_PEAK_GBS, 4)}
+    del tk, be
+    torch.cuda.empty_cache()
+    return out
+
+
 def split_model_side(model, dev, world, rank, local, barrier, steps=16, warmup=4):
     """BASELINE config 4 on the same executor: `model`'s full decode token row-split over
     the job's ranks (every rank its rows and heads, one RCCL ALL_GATHER node per stage,
@@ -547,12 +604,9 @@ def split_model_side(model, dev, world, rank, local, barrier, steps=16, warmup=4
     wall time of the slowest rank. Collective: every rank calls it."""
     be = g.Backend(local)
     if world > 1:
-        uid = torch.zeros(g.lib().mi355x_comm_id_size(), dtype=torch.uint8)
-        if rank == 0:
-            uid.copy_(torch.frombuffer(bytearray(g.comm_unique_id()), dtype=torch.uint8))
-        import torch.distributed as dist
-        dist.broadcast(uid, 0)
-        be.set_comm(rank, world, bytes(uid.numpy().tobytes()))
+        err = connect(be, world, rank)
+        if err is not None:
+            return {"model": model, "parallelism": f"rowsplit{world}", "error": err}
     n_ctx = max(128, (max(steps, warmup) + 31) // 32 * 32)
     tk = Token(model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank) if world > 1 else None)
     for i in range(warmup):
@@ -629,6 +683,8 @@ def main():
         # the data path's collectives are the backend's own RCCL ALL_GATHER nodes
         import torch.distributed as dist
         dist.init_process_group("gloo")
+    if os.environ.get("BENCH_ONE_DEVICE"):  # rehearsal of the multi-rank control plane on a 1-GPU box
+        local = int(os.environ["BENCH_ONE_DEVICE"])
     dev = torch.device(f"cuda:{local}")
     torch.cuda.set_device(dev)
     if not g.device_available():
@@ -645,16 +701,16 @@ def main():
         from ggml_mi355x.gguf import GGUFFile
         gguf = GGUFFile(args.gguf)
     rowsplit = mode == "rowsplit"  # (--mode rowsplit at N = 1: the same graph, gathers over a 1-rank RCCL comm)
+    comm_error = None
     if args.workload == "token":
         be = g.Backend(local)
         if rowsplit:
-            uid = torch.zeros(g.lib().mi355x_comm_id_size(), dtype=torch.uint8)
-            if rank == 0:
-                uid.copy_(torch.frombuffer(bytearray(g.comm_unique_id()), dtype=torch.uint8))
-            if world > 1:
-                import torch.distributed as dist
-                dist.broadcast(uid, 0)
-            be.set_comm(rank, world, bytes(uid.numpy().tobytes()))
+            comm_error = connect(be, world, rank)
+            if comm_error is not None:
+                # every rank saw the failure (agreed over gloo): measure replicas instead of
+                # crashing the scaling run, and say so in the line
+                rowsplit = False
+                be = g.Backend(local)
         n_ctx = max(128, (max(args.steps, args.warmup, args.tg) + 31) // 32 * 32)
         chain = Token(args.model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank) if rowsplit else None)
         stream = torch.cuda.ExternalStream(be.stream)
@@ -714,6 +770,9 @@ def main():
         barrier()
     per = timed_kernel_stats(be, chain, tokens=4)
     tg = tg_side(chain, args.tg, barrier) if isinstance(chain, Token) and args.tg > 0 else None
+    reps = None
+    if isinstance(chain, Token) and rowsplit and world > 1:
+        reps = replicas_side(args.model, dev, world, rank, local, barrier)
     l70 = None
     if isinstance(chain, Token) and not args.no_70b and args.model != "llama-3-70b":
         l70 = split_model_side("llama-3-70b", dev, world, rank, local, barrier)
@@ -806,6 +865,8 @@ def main():
             "matmul_chain": side,
             "llama3_8b": l3,
             "llama3_70b": l70,
+            "replicas": reps,
+            "rowsplit_error": comm_error,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)
