@@ -94,6 +94,8 @@ constexpr size_t kMaxLds = 160 * 1024;   // LDS per CU (one workgroup may use it
 constexpr size_t kTargetLds = 80 * 1024; // aim for >= 2 resident workgroups per CU
 constexpr int64_t kFusedQMaxNb = 32;      // kq_gemv: in-kernel quantization up to K = 8192
 constexpr int64_t kRowsFusedMaxNb = ROWS_QPASS * 4 * ROWS_WAVES;  // kq_rows: up to K = 36864
+constexpr double kRowsSmallBytes = 10e6;  // launches below this many weight bytes: ROWS_WAVES_SMALL waves
+std::atomic<int> g_rows_waves{0};         // mi355x_gemv_waves: 0 = by size, else fixed
 
 uint64_t *g_stamps = nullptr;  // diagnostics (mi355x_diag_stamps)
 int64_t g_stamps_cap = 0;
@@ -422,8 +424,23 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     }
     a.stamps = g_stamps;
     a.stamps_cap = g_stamps_cap;
-    // Waves: one workgroup of ROWS_WAVES per CU; each matrix gets waves in
-    // proportion to its bytes (never more waves than rows), rows split evenly.
+    // Waves: one workgroup per CU of ROWS_WAVES waves, or of ROWS_WAVES_SMALL for a launch
+    // under kRowsSmallBytes of weights (measured on the graph-replayed token: fewer waves
+    // to dispatch, the short stream does not need them; profiles/r02_rows_waves.md). Each
+    // matrix gets waves in proportion to its bytes (never more waves than rows), rows
+    // split evenly.
+    static const double small_bytes = [] {  // A/B knob: MI355X_GEMV_SMALL_MB (0: never)
+        const char *e = getenv("MI355X_GEMV_SMALL_MB");
+        return e ? atof(e) * 1e6 : kRowsSmallBytes;
+    }();
+    if (waves_per_cu <= 0) {
+        const int fixed = g_rows_waves.load();
+        const int want = fixed > 0 ? fixed : bytes_total * nb < small_bytes ? ROWS_WAVES_SMALL : ROWS_WAVES;
+        // the fused quantization covers ROWS_QPASS passes of 4 superblocks per wave
+        waves_per_cu = !fusedq || nb <= ROWS_QPASS * 4 * want ? want : ROWS_WAVES;
+    }
+    if (waves_per_cu > ROWS_WAVES) return MI355X_E_INVAL;
+    pl.nwv = waves_per_cu;
     static const int wpc_env = [] {  // experiment knob: cap on active waves per CU
         const char *e = getenv("MI355X_GEMV_WPC");
         return e ? atoi(e) : 0;
@@ -474,7 +491,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     int bR_full = (int)(ROWS_RECS / nb) / u * u;
     if (bR_full < u) bR_full = u;
     a.bR = a.rpw <= bR_full ? a.rpw : bR_full;
-    const RowsLayout L = rows_layout((int)nb, tmask, a.bR, a.rpw);
+    const RowsLayout L = rows_layout((int)nb, tmask, a.bR, a.rpw, pl.nwv);
     if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
     pl.lds = (size_t)L.total;
     const int64_t grid = waves < num_cus() ? waves : num_cus();
@@ -503,10 +520,10 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
     allow_lds((const void *)pl.fn, pl.lds);
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
-        hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(ROWS_WAVES * 64), (uint32_t)pl.lds, stream, e0, e1, 0, a);
+        hipExtLaunchKernelGGL(pl.fn, pl.grid, dim3(pl.nwv * 64), (uint32_t)pl.lds, stream, e0, e1, 0, a);
         timing_log(rows_name(pl), rows_bytes(a, pl.fusedq), e0, e1);
     } else {
-        hipLaunchKernelGGL(pl.fn, pl.grid, dim3(ROWS_WAVES * 64), pl.lds, stream, a);
+        hipLaunchKernelGGL(pl.fn, pl.grid, dim3(pl.nwv * 64), pl.lds, stream, a);
     }
     const hipError_t e = hipGetLastError();
     return e == hipSuccess ? MI355X_OK : (int)e;
@@ -981,6 +998,11 @@ int mi355x_mmq_impl(int impl) {
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
     return prev;
+}
+
+int mi355x_gemv_waves(int waves) {
+    if (waves < 0 || waves > ROWS_WAVES) return MI355X_E_INVAL;
+    return g_rows_waves.exchange(waves);
 }
 
 int mi355x_diag_stamps(void *buf, size_t bytes) {

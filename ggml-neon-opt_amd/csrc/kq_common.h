@@ -82,7 +82,10 @@ __host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg
 #ifndef KQ_ROWS_WAVES
 #define KQ_ROWS_WAVES 12
 #endif
-constexpr int ROWS_WAVES = KQ_ROWS_WAVES;
+constexpr int ROWS_WAVES = KQ_ROWS_WAVES;  // the most waves per workgroup (LDS layout, launch bounds)
+// Small launches run ROWS_WAVES_SMALL waves per workgroup (the wave count is a launch
+// parameter: blockDim.x / 64): fewer waves to dispatch for a stream that is short anyway.
+constexpr int ROWS_WAVES_SMALL = 6;
 constexpr int ROWS_QPASS = 3;  // fused-quantization passes of 4*ROWS_WAVES superblocks
 // L2 prefetch issued with the first weight step (waves whose stream outlasts the
 // ring): while the activation is fetched and quantized, each wave touches the next
@@ -160,16 +163,17 @@ __host__ __device__ constexpr int rows_ring(int tmask) {
 struct RowsLayout {
     int act, ring, ring_stride, recs, recs_stride, outs, outs_stride, sums, total;
 };
-__host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int rpw) {
+// nwv = the launch's waves per workgroup (blockDim.x / 64)
+__host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int rpw, int nwv) {
     RowsLayout L;
     L.act = 0;
     L.ring = nb * Q8L_STRIDE;
     L.ring_stride = rows_ring(tmask);
-    L.recs = L.ring + ROWS_WAVES * L.ring_stride;
+    L.recs = L.ring + nwv * L.ring_stride;
     L.recs_stride = bR * nb * 16;
-    L.outs = L.recs + ROWS_WAVES * L.recs_stride;
+    L.outs = L.recs + nwv * L.recs_stride;
     L.outs_stride = (rpw * 4 + 15) & ~15;
-    L.sums = L.outs + ROWS_WAVES * L.outs_stride;  // ROWS_PRO_NORM: per-superblock sums of squares (double)
+    L.sums = L.outs + nwv * L.outs_stride;  // ROWS_PRO_NORM: per-superblock sums of squares (double)
     L.total = L.sums + nb * 8;
     return L;
 }

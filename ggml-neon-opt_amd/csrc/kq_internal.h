@@ -33,11 +33,14 @@ struct RowsPlan {
     rows_fn fn;
     int tmask;
     bool fusedq;
+    int nwv;  // waves per workgroup (one workgroup per CU): ROWS_WAVES, or ROWS_WAVES_SMALL
 };
 // Row-stream decode GEMV (kq_rows): returns MI355X_E_UNSUPPORTED when the rows are
-// not contiguous or not aligned for it (callers then use kq_gemv).
+// not contiguous or not aligned for it (callers then use kq_gemv). waves_per_cu = 0:
+// ROWS_WAVES_SMALL waves per workgroup for launches under kRowsSmallBytes of weights,
+// ROWS_WAVES otherwise.
 int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, RowsPlan &pl,
-              int waves_per_cu = ROWS_WAVES);
+              int waves_per_cu = 0);
 int launch_rows(const RowsPlan &pl, hipStream_t stream);
 bool rows_enabled();
 int launch_quantize(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,

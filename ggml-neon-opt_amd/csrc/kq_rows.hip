@@ -51,6 +51,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     constexpr int D = rows_depth(TYPE);
     static_assert(D >= 2 && D <= 4, "vm_wait_k covers 3 steps in flight");
     const int nb = a.nb, bR = a.bR;
+    const int nwv = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6));  // waves in this workgroup
     const int q = lane >> 2, s = lane & 3;
     uint8_t *const ring = smem + L.ring + wave * L.ring_stride;
     uint8_t *const ring_end = ring + D * SLOT;
@@ -98,7 +99,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     const int pre0 = T < pre_cap ? T : pre_cap;     // 0..3
     uint64_t sx = 0, sq = 0, sf = 0;  // diagnostics: x landed, quantized, first step computed
     if (FUSEDQ) {
-        constexpr int PASS = 4 * ROWS_WAVES;  // superblocks per workgroup pass
+        const int PASS = 4 * nwv;  // superblocks per workgroup pass
         u32x4 xv[ROWS_QPASS][4] = {};
         u32x4 x2v[ROWS_QPASS][4] = {};  // norm weight / up, same elements as xv
         const int qiters = (nb + PASS - 1) / PASS;
@@ -200,7 +201,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         }
     } else {
         const int ng = nb * (Q8L_STRIDE / 16);
-        for (int j = wave; 64 * j < ng; j += ROWS_WAVES) {
+        for (int j = wave; 64 * j < ng; j += nwv) {
             const int k = 64 * j + lane;
             if (k < ng) dma16(a.xq + 16 * k, (LDS void *)(smem + L.act + 1024 * j));
         }
@@ -321,7 +322,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         }
     }
     if (a.stamps) {
-        const int64_t o = ((int64_t)blockIdx.x * ROWS_WAVES + wave) * 8;
+        const int64_t o = ((int64_t)blockIdx.x * ROWS_WAVES + wave) * 8;  // stamp slots sized for the most waves
         if (lane == 0 && o + 7 < a.stamps_cap) {
             a.stamps[o] = st0;
             a.stamps[o + 1] = st1;
@@ -341,7 +342,7 @@ __global__ void __launch_bounds__(ROWS_WAVES * 64) kq_rows(const RowsArgs a) {
     const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const RowsLayout L = rows_layout(a.nb, TMASK, a.bR, a.rpw);
+    const RowsLayout L = rows_layout(a.nb, TMASK, a.bR, a.rpw, __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6)));
 
     const int gw = wave * gridDim.x + blockIdx.x;  // active waves spread over every CU
     WaveWork ww;

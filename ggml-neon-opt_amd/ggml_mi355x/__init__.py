@@ -53,6 +53,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_comm_id_size", "mi355x_comm_get_unique_id", "mi355x_backend_set_comm", "mi355x_backend_comm_world",
     "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph", "mi355x_attn_impl",
     "mi355x_mmq_impl",
+    "mi355x_gemv_waves",
 )
 
 
@@ -193,6 +194,8 @@ def lib():
     L.mi355x_attn_impl.restype = i32
     L.mi355x_mmq_impl.argtypes = [i32]
     L.mi355x_mmq_impl.restype = i32
+    L.mi355x_gemv_waves.argtypes = [i32]
+    L.mi355x_gemv_waves.restype = i32
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
               "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode"):
         getattr(L, n).restype = i32
@@ -360,6 +363,11 @@ def gemv_fused(mats, x, stream=None, workspace=None):
 def mmq_impl(impl):
     """Prefill GEMM variant (MMQ_*); returns the previous."""
     return int(lib().mi355x_mmq_impl(impl))
+
+
+def gemv_waves(waves):
+    """kq_rows waves per workgroup: 0 = by launch size, else fixed (1..12); returns the previous."""
+    return int(lib().mi355x_gemv_waves(waves))
 
 
 def attn_impl(impl):

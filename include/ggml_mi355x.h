@@ -247,6 +247,12 @@ int mi355x_gemv_impl(int impl);
 #define MI355X_MMQ_TILE64 1
 #define MI355X_MMQ_K4 2
 int mi355x_mmq_impl(int impl);
+/* Decode GEMV (kq_rows) waves per workgroup (A/B runs, parity of both launch shapes):
+ * 0 = by launch size (6 waves under 10 MB of weights, else 12; env MI355X_GEMV_SMALL_MB
+ * moves the threshold), or a fixed count 1..12 where the launch allows it (the in-kernel
+ * quantization covers 12 superblocks per wave). Returns the previous value, or
+ * MI355X_E_INVAL. */
+int mi355x_gemv_waves(int waves);
 
 /* --------------------------------------- decode ops of the llama graph (§8f) */
 /* The non-matmul nodes of one llama decode token (llm_build_llama, out.folded:249),

@@ -36,10 +36,14 @@ def dev():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=[0, 1], ids=["rows", "tasks"])
+@pytest.fixture(params=[(0, 0), (1, 0), (0, 12), (0, 6)], ids=["rows", "tasks", "rows12", "rows6"])
 def impl(request):
-    """Runs a decode-GEMV test on both kernels: kq_rows (default) and kq_gemv."""
+    """Runs a decode-GEMV test on both kernels, kq_rows (default) and kq_gemv, and kq_rows
+    at both launch shapes: waves per workgroup by launch size (default), 12 and 6."""
     import ggml_mi355x as g
-    prev = g.gemv_impl(request.param)
-    yield request.param
+    which, waves = request.param
+    prev = g.gemv_impl(which)
+    prev_w = g.gemv_waves(waves)
+    yield which
     g.gemv_impl(prev)
+    g.gemv_waves(prev_w)

@@ -6,7 +6,7 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 OUT=gpurun_out/ab_env.log
 : > $OUT
-for round in 1 2; do
+for round in $(seq ${ROUNDS:-2}); do
   for E in "$@"; do
     env $E timeout -k 10 200 python bench.py --steps 64 --warmup 8 --no-cpu-baseline --no-large --no-prefill --no-8b --no-70b --no-chain --tg 0 ${BENCH_ARGS:-} > gpurun_out/ab_one.json 2>/dev/null || exit $?
     python - "$E" >> $OUT <<'PY' || exit $?
