@@ -137,7 +137,8 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
             const i32x16 d1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&q1, zero, 0, 0, 0);
             const int g0 = sbyte(SC, 2 * c), g1 = sbyte(SC, 2 * c + 1);  // int8 group scales of row n
 #pragma unroll
-            for (int i = 0; i < 16; ++i) sumi[i] += g0 * d0[i] + g1 * d1[i];
+            for (int i = 0; i < 16; ++i)  // 24-bit multiplies (full rate; |d| < 2^17, |g| < 2^7)
+                sumi[i] += __mul24(g0, d0[i]) + __mul24(g1, d1[i]);
         }
     }
     const float xd = h2f(dh);
@@ -285,10 +286,10 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a) {
                 const i32x16 zero = {};
                 i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, zero, 0, 0, 0);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) sumi[i] += sc_lo * c[i];
+                for (int i = 0; i < 16; ++i) sumi[i] += __mul24(sc_lo, c[i]);  // |c| < 2^17: full-rate i24
                 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&hi, zero, 0, 0, 0);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) sumi[i] += sc_hi * c[i];
+                for (int i = 0; i < 16; ++i) sumi[i] += __mul24(sc_hi, c[i]);
             }
         }
         if (TYPE == Q4_K && !KQ_MMQ_Q4_VALU) {
