@@ -184,7 +184,7 @@ __device__ __forceinline__ void lane_q4K(const Regs &r, const uint8_t *aq, const
     const u32x4 ahi = *(const u32x4a *)(aq + 64 * j + 32 + 16 * h);
     const u32x4 lo = r.b & 0x0f0f0f0fu;
     const u32x4 hi = (r.b >> 4) & 0x0f0f0f0fu;
-    isum = dot16(lo, alo) * s.sc_lo + dot16(hi, ahi) * s.sc_hi;
+    isum = __mul24(dot16(lo, alo), s.sc_lo) + __mul24(dot16(hi, ahi), s.sc_hi);  // |dot| < 2^17: i24
     const uint32_t bs2 = *(const uint32_t *)(abs + 2 * p);
     imin = ((int)(int16_t)(bs2 & 0xffffu) + (int)(int16_t)(bs2 >> 16)) * s.mn;
 }
@@ -198,7 +198,7 @@ __device__ __forceinline__ void lane_q5K(const Regs &r, const uint8_t *aq, const
     const uint32_t sl = (uint32_t)(2 * j), shh = (uint32_t)(2 * j + 1);
     const u32x4 lo = (r.c & 0x0f0f0f0fu) | (((r.b >> sl) & 0x01010101u) << 4);
     const u32x4 hi = ((r.c >> 4) & 0x0f0f0f0fu) | (((r.b >> shh) & 0x01010101u) << 4);
-    isum = dot16(lo, alo) * s.sc_lo + dot16(hi, ahi) * s.sc_hi;
+    isum = __mul24(dot16(lo, alo), s.sc_lo) + __mul24(dot16(hi, ahi), s.sc_hi);  // |dot| < 2^17: i24
     const uint32_t bs2 = *(const uint32_t *)(abs + 2 * p);
     imin = ((int)(int16_t)(bs2 & 0xffffu) + (int)(int16_t)(bs2 >> 16)) * s.mn;
 }
@@ -222,7 +222,7 @@ __device__ __forceinline__ void lane_q6K(const Regs &r, const uint8_t *aq, const
     const u32x4 alo = *(const u32x4a *)(aq + elo);
     const u32x4 ahi = *(const u32x4a *)(aq + elo + 64);
     const int sb = elo >> 4;
-    isum = dot16(qlo, alo) * sbyte(SC, sb) + dot16(qhi, ahi) * sbyte(SC, sb + 4);
+    isum = __mul24(dot16(qlo, alo), sbyte(SC, sb)) + __mul24(dot16(qhi, ahi), sbyte(SC, sb + 4));  // i24
     const uint32_t bs2 = *(const uint32_t *)(abs + 2 * p);
     imin = (int)(int16_t)(bs2 & 0xffffu) * sbyte(SC, 2 * p) + (int)(int16_t)(bs2 >> 16) * sbyte(SC, 2 * p + 1);
     dh = r.dh;

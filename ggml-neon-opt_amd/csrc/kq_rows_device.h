@@ -146,7 +146,7 @@ __device__ __forceinline__ QuadOut quad_q4K(const uint8_t *blk, const uint8_t *a
     const int dhi = dotacc((q1 >> 4) & 0x0f0f0f0fu, a3, dotacc((q0 >> 4) & 0x0f0f0f0fu, a2, 0));
     const uint2 bs = *(const uint2 *)(ab + 272 + 8 * s);
     QuadOut r;
-    r.isum = dlo * s0.sc_lo + dhi * s0.sc_hi;
+    r.isum = __mul24(dlo, s0.sc_lo) + __mul24(dhi, s0.sc_hi);  // |dot| < 2^17: full-rate i24
     r.imin = ((int)(int16_t)(bs.x & 0xffffu) + (int)(int16_t)(bs.x >> 16)) * s0.mn +
              ((int)(int16_t)(bs.y & 0xffffu) + (int)(int16_t)(bs.y >> 16)) * s1.mn;
     r.dh = hdr.x;
@@ -172,7 +172,7 @@ __device__ __forceinline__ QuadOut quad_q5K(const uint8_t *blk, const uint8_t *a
     const int dhi = dotacc(hi1, a3, dotacc(hi0, a2, 0));
     const uint2 bs = *(const uint2 *)(ab + 272 + 8 * s);
     QuadOut r;
-    r.isum = dlo * s0.sc_lo + dhi * s0.sc_hi;
+    r.isum = __mul24(dlo, s0.sc_lo) + __mul24(dhi, s0.sc_hi);  // |dot| < 2^17: full-rate i24
     r.imin = ((int)(int16_t)(bs.x & 0xffffu) + (int)(int16_t)(bs.x >> 16)) * s0.mn +
              ((int)(int16_t)(bs.y & 0xffffu) + (int)(int16_t)(bs.y >> 16)) * s1.mn;
     r.dh = hdr.x;
@@ -204,7 +204,8 @@ __device__ __forceinline__ QuadOut quad_q6K(const uint8_t *blk, const uint8_t *a
     const int d10 = dotacc(ql1, *(const u32x4 *)(aq + 16), 0);
     const int d11 = dotacc(qh1, *(const u32x4 *)(aq + 80), 0);
     QuadOut r;
-    r.isum = d00 * sbyte(SC, sb) + d01 * sbyte(SC, sb + 4) + d10 * sbyte(SC, sb + 1) + d11 * sbyte(SC, sb + 5);
+    r.isum = __mul24(d00, sbyte(SC, sb)) + __mul24(d01, sbyte(SC, sb + 4)) + __mul24(d10, sbyte(SC, sb + 1)) +
+             __mul24(d11, sbyte(SC, sb + 5));  // |dot| < 2^17: full-rate i24
     const uint2 bs = *(const uint2 *)(ab + 272 + 8 * s);
     r.imin = (int)(int16_t)(bs.x & 0xffffu) * sbyte(SC, 4 * s) + (int)(int16_t)(bs.x >> 16) * sbyte(SC, 4 * s + 1) +
              (int)(int16_t)(bs.y & 0xffffu) * sbyte(SC, 4 * s + 2) + (int)(int16_t)(bs.y >> 16) * sbyte(SC, 4 * s + 3);
