@@ -338,6 +338,34 @@ def prefill_chain(chain, dev, M=512, reps=3):
             "note": "all chain matmuls at ne11=M (quantize + kq_mmq per matmul, eager)"}
 
 
+def prompt_side(tk, be, n_tok=512, reps=3):
+    """llama-bench's pp512 through the graph: one 512-token prompt batch of the same model
+    (LlamaDecoder.prompt: every MUL_MAT at ne11 = 512 on the int8-MFMA GEMMs, batched
+    norms and adds, the prompt attention over the batch's causal cells, the head on the
+    last token), hipGraph replay, on a decoder of n_ctx = n_tok sharing tk's weights."""
+    from ggml_mi355x.llama import LlamaDecoder
+    dec = LlamaDecoder(be, tk.hp, tk.w, n_tok)
+    rng = np.random.default_rng(0x5EED)
+    toks = rng.integers(0, tk.hp["n_vocab"], size=n_tok).tolist()
+    dec.prompt(toks, 0)  # capture
+    be.synchronize()
+    st = torch.cuda.ExternalStream(be.stream)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record(st)
+    for _ in range(reps):
+        dec.prompt(toks, 0)
+    e1.record(st)
+    be.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    out = {"tokens": n_tok, "ms_per_batch": round(ms, 3), "tok_s": round(n_tok / (ms * 1e-3), 1),
+           "nodes": len(dec._prompt_graph(n_tok)["nodes"]),
+           "note": "whole prompt through the graph (MUL_MAT ne11=512 on kq_mmq, batched norms, prompt attention, "
+                   "head on the last token), hipGraph replay"}
+    del dec
+    torch.cuda.empty_cache()
+    return out
+
+
 def chain_side(model, dev, be, steps=64, warmup=8):
     """The per-token MUL_MAT chain alone (no norm/rope/attention/swiglu), hipGraph replay:
     the figure earlier rounds reported as the headline."""
@@ -384,7 +412,8 @@ def model_side(model, dev, steps=64, warmup=8):
     out = {"tg_tok_s": round(1e3 / ms, 1), "ms_per_token": round(ms, 4), "tg_steps": steps,
            "weights_MB_per_token": round(tk.bytes_per_token / 1e6, 1),
            "effective_GBps": round(tk.bytes_per_token / (ms * 1e-3) / 1e9, 1),
-           "launches_per_token": tk.launches(), "pp512": prefill_chain(tk, dev)}
+           "launches_per_token": tk.launches(), "pp512_graph": prompt_side(tk, be),
+           "pp512": prefill_chain(tk, dev)}
     del tk, be
     torch.cuda.empty_cache()
     return out
@@ -816,6 +845,9 @@ def main():
         if isinstance(chain, Token) and not args.no_8b and world == 1 and args.model != "llama-3-8b":
             l3 = model_side("llama-3-8b", dev)
         prefill = None if args.no_prefill or world > 1 else prefill_chain(chain, dev)
+        pp_graph = None
+        if isinstance(chain, Token) and not args.no_prefill and world == 1:
+            pp_graph = prompt_side(chain, be)
         if prefill is not None:
             prefill["roofline"] = {"bound": "mfma", "achieved": prefill["int_TOPS"], "peak": I8_PEAK_TOPS,
                                    "unit": "TOPS (int8 dense)", "frac": round(prefill["int_TOPS"] / I8_PEAK_TOPS, 4),
@@ -862,6 +894,7 @@ def main():
             "tg128": tg,
             "gemv_large": large,
             "prefill_pp512": prefill,
+            "pp512": pp_graph,
             "matmul_chain": side,
             "llama3_8b": l3,
             "llama3_70b": l70,

@@ -27,9 +27,14 @@ struct mi355x_backend {
     std::string name;
     void *workspace = nullptr;
     size_t workspace_size = 0;
-    std::vector<uint64_t> graph_key;
-    hipGraph_t graph = nullptr;
-    hipGraphExec_t graph_exec = nullptr;
+    // captured hipGraphs by node-list key, most recently used last (the decode token and
+    // a prompt batch alternate without recapturing)
+    struct Captured {
+        std::vector<uint64_t> key;
+        hipGraph_t graph = nullptr;
+        hipGraphExec_t exec = nullptr;
+    };
+    std::vector<Captured> graphs;
     bool fuse = true;
     ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
     int rank = 0, world = 0;
@@ -86,12 +91,32 @@ Rccl &rccl() {
 
 bool is_kquant(int t) { return t == MI355X_TYPE_Q4_K || t == MI355X_TYPE_Q5_K || t == MI355X_TYPE_Q6_K; }
 
+constexpr size_t kMaxGraphs = 4;
+
+void destroy_captured(mi355x_backend::Captured &c) {
+    if (c.exec) hipGraphExecDestroy(c.exec);
+    if (c.graph) hipGraphDestroy(c.graph);
+    c.exec = nullptr;
+    c.graph = nullptr;
+}
+
 void drop_graph(mi355x_backend *b) {
-    if (b->graph_exec) hipGraphExecDestroy(b->graph_exec);
-    if (b->graph) hipGraphDestroy(b->graph);
-    b->graph_exec = nullptr;
-    b->graph = nullptr;
-    b->graph_key.clear();
+    for (auto &c : b->graphs) destroy_captured(c);
+    b->graphs.clear();
+}
+
+// the captured graph of this node list (moved to the back: most recently used), or null
+mi355x_backend::Captured *find_graph(mi355x_backend *b, const std::vector<uint64_t> &key) {
+    for (size_t i = 0; i < b->graphs.size(); ++i)
+        if (b->graphs[i].key == key) {
+            if (i + 1 != b->graphs.size()) {
+                mi355x_backend::Captured c = b->graphs[i];
+                b->graphs.erase(b->graphs.begin() + (long)i);
+                b->graphs.push_back(c);
+            }
+            return &b->graphs.back();
+        }
+    return nullptr;
 }
 
 // One launch: a MUL_MAT node, or a run of ne11 == 1 MUL_MAT nodes sharing src1
@@ -291,9 +316,10 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
             return mi355x_rms_norm((const float *)t->src[0]->data, nullptr, (float *)t->data, t->ne[0],
                                    nelem(t) / t->ne[0], f_of(t->op_params[0]), st);
         case MI355X_OP_MUL:
-            return mi355x_mul((const float *)t->src[0]->data, (const float *)t->src[1]->data, (float *)t->data, nelem(t), st);
-        case MI355X_OP_ADD:
-            return mi355x_add((const float *)t->src[0]->data, (const float *)t->src[1]->data, (float *)t->data, nelem(t), st);
+        case MI355X_OP_ADD:  // src1 of one row is repeated over src0's rows (ggml broadcast)
+            if (!kq::device_ok()) return MI355X_E_NODEVICE;
+            return kq::launch_binary(t->op == MI355X_OP_ADD ? 0 : 1, (const float *)t->src[0]->data,
+                                 (const float *)t->src[1]->data, (float *)t->data, nelem(t), st, nelem(t->src[1]));
         case MI355X_OP_SWIGLU:
             return mi355x_swiglu((const float *)t->src[0]->data, (const float *)t->src[1]->data, (float *)t->data,
                                  nelem(t), st);
@@ -333,6 +359,11 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
             a.head_dim = t->op_params[2];
             a.scale = f_of(t->op_params[3]);
             a.n_ctx = (int)t->src[4]->ne[1];
+            const int64_t n_tok = t->src[0]->ne[1];
+            if (n_tok > 1) {  // a prompt batch: all cells first, then every query (causal)
+                a.rope_row = 0;
+                return mi355x_attn_prompt(&a, (int)n_tok, st);
+            }
             a.rope_row = t->src[6]->ne[1] == 1 ? 1 : 0;  // the position's row, staged with pos
             return mi355x_attn_decode(&a, st);
         }
@@ -507,6 +538,9 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
                    nelem(op->src[0]) == nelem(op) && ((uintptr_t)op->src[0]->data & 15u) == 0;
         case MI355X_OP_MUL:
         case MI355X_OP_ADD:
+            // src1 the same shape, or one row repeated over the rows (ggml_mul by the norm weight)
+            return contig_f32(op) && contig_f32(op->src[0]) && contig_f32(op->src[1]) && nelem(op->src[0]) == nelem(op) &&
+                   (nelem(op->src[1]) == nelem(op) || (nelem(op->src[1]) == op->ne[0] && op->nb[1] == (size_t)op->ne[0] * 4));
         case MI355X_OP_SWIGLU:
             return contig_f32(op) && contig_f32(op->src[0]) && contig_f32(op->src[1]) &&
                    nelem(op->src[0]) == nelem(op) && nelem(op->src[1]) == nelem(op);
@@ -534,12 +568,19 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
             if (n_ctx < 32 || n_ctx % 32 || n_ctx > 8192) return 0;
             for (int s = 0; s < 3; ++s)
                 if (!contig_f32(op->src[s])) return 0;
-            if (nelem(op->src[0]) != (int64_t)nh * hd || nelem(op->src[1]) != (int64_t)nkv * hd ||
-                nelem(op->src[2]) != (int64_t)nkv * hd)
+            // T tokens (T > 1: a prompt batch, rows packed): q [nh*hd, T], k, v [kvw, T], pos [T]
+            const int64_t T = op->src[0]->ne[1];
+            if (T < 1 || T > 0x7fffffff || op->src[0]->ne[0] != (int64_t)nh * hd) return 0;
+            if (nelem(op->src[0]) != (int64_t)nh * hd * T || nelem(op->src[1]) != (int64_t)nkv * hd * T ||
+                nelem(op->src[2]) != (int64_t)nkv * hd * T || op->src[3]->ne[0] != T)
                 return 0;
+            if (T > 1 && (op->src[0]->nb[1] != (size_t)nh * hd * 4 || op->src[1]->nb[1] != (size_t)nkv * hd * 4 ||
+                          op->src[2]->nb[1] != (size_t)nkv * hd * 4 || op->src[6]->ne[1] < n_ctx))
+                return 0;  // packed rows; the whole rope table (one position per token)
             if (op->src[6]->ne[1] != 1 && op->src[6]->ne[1] < op->src[4]->ne[1]) return 0;  // row or table
             if (op->src[6]->ne[0] != hd) return 0;
-            return contig_f32(op) && op->ne[0] == (int64_t)nh * hd;
+            return contig_f32(op) && op->ne[0] == (int64_t)nh * hd && op->ne[1] == T &&
+                   (T == 1 || op->nb[1] == (size_t)nh * hd * 4);
         }
         default:
             return 0;
@@ -619,10 +660,10 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
     DeviceGuard dg(b->device);
     // replay fast path: the node list of the captured graph (every decode step after
     // the first) was validated, planned and captured under this key already
-    if (use_graph && b->graph_exec) {
+    if (use_graph && !b->graphs.empty()) {
         const std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);
-        if (key == b->graph_key) {
-            const hipError_t e = hipGraphLaunch(b->graph_exec, b->stream);
+        if (mi355x_backend::Captured *c = find_graph(b, key)) {
+            const hipError_t e = hipGraphLaunch(c->exec, b->stream);
             return e == hipSuccess ? 0 : (int)e;
         }
     }
@@ -651,8 +692,8 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
     const std::vector<Launch> launches = plan_launches(nodes, n_nodes, b->fuse);
     if (!use_graph) return enqueue(b, nodes, launches);
     std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);
-    if (!b->graph_exec || key != b->graph_key) {
-        drop_graph(b);
+    mi355x_backend::Captured *c = find_graph(b, key);
+    if (!c) {
         if (hipStreamBeginCapture(b->stream, hipStreamCaptureModeThreadLocal) != hipSuccess)
             return MI355X_E_UNSUPPORTED;
         const int rc = enqueue(b, nodes, launches);
@@ -667,11 +708,19 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
             hipGraphDestroy(g);
             return MI355X_E_UNSUPPORTED;
         }
-        b->graph = g;
-        b->graph_exec = ge;
-        b->graph_key.swap(key);
+        if (b->graphs.size() == kMaxGraphs) {  // the least recently used goes
+            hipStreamSynchronize(b->stream);
+            destroy_captured(b->graphs.front());
+            b->graphs.erase(b->graphs.begin());
+        }
+        mi355x_backend::Captured nc;
+        nc.key.swap(key);
+        nc.graph = g;
+        nc.exec = ge;
+        b->graphs.push_back(nc);
+        c = &b->graphs.back();
     }
-    const hipError_t e = hipGraphLaunch(b->graph_exec, b->stream);
+    const hipError_t e = hipGraphLaunch(c->exec, b->stream);
     return e == hipSuccess ? 0 : (int)e;
 }
 

@@ -49,7 +49,9 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
             hipStream_t stream, const mi355x_gemv_ext *ext = nullptr);
 // kq_ops.hip
 int launch_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t nrows, float eps, hipStream_t s);
-int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s);  // 0 add, 1 mul
+int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s,
+                  int64_t nb = 0);  // 0 add, 1 mul; b of nb elements repeated (0: nb = n)
+int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s);
 int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream_t s);
 int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a);  // + check_attn
 int launch_attn(const AttnArgs &a, hipStream_t s);

@@ -142,10 +142,14 @@ __global__ void __launch_bounds__(256) kq_rms_norm(const float *__restrict__ x, 
 }
 
 // ------------------------------------------------------------ elementwise
+// b has nb elements, repeated over a's rows (ggml_add / ggml_mul broadcast of src1 over
+// ne1: the norm weights of a batch); nb == n is the plain element-wise op.
 __global__ void __launch_bounds__(256) kq_binary(int op, const float *__restrict__ a, const float *__restrict__ b,
-                                                 float *__restrict__ y, int64_t n) {
-    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256)
-        y[i] = op == 0 ? a[i] + b[i] : a[i] * b[i];
+                                                 float *__restrict__ y, int64_t n, int64_t nb) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float bv = b[nb == n ? i : i % nb];
+        y[i] = op == 0 ? a[i] + bv : a[i] * bv;
+    }
 }
 
 // ggml_vec_swiglu_f32: NEON body for the first n & ~3 elements, libm tail otherwise.
@@ -455,6 +459,303 @@ __global__ void __launch_bounds__(1024) kq_attn_group(const AttnArgs a) {
     attn_group<HD>(a, blockIdx.x, smem, wave, (int)(blockDim.x >> 6), lane);
 }
 
+// ------------------------------------------------------------ prompt (batched) attention
+// A prompt of T tokens in one graph (llama-bench pp: ggml's batched non-flash block —
+// SET_ROWS writes the batch's T new cells, then KQ, soft_max with the causal mask and KQV
+// for every query), two launches:
+//  kq_kv_store: rope(k) -> f16 K cell, v -> f16 V cell (transposed) per (token, kv head);
+//  kq_attn_prompt: one workgroup per (query head, token): the decode kernel's per-query
+//  arithmetic (the general path of kq_attn_decode: KQ with the NEON FP16 structure, max,
+//  ggml_v_expf, vaddvq group sums, the in-order double sum, KQV, the f16 reduce) reading
+//  every cell from the caches. Cells after the query's position are masked: they add exact
+//  zeros whatever they hold, so each query's output is the decode token's bit for bit.
+template <int HD>
+__global__ void __launch_bounds__(256) kq_kv_store(const AttnArgs a) {
+    const int i = blockIdx.x, g = blockIdx.y, t = threadIdx.x;
+    const int pos = a.pos[i];
+    if (pos < 0 || pos >= a.n_ctx) return;  // no cell for this position (its output is NaN)
+    const int kvw = a.n_head_kv * HD;
+    const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
+    if (t < HD / 2) {
+        const float *kp = a.k + (int64_t)i * kvw + (int64_t)g * HD + 2 * t;
+        const float2 rk = rope_pair(kp[0], kp[1], tc[2 * t], tc[2 * t + 1]);
+        const uint16_t k0 = h2u(f2h_rne(rk.x)), k1 = h2u(f2h_rne(rk.y));
+        *(uint32_t *)(a.k_cache + (int64_t)pos * kvw + (int64_t)g * HD + 2 * t) = k0 | ((uint32_t)k1 << 16);
+    } else if (t < HD / 2 + HD) {
+        const int d = t - HD / 2;
+        a.v_cache[(int64_t)(g * HD + d) * a.n_ctx + pos] = h2u(f2h_rne(a.v[(int64_t)i * kvw + (int64_t)g * HD + d]));
+    }
+}
+
+// LDS: q16 (HD f16) | w (n_ctx f32) | p16 (n_ctx f16) | red (HD*32 h16) | scal (4 f32) | gsum (n_ctx/4 f64)
+size_t attn_prompt_lds(int hd, int n_ctx) {
+    return (size_t)2 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + (size_t)(n_ctx / 4) * 8;
+}
+
+template <int HD>
+__global__ void __launch_bounds__(256) kq_attn_prompt(const AttnArgs a) {
+    constexpr int KV4 = HD / 8;          // 16-B pieces of one K-cache row
+    constexpr int ITEMS = HD * 4 / 256;  // KQV (d, j) items per thread
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int h = blockIdx.x, i = (int)gridDim.y - 1 - (int)blockIdx.y, t = threadIdx.x;  // latest tokens first
+    const int g = h / (a.n_head / a.n_head_kv);
+    const int kvw = a.n_head_kv * HD;
+    const int64_t qrow = (int64_t)i * a.n_head * HD;
+    const int pos_in = a.pos[i];
+    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;
+    const int pos = bad ? 0 : pos_in;
+    int n_kv = (pos + 1 + 31) / 32 * 32;
+    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
+    uint16_t *q16 = (uint16_t *)smem;
+    float *w = (float *)(smem + 2 * HD);
+    uint16_t *p16 = (uint16_t *)(w + a.n_ctx);
+    h16 *red = (h16 *)(p16 + a.n_ctx);
+    float *scal = (float *)(red + HD * 32);
+    double *gsum = (double *)(scal + 4);
+
+    if (t < HD / 2) {  // rope(q) at the query's position -> f16
+        const float *qp = a.q + qrow + (int64_t)h * HD + 2 * t;
+        const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
+        const float2 rq = rope_pair(qp[0], qp[1], tc[2 * t], tc[2 * t + 1]);
+        q16[2 * t] = h2u(f2h_rne(rq.x));
+        q16[2 * t + 1] = h2u(f2h_rne(rq.y));
+    }
+    __syncthreads();
+    // KQ + scale + causal mask
+    for (int c = t; c < n_kv; c += 256) {
+        float sc = -INFINITY;
+        if (c <= pos) {
+            uint4 kv[KV4];
+            const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+#pragma unroll
+            for (int k = 0; k < KV4; ++k) kv[k] = kr[k];
+            sc = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+        }
+        w[c] = sc;
+    }
+    __syncthreads();
+    // soft_max: max (order-free), v_expf and the vaddvq group sums, the in-order double sum
+    if (t < 64) {
+        float m = -INFINITY;
+        for (int c = t; c < n_kv; c += 64) m = fmaxf(m, w[c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if (t == 0) scal[0] = m;
+    }
+    __syncthreads();
+    const float mx = scal[0];
+    for (int gi = t; gi < n_kv / 4; gi += 256) {
+        float e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float wv = w[4 * gi + k];
+            e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
+        gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));
+    }
+    __syncthreads();
+    if (t == 0) scal[1] = (float)(1.0 / seq_sum_lds(gsum, n_kv / 4));
+    __syncthreads();
+    const float inv = scal[1];
+    for (int c = t; c < n_kv; c += 256) p16[c] = h2u(f2h_rne(w[c] * inv));
+    __syncthreads();
+    // KQV: thread (d, j) -> accumulator j of output d (cells 32it + 8j + l)
+    const int n_it = (pos + 32) / 32;
+#pragma unroll
+    for (int ii = 0; ii < ITEMS; ++ii) {
+        const int item = t + 256 * ii;
+        const int d = item >> 2, j = item & 3;
+        const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
+        h16 acc[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) acc[l] = (h16)0.0f;
+        for (int it0 = 0; it0 < n_it; it0 += 4) {  // 4 V chunks in flight per round trip
+            uint4 vq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vq[k] = it0 + k < n_it ? *(const uint4 *)(vr + 32 * (it0 + k) + 8 * j) : uint4{};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (it0 + k >= n_it) break;
+                const int c0 = 32 * (it0 + k) + 8 * j;
+                const uint4 pp = *(const uint4 *)(p16 + c0);
+                const uint32_t vw[4] = {vq[k].x, vq[k].y, vq[k].z, vq[k].w}, pw[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+                for (int l = 0; l < 8; ++l)
+                    acc[l] = hfma(u2h((uint16_t)(vw[l >> 1] >> (16 * (l & 1)))),
+                                  u2h((uint16_t)(pw[l >> 1] >> (16 * (l & 1)))), acc[l]);
+            }
+        }
+#pragma unroll
+        for (int l = 0; l < 8; ++l) red[(d * 4 + j) * 8 + l] = acc[l];
+    }
+    __syncthreads();
+    for (int d = t; d < HD; d += 256) {
+        h16 s8[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const h16 s0 = red[(d * 4 + 0) * 8 + l] + red[(d * 4 + 2) * 8 + l];
+            const h16 s1 = red[(d * 4 + 1) * 8 + l] + red[(d * 4 + 3) * 8 + l];
+            s8[l] = s0 + s1;
+        }
+        const float o = f16x8_reduce(s8);
+        a.out[qrow + (int64_t)h * HD + d] = bad ? __builtin_nanf("") : o;
+    }
+}
+
+// The same per-query arithmetic with one workgroup per (kv group, token): the group's gsz
+// query heads share every K row and V chunk the workgroup loads (1/gsz of the cache reads
+// of kq_attn_prompt), each head keeping its own scores, soft_max and accumulators.
+constexpr int PROMPT_GMAX = 8;  // query heads per kv group handled by kq_attn_prompt_group
+#ifndef KQ_PROMPT_DIAG
+#define KQ_PROMPT_DIAG 0  // timing-only builds: 1 no KQ dots, 2 no soft_max sums, 4 no KQV
+#endif
+
+// LDS: q16 [gsz][HD] | w [gsz][n_ctx] f32 | p16 [gsz][n_ctx] | red [gsz][HD*32] h16 |
+//      scal [gsz][4] f32 | gsum [gsz][n_ctx/4] f64
+size_t attn_prompt_group_lds(int hd, int n_ctx, int gsz) {
+    return (size_t)gsz * ((size_t)2 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + (size_t)(n_ctx / 4) * 8);
+}
+
+template <int HD>
+__global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
+    constexpr int KV4 = HD / 8;
+    constexpr int ITEMS = HD * 4 / 256;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    // the latest tokens (the most cells) are dispatched first: a shorter tail
+    const int g = blockIdx.x, i = (int)gridDim.y - 1 - (int)blockIdx.y, t = threadIdx.x;
+    const int gsz = a.n_head / a.n_head_kv;  // <= PROMPT_GMAX (host check)
+    const int kvw = a.n_head_kv * HD;
+    const int64_t qrow = (int64_t)i * a.n_head * HD;
+    const int pos_in = a.pos[i];
+    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;
+    const int pos = bad ? 0 : pos_in;
+    int n_kv = (pos + 1 + 31) / 32 * 32;
+    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
+    const int nc = a.n_ctx;
+    uint16_t *q16 = (uint16_t *)smem;                       // [gsz][HD]
+    float *w = (float *)(q16 + gsz * HD);                   // [gsz][nc]
+    uint16_t *p16 = (uint16_t *)(w + gsz * nc);             // [gsz][nc]
+    h16 *red = (h16 *)(p16 + gsz * nc);                     // [gsz][HD*32]
+    float *scal = (float *)(red + gsz * HD * 32);           // [gsz][4]
+    double *gsum = (double *)(scal + 4 * gsz);              // [gsz][nc/4]
+
+    for (int u = t; u < gsz * (HD / 2); u += 256) {  // rope(q) of the group's heads -> f16
+        const int hh = u / (HD / 2), pr = u - hh * (HD / 2);
+        const float *qp = a.q + qrow + (int64_t)(g * gsz + hh) * HD + 2 * pr;
+        const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
+        const float2 rq = rope_pair(qp[0], qp[1], tc[2 * pr], tc[2 * pr + 1]);
+        q16[hh * HD + 2 * pr] = h2u(f2h_rne(rq.x));
+        q16[hh * HD + 2 * pr + 1] = h2u(f2h_rne(rq.y));
+    }
+    __syncthreads();
+    // KQ: thread t owns cells t, t + 256, ...: one K row load serves every head of the group
+    for (int c = t; c < n_kv; c += 256) {
+        if (c <= pos) {
+            uint4 kv[KV4];
+            const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+#pragma unroll
+            for (int k = 0; k < KV4; ++k) kv[k] = kr[k];
+#pragma unroll
+            for (int hh = 0; hh < PROMPT_GMAX; ++hh)
+                if (hh < gsz)
+                    w[hh * nc + c] = (KQ_PROMPT_DIAG & 1) ? __uint_as_float(kv[0].x ^ kv[KV4 - 1].w) * 1e-30f
+                                                          : vec_dot_f16_rows<HD>(kv, (const uint4 *)(q16 + hh * HD)) * a.scale;
+        } else {
+            for (int hh = 0; hh < gsz; ++hh) w[hh * nc + c] = -INFINITY;
+        }
+    }
+    __syncthreads();
+    // soft_max per head: max (one wave per head, order-free), exp + vaddvq group sums
+    for (int hh = t >> 6; hh < gsz; hh += 4) {
+        const int l = t & 63;
+        float m = -INFINITY;
+        for (int c = l; c < n_kv; c += 64) m = fmaxf(m, w[hh * nc + c]);
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+        if (l == 0) scal[4 * hh] = m;
+    }
+    __syncthreads();
+    const int ng = n_kv / 4;
+    for (int u = t; u < gsz * ng; u += 256) {
+        const int hh = u / ng, gi = u - hh * ng;
+        const float mx = scal[4 * hh];
+        float e[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float wv = w[hh * nc + 4 * gi + k];
+            e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) w[hh * nc + 4 * gi + k] = e[k];
+        gsum[hh * (nc / 4) + gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));
+    }
+    __syncthreads();
+    if ((t & 63) == 0 && (t >> 6) < gsz)  // the in-order double sums, one lane per head
+        for (int hh = t >> 6; hh < gsz; hh += 4)
+            scal[4 * hh + 1] = (KQ_PROMPT_DIAG & 2) ? (float)gsum[hh * (nc / 4)] : (float)(1.0 / seq_sum_lds(gsum + hh * (nc / 4), ng));
+    __syncthreads();
+    for (int u = t; u < gsz * n_kv; u += 256) {
+        const int hh = u / n_kv, c = u - hh * n_kv;
+        p16[hh * nc + c] = h2u(f2h_rne(w[hh * nc + c] * scal[4 * hh + 1]));
+    }
+    __syncthreads();
+    // KQV: thread (d, j) -> accumulator j of output d of every head; one V chunk per (d, j, it)
+    const int n_it = (KQ_PROMPT_DIAG & 4) ? 1 : (pos + 32) / 32;
+#pragma unroll
+    for (int ii = 0; ii < ITEMS; ++ii) {
+        const int item = t + 256 * ii;
+        const int d = item >> 2, j = item & 3;
+        const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * nc;
+        h16 acc[PROMPT_GMAX][8];
+#pragma unroll
+        for (int hh = 0; hh < PROMPT_GMAX; ++hh)
+#pragma unroll
+            for (int l = 0; l < 8; ++l) acc[hh][l] = (h16)0.0f;
+        for (int it0 = 0; it0 < n_it; it0 += 4) {  // 4 V chunks in flight per round trip
+            uint4 vq[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) vq[k] = it0 + k < n_it ? *(const uint4 *)(vr + 32 * (it0 + k) + 8 * j) : uint4{};
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                if (it0 + k >= n_it) break;
+                const int c0 = 32 * (it0 + k) + 8 * j;
+                const uint32_t vw[4] = {vq[k].x, vq[k].y, vq[k].z, vq[k].w};
+#pragma unroll
+                for (int hh = 0; hh < PROMPT_GMAX; ++hh) {
+                    if (hh >= gsz) break;
+                    const uint4 pp = *(const uint4 *)(p16 + hh * nc + c0);
+                    const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+#pragma unroll
+                    for (int l = 0; l < 8; ++l)
+                        acc[hh][l] = hfma(u2h((uint16_t)(vw[l >> 1] >> (16 * (l & 1)))),
+                                          u2h((uint16_t)(pw[l >> 1] >> (16 * (l & 1)))), acc[hh][l]);
+                }
+            }
+        }
+#pragma unroll
+        for (int hh = 0; hh < PROMPT_GMAX; ++hh)
+            if (hh < gsz)
+#pragma unroll
+                for (int l = 0; l < 8; ++l) red[hh * HD * 32 + (d * 4 + j) * 8 + l] = acc[hh][l];
+    }
+    __syncthreads();
+    for (int u = t; u < gsz * HD; u += 256) {
+        const int hh = u / HD, d = u - hh * HD;
+        const h16 *rr = red + hh * HD * 32;
+        h16 s8[8];
+#pragma unroll
+        for (int l = 0; l < 8; ++l) {
+            const h16 s0 = rr[(d * 4 + 0) * 8 + l] + rr[(d * 4 + 2) * 8 + l];
+            const h16 s1 = rr[(d * 4 + 1) * 8 + l] + rr[(d * 4 + 3) * 8 + l];
+            s8[l] = s0 + s1;
+        }
+        const float o = f16x8_reduce(s8);
+        a.out[qrow + (int64_t)(g * gsz + hh) * HD + d] = bad ? __builtin_nanf("") : o;
+    }
+}
+
 size_t attn_lds(int hd, int n_ctx) {
     const size_t gsum = (size_t)(n_ctx / 4) * 8 <= (size_t)hd * 64 ? 0 : (size_t)(n_ctx / 4) * 8;
     return (size_t)6 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + gsum;
@@ -490,10 +791,12 @@ int launch_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t
                         dim3((unsigned)nrows), dim3(256), (size_t)(n / QK) * 8 + 8, s, x, w, y, n, eps);
 }
 
-int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s) {
+int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s, int64_t nb) {
     if (n == 0) return MI355X_OK;
-    return timed_launch(op == 0 ? "kq::kq_add" : "kq::kq_mul", n * 12.0, kq_binary, dim3(elem_grid(n)), dim3(256), 0,
-                        s, op, a, b, y, n);
+    if (nb <= 0) nb = n;
+    if (n % nb) return MI355X_E_INVAL;
+    return timed_launch(op == 0 ? "kq::kq_add" : "kq::kq_mul", n * 8.0 + nb * 4.0, kq_binary, dim3(elem_grid(n)),
+                        dim3(256), 0, s, op, a, b, y, n, nb);
 }
 
 int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream_t s) {
@@ -550,6 +853,40 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     if (a.head_dim == 64)
         return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64>, dim3(a.n_head), dim3(256), lds, s, a);
     return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128>, dim3(a.n_head), dim3(256), lds, s, a);
+}
+
+// mi355x_attn_prompt_impl: MI355X_ATTN_GROUP (default: one workgroup per kv group and token
+// where the group fits) or MI355X_ATTN_HEAD (one per query head and token)
+std::atomic<int> g_prompt_impl{MI355X_ATTN_GROUP};
+
+int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
+    if (n_tok <= 0) return MI355X_OK;
+    const size_t lds = attn_prompt_lds(a.head_dim, a.n_ctx);
+    const int gsz = a.n_head / a.n_head_kv;
+    const size_t glds = attn_prompt_group_lds(a.head_dim, a.n_ctx, gsz);
+    // one workgroup per (kv group, token) where the group's heads fit: 1/gsz of the cache reads
+    const bool group = gsz <= PROMPT_GMAX && glds <= 160 * 1024 && g_prompt_impl.load() == MI355X_ATTN_GROUP;
+    const dim3 gs((unsigned)n_tok, (unsigned)a.n_head_kv), ga((unsigned)a.n_head, (unsigned)n_tok);
+    const dim3 gg((unsigned)a.n_head_kv, (unsigned)n_tok);
+    int rc;
+    if (a.head_dim == 64) {
+        rc = timed_launch("kq::kq_kv_store<64>", 0.0, kq_kv_store<64>, gs, dim3(256), 0, s, a);
+        if (rc) return rc;
+        if (group) {
+            allow_lds((const void *)kq_attn_prompt_group<64>, glds);
+            return timed_launch("kq::kq_attn_prompt_group<64>", 0.0, kq_attn_prompt_group<64>, gg, dim3(256), glds, s, a);
+        }
+        allow_lds((const void *)kq_attn_prompt<64>, lds);
+        return timed_launch("kq::kq_attn_prompt<64>", 0.0, kq_attn_prompt<64>, ga, dim3(256), lds, s, a);
+    }
+    rc = timed_launch("kq::kq_kv_store<128>", 0.0, kq_kv_store<128>, gs, dim3(256), 0, s, a);
+    if (rc) return rc;
+    if (group) {
+        allow_lds((const void *)kq_attn_prompt_group<128>, glds);
+        return timed_launch("kq::kq_attn_prompt_group<128>", 0.0, kq_attn_prompt_group<128>, gg, dim3(256), glds, s, a);
+    }
+    allow_lds((const void *)kq_attn_prompt<128>, lds);
+    return timed_launch("kq::kq_attn_prompt<128>", 0.0, kq_attn_prompt<128>, ga, dim3(256), lds, s, a);
 }
 
 int check_attn(const AttnArgs &a) {
@@ -654,6 +991,23 @@ int mi355x_attn_decode(const mi355x_attn_desc *d, void *stream) {
     if (rc) return rc;
     if (!device_ok()) return MI355X_E_NODEVICE;
     return launch_attn(a, (hipStream_t)stream);
+}
+
+int mi355x_attn_prompt(const mi355x_attn_desc *d, int n_tokens, void *stream) {
+    if (!d || n_tokens < 0) return MI355X_E_INVAL;
+    if (d->rope_row) return MI355X_E_INVAL;  // per-token positions: the whole rope table
+    AttnArgs a;
+    const int rc = attn_args_from(d, a);
+    if (rc) return rc;
+    if (attn_prompt_lds(a.head_dim, a.n_ctx) > 160 * 1024) return MI355X_E_UNSUPPORTED;
+    if (n_tokens == 0) return MI355X_OK;
+    if (!device_ok()) return MI355X_E_NODEVICE;
+    return launch_attn_prompt(a, n_tokens, (hipStream_t)stream);
+}
+
+int mi355x_attn_prompt_impl(int impl) {
+    if (impl != MI355X_ATTN_GROUP && impl != MI355X_ATTN_HEAD) return MI355X_E_INVAL;
+    return g_prompt_impl.exchange(impl);
 }
 
 int mi355x_attn_impl(int impl) {

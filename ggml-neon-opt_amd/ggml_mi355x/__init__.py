@@ -54,6 +54,8 @@ EXPORTED_SYMBOLS = (
     "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph", "mi355x_attn_impl",
     "mi355x_mmq_impl",
     "mi355x_gemv_waves",
+    "mi355x_attn_prompt",
+    "mi355x_attn_prompt_impl",
 )
 
 
@@ -190,6 +192,9 @@ def lib():
     L.mi355x_rope_table.argtypes = [vp, i32, i32, f32, f32, vp]
     L.mi355x_rope.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, vp]
     L.mi355x_attn_decode.argtypes = [ctypes.POINTER(AttnDesc), vp]
+    L.mi355x_attn_prompt.argtypes = [ctypes.POINTER(AttnDesc), i32, vp]
+    L.mi355x_attn_prompt_impl.argtypes = [i32]
+    L.mi355x_attn_prompt_impl.restype = i32
     L.mi355x_attn_impl.argtypes = [i32]
     L.mi355x_attn_impl.restype = i32
     L.mi355x_mmq_impl.argtypes = [i32]
@@ -197,7 +202,7 @@ def lib():
     L.mi355x_gemv_waves.argtypes = [i32]
     L.mi355x_gemv_waves.restype = i32
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
-              "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode"):
+              "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode", "mi355x_attn_prompt"):
         getattr(L, n).restype = i32
     L.mi355x_lower_ggml_graph.argtypes = [ctypes.POINTER(ctypes.POINTER(GTensor)), i32, ctypes.POINTER(LowerOpts),
                                           ctypes.POINTER(Tensor), i32, ctypes.POINTER(ctypes.POINTER(Tensor)), i32,
@@ -370,6 +375,11 @@ def gemv_waves(waves):
     return int(lib().mi355x_gemv_waves(waves))
 
 
+def attn_prompt_impl(impl):
+    """Prompt attention: ATTN_GROUP (per kv group and token, default) / ATTN_HEAD; returns the previous."""
+    return int(lib().mi355x_attn_prompt_impl(impl))
+
+
 def attn_impl(impl):
     """ATTN_GROUP (one workgroup per kv group, default) / ATTN_HEAD; returns the previous."""
     return int(lib().mi355x_attn_impl(impl))
@@ -470,6 +480,17 @@ def attn_decode(q, k, v, pos, table, k_cache, v_cache, n_head, n_head_kv, head_d
                  v_cache.data_ptr(), out.data_ptr(), k_cache.shape[0], n_head, n_head_kv, head_dim, scale,
                  1 if rope_row else 0)
     _check(lib().mi355x_attn_decode(ctypes.byref(a), _stream(stream)), "mi355x_attn_decode")
+    return out
+
+
+def attn_prompt(q, k, v, pos, table, k_cache, v_cache, n_head, n_head_kv, head_dim, scale, out=None, stream=None):
+    """A prompt batch of T tokens: q (T, n_head*hd), k, v (T, n_head_kv*hd) f32, pos int32 cuda (T,),
+    table the whole rope table; writes the T cells, returns out (T, n_head*hd)."""
+    T = pos.numel()
+    out = _torch().empty((T, n_head * head_dim), dtype=_torch().float32, device=q.device) if out is None else out
+    a = AttnDesc(q.data_ptr(), k.data_ptr(), v.data_ptr(), pos.data_ptr(), table.data_ptr(), k_cache.data_ptr(),
+                 v_cache.data_ptr(), out.data_ptr(), k_cache.shape[0], n_head, n_head_kv, head_dim, scale, 0)
+    _check(lib().mi355x_attn_prompt(ctypes.byref(a), T, _stream(stream)), "mi355x_attn_prompt")
     return out
 
 

@@ -23,6 +23,11 @@ import ctypes
 from . import (FLAG_OUTPUT, OP_ADD, OP_ALL_GATHER, OP_ATTN_DECODE, OP_GET_ROWS, OP_MUL, OP_MUL_MAT, OP_RMS_NORM,
                OP_SWIGLU, TYPE_F16, TYPE_F32, TYPE_I32, Backend, Mi355xError, f32_bits, make_tensor, rope_table)
 
+def torch_tensor(values):
+    import torch
+    return torch.tensor(list(values), dtype=torch.int32)
+
+
 LAYER_MATS = ("attn_q", "attn_k", "attn_v", "attn_output", "ffn_gate", "ffn_up", "ffn_down")
 
 
@@ -187,6 +192,112 @@ class LlamaDecoder:
     def reset(self):
         for c in self.k_cache + self.v_cache:
             c.zero_()
+
+    # ------------------------------------------------------------ prompt processing
+    def _prompt_graph(self, n_tok: int):
+        """Node list of a prompt batch of n_tok tokens (llm_build_llama over a ubatch,
+        ggml's batched non-flash attention; llama-bench pp): the same weights, caches and
+        rope table as the decode token. MUL_MATs take ne11 = n_tok columns (the int8-MFMA
+        GEMMs), RMS_NORM/MUL/ADD/SWIGLU run on [n, n_tok], the attention node writes the
+        batch's cells then runs every query causally, and only the last token's row goes
+        through the output norm and head (llama.cpp computes the logits of the last token
+        of a prompt)."""
+        import torch
+        cached = getattr(self, "_prompts", {}).get(n_tok)
+        if cached is not None:
+            return cached
+        if self.split is not None:
+            raise Mi355xError("prompt processing runs on one GPU (no row split)")
+        hp, weights, n_ctx = self.hp, self.w, self.n_ctx
+        dev = weights["output_norm"].device
+        E, V = hp["n_embd"], hp["n_vocab"]
+        hd, nh, nkv = hp["head_dim"], hp["n_head"], hp["n_head_kv"]
+        kvw = nkv * hd
+        T, bufs, nodes = [], [], []
+        inp = torch.zeros(2 * n_tok, dtype=torch.int32, device=dev)  # token ids | positions
+
+        def leaf(t, type_, ne0, ne1=1, row_stride=None):
+            x = make_tensor(type_, ne0, ne1, t.data_ptr(), row_stride=row_stride)
+            T.append(x)
+            return x
+
+        def node(op, n, srcs, params=None, flags=0, ne1=1):
+            b = torch.zeros(n * ne1, dtype=torch.float32, device=dev)
+            bufs.append(b)
+            x = make_tensor(TYPE_F32, n, ne1, b.data_ptr(), op=op, srcs=srcs, op_params=params, flags=flags)
+            T.append(x)
+            nodes.append(x)
+            return x, b
+
+        def mm(name, x):
+            t, w = weights[name]
+            wt = leaf(w, t, w.shape[1] * 256 // {12: 144, 13: 176, 14: 210}[t], w.shape[0], row_stride=w.stride(0))
+            return node(OP_MUL_MAT, wt.ne[1], [wt, x], ne1=x.ne[1])[0]
+
+        eps_bits = [f32_bits(hp["eps"])]
+        tok = leaf(inp[:n_tok], TYPE_I32, n_tok)
+        pos = leaf(inp[n_tok:], TYPE_I32, n_tok)
+        tab = leaf(self.table, TYPE_F32, hd, n_ctx)
+        et, ew = weights["token_embd"]
+        emb_t = leaf(ew, et, E, ew.shape[0], row_stride=ew.stride(0) * ew.element_size())
+        x, xb = node(OP_GET_ROWS, E, [emb_t, tok], ne1=n_tok)
+        scale = f32_bits(float(torch.tensor(1.0) / torch.sqrt(torch.tensor(float(hd)))))
+        for i in range(hp["n_layer"]):
+            p = f"blk.{i}."
+            n1, _ = node(OP_RMS_NORM, E, [x], eps_bits, ne1=n_tok)
+            m1, _ = node(OP_MUL, E, [n1, leaf(weights[p + "attn_norm"], TYPE_F32, E)], ne1=n_tok)
+            q, k, v = mm(p + "attn_q", m1), mm(p + "attn_k", m1), mm(p + "attn_v", m1)
+            kc = leaf(self.k_cache[i], TYPE_F16, kvw, n_ctx)
+            vc = leaf(self.v_cache[i], TYPE_F16, n_ctx, kvw)
+            att, _ = node(OP_ATTN_DECODE, nh * hd, [q, k, v, pos, kc, vc, tab], [nh, nkv, hd, scale], ne1=n_tok)
+            o = mm(p + "attn_output", att)
+            ffn_inp, _ = node(OP_ADD, E, [o, x], ne1=n_tok)
+            n2, _ = node(OP_RMS_NORM, E, [ffn_inp], eps_bits, ne1=n_tok)
+            m2, _ = node(OP_MUL, E, [n2, leaf(weights[p + "ffn_norm"], TYPE_F32, E)], ne1=n_tok)
+            gt, up = mm(p + "ffn_gate", m2), mm(p + "ffn_up", m2)
+            glu, _ = node(OP_SWIGLU, gt.ne[0], [gt, up], ne1=n_tok)
+            dn = mm(p + "ffn_down", glu)
+            x, xb = node(OP_ADD, E, [dn, ffn_inp], ne1=n_tok)
+        last = leaf(xb[(n_tok - 1) * E:], TYPE_F32, E)  # the last token's row (inp_out_ids)
+        n3, _ = node(OP_RMS_NORM, E, [last], eps_bits)
+        m3, _ = node(OP_MUL, E, [n3, leaf(weights["output_norm"], TYPE_F32, E)])
+        t_out, w_out = weights["output"]
+        wt = leaf(w_out, t_out, w_out.shape[1] * 256 // {12: 144, 13: 176, 14: 210}[t_out], w_out.shape[0],
+                  row_stride=w_out.stride(0))
+        _, logits = node(OP_MUL_MAT, V, [wt, m3], flags=FLAG_OUTPUT)
+        g = dict(inp=inp, nodes=nodes, tensors=T, bufs=bufs, logits=logits, hidden=xb,
+                 arr=(ctypes.POINTER(type(T[0])) * len(nodes))(*[ctypes.pointer(n) for n in nodes]),
+                 host=torch.zeros(2 * n_tok, dtype=torch.int32).pin_memory())
+        if not hasattr(self, "_prompts"):
+            self._prompts = {}
+        self._prompts[n_tok] = g
+        torch.cuda.synchronize()  # zeroed buffers (torch's stream) before the backend stream runs
+        return g
+
+    def prompt(self, tokens, start_pos: int = 0, use_graph: bool = True):
+        """Enqueue a prompt batch (positions start_pos ..): writes its KV cells and returns
+        the device logits of its last token (no synchronization). The logits and the cache
+        equal those of decoding the tokens one by one with step(), bit for bit."""
+        n_tok = len(tokens)
+        if n_tok < 1 or start_pos < 0 or start_pos + n_tok > self.n_ctx:
+            raise Mi355xError(f"prompt of {n_tok} tokens at {start_pos} outside the KV cache (n_ctx {self.n_ctx})")
+        if any(not 0 <= t < self.hp["n_vocab"] for t in tokens):
+            raise Mi355xError("prompt token outside the vocabulary")
+        from . import lib
+        g = self._prompt_graph(n_tok)
+        self.b.synchronize()  # the pinned staging row is reused: the previous prompt's copy is done
+        host = g["host"]
+        host[:n_tok] = torch_tensor(tokens)
+        host[n_tok:] = torch_tensor(range(start_pos, start_pos + n_tok))
+        L = lib()
+        rc = L.mi355x_backend_set_tensor(self.b.h, g["inp"].data_ptr(), host.data_ptr(), 4 * host.numel())
+        if rc:
+            raise Mi355xError(f"set_tensor failed ({rc})")
+        rc = L.mi355x_backend_graph_compute(self.b.h, g["arr"], len(g["nodes"]), 1 if use_graph else 0)
+        if rc:
+            raise Mi355xError(f"graph_compute failed ({rc})")
+        self.prompt_hidden = g["hidden"]
+        return g["logits"]
 
     def step(self, token: int, pos: int, use_graph: bool = True):
         """Enqueue one token (no synchronization); returns the device logits tensor."""

@@ -308,6 +308,15 @@ typedef struct {
                                   (staged by the caller with *pos), read without waiting for pos */
 } mi355x_attn_desc;
 int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
+/* The same block for a prompt of n_tokens tokens in one graph (llama-bench pp: ggml's
+ * batched non-flash path — SET_ROWS of the batch's cells, then KQ / soft_max with the
+ * causal mask / KQV per query): q [n_tokens][n_head*head_dim], k, v [n_tokens][kvw],
+ * pos device int32 [n_tokens], out [n_tokens][n_head*head_dim]; rope_row must be 0 (the
+ * whole table). All cells are written first, then every query attends to the cells at or
+ * before its position: each output row equals mi355x_attn_decode's for that token after
+ * the tokens before it, bit for bit. A position outside the cache gives a NaN row and no
+ * cell. */
+int mi355x_attn_prompt(const mi355x_attn_desc *a, int n_tokens, void *stream);
 /* Attention kernel selector (A/B runs, parity of both): MI355X_ATTN_HEAD (default: one
  * workgroup per query head, the fastest launch) or MI355X_ATTN_GROUP (one workgroup per KV
  * group where its cells fit in LDS: cells [0, n_kv) read once and shared by the group's
@@ -316,6 +325,11 @@ int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
 #define MI355X_ATTN_GROUP 0
 #define MI355X_ATTN_HEAD 1
 int mi355x_attn_impl(int impl);
+/* Prompt attention selector (A/B runs, parity of both): MI355X_ATTN_GROUP (default: one
+ * workgroup per kv group and token, the group's query heads sharing every K/V load, where
+ * n_head/n_head_kv <= 8 and its LDS fits) or MI355X_ATTN_HEAD (one per query head and
+ * token). Returns the previous value, or MI355X_E_INVAL. */
+int mi355x_attn_prompt_impl(int impl);
 
 /* --------------------------------------------- ggml-backend mirror (C++) */
 /* A minimal mirror of ggml-backend's device/buffer/graph interface

@@ -363,3 +363,83 @@ def test_fusion_respects_reused_buffers_and_views(dev, O, oracle, npo, view_offs
         assert bits_equal(h4, O.add(mm[view_offset:], res2[view_offset:])), first_mismatch(
             h4, O.add(mm[view_offset:], res2[view_offset:]))
     be.close()
+
+
+# ---------------------------------------------------------------- prompt processing (batched)
+@pytest.fixture(params=[0, 1], ids=["pgroup", "phead"])
+def prompt_impl(request):
+    """Runs a prompt test on both prompt-attention kernels (per kv group and token, the
+    default; per query head and token)."""
+    import ggml_mi355x as g
+    prev = g.attn_prompt_impl(request.param)
+    yield request.param
+    g.attn_prompt_impl(prev)
+
+
+@pytest.mark.parametrize("hd", [64, 128])
+def test_llama_prompt_equals_tokens(dev, O, hd, prompt_impl):
+    """A prompt batch through one graph (MUL_MAT at ne11 = T on the int8-MFMA GEMMs,
+    batched norms, the prompt attention: all cells, then every query causally) gives the
+    logits of its last token and the KV caches of decoding the tokens one by one, bit for
+    bit, and equal to the oracle's sequential llm_build_llama; a second batch continues
+    from the cache (start_pos > 0); decode steps after it (the cached hipGraphs alternate)."""
+    import torch
+    from tests import llama_model as LM
+    from ggml_mi355x.llama import hparams
+    hp = hparams(2048, 2, 2048 // hd, 4 if hd == 64 else 8, 5632, 4096)
+    n_ctx = 128
+    w, b, dec = _decoder(dev, hp, 5, n_ctx, True)
+    model, cache = LM.oracle_model(hp, w, n_ctx)
+    rng = np.random.default_rng(11)
+    tokens = rng.integers(0, hp["n_vocab"], size=53).tolist()
+    first, second = tokens[:37], tokens[37:50]
+    lg = dec.prompt(first, 0)
+    b.synchronize()
+    got1 = lg.cpu().numpy().copy()
+    kc1 = [c.clone() for c in dec.k_cache]
+    vc1 = [c.clone() for c in dec.v_cache]
+    for p, tok in enumerate(first):
+        ref, _ = O.decode_token(model, tok, p, cache)
+    assert bits_equal(got1, ref), first_mismatch(got1, ref)
+    lg = dec.prompt(second, len(first))
+    b.synchronize()
+    got2 = lg.cpu().numpy().copy()
+    for p, tok in enumerate(second, start=len(first)):
+        ref, _ = O.decode_token(model, tok, p, cache)
+    assert bits_equal(got2, ref), first_mismatch(got2, ref)
+    # decode continues from the prompt's cache; then the same tokens decoded one by one
+    # from an empty cache reproduce the prompt's caches exactly
+    for p, tok in enumerate(tokens[50:], start=50):
+        dec.step(tok, p)
+        b.synchronize()
+        ref, _ = O.decode_token(model, tok, p, cache)
+        assert bits_equal(dec.logits.cpu().numpy(), ref), p
+    dec.reset()
+    for p, tok in enumerate(first):
+        dec.step(tok, p)
+    b.synchronize()
+    for i in range(hp["n_layer"]):
+        assert torch.equal(dec.k_cache[i], kc1[i]) and torch.equal(dec.v_cache[i], vc1[i]), i
+    torch.cuda.synchronize()
+    b.close()
+
+
+def test_attn_prompt_rejects_bad_position(dev, prompt_impl):
+    """A position outside the cache: that token's row is NaN, no cell is written."""
+    import torch
+    import ggml_mi355x as g
+    hd, nh, nkv, n_ctx, T = 64, 8, 2, 64, 5
+    table = g.rope_table(n_ctx, hd, 10000.0, 1.0, device=dev)
+    q = torch.randn(T, nh * hd, device=dev)
+    k = torch.randn(T, nkv * hd, device=dev)
+    v = torch.randn(T, nkv * hd, device=dev)
+    kc = torch.zeros((n_ctx, nkv * hd), dtype=torch.int16, device=dev)
+    vc = torch.zeros((nkv * hd, n_ctx), dtype=torch.int16, device=dev)
+    pos = torch.tensor([0, 1, n_ctx + 3, 3, -1], dtype=torch.int32, device=dev)
+    out = g.attn_prompt(q, k, v, pos, table, kc, vc, nh, nkv, hd, 0.125)
+    torch.cuda.synchronize()
+    o = out.cpu()
+    assert torch.isnan(o[2]).all() and torch.isnan(o[4]).all()
+    assert torch.isfinite(o[[0, 1, 3]]).all()
+    assert (kc[2] == 0).all() and (kc[4:] == 0).all()
+    assert (kc[[0, 1, 3]] != 0).any(dim=1).all()
