@@ -372,10 +372,57 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
     }
 }
 
+// A MUL_MAT of ne11 >= 16 columns on the int8-MFMA GEMM whose activation the previous
+// launch already quantized into the workspace (q/k/v and gate/up of a prompt batch read
+// one normed activation): the GEMM alone. q8_src tracks what the workspace holds.
+struct Q8State {
+    const void *src = nullptr;
+    int64_t k = 0, m = 0;
+    size_t nb = 0;
+};
+
+int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8) {
+    const mi355x_tensor *w = t->src[0], *x = t->src[1];
+    const int64_t K = w->ne[0], M = x->ne[1];
+    const bool same = q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1];
+    if (!same) {
+        const int rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
+                                               b->stream);
+        if (rc) {
+            q8 = Q8State();
+            return rc;
+        }
+        q8.src = x->data;
+        q8.k = K;
+        q8.m = M;
+        q8.nb = x->nb[1];
+    }
+    const int rc = kq::launch_mmq(w->type, w->data, K, w->ne[1], w->nb[1], (const uint8_t *)b->workspace, M,
+                                  (float *)t->data, (int64_t)(t->nb[1] / 4), b->stream);
+    if (rc || t->data == q8.src) q8 = Q8State();  // (an output over its own activation)
+    return rc;
+}
+
+bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
+    if (t->op != MI355X_OP_MUL_MAT) return false;
+    const mi355x_tensor *w = t->src[0], *x = t->src[1];
+    if (x->ne[1] < 16 || (x->nb[1] & 3u) || (t->nb[1] & 3u) || ((uintptr_t)b->workspace & 15u)) return false;
+    if (!kq::mmq_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1])) return false;
+    return b->workspace_size >= mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], x->ne[1]);
+}
+
 int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<Launch> &launches) {
+    Q8State q8;
+    if (!kq::device_ok()) return MI355X_E_NODEVICE;
     for (const Launch &l : launches) {
         const mi355x_tensor *t = nodes[l.first];
         int rc;
+        if (l.kind != 1 && l.count == 1 && batched_mm_shares(b, t)) {
+            rc = enqueue_batched_mm(b, t, q8);
+            if (rc) return rc;
+            continue;
+        }
+        q8 = Q8State();  // any other launch may overwrite the workspace or the activation
         if (l.kind == 1) {
             const mi355x_tensor *w = t->src[0];
             mi355x_gemv_desc d[MI355X_MAX_FUSED];

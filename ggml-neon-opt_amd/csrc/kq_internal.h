@@ -52,6 +52,12 @@ int launch_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t
 int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s,
                   int64_t nb = 0);  // 0 add, 1 mul; b of nb elements repeated (0: nb = n)
 int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s);
+// prefill (ne11 >= 16) pieces, for the backend's shared-activation runs
+bool mmq_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M);
+int launch_quantize_q8L(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
+                        hipStream_t stream);
+int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
+               float *y, int64_t y_col_stride, hipStream_t stream);
 int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream_t s);
 int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a);  // + check_attn
 int launch_attn(const AttnArgs &a, hipStream_t s);

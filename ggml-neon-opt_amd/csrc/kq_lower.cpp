@@ -130,7 +130,7 @@ struct Lower {
     }
 
     bool rope_ok(const mi355x_gtensor *r, int hd) const {
-        if (!r || r->op != MI355X_GOP_ROPE || r->ne[2] != 1) return false;  // one token
+        if (!r || r->op != MI355X_GOP_ROPE || r->ne[2] < 1 || r->ne[3] != 1) return false;  // [hd, heads, tokens]
         if (r->op_params[1] != hd || r->op_params[2] != 0) return false;   // n_dims, mode NORMAL
         if (f_of(r->op_params[5]) != opts->rope_freq_base || f_of(r->op_params[6]) != opts->rope_freq_scale)
             return false;
@@ -167,6 +167,8 @@ struct Lower {
         if (!rk || rk->op != MI355X_GOP_ROPE || !rope_ok(rk, hd) || rk->ne[0] != hd) return false;
         const int nkv = (int)rk->ne[1];
         if (nkv <= 0 || nh % nkv) return false;
+        const int64_t T = rq->ne[2];  // tokens of the batch (1: a decode token; > 1: a prompt)
+        if (rk->ne[2] != T) return false;
         const mi355x_gtensor *qmm = root(rq->src[0]), *kmm = root(rk->src[0]), *vmm = root(sv->src[0]);
         if (!qmm || !kmm || !vmm || qmm->op != MI355X_GOP_MUL_MAT || kmm->op != MI355X_GOP_MUL_MAT ||
             vmm->op != MI355X_GOP_MUL_MAT)
@@ -174,7 +176,7 @@ struct Lower {
         // the block's inner values feed nothing outside it
         if (uses[rq] != 1 || uses[rk] != 1 || uses[sm] != 1 || uses[kq] != 1 || uses[kqv] != 1) return false;
         const mi355x_gtensor *pos = rq->src[1];
-        if (!pos || root(rk->src[1]) != root(pos) || pos->type != kTypeI32) return false;
+        if (!pos || root(rk->src[1]) != root(pos) || pos->type != kTypeI32 || pos->ne[0] != T) return false;
         if (kcache->type != kTypeF16 || vcache->type != kTypeF16 || kcache->ne[0] != (int64_t)nkv * hd ||
             vcache->ne[1] != (int64_t)nkv * hd || vcache->ne[0] != kcache->ne[1])
             return false;
@@ -193,9 +195,11 @@ struct Lower {
                                 {value(qmm), value(kmm), value(vmm), leaf(root(pos)), leaf(kcache), leaf(vcache), tab});
         if (!a) return false;
         a->ne[0] = (int64_t)nh * hd;
-        a->ne[1] = a->ne[2] = a->ne[3] = 1;
+        a->ne[1] = T;
+        a->ne[2] = a->ne[3] = 1;
         a->nb[0] = 4;
-        a->nb[1] = a->nb[2] = a->nb[3] = (size_t)nh * hd * 4;
+        a->nb[1] = (size_t)nh * hd * 4;
+        a->nb[2] = a->nb[3] = (size_t)nh * hd * 4 * (size_t)T;
         a->op_params[0] = nh;
         a->op_params[1] = nkv;
         a->op_params[2] = hd;

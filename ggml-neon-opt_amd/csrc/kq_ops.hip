@@ -407,9 +407,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         const int item = t + 256 * ii;
         const int d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
-        h16 acc[8];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) acc[l] = (h16)0.0f;
+        uint32_t acc[4] = {};  // lanes 2k, 2k+1 of accumulator j in word k
         for (int it = 0; it < n_it; ++it) {  // VPF prefetched iterations, then global loads
             const int c0 = 32 * it + 8 * j;
             uint4 vv;
@@ -428,12 +426,9 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
                 vw[l >> 1] = (vw[l >> 1] & (0xffff0000u >> (16 * (l & 1)))) | ((uint32_t)v16[d] << (16 * (l & 1)));
             }
 #pragma unroll
-            for (int l = 0; l < 8; ++l)
-                acc[l] = hfma(u2h((uint16_t)(vw[l >> 1] >> (16 * (l & 1)))), u2h((uint16_t)(pw[l >> 1] >> (16 * (l & 1)))),
-                              acc[l]);
+            for (int k = 0; k < 4; ++k) acc[k] = pk_fma_w(vw[k], pw[k], acc[k]);
         }
-#pragma unroll
-        for (int l = 0; l < 8; ++l) red[(d * 4 + j) * 8 + l] = acc[l];
+        *(uint4 *)(red + (d * 4 + j) * 8) = uint4{acc[0], acc[1], acc[2], acc[3]};
     }
     __syncthreads();
     for (int d = t; d < HD; d += 256) {
@@ -487,9 +482,9 @@ __global__ void __launch_bounds__(256) kq_kv_store(const AttnArgs a) {
     }
 }
 
-// LDS: q16 (HD f16) | w (n_ctx f32) | p16 (n_ctx f16) | red (HD*32 h16) | scal (4 f32) | gsum (n_ctx/4 f64)
+// LDS: q16 (HD f16) | w (n_ctx f32) | p16 (n_ctx f16) | scal (4 f32) | gsum (n_ctx/4 f64)
 size_t attn_prompt_lds(int hd, int n_ctx) {
-    return (size_t)2 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + (size_t)(n_ctx / 4) * 8;
+    return (size_t)2 * hd + (size_t)n_ctx * 6 + 16 + (size_t)(n_ctx / 4) * 8;
 }
 
 template <int HD>
@@ -509,8 +504,7 @@ __global__ void __launch_bounds__(256) kq_attn_prompt(const AttnArgs a) {
     uint16_t *q16 = (uint16_t *)smem;
     float *w = (float *)(smem + 2 * HD);
     uint16_t *p16 = (uint16_t *)(w + a.n_ctx);
-    h16 *red = (h16 *)(p16 + a.n_ctx);
-    float *scal = (float *)(red + HD * 32);
+    float *scal = (float *)(p16 + a.n_ctx);
     double *gsum = (double *)(scal + 4);
 
     if (t < HD / 2) {  // rope(q) at the query's position -> f16
@@ -568,9 +562,7 @@ __global__ void __launch_bounds__(256) kq_attn_prompt(const AttnArgs a) {
         const int item = t + 256 * ii;
         const int d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
-        h16 acc[8];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) acc[l] = (h16)0.0f;
+        uint32_t acc[4] = {};  // lanes 2k, 2k+1 of accumulator j in word k
         for (int it0 = 0; it0 < n_it; it0 += 4) {  // 4 V chunks in flight per round trip
             uint4 vq[4];
 #pragma unroll
@@ -578,29 +570,15 @@ __global__ void __launch_bounds__(256) kq_attn_prompt(const AttnArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
                 if (it0 + k >= n_it) break;
-                const int c0 = 32 * (it0 + k) + 8 * j;
-                const uint4 pp = *(const uint4 *)(p16 + c0);
-                const uint32_t vw[4] = {vq[k].x, vq[k].y, vq[k].z, vq[k].w}, pw[4] = {pp.x, pp.y, pp.z, pp.w};
-#pragma unroll
-                for (int l = 0; l < 8; ++l)
-                    acc[l] = hfma(u2h((uint16_t)(vw[l >> 1] >> (16 * (l & 1)))),
-                                  u2h((uint16_t)(pw[l >> 1] >> (16 * (l & 1)))), acc[l]);
+                const uint4 pp = *(const uint4 *)(p16 + 32 * (it0 + k) + 8 * j);
+                acc[0] = pk_fma_w(vq[k].x, pp.x, acc[0]);
+                acc[1] = pk_fma_w(vq[k].y, pp.y, acc[1]);
+                acc[2] = pk_fma_w(vq[k].z, pp.z, acc[2]);
+                acc[3] = pk_fma_w(vq[k].w, pp.w, acc[3]);
             }
         }
-#pragma unroll
-        for (int l = 0; l < 8; ++l) red[(d * 4 + j) * 8 + l] = acc[l];
-    }
-    __syncthreads();
-    for (int d = t; d < HD; d += 256) {
-        h16 s8[8];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            const h16 s0 = red[(d * 4 + 0) * 8 + l] + red[(d * 4 + 2) * 8 + l];
-            const h16 s1 = red[(d * 4 + 1) * 8 + l] + red[(d * 4 + 3) * 8 + l];
-            s8[l] = s0 + s1;
-        }
-        const float o = f16x8_reduce(s8);
-        a.out[qrow + (int64_t)h * HD + d] = bad ? __builtin_nanf("") : o;
+        const float o = f16x8_reduce_quad(acc);  // accumulators j = 0..3 of output d: one quad
+        if (j == 0) a.out[qrow + (int64_t)h * HD + d] = bad ? __builtin_nanf("") : o;
     }
 }
 
@@ -612,10 +590,10 @@ constexpr int PROMPT_GMAX = 8;  // query heads per kv group handled by kq_attn_p
 #define KQ_PROMPT_DIAG 0  // timing-only builds: 1 no KQ dots, 2 no soft_max sums, 4 no KQV
 #endif
 
-// LDS: q16 [gsz][HD] | w [gsz][n_ctx] f32 | p16 [gsz][n_ctx] | red [gsz][HD*32] h16 |
-//      scal [gsz][4] f32 | gsum [gsz][n_ctx/4] f64
+// LDS: q16 [gsz][HD] | w [gsz][n_ctx] f32 | p16 [gsz][n_ctx] | scal [gsz][4] f32 |
+//      gsum [gsz][n_ctx/4] f64 (the KQV accumulators are reduced across lanes, not in LDS)
 size_t attn_prompt_group_lds(int hd, int n_ctx, int gsz) {
-    return (size_t)gsz * ((size_t)2 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + (size_t)(n_ctx / 4) * 8);
+    return (size_t)gsz * ((size_t)2 * hd + (size_t)n_ctx * 6 + 16 + (size_t)(n_ctx / 4) * 8);
 }
 
 template <int HD>
@@ -637,8 +615,7 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
     uint16_t *q16 = (uint16_t *)smem;                       // [gsz][HD]
     float *w = (float *)(q16 + gsz * HD);                   // [gsz][nc]
     uint16_t *p16 = (uint16_t *)(w + gsz * nc);             // [gsz][nc]
-    h16 *red = (h16 *)(p16 + gsz * nc);                     // [gsz][HD*32]
-    float *scal = (float *)(red + gsz * HD * 32);           // [gsz][4]
+    float *scal = (float *)(p16 + gsz * nc);                // [gsz][4]
     double *gsum = (double *)(scal + 4 * gsz);              // [gsz][nc/4]
 
     for (int u = t; u < gsz * (HD / 2); u += 256) {  // rope(q) of the group's heads -> f16
@@ -708,11 +685,7 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
         const int item = t + 256 * ii;
         const int d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * nc;
-        h16 acc[PROMPT_GMAX][8];
-#pragma unroll
-        for (int hh = 0; hh < PROMPT_GMAX; ++hh)
-#pragma unroll
-            for (int l = 0; l < 8; ++l) acc[hh][l] = (h16)0.0f;
+        uint32_t acc[PROMPT_GMAX][4] = {};  // lanes 2k, 2k+1 of head hh's accumulator j in word k
         for (int it0 = 0; it0 < n_it; it0 += 4) {  // 4 V chunks in flight per round trip
             uint4 vq[4];
 #pragma unroll
@@ -726,33 +699,20 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
                 for (int hh = 0; hh < PROMPT_GMAX; ++hh) {
                     if (hh >= gsz) break;
                     const uint4 pp = *(const uint4 *)(p16 + hh * nc + c0);
-                    const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
-#pragma unroll
-                    for (int l = 0; l < 8; ++l)
-                        acc[hh][l] = hfma(u2h((uint16_t)(vw[l >> 1] >> (16 * (l & 1)))),
-                                          u2h((uint16_t)(pw[l >> 1] >> (16 * (l & 1)))), acc[hh][l]);
+                    acc[hh][0] = pk_fma_w(vw[0], pp.x, acc[hh][0]);
+                    acc[hh][1] = pk_fma_w(vw[1], pp.y, acc[hh][1]);
+                    acc[hh][2] = pk_fma_w(vw[2], pp.z, acc[hh][2]);
+                    acc[hh][3] = pk_fma_w(vw[3], pp.w, acc[hh][3]);
                 }
             }
         }
+        // the 4 accumulators of output d sit in the 4 lanes of a quad (j = t & 3)
 #pragma unroll
-        for (int hh = 0; hh < PROMPT_GMAX; ++hh)
-            if (hh < gsz)
-#pragma unroll
-                for (int l = 0; l < 8; ++l) red[hh * HD * 32 + (d * 4 + j) * 8 + l] = acc[hh][l];
-    }
-    __syncthreads();
-    for (int u = t; u < gsz * HD; u += 256) {
-        const int hh = u / HD, d = u - hh * HD;
-        const h16 *rr = red + hh * HD * 32;
-        h16 s8[8];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            const h16 s0 = rr[(d * 4 + 0) * 8 + l] + rr[(d * 4 + 2) * 8 + l];
-            const h16 s1 = rr[(d * 4 + 1) * 8 + l] + rr[(d * 4 + 3) * 8 + l];
-            s8[l] = s0 + s1;
+        for (int hh = 0; hh < PROMPT_GMAX; ++hh) {
+            if (hh >= gsz) break;
+            const float o = f16x8_reduce_quad(acc[hh]);
+            if (j == 0) a.out[qrow + (int64_t)(g * gsz + hh) * HD + d] = bad ? __builtin_nanf("") : o;
         }
-        const float o = f16x8_reduce(s8);
-        a.out[qrow + (int64_t)(g * gsz + hh) * HD + d] = bad ? __builtin_nanf("") : o;
     }
 }
 

@@ -71,34 +71,62 @@ __device__ __forceinline__ float f16x8_reduce(const h16 s[8]) {
     return (t[0] + t[1]) + (t[2] + t[3]);
 }
 
+// Two f16 lanes per 32-bit word: one v_pk_fma_f16 runs the NEON lanes 2k and 2k+1 (each
+// half an IEEE f16 fma, the scalar v_fma_f16's result), so the lanes stay in their words.
+typedef _Float16 h16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h16x2 w2h(uint32_t w) { return __builtin_bit_cast(h16x2, w); }
+__device__ __forceinline__ uint32_t h2w(h16x2 h) { return __builtin_bit_cast(uint32_t, h); }
+__device__ __forceinline__ uint32_t pk_fma_w(uint32_t a, uint32_t b, uint32_t c) {
+    return h2w(__builtin_elementwise_fma(w2h(a), w2h(b), w2h(c)));
+}
+__device__ __forceinline__ h16 lane_of(const uint32_t w[4], int l) {
+    return u2h((uint16_t)(w[l >> 1] >> (16 * (l & 1))));
+}
+
+__device__ __forceinline__ uint32_t pk_add_w(uint32_t a, uint32_t b) { return h2w(w2h(a) + w2h(b)); }
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_w(uint32_t v) {
+    return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, CTRL, 0xF, 0xF, true);
+}
+// The GGML_F16_VEC_REDUCE of 4 accumulators held by the 4 lanes of a quad (lane j of the
+// quad: accumulator j, 8 f16 lanes in 4 words): sum[0] += sum[2], sum[1] += sum[3],
+// sum[0] += sum[1] per f16 lane (IEEE adds, commutative), then the f32 tail; the result
+// is valid in the quad's lane 0. Every lane of the wave must be active.
+__device__ __forceinline__ float f16x8_reduce_quad(const uint32_t acc[4]) {
+    uint32_t s[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const uint32_t t = pk_add_w(acc[k], dpp_w<0x4E>(acc[k]));  // j0: a0 + a2, j1: a1 + a3
+        s[k] = pk_add_w(t, dpp_w<0xB1>(t));                        // j0: (a0 + a2) + (a1 + a3)
+    }
+    h16 v[8];
+#pragma unroll
+    for (int l = 0; l < 8; ++l) v[l] = lane_of(s, l);
+    return f16x8_reduce(v);
+}
+
 // ggml_vec_dot_f16 (NEON FP16) of two f16 rows held as 8-element vectors of 16-B:
-// x[v], y[v] for v in [0, n/8); n % 32 == 0. Returns the f32 result.
+// x[v], y[v] for v in [0, n/8); n % 32 == 0. Returns the f32 result. Accumulator j of
+// the 4 (vfmaq_f16 on sum[j]) holds lanes 2k, 2k+1 in word acc[j][k].
 template <int N>
 __device__ __forceinline__ float vec_dot_f16_rows(const uint4 *x, const uint4 *y) {
     static_assert(N % 32 == 0, "n % 32");
-    h16 acc[4][8];
-#pragma unroll
-    for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int l = 0; l < 8; ++l) acc[j][l] = (h16)0.0f;
+    uint32_t acc[4][4] = {};
 #pragma unroll
     for (int it = 0; it < N / 32; ++it)
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
             const uint4 xv = x[4 * it + j], yv = y[4 * it + j];
-            const uint32_t xw[4] = {xv.x, xv.y, xv.z, xv.w}, yw[4] = {yv.x, yv.y, yv.z, yv.w};
-#pragma unroll
-            for (int l = 0; l < 8; ++l) {
-                const uint16_t xb = (uint16_t)(xw[l >> 1] >> (16 * (l & 1)));
-                const uint16_t yb = (uint16_t)(yw[l >> 1] >> (16 * (l & 1)));
-                acc[j][l] = hfma(u2h(xb), u2h(yb), acc[j][l]);
-            }
+            acc[j][0] = pk_fma_w(xv.x, yv.x, acc[j][0]);
+            acc[j][1] = pk_fma_w(xv.y, yv.y, acc[j][1]);
+            acc[j][2] = pk_fma_w(xv.z, yv.z, acc[j][2]);
+            acc[j][3] = pk_fma_w(xv.w, yv.w, acc[j][3]);
         }
     h16 s[8];
 #pragma unroll
     for (int l = 0; l < 8; ++l) {
-        const h16 s0 = acc[0][l] + acc[2][l];
-        const h16 s1 = acc[1][l] + acc[3][l];
+        const h16 s0 = lane_of(acc[0], l) + lane_of(acc[2], l);
+        const h16 s1 = lane_of(acc[1], l) + lane_of(acc[3], l);
         s[l] = s0 + s1;
     }
     return f16x8_reduce(s);

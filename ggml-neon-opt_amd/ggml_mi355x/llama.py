@@ -214,7 +214,7 @@ class LlamaDecoder:
         hd, nh, nkv = hp["head_dim"], hp["n_head"], hp["n_head_kv"]
         kvw = nkv * hd
         T, bufs, nodes = [], [], []
-        inp = torch.zeros(2 * n_tok, dtype=torch.int32, device=dev)  # token ids | positions
+        inp = torch.zeros(2 * n_tok + 1, dtype=torch.int32, device=dev)  # token ids | positions | out id
 
         def leaf(t, type_, ne0, ne1=1, row_stride=None):
             x = make_tensor(type_, ne0, ne1, t.data_ptr(), row_stride=row_stride)
@@ -236,7 +236,8 @@ class LlamaDecoder:
 
         eps_bits = [f32_bits(hp["eps"])]
         tok = leaf(inp[:n_tok], TYPE_I32, n_tok)
-        pos = leaf(inp[n_tok:], TYPE_I32, n_tok)
+        pos = leaf(inp[n_tok:2 * n_tok], TYPE_I32, n_tok)
+        out_ids = leaf(inp[2 * n_tok:], TYPE_I32, 1)  # inp_out_ids: the last token's row
         tab = leaf(self.table, TYPE_F32, hd, n_ctx)
         et, ew = weights["token_embd"]
         emb_t = leaf(ew, et, E, ew.shape[0], row_stride=ew.stride(0) * ew.element_size())
@@ -251,27 +252,34 @@ class LlamaDecoder:
             vc = leaf(self.v_cache[i], TYPE_F16, n_ctx, kvw)
             att, _ = node(OP_ATTN_DECODE, nh * hd, [q, k, v, pos, kc, vc, tab], [nh, nkv, hd, scale], ne1=n_tok)
             o = mm(p + "attn_output", att)
-            ffn_inp, _ = node(OP_ADD, E, [o, x], ne1=n_tok)
-            n2, _ = node(OP_RMS_NORM, E, [ffn_inp], eps_bits, ne1=n_tok)
-            m2, _ = node(OP_MUL, E, [n2, leaf(weights[p + "ffn_norm"], TYPE_F32, E)], ne1=n_tok)
+            rows = n_tok
+            if i == hp["n_layer"] - 1 and n_tok > 1:
+                # llm_build_llama's inp_out_ids: after the last attention only the rows whose
+                # logits are wanted (the last token's) go on: GET_ROWS of attn_out and inpSA
+                o, _ = node(OP_GET_ROWS, E, [o, out_ids])
+                x, _ = node(OP_GET_ROWS, E, [x, out_ids])
+                rows = 1
+            ffn_inp, _ = node(OP_ADD, E, [o, x], ne1=rows)
+            n2, _ = node(OP_RMS_NORM, E, [ffn_inp], eps_bits, ne1=rows)
+            m2, _ = node(OP_MUL, E, [n2, leaf(weights[p + "ffn_norm"], TYPE_F32, E)], ne1=rows)
             gt, up = mm(p + "ffn_gate", m2), mm(p + "ffn_up", m2)
-            glu, _ = node(OP_SWIGLU, gt.ne[0], [gt, up], ne1=n_tok)
+            glu, _ = node(OP_SWIGLU, gt.ne[0], [gt, up], ne1=rows)
             dn = mm(p + "ffn_down", glu)
-            x, xb = node(OP_ADD, E, [dn, ffn_inp], ne1=n_tok)
-        last = leaf(xb[(n_tok - 1) * E:], TYPE_F32, E)  # the last token's row (inp_out_ids)
-        n3, _ = node(OP_RMS_NORM, E, [last], eps_bits)
+            x, xb = node(OP_ADD, E, [dn, ffn_inp], ne1=rows)
+        n3, _ = node(OP_RMS_NORM, E, [x], eps_bits)
         m3, _ = node(OP_MUL, E, [n3, leaf(weights["output_norm"], TYPE_F32, E)])
         t_out, w_out = weights["output"]
         wt = leaf(w_out, t_out, w_out.shape[1] * 256 // {12: 144, 13: 176, 14: 210}[t_out], w_out.shape[0],
                   row_stride=w_out.stride(0))
         _, logits = node(OP_MUL_MAT, V, [wt, m3], flags=FLAG_OUTPUT)
-        g = dict(inp=inp, nodes=nodes, tensors=T, bufs=bufs, logits=logits, hidden=xb,
+        g = dict(inp=inp, nodes=nodes, tensors=T, bufs=bufs, logits=logits, hidden=xb, pos=pos,
                  arr=(ctypes.POINTER(type(T[0])) * len(nodes))(*[ctypes.pointer(n) for n in nodes]),
-                 host=torch.zeros(2 * n_tok, dtype=torch.int32).pin_memory())
+                 host=torch.zeros(2 * n_tok + 1, dtype=torch.int32).pin_memory() if self.b is not None else None)
         if not hasattr(self, "_prompts"):
             self._prompts = {}
         self._prompts[n_tok] = g
-        torch.cuda.synchronize()  # zeroed buffers (torch's stream) before the backend stream runs
+        if self.b is not None:
+            torch.cuda.synchronize()  # zeroed buffers (torch's stream) before the backend stream runs
         return g
 
     def prompt(self, tokens, start_pos: int = 0, use_graph: bool = True):
@@ -288,7 +296,8 @@ class LlamaDecoder:
         self.b.synchronize()  # the pinned staging row is reused: the previous prompt's copy is done
         host = g["host"]
         host[:n_tok] = torch_tensor(tokens)
-        host[n_tok:] = torch_tensor(range(start_pos, start_pos + n_tok))
+        host[n_tok:2 * n_tok] = torch_tensor(range(start_pos, start_pos + n_tok))
+        host[2 * n_tok] = n_tok - 1
         L = lib()
         rc = L.mi355x_backend_set_tensor(self.b.h, g["inp"].data_ptr(), host.data_ptr(), 4 * host.numel())
         if rc:

@@ -113,3 +113,27 @@ def test_lowering_supports_every_lowered_node():
     ops = [n.op for n in nodes]
     assert ops.count(g.OP_ATTN_DECODE) == hp["n_layer"]
     assert np.count_nonzero(np.array(ops) == g.OP_MUL_MAT) == 7 * hp["n_layer"] + 1
+
+
+@pytest.mark.parametrize("n_tok", [2, 37])
+def test_llama_prompt_graph_lowers_to_decoder_nodes(n_tok):
+    """A prompt ubatch of llm_build_llama (T tokens, the inp_out_ids GET_ROWS of the last
+    layer) lowers to exactly LlamaDecoder's prompt node list: batched MUL_MATs, the
+    attention block -> one ATTN_DECODE node of T tokens, and every node passes supports_op."""
+    hp = hparams(512, 2, 8, 2, 768, 1024)
+    n_ctx = 64
+    wt, dec = _describe(hp, n_ctx)
+    pg = dec._prompt_graph(n_tok)
+    L = _leaves(hp, wt, dec)
+    L["inp_tokens"] = pg["inp"][:n_tok].data_ptr()
+    L["inp_pos"] = pg["inp"][n_tok:2 * n_tok].data_ptr()
+    L["inp_out_ids"] = pg["inp"][2 * n_tok:].data_ptr()
+    G = GG.llama_decode_graph(hp, L, n_ctx, n_tokens=n_tok)
+    rc, nodes, keep = g.lower_ggml_graph(G.nodes, dec.table.data_ptr(), n_ctx, hp["freq_base"])
+    assert rc == 0
+    got, want = canon(nodes), canon(pg["nodes"])
+    assert len(got) == len(want)
+    for i, (a, b) in enumerate(zip(got, want)):
+        assert a == b, (i, a, b)
+    assert all(g.supports_op(n) for n in nodes)
+    assert [n.op for n in nodes].count(g.OP_ATTN_DECODE) == hp["n_layer"]
