@@ -30,6 +30,12 @@ __global__ void kq_mmq_k4(const MmqArgs a);
 #ifndef KQ_K4_NWV
 #define KQ_K4_NWV 8  // waves of the kq_mmq_k4 instantiation (experiment builds: kq_mmq.hip)
 #endif
+#ifndef KQ_K4_CT
+#define KQ_K4_CT 2
+#endif
+#ifndef KQ_K4_DEPTH
+#define KQ_K4_DEPTH 4
+#endif
 
 namespace {
 
@@ -593,14 +599,14 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
         // workgroup) where its grid fills most of the chip; measured ~7 % faster there and
         // slower on half-empty grids (profiles/r02_prefill_ablation.md)
         const int impl = mmq_impl();
-        constexpr int RT = 32 * KQ_K4_NWV;  // weight rows per workgroup
-        const int64_t g82 = ((N + RT - 1) / RT) * ((M + 63) / 64) * RT / 256;
+        constexpr int RT = 32 * KQ_K4_NWV, CT = 32 * KQ_K4_CT;  // weight rows / columns per workgroup
+        const int64_t g82 = ((N + RT - 1) / RT) * ((M + CT - 1) / CT) * RT * CT / (256 * 64);
         if (impl == MI355X_MMQ_K4 || (impl == MI355X_MMQ_AUTO && g82 >= 160)) {
-            fn = (const void *)kq_mmq_k4<KQ_K4_NWV, 2>;
-            lds = (size_t)4 * 64 * Q8L_STRIDE;
-            grid = dim3((unsigned)((M + 63) / 64), (unsigned)((N + RT - 1) / RT), 1);
+            fn = (const void *)kq_mmq_k4<KQ_K4_NWV, KQ_K4_CT>;
+            lds = (size_t)KQ_K4_DEPTH * CT * Q8L_STRIDE;
+            grid = dim3((unsigned)((M + CT - 1) / CT), (unsigned)((N + RT - 1) / RT), 1);
             block = dim3(64 * KQ_K4_NWV);
-            name = KQ_K4_NWV == 8 ? "kq::kq_mmq_k4<8, 2>" : "kq::kq_mmq_k4<NWV, 2>";
+            name = KQ_K4_NWV == 8 && KQ_K4_CT == 2 ? "kq::kq_mmq_k4<8, 2>" : "kq::kq_mmq_k4<NWV, CT>";
         }
     }
     allow_lds(fn, lds);

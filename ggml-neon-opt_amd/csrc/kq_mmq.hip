@@ -44,6 +44,12 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #ifndef KQ_K4_NWV
 #define KQ_K4_NWV 8
 #endif
+#ifndef KQ_K4_CT
+#define KQ_K4_CT 2  // 32-column MFMA tiles per wave (one scale-split weight operand feeds them all)
+#endif
+#ifndef KQ_K4_DEPTH
+#define KQ_K4_DEPTH 4
+#endif
 // Q6_K chunk loop unrolled by 2 and kq_mmq held to 2 waves per SIMD: fully unrolled, the
 // compiler kept every chunk's MFMA results live (376 VGPRs, one wave per SIMD); now 146
 // and Q6_K prefill 23-29 % faster, Q5_K 4 % (profiles/r02_prefill_ablation.md).
@@ -377,7 +383,8 @@ struct K4Cfg {
     static constexpr int GRAN = SLOT / 16;                 // 608 / 1216 granules
     static constexpr int AINS = (GRAN + 63) / 64;          // 10 / 19 DMA instructions
     static constexpr int NA = (AINS + NWV - 1) / NWV;      // per wave and step
-    static constexpr int DEPTH = 4;
+    static constexpr int DEPTH = KQ_K4_DEPTH;
+    static_assert(DEPTH >= 4, "step b issues dma(b + 3) into slot (b + 3) % DEPTH while slot b is read");
     static constexpr int LDS_BYTES = DEPTH * SLOT;
 };
 
@@ -545,7 +552,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
     }
 }
 
-template __global__ void kq_mmq_k4<KQ_K4_NWV, 2>(const MmqArgs a);
+template __global__ void kq_mmq_k4<KQ_K4_NWV, KQ_K4_CT>(const MmqArgs a);
 
 template __global__ void kq_mmq<Q4_K>(const MmqArgs a);
 template __global__ void kq_mmq<Q5_K>(const MmqArgs a);
