@@ -428,19 +428,8 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) acc[k] = pk_fma_w(vw[k], pw[k], acc[k]);
         }
-        *(uint4 *)(red + (d * 4 + j) * 8) = uint4{acc[0], acc[1], acc[2], acc[3]};
-    }
-    __syncthreads();
-    for (int d = t; d < HD; d += 256) {
-        h16 s[8];
-#pragma unroll
-        for (int l = 0; l < 8; ++l) {
-            const h16 s0 = red[(d * 4 + 0) * 8 + l] + red[(d * 4 + 2) * 8 + l];
-            const h16 s1 = red[(d * 4 + 1) * 8 + l] + red[(d * 4 + 3) * 8 + l];
-            s[l] = s0 + s1;
-        }
-        const float o = f16x8_reduce(s);
-        a.out[(int64_t)h * HD + d] = bad ? __builtin_nanf("") : o;
+        const float o = f16x8_reduce_quad(acc);  // accumulators j = 0..3 of output d: one quad of lanes
+        if (j == 0) a.out[(int64_t)h * HD + d] = bad ? __builtin_nanf("") : o;
     }
 }
 
