@@ -399,7 +399,10 @@ int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8) {
     }
     const int rc = kq::launch_mmq(w->type, w->data, K, w->ne[1], w->nb[1], (const uint8_t *)b->workspace, M,
                                   (float *)t->data, (int64_t)(t->nb[1] / 4), b->stream);
-    if (rc || t->data == q8.src) q8 = Q8State();  // (an output over its own activation)
+    // an output overlapping the quantized activation's bytes invalidates it
+    const uintptr_t o0 = (uintptr_t)t->data, o1 = o0 + (size_t)t->nb[1] * (size_t)t->ne[1];
+    const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;
+    if (rc || (o0 < s1 && s0 < o1)) q8 = Q8State();
     return rc;
 }
 
