@@ -574,8 +574,10 @@ int mmq_impl() {
 }
 
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
-               float *y, int64_t y_col_stride, hipStream_t stream) {
+               float *y, int64_t y_col_stride, hipStream_t stream, const float *res, int64_t res_col_stride) {
     MmqArgs a;
+    a.res = res;
+    a.res_col_stride = res_col_stride;
     a.w = (const uint8_t *)w;
     a.row_stride = (int64_t)row_stride;
     a.n_rows = (int)N;

@@ -123,7 +123,8 @@ mi355x_backend::Captured *find_graph(mi355x_backend *b, const std::vector<uint64
 // (kind GEMV, with its fused neighbours), or any other single node.
 struct Launch {
     int first, count;  // nodes[first .. first+count): the MUL_MAT run, or the single node
-    int kind = 0;      // 0 single node, 1 MUL_MAT run
+    int kind = 0;      // 0 single node, 1 MUL_MAT run (GEMV), 2 prefill prologue -> Q8L, 3 batched MUL_MAT + ADD
+    const mi355x_tensor *q8_of = nullptr;  // kind 2: the node whose (never written) output the Q8L blocks stand for
     int pro = MI355X_PRO_NONE;
     const float *x = nullptr, *x2 = nullptr;  // GEMV input (prologue source) and its second operand
     float eps = 0.f;
@@ -188,13 +189,62 @@ std::vector<int> count_readers(mi355x_tensor *const *nodes, int n) {
     return r;
 }
 
+int64_t nelem(const mi355x_tensor *t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
+
 bool elidable(const mi355x_tensor *t, int readers) {
     return readers == 1 && !(t->flags & MI355X_TENSOR_FLAG_OUTPUT);
 }
 
 bool is_gemv_node(const mi355x_tensor *t) { return t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] == 1; }
 
-std::vector<Launch> plan_launches(mi355x_tensor *const *nodes, int n, bool fuse) {
+// A MUL_MAT of ne11 >= 16 columns on the int8-MFMA GEMM whose activation the previous
+// launch already quantized into the workspace (q/k/v and gate/up of a prompt batch read
+// one normed activation): the GEMM alone. q8_src tracks what the workspace holds.
+struct Q8State {
+    const void *src = nullptr;
+    int64_t k = 0, m = 0;
+    size_t nb = 0;
+};
+
+int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8, float *y = nullptr,
+                       int64_t y_stride = 0, const float *res = nullptr, int64_t res_stride = 0) {
+    const mi355x_tensor *w = t->src[0], *x = t->src[1];
+    if (!y) {
+        y = (float *)t->data;
+        y_stride = (int64_t)(t->nb[1] / 4);
+    }
+    const int64_t K = w->ne[0], M = x->ne[1];
+    const bool same = q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1];
+    if (!same) {
+        const int rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
+                                               b->stream);
+        if (rc) {
+            q8 = Q8State();
+            return rc;
+        }
+        q8.src = x->data;
+        q8.k = K;
+        q8.m = M;
+        q8.nb = x->nb[1];
+    }
+    const int rc = kq::launch_mmq(w->type, w->data, K, w->ne[1], w->nb[1], (const uint8_t *)b->workspace, M, y,
+                                  y_stride, b->stream, res, res_stride);
+    // an output overlapping the quantized activation's bytes invalidates it
+    const uintptr_t o0 = (uintptr_t)y, o1 = o0 + (size_t)y_stride * 4 * (size_t)t->ne[1];
+    const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;
+    if (rc || (o0 < s1 && s0 < o1)) q8 = Q8State();
+    return rc;
+}
+
+bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
+    if (t->op != MI355X_OP_MUL_MAT) return false;
+    const mi355x_tensor *w = t->src[0], *x = t->src[1];
+    if (x->ne[1] < 16 || (x->nb[1] & 3u) || (t->nb[1] & 3u) || ((uintptr_t)b->workspace & 15u)) return false;
+    if (!kq::mmq_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1])) return false;
+    return b->workspace_size >= mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], x->ne[1]);
+}
+
+std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const *nodes, int n, bool fuse) {
     std::vector<Launch> out;
     const std::vector<int> readers = fuse ? count_readers(nodes, n) : std::vector<int>(n, 0);
     auto index_of = [&](const mi355x_tensor *u, int lo, int hi) {
@@ -279,6 +329,67 @@ std::vector<Launch> plan_launches(mi355x_tensor *const *nodes, int n, bool fuse)
             i = end;
             continue;
         }
+        // prefill (batched, ne11 >= 16) fusions: the normed / swiglu'd activation goes straight
+        // into the GEMMs' Q8L blocks (never written as f32), and MUL_MAT -> ADD as the GEMM's
+        // epilogue; only where every consumer takes the shared-activation GEMM
+        if (fuse) {
+            auto shares_run = [&](int first, const mi355x_tensor *src, int &cnt) {
+                cnt = 0;
+                while (first + cnt < n && nodes[first + cnt]->op == MI355X_OP_MUL_MAT &&
+                       nodes[first + cnt]->src[1] == src && batched_mm_shares(b, nodes[first + cnt]))
+                    ++cnt;
+                return cnt > 0;
+            };
+            int cnt = 0;
+            if (t->op == MI355X_OP_RMS_NORM && t->ne[1] >= 16 && i + 2 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
+                nodes[i + 1]->src[0] == t && elidable(t, readers[i]) && nodes[i + 1]->ne[0] == t->ne[0] &&
+                nodes[i + 1]->ne[1] == t->ne[1] && nodes[i + 1]->src[1]->ne[0] == t->ne[0] &&
+                nelem(nodes[i + 1]->src[1]) == t->ne[0] && t->nb[1] == (size_t)t->ne[0] * 4 &&
+                t->src[0]->nb[1] == (size_t)t->ne[0] * 4 && ((uintptr_t)t->src[0]->data & 15u) == 0 &&
+                !(nodes[i + 1]->flags & MI355X_TENSOR_FLAG_OUTPUT) && shares_run(i + 2, nodes[i + 1], cnt) &&
+                readers[i + 1] == cnt) {
+                l.kind = 2;
+                l.pro = MI355X_PRO_RMS_NORM;
+                l.x = (const float *)t->src[0]->data;
+                l.x2 = (const float *)nodes[i + 1]->src[1]->data;
+                l.eps = f_of(t->op_params[0]);
+                l.q8_of = nodes[i + 1];
+                l.count = 2;
+                out.push_back(l);
+                i += 2;
+                continue;
+            }
+            if (t->op == MI355X_OP_SWIGLU && t->ne[1] >= 16 && t->ne[0] % MI355X_QK_K == 0 &&
+                t->nb[1] == (size_t)t->ne[0] * 4 && t->src[0]->nb[1] == t->nb[1] && t->src[1]->nb[1] == t->nb[1] &&
+                nelem(t->src[0]) == nelem(t) && nelem(t->src[1]) == nelem(t) && !(t->flags & MI355X_TENSOR_FLAG_OUTPUT) &&
+                shares_run(i + 1, t, cnt) && readers[i] == cnt) {
+                l.kind = 2;
+                l.pro = MI355X_PRO_SWIGLU;
+                l.x = (const float *)t->src[0]->data;
+                l.x2 = (const float *)t->src[1]->data;
+                l.q8_of = t;
+                out.push_back(l);
+                i += 1;
+                continue;
+            }
+            if (t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] >= 16 && i + 1 < n && nodes[i + 1]->op == MI355X_OP_ADD &&
+                elidable(t, readers[i]) && batched_mm_shares(b, t)) {
+                const mi355x_tensor *ad = nodes[i + 1];
+                const int s_mm = ad->src[0] == t ? 0 : ad->src[1] == t ? 1 : -1;
+                const mi355x_tensor *other = s_mm >= 0 ? ad->src[1 - s_mm] : nullptr;
+                if (other && ad->ne[0] == t->ne[0] && ad->ne[1] == t->ne[1] && other->ne[0] == t->ne[0] &&
+                    other->ne[1] == t->ne[1] && other->nb[0] == 4 && ad->nb[0] == 4 && ad->type == MI355X_TYPE_F32 &&
+                    other->type == MI355X_TYPE_F32) {
+                    l.kind = 3;
+                    l.res[0] = (const float *)other->data;
+                    l.y[0] = (float *)ad->data;
+                    l.count = 2;
+                    out.push_back(l);
+                    i += 2;
+                    continue;
+                }
+            }
+        }
         // single node (with RMS_NORM -> MUL fused when the norm output is only read by the MUL)
         if (fuse && t->op == MI355X_OP_RMS_NORM && i + 1 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
             nodes[i + 1]->src[0] == t && elidable(t, readers[i]) && nodes[i + 1]->ne[0] == t->ne[0] &&
@@ -293,7 +404,6 @@ std::vector<Launch> plan_launches(mi355x_tensor *const *nodes, int n, bool fuse)
     return out;
 }
 
-int64_t nelem(const mi355x_tensor *t) { return t->ne[0] * t->ne[1] * t->ne[2] * t->ne[3]; }
 
 int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
     hipStream_t st = b->stream;
@@ -372,54 +482,32 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
     }
 }
 
-// A MUL_MAT of ne11 >= 16 columns on the int8-MFMA GEMM whose activation the previous
-// launch already quantized into the workspace (q/k/v and gate/up of a prompt batch read
-// one normed activation): the GEMM alone. q8_src tracks what the workspace holds.
-struct Q8State {
-    const void *src = nullptr;
-    int64_t k = 0, m = 0;
-    size_t nb = 0;
-};
-
-int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8) {
-    const mi355x_tensor *w = t->src[0], *x = t->src[1];
-    const int64_t K = w->ne[0], M = x->ne[1];
-    const bool same = q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1];
-    if (!same) {
-        const int rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
-                                               b->stream);
-        if (rc) {
-            q8 = Q8State();
-            return rc;
-        }
-        q8.src = x->data;
-        q8.k = K;
-        q8.m = M;
-        q8.nb = x->nb[1];
-    }
-    const int rc = kq::launch_mmq(w->type, w->data, K, w->ne[1], w->nb[1], (const uint8_t *)b->workspace, M,
-                                  (float *)t->data, (int64_t)(t->nb[1] / 4), b->stream);
-    // an output overlapping the quantized activation's bytes invalidates it
-    const uintptr_t o0 = (uintptr_t)t->data, o1 = o0 + (size_t)t->nb[1] * (size_t)t->ne[1];
-    const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;
-    if (rc || (o0 < s1 && s0 < o1)) q8 = Q8State();
-    return rc;
-}
-
-bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
-    if (t->op != MI355X_OP_MUL_MAT) return false;
-    const mi355x_tensor *w = t->src[0], *x = t->src[1];
-    if (x->ne[1] < 16 || (x->nb[1] & 3u) || (t->nb[1] & 3u) || ((uintptr_t)b->workspace & 15u)) return false;
-    if (!kq::mmq_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1])) return false;
-    return b->workspace_size >= mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], x->ne[1]);
-}
-
 int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<Launch> &launches) {
     Q8State q8;
     if (!kq::device_ok()) return MI355X_E_NODEVICE;
     for (const Launch &l : launches) {
         const mi355x_tensor *t = nodes[l.first];
         int rc;
+        if (l.kind == 2) {  // prefill prologue: the activation's Q8L blocks for the MUL_MATs after it
+            const mi355x_tensor *m = l.q8_of;
+            const int64_t K = m->ne[0], M = m->ne[1];
+            rc = l.pro == MI355X_PRO_RMS_NORM
+                     ? kq::launch_rms_norm_q8L(l.x, l.x2, b->workspace, K, M, l.eps, b->stream)
+                     : kq::launch_swiglu_q8L(l.x, l.x2, b->workspace, K, M, b->stream);
+            if (rc) return rc;
+            q8.src = m->data;
+            q8.k = K;
+            q8.m = M;
+            q8.nb = m->nb[1];
+            continue;
+        }
+        if (l.kind == 3) {  // batched MUL_MAT with the residual ADD as its epilogue
+            const mi355x_tensor *ad = nodes[l.first + 1];
+            const mi355x_tensor *other = ad->src[0] == t ? ad->src[1] : ad->src[0];
+            rc = enqueue_batched_mm(b, t, q8, l.y[0], (int64_t)(ad->nb[1] / 4), l.res[0], (int64_t)(other->nb[1] / 4));
+            if (rc) return rc;
+            continue;
+        }
         if (l.kind != 1 && l.count == 1 && batched_mm_shares(b, t)) {
             rc = enqueue_batched_mm(b, t, q8);
             if (rc) return rc;
@@ -739,7 +827,7 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
         if (hipMalloc(&b->workspace, ws) != hipSuccess) return MI355X_E_WORKSPACE;
         b->workspace_size = ws;
     }
-    const std::vector<Launch> launches = plan_launches(nodes, n_nodes, b->fuse);
+    const std::vector<Launch> launches = plan_launches(b, nodes, n_nodes, b->fuse);
     if (!use_graph) return enqueue(b, nodes, launches);
     std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);
     mi355x_backend::Captured *c = find_graph(b, key);

@@ -204,6 +204,8 @@ struct MmqArgs {
     float *y;                // dst column j at y + j * y_col_stride
     int64_t y_col_stride;    // floats
     int nb;
+    const float *res;        // ADD epilogue (null: none): y = mul_mat + res, res column j at
+    int64_t res_col_stride;  //   res + j * res_col_stride (the one f32 add of ggml_add)
 };
 
 }  // namespace kq

@@ -57,7 +57,11 @@ bool mmq_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t 
 int launch_quantize_q8L(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
                         hipStream_t stream);
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
-               float *y, int64_t y_col_stride, hipStream_t stream);
+               float *y, int64_t y_col_stride, hipStream_t stream, const float *res = nullptr,
+               int64_t res_col_stride = 0);  // res: ADD epilogue
+// prefill prologues: rms_norm(x) * w -> Q8L, swiglu(g, u) -> Q8L (nrows rows of n)
+int launch_rms_norm_q8L(const float *x, const float *w, void *yq, int64_t n, int64_t nrows, float eps, hipStream_t s);
+int launch_swiglu_q8L(const float *g, const float *u, void *yq, int64_t n, int64_t nrows, hipStream_t s);
 int launch_swiglu(const float *g, const float *u, float *y, int64_t n, hipStream_t s);
 int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a);  // + check_attn
 int launch_attn(const AttnArgs &a, hipStream_t s);

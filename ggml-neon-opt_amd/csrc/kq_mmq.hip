@@ -348,7 +348,8 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int m = col0 + 32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (m < a.m_cols) a.y[(int64_t)m * a.y_col_stride + n] = sumf[i];
+            if (m < a.m_cols)
+                a.y[(int64_t)m * a.y_col_stride + n] = a.res ? sumf[i] + a.res[(int64_t)m * a.res_col_stride + n] : sumf[i];
         }
     }
 }
@@ -547,7 +548,9 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const int m = col0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (m < a.m_cols) a.y[(int64_t)m * a.y_col_stride + n] = sumf[c][i];
+                if (m < a.m_cols)
+                    a.y[(int64_t)m * a.y_col_stride + n] =
+                        a.res ? sumf[c][i] + a.res[(int64_t)m * a.res_col_stride + n] : sumf[c][i];
             }
     }
 }

@@ -21,6 +21,9 @@
 //    304-B "Q8L" blocks: d @0, qs @16, bsums @272): 16 lanes per superblock, x
 //    loaded by inline-asm global loads issued before the weight DMAs (K <= 8192);
 //    above that kq_quantize_q8L writes Q8L blocks to a workspace, copied by DMA.
+#include <hip/hip_ext.h>
+
+#include "kq_internal.h"
 #include "kq_ops_device.h"
 #include "kq_rows_device.h"
 
@@ -39,6 +42,116 @@ __global__ void __launch_bounds__(WG_THREADS) kq_quantize_q8L(const float *__res
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = *(const u32x4 *)(xb + 4 * k);
     quant16_store(v, lane & 15, y + bi * Q8L_STRIDE);
+}
+
+// ------------------------------------------------------------ prefill prologues
+// The prompt graph's RMS_NORM -> MUL(norm weight) -> MUL_MATs and SWIGLU -> MUL_MAT:
+// the op's arithmetic exactly as kq_rms_norm / kq_swiglu compute it (same sum order and
+// exactness guard, (x*scale)*w; silu(g)*u on the NEON path), quantized straight into the
+// GEMMs' Q8L blocks (row r's superblock b at (r*nb + b)*304); the f32 intermediate is
+// never written.
+__global__ void __launch_bounds__(256) kq_rms_norm_q8L(const float *__restrict__ x, const float *__restrict__ w,
+                                                       uint8_t *__restrict__ yq, int64_t n, float eps) {
+    extern __shared__ __attribute__((aligned(16))) double sb_sum[];
+    const int64_t row = blockIdx.x;
+    const float *xr = x + row * n;
+    const int nb = (int)(n / QK);
+    const int rid = threadIdx.x >> 4, l = threadIdx.x & 15;
+    for (int b0 = 0; b0 < nb; b0 += 16) {
+        const int b = b0 + rid;
+        double s = 0.0;
+        if (b < nb) {
+            float v[16];
+            const float4 *p = (const float4 *)(xr + (int64_t)b * QK + 16 * l);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 t = p[k];
+                v[4 * k] = t.x, v[4 * k + 1] = t.y, v[4 * k + 2] = t.z, v[4 * k + 3] = t.w;
+            }
+            s = sumsq16(v);
+        }
+        s = row16_sum(s);
+        if (b < nb && l == 0) sb_sum[b] = s;
+    }
+    __syncthreads();
+    double total = seq_sum_lds(sb_sum, nb);  // superblocks in order
+    if (rms_mean_ambiguous(div_by_count(total, n), n)) {  // ggml's sequential order (block-uniform)
+        __syncthreads();
+        if (threadIdx.x < 64) {
+            const double s = seq_sumsq_wave(xr, n, threadIdx.x);
+            if (threadIdx.x == 0) sb_sum[0] = s;
+        }
+        __syncthreads();
+        total = sb_sum[0];
+    }
+    const float mean = (float)div_by_count(total, n);
+    const float scale = 1.0f / sqrtf(mean + eps);
+    for (int b0 = 0; b0 < nb; b0 += 16) {
+        const int b = b0 + rid;  // uniform over the 16-lane row: quant16_store's DPP row
+        if (b >= nb) continue;
+        const float4 *p = (const float4 *)(xr + (int64_t)b * QK + 16 * l);
+        const float4 *q = (const float4 *)(w + (int64_t)b * QK + 16 * l);
+        u32x4 v[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const float4 t = p[k], m = q[k];
+            v[k].x = __float_as_uint((t.x * scale) * m.x);
+            v[k].y = __float_as_uint((t.y * scale) * m.y);
+            v[k].z = __float_as_uint((t.z * scale) * m.z);
+            v[k].w = __float_as_uint((t.w * scale) * m.w);
+        }
+        quant16_store(v, l, yq + (row * nb + b) * Q8L_STRIDE);
+    }
+}
+
+__global__ void __launch_bounds__(256) kq_swiglu_q8L(const float *__restrict__ g, const float *__restrict__ u,
+                                                     uint8_t *__restrict__ yq, int nb, int64_t nblocks) {
+    const int64_t bi = (int64_t)blockIdx.x * 16 + (threadIdx.x >> 4);  // superblock (row * nb + b)
+    if (bi >= nblocks) return;  // whole 16-lane rows drop out together
+    const int l = threadIdx.x & 15;
+    const int64_t e0 = bi * QK + 16 * l;  // rows are contiguous: element index = superblock * 256 + ...
+    u32x4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        const float4 gv = *(const float4 *)(g + e0 + 4 * k), uv = *(const float4 *)(u + e0 + 4 * k);
+        v[k].x = __float_as_uint(v_silu(gv.x) * uv.x);
+        v[k].y = __float_as_uint(v_silu(gv.y) * uv.y);
+        v[k].z = __float_as_uint(v_silu(gv.z) * uv.z);
+        v[k].w = __float_as_uint(v_silu(gv.w) * uv.w);
+    }
+    (void)nb;
+    quant16_store(v, l, yq + bi * Q8L_STRIDE);
+}
+
+int launch_rms_norm_q8L(const float *x, const float *w, void *yq, int64_t n, int64_t nrows, float eps, hipStream_t s) {
+    if (nrows == 0) return MI355X_OK;
+    hipEvent_t e0, e1;
+    const size_t lds = (size_t)(n / QK) * 8 + 8;
+    if (timing_slot(s, e0, e1)) {
+        hipExtLaunchKernelGGL(kq_rms_norm_q8L, dim3((unsigned)nrows), dim3(256), (uint32_t)lds, s, e0, e1, 0, x, w,
+                              (uint8_t *)yq, n, eps);
+        timing_log("kq::kq_rms_norm_q8L", (double)nrows * (n * 4.0 + (n / QK) * (double)Q8L_STRIDE) + n * 4.0, e0, e1);
+    } else {
+        hipLaunchKernelGGL(kq_rms_norm_q8L, dim3((unsigned)nrows), dim3(256), lds, s, x, w, (uint8_t *)yq, n, eps);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+int launch_swiglu_q8L(const float *g, const float *u, void *yq, int64_t n, int64_t nrows, hipStream_t s) {
+    const int64_t nb = n / QK, nblocks = nb * nrows;
+    if (nblocks == 0) return MI355X_OK;
+    const int64_t wgs = (nblocks + 15) / 16;
+    hipEvent_t e0, e1;
+    if (timing_slot(s, e0, e1)) {
+        hipExtLaunchKernelGGL(kq_swiglu_q8L, dim3((unsigned)wgs), dim3(256), 0, s, e0, e1, 0, g, u, (uint8_t *)yq,
+                              (int)nb, nblocks);
+        timing_log("kq::kq_swiglu_q8L", (double)nblocks * (QK * 8.0 + Q8L_STRIDE), e0, e1);
+    } else {
+        hipLaunchKernelGGL(kq_swiglu_q8L, dim3((unsigned)wgs), dim3(256), 0, s, g, u, (uint8_t *)yq, (int)nb, nblocks);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
 }
 
 template <int TYPE, bool FUSEDQ, int PRO>
