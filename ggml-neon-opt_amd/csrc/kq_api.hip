@@ -576,6 +576,8 @@ int mmq_impl() {
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
                float *y, int64_t y_col_stride, hipStream_t stream, const float *res, int64_t res_col_stride) {
     MmqArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n_mat = 1;
     a.res = res;
     a.res_col_stride = res_col_stride;
     a.w = (const uint8_t *)w;
@@ -622,6 +624,68 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
                    e0, e1);
     } else {
         e = hipLaunchKernel(fn, grid, block, args, lds, stream);
+    }
+    if (e != hipSuccess) return (int)e;
+    e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+// Whether launch_mmq would run this GEMM on the 64 x 64 tile kernel (not kq_mmq_k4).
+bool mmq_tile64(int type, int64_t N, int64_t M) {
+    if (type != Q4_K) return true;
+    const int impl = mmq_impl();
+    constexpr int RT = 32 * KQ_K4_NWV, CT = 32 * KQ_K4_CT;
+    const int64_t g82 = ((N + RT - 1) / RT) * ((M + CT - 1) / CT) * RT * CT / (256 * 64);
+    return !(impl == MI355X_MMQ_K4 || (impl == MI355X_MMQ_AUTO && g82 >= 160));
+}
+
+// Up to 4 matrices of one type on one Q8L activation in ONE 64 x 64-tile launch (a prompt
+// batch's q/k/v: the small k/v GEMMs no longer run as half-empty launches of their own).
+int launch_mmq_multi(int type, int n_mat, const void *const *w, const int64_t *N, const size_t *row_stride,
+                     float *const *y, const int64_t *y_col_stride, int64_t K, const uint8_t *xq, int64_t M,
+                     hipStream_t stream) {
+    if (n_mat < 1 || n_mat > 4) return MI355X_E_INVAL;
+    MmqArgs a;
+    memset(&a, 0, sizeof(a));
+    a.n_mat = n_mat;
+    a.xq = xq;
+    a.nb = (int)(K / QK);
+    a.xq_col_stride = (int64_t)a.nb * Q8L_STRIDE;
+    a.m_cols = (int)M;
+    int tiles = 0;
+    double wbytes = 0, ybytes = 0;
+    for (int d = 0; d < n_mat; ++d) {
+        a.tile0[d] = tiles;
+        a.mw[d] = (const uint8_t *)w[d];
+        a.mrow_stride[d] = (int64_t)row_stride[d];
+        a.mn_rows[d] = (int)N[d];
+        a.my[d] = y[d];
+        a.my_col_stride[d] = y_col_stride[d];
+        tiles += (int)((N[d] + 63) / 64);
+        wbytes += (double)N[d] * a.nb * block_bytes(type);
+        ybytes += (double)M * N[d] * 4.0;
+    }
+    a.tile0[n_mat] = tiles;
+    a.w = a.mw[0];
+    a.row_stride = a.mrow_stride[0];
+    a.n_rows = a.mn_rows[0];
+    a.y = a.my[0];
+    a.y_col_stride = a.my_col_stride[0];
+    const void *fn = type == Q5_K ? (const void *)kq_mmq<Q5_K>
+                   : type == Q6_K ? (const void *)kq_mmq<Q6_K>
+                                  : (const void *)kq_mmq<Q4_K>;
+    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16;
+    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)tiles, 1);
+    allow_lds(fn, lds);
+    hipEvent_t e0, e1;
+    void *args[] = {&a};
+    hipError_t e;
+    if (timing_slot(stream, e0, e1)) {
+        e = hipExtLaunchKernel(fn, grid, dim3(256), args, lds, stream, e0, e1, 0);
+        timing_log(std::string("kq::kq_mmq<") + std::to_string(type) + ">", wbytes + (double)M * a.nb * Q8L_STRIDE + ybytes,
+                   e0, e1);
+    } else {
+        e = hipLaunchKernel(fn, grid, dim3(256), args, lds, stream);
     }
     if (e != hipSuccess) return (int)e;
     e = hipGetLastError();

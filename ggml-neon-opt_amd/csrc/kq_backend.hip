@@ -123,7 +123,8 @@ mi355x_backend::Captured *find_graph(mi355x_backend *b, const std::vector<uint64
 // (kind GEMV, with its fused neighbours), or any other single node.
 struct Launch {
     int first, count;  // nodes[first .. first+count): the MUL_MAT run, or the single node
-    int kind = 0;      // 0 single node, 1 MUL_MAT run (GEMV), 2 prefill prologue -> Q8L, 3 batched MUL_MAT + ADD
+    int kind = 0;      // 0 single node, 1 MUL_MAT run (GEMV), 2 prefill prologue -> Q8L, 3 batched MUL_MAT + ADD,
+                       // 4 batched MUL_MATs of one type on one activation in one tile-GEMM launch
     const mi355x_tensor *q8_of = nullptr;  // kind 2: the node whose (never written) output the Q8L blocks stand for
     int pro = MI355X_PRO_NONE;
     const float *x = nullptr, *x2 = nullptr;  // GEMV input (prologue source) and its second operand
@@ -372,6 +373,25 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 i += 1;
                 continue;
             }
+            if (t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] >= 16 && batched_mm_shares(b, t) &&
+                kq::mmq_tile64(t->src[0]->type, t->src[0]->ne[1], t->src[1]->ne[1])) {
+                int run = 1;
+                while (i + run < n && run < 4) {
+                    const mi355x_tensor *u = nodes[i + run];
+                    if (u->op != MI355X_OP_MUL_MAT || u->src[1] != t->src[1] || u->src[0]->type != t->src[0]->type ||
+                        u->src[0]->ne[0] != t->src[0]->ne[0] || !batched_mm_shares(b, u) ||
+                        !kq::mmq_tile64(u->src[0]->type, u->src[0]->ne[1], u->src[1]->ne[1]))
+                        break;
+                    ++run;
+                }
+                if (run >= 2) {
+                    l.kind = 4;
+                    l.count = run;
+                    out.push_back(l);
+                    i += run;
+                    continue;
+                }
+            }
             if (t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] >= 16 && i + 1 < n && nodes[i + 1]->op == MI355X_OP_ADD &&
                 elidable(t, readers[i]) && batched_mm_shares(b, t)) {
                 const mi355x_tensor *ad = nodes[i + 1];
@@ -499,6 +519,40 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
             q8.k = K;
             q8.m = M;
             q8.nb = m->nb[1];
+            continue;
+        }
+        if (l.kind == 4) {  // several batched MUL_MATs on one activation: one tile-GEMM launch
+            const mi355x_tensor *x = t->src[1];
+            const int64_t K = t->src[0]->ne[0], M = x->ne[1];
+            if (!(q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1])) {
+                rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
+                                             b->stream);
+                if (rc) return rc;
+                q8.src = x->data;
+                q8.k = K;
+                q8.m = M;
+                q8.nb = x->nb[1];
+            }
+            const void *w[4];
+            int64_t N[4], ycs[4];
+            size_t rs[4];
+            float *y[4];
+            for (int k = 0; k < l.count; ++k) {
+                const mi355x_tensor *u = nodes[l.first + k];
+                w[k] = u->src[0]->data;
+                N[k] = u->src[0]->ne[1];
+                rs[k] = u->src[0]->nb[1];
+                y[k] = (float *)u->data;
+                ycs[k] = (int64_t)(u->nb[1] / 4);
+            }
+            rc = kq::launch_mmq_multi(t->src[0]->type, l.count, w, N, rs, y, ycs, K, (const uint8_t *)b->workspace, M,
+                                      b->stream);
+            if (rc) return rc;
+            const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;
+            for (int k = 0; k < l.count; ++k) {  // an output over the quantized activation invalidates it
+                const uintptr_t o0 = (uintptr_t)y[k], o1 = o0 + (size_t)ycs[k] * 4 * (size_t)M;
+                if (o0 < s1 && s0 < o1) q8 = Q8State();
+            }
             continue;
         }
         if (l.kind == 3) {  // batched MUL_MAT with the residual ADD as its epilogue

@@ -206,6 +206,16 @@ struct MmqArgs {
     int nb;
     const float *res;        // ADD epilogue (null: none): y = mul_mat + res, res column j at
     int64_t res_col_stride;  //   res + j * res_col_stride (the one f32 add of ggml_add)
+    // kq_mmq (64 x 64 tiles) over up to 4 matrices of one type sharing the activation
+    // (q/k/v of a prompt batch): row tiles [tile0[d], tile0[d+1]) are matrix d's; n_mat 1:
+    // the fields above only
+    int n_mat;
+    int tile0[5];
+    const uint8_t *mw[4];
+    int64_t mrow_stride[4];
+    int mn_rows[4];
+    float *my[4];
+    int64_t my_col_stride[4];
 };
 
 }  // namespace kq

@@ -157,7 +157,8 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
 }
 
 template <int TYPE>
-__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a) {
+__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) {
+    MmqArgs a = a0;  // (the matrix of this row tile, below)
     constexpr int BSZ = block_bytes(TYPE);
     constexpr int NB_I = mmq_b_instr(TYPE);
     constexpr int NW = mmq_nw(TYPE);
@@ -181,6 +182,18 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a) {
             ty = 8 * grp + in % 8;
             tx = in / 8;
         }
+    }
+    if (a0.n_mat > 1) {  // several matrices on one activation: this row tile's matrix
+        int d = 0;
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+            if (k < a0.n_mat && ty >= a0.tile0[k]) d = k;
+        a.w = a0.mw[d];
+        a.row_stride = a0.mrow_stride[d];
+        a.n_rows = a0.mn_rows[d];
+        a.y = a0.my[d];
+        a.y_col_stride = a0.my_col_stride[d];
+        ty -= a0.tile0[d];
     }
     const int col0 = tx * MMQ_TILE, row0 = ty * MMQ_TILE;
     const int nb = a.nb;
