@@ -237,6 +237,22 @@ int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8, f
     return rc;
 }
 
+void attn_desc_of(const mi355x_tensor *t, mi355x_attn_desc &a) {
+    a.q = (const float *)t->src[0]->data;
+    a.k = (const float *)t->src[1]->data;
+    a.v = (const float *)t->src[2]->data;
+    a.pos = (const int32_t *)t->src[3]->data;
+    a.k_cache = (uint16_t *)t->src[4]->data;
+    a.v_cache = (uint16_t *)t->src[5]->data;
+    a.rope_table = (const float *)t->src[6]->data;
+    a.out = (float *)t->data;
+    a.n_head = t->op_params[0];
+    a.n_head_kv = t->op_params[1];
+    a.head_dim = t->op_params[2];
+    a.scale = f_of(t->op_params[3]);
+    a.n_ctx = (int)t->src[4]->ne[1];
+}
+
 bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
     if (t->op != MI355X_OP_MUL_MAT) return false;
     const mi355x_tensor *w = t->src[0], *x = t->src[1];
@@ -476,19 +492,7 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
         }
         case MI355X_OP_ATTN_DECODE: {
             mi355x_attn_desc a;
-            a.q = (const float *)t->src[0]->data;
-            a.k = (const float *)t->src[1]->data;
-            a.v = (const float *)t->src[2]->data;
-            a.pos = (const int32_t *)t->src[3]->data;
-            a.k_cache = (uint16_t *)t->src[4]->data;
-            a.v_cache = (uint16_t *)t->src[5]->data;
-            a.rope_table = (const float *)t->src[6]->data;
-            a.out = (float *)t->data;
-            a.n_head = t->op_params[0];
-            a.n_head_kv = t->op_params[1];
-            a.head_dim = t->op_params[2];
-            a.scale = f_of(t->op_params[3]);
-            a.n_ctx = (int)t->src[4]->ne[1];
+            attn_desc_of(t, a);
             const int64_t n_tok = t->src[0]->ne[1];
             if (n_tok > 1) {  // a prompt batch: all cells first, then every query (causal)
                 a.rope_row = 0;
@@ -502,12 +506,49 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
     }
 }
 
+// A prompt ATTN_DECODE (>= 16 tokens, contiguous rows) whose output is the activation of the
+// batched MUL_MAT the next launch starts with, on the group kernel that can write its Q8L rows.
+bool attn_feeds_batched_mm(const mi355x_backend *b, const mi355x_tensor *t, const Launch &next,
+                           mi355x_tensor *const *nodes) {
+    if (t->src[0]->ne[1] < 16 || t->nb[1] != (size_t)t->ne[0] * 4) return false;
+    if (next.kind != 0 && next.kind != 3 && next.kind != 4) return false;
+    const mi355x_tensor *m = nodes[next.first];
+    if (m->op != MI355X_OP_MUL_MAT || m->src[1] != t || m->src[0]->ne[0] != t->ne[0]) return false;
+    if (next.kind == 0 && next.count != 1) return false;
+    if (!batched_mm_shares(b, m)) return false;
+    mi355x_attn_desc d;
+    attn_desc_of(t, d);
+    d.rope_row = 0;
+    kq::AttnArgs a;
+    return kq::attn_args_from(&d, a) == 0 && kq::attn_prompt_q8_ok(a);
+}
+
 int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<Launch> &launches) {
     Q8State q8;
     if (!kq::device_ok()) return MI355X_E_NODEVICE;
-    for (const Launch &l : launches) {
+    for (size_t li = 0; li < launches.size(); ++li) {
+        const Launch &l = launches[li];
         const mi355x_tensor *t = nodes[l.first];
         int rc;
+        if (l.kind == 0 && t->op == MI355X_OP_ATTN_DECODE && li + 1 < launches.size() &&
+            attn_feeds_batched_mm(b, t, launches[li + 1], nodes)) {
+            // prompt attention whose output only the next launch's GEMM reads (the o-proj):
+            // the group kernel also writes that GEMM's Q8L blocks, no kq_quantize_q8L launch
+            mi355x_attn_desc d;
+            attn_desc_of(t, d);
+            d.rope_row = 0;
+            kq::AttnArgs a;
+            rc = kq::attn_args_from(&d, a);
+            if (rc) return rc;
+            a.q8_out = (uint8_t *)b->workspace;
+            rc = kq::launch_attn_prompt(a, (int)t->src[0]->ne[1], b->stream);
+            if (rc) return rc;
+            q8.src = t->data;
+            q8.k = t->ne[0];
+            q8.m = t->ne[1];
+            q8.nb = t->nb[1];
+            continue;
+        }
         if (l.kind == 2) {  // prefill prologue: the activation's Q8L blocks for the MUL_MATs after it
             const mi355x_tensor *m = l.q8_of;
             const int64_t K = m->ne[0], M = m->ne[1];

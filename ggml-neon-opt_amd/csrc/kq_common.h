@@ -190,6 +190,8 @@ struct AttnArgs {
     float scale;
     int diag;  // diagnostics only (MI355X_ATTN_DIAG): 1/2/3 stop after loads/KQ/soft_max, 4 empty
     int rope_row;  // rope_table holds only the row of *pos (no position-dependent load)
+    uint8_t *q8_out;  // prompt batch (kq_attn_prompt_group): also the output rows as Q8L blocks
+                      // for the next GEMM (row i's superblock b at (i*nb + b)*304), or null
 };
 
 // ---------------------------------------------------------------- batched (prefill) MFMA GEMM

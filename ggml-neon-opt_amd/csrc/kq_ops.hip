@@ -29,6 +29,7 @@
 #include "kq_attn_device.h"
 #include "kq_device.h"
 #include "kq_ops_device.h"
+#include "kq_rows_device.h"
 
 namespace kq {
 
@@ -658,9 +659,8 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
         gsum[hh * (nc / 4) + gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));
     }
     __syncthreads();
-    if ((t & 63) == 0 && (t >> 6) < gsz)  // the in-order double sums, one lane per head
-        for (int hh = t >> 6; hh < gsz; hh += 4)
-            scal[4 * hh + 1] = (KQ_PROMPT_DIAG & 2) ? (float)gsum[hh * (nc / 4)] : (float)(1.0 / seq_sum_lds(gsum + hh * (nc / 4), ng));
+    if (t < gsz)  // the in-order double sums: lane hh of wave 0 runs head hh's, all heads at once
+        scal[4 * t + 1] = (KQ_PROMPT_DIAG & 2) ? (float)gsum[t * (nc / 4)] : (float)(1.0 / seq_sum_lds(gsum + t * (nc / 4), ng));
     __syncthreads();
     for (int u = t; u < gsz * n_kv; u += 256) {
         const int hh = u / n_kv, c = u - hh * n_kv;
@@ -699,8 +699,26 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
 #pragma unroll
         for (int hh = 0; hh < PROMPT_GMAX; ++hh) {
             if (hh >= gsz) break;
-            const float o = f16x8_reduce_quad(acc[hh]);
-            if (j == 0) a.out[qrow + (int64_t)(g * gsz + hh) * HD + d] = bad ? __builtin_nanf("") : o;
+            const float o = bad ? __builtin_nanf("") : f16x8_reduce_quad(acc[hh]);
+            if (j == 0) {
+                a.out[qrow + (int64_t)(g * gsz + hh) * HD + d] = o;
+                if (a.q8_out) w[hh * HD + d] = o;  // staged for the Q8L blocks (w is free now)
+            }
+        }
+    }
+    if (a.q8_out) {  // the group's gsz*HD outputs (whole superblocks of the row) -> Q8L
+        __syncthreads();
+        const int nsb = gsz * HD / QK, rid = t >> 4, l = t & 15;
+        if (rid < nsb) {  // uniform over each 16-lane row (quant16_store's DPP row)
+            const float *src = w + rid * QK + 16 * l;
+            u32x4 v[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float4 f = ((const float4 *)src)[k];
+                v[k] = u32x4{__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
+            }
+            const int64_t nbr = (int64_t)a.n_head * HD / QK;  // superblocks per row
+            quant16_store(v, l, a.q8_out + ((int64_t)i * nbr + (int64_t)g * nsb + rid) * Q8L_STRIDE);
         }
     }
 }
@@ -808,13 +826,26 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
 // where the group fits) or MI355X_ATTN_HEAD (one per query head and token)
 std::atomic<int> g_prompt_impl{MI355X_ATTN_GROUP};
 
+bool attn_prompt_group_ok(const AttnArgs &a) {
+    const int gsz = a.n_head / a.n_head_kv;
+    return gsz <= PROMPT_GMAX && attn_prompt_group_lds(a.head_dim, a.n_ctx, gsz) <= 160 * 1024 &&
+           g_prompt_impl.load() == MI355X_ATTN_GROUP;
+}
+
+// Q8L rows written by the group kernel: its slice (gsz*head_dim) must be whole superblocks
+bool attn_prompt_q8_ok(const AttnArgs &a) {
+    return attn_prompt_group_ok(a) && ((a.n_head / a.n_head_kv) * a.head_dim) % QK == 0 &&
+           a.n_ctx >= a.head_dim;  // staged in the score rows: gsz*head_dim floats
+}
+
 int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
     if (n_tok <= 0) return MI355X_OK;
     const size_t lds = attn_prompt_lds(a.head_dim, a.n_ctx);
     const int gsz = a.n_head / a.n_head_kv;
     const size_t glds = attn_prompt_group_lds(a.head_dim, a.n_ctx, gsz);
     // one workgroup per (kv group, token) where the group's heads fit: 1/gsz of the cache reads
-    const bool group = gsz <= PROMPT_GMAX && glds <= 160 * 1024 && g_prompt_impl.load() == MI355X_ATTN_GROUP;
+    const bool group = attn_prompt_group_ok(a);
+    if (a.q8_out && !group) return MI355X_E_INVAL;  // only the group kernel writes the Q8L rows
     const dim3 gs((unsigned)n_tok, (unsigned)a.n_head_kv), ga((unsigned)a.n_head, (unsigned)n_tok);
     const dim3 gg((unsigned)a.n_head_kv, (unsigned)n_tok);
     int rc;
@@ -986,6 +1017,7 @@ int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a) {
     a.head_dim = d->head_dim;
     a.scale = d->scale;
     a.rope_row = d->rope_row ? 1 : 0;
+    a.q8_out = nullptr;
     static const int diag = [] {
         const char *e = getenv("MI355X_ATTN_DIAG");
         return e ? atoi(e) : 0;
