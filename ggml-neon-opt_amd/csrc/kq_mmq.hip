@@ -64,6 +64,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #else
 #define KQ_MMQ_WPE_ATTR
 #endif
+#ifndef KQ_MMQ_Q6_VALU
+#define KQ_MMQ_Q6_VALU 0  // experiment build: Q6_K group scales on VALU (round-2 kernel)
+#endif
 #ifndef KQ_MMQ_Q4_VALU
 #define KQ_MMQ_Q4_VALU 0
 #endif
@@ -98,12 +101,12 @@ __host__ __device__ constexpr int mmq_b_instr(int type) { return MMQ_TILE * mmq_
 __host__ __device__ constexpr int mmq_nw(int type) { return (MMQ_A_INSTR + mmq_b_instr(type) + 3) / 4; }
 __host__ __device__ constexpr int mmq_buf(int type) { return MMQ_A_BYTES + MMQ_TILE * mmq_row_bytes(type); }
 
-// Q6_K superblock of one 32x32 tile: 8 chunks of 32 elements; a lane's 16 values
+// (KQ_MMQ_Q6_VALU experiment build) Q6_K superblock of one 32x32 tile: 8 chunks of 32 elements; a lane's 16 values
 // of a chunk are one 16-element scale group, so two MFMAs per chunk (the other
 // half's operand zeroed) give each group's dot, scaled by its int8 scale on VALU.
 // The weight operand is q - 32 (sign-extended 6-bit), so the sum is directly the
 // reference's isum - 32*isum_mins (README.md:369-394 / lane_q6K): no mins term.
-__device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *buf, const uint8_t *At, int n, int b,
+__device__ __forceinline__ void q6_superblock_valu(const MmqArgs &a, const uint8_t *buf, const uint8_t *At, int n, int b,
                                               int r, int h, int wm, int wn, f32x16 &sumf) {
     const int nrow = n < a.n_rows ? n : a.n_rows - 1;  // the DMA clamped the same way
     const uint32_t mis = (uint32_t)((uintptr_t)(a.w + (int64_t)nrow * a.row_stride + (int64_t)b * 210) & 15u);
@@ -153,6 +156,63 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
         const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
         const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
         sumf[i] = fmaf(xd * yd, (float)sumi[i], sumf[i]);  // sum += d_all*y.d*(isum - 32*isum_mins)
+    }
+}
+
+// Q6_K superblock of one 32x32 tile: 8 chunks of 32 elements; a lane's 16 values of a
+// chunk are one 16-element scale group g (int8 scale sc). The scaled weight
+// W = sc * (q - 32) (|W| <= 4096) rides in the MFMA operands as two int8 bytes,
+// W = 256 * hi + lo with lo in [-128, 127] and hi = (W + 128) >> 8 in [-16, 16]: one
+// packed 16-bit multiply-add per two values gives T = W + 128 = q*sc + (128 - 32 sc),
+// whose high byte is hi and whose low byte xor 0x80 is lo. Both sums accumulate over
+// the whole superblock in the matrix core, sumi = 256 * S_hi + S_lo exactly -- the
+// reference's isum - 32*isum_mins with its scales (README.md:369-394 / lane_q6K) --
+// instead of two half-empty MFMAs and 32 VALU multiplies per chunk.
+__device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *buf, const uint8_t *At, int n, int b,
+                                              int r, int h, int wm, int wn, f32x16 &sumf) {
+    const int nrow = n < a.n_rows ? n : a.n_rows - 1;  // the DMA clamped the same way
+    const uint32_t mis = (uint32_t)((uintptr_t)(a.w + (int64_t)nrow * a.row_stride + (int64_t)b * 210) & 15u);
+    const uint8_t *region = buf + MMQ_A_BYTES + (32 * wn + r) * 224 + mis;
+    const uint32_t s4 = (uint32_t)((uintptr_t)region & 3u);
+    const uint8_t *bb = region - s4;
+    const u32x4 SC = realign(*(const u32x4a *)(bb + 192), *(const uint32_t *)(bb + 208), s4);
+    const uint32_t dh = (*(const uint32_t *)(bb + 208) >> (8u * s4)) & 0xffffu;
+    i32x16 shi = {}, slo = {};
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh) {
+        const u32x4 L0 = realign(*(const u32x4a *)(bb + 64 * nh + 16 * h), *(const uint32_t *)(bb + 64 * nh + 16 * h + 16), s4);
+        const u32x4 L1 = realign(*(const u32x4a *)(bb + 64 * nh + 32 + 16 * h),
+                                 *(const uint32_t *)(bb + 64 * nh + 48 + 16 * h), s4);
+        const u32x4 H = realign(*(const u32x4a *)(bb + 128 + 32 * nh + 16 * h),
+                                *(const uint32_t *)(bb + 144 + 32 * nh + 16 * h), s4);
+#pragma unroll KQ_MMQ_Q6_UNROLL
+        for (int cc = 0; cc < 4; ++cc) {
+            const int c = 4 * nh + cc;  // chunk: elements 32c .. 32c+31
+            const u32x4 L = (cc & 1) ? L1 : L0;
+            const uint32_t sh = (uint32_t)(cc >> 1) * 4u;
+            const int sc = h ? sbyte(SC, 2 * c + 1) : sbyte(SC, 2 * c);
+            const uint32_t scw = (uint32_t)sc & 0xffffu, cw = (uint32_t)(128 - 32 * sc) & 0xffffu;
+            const u16x2 scp = {(uint16_t)scw, (uint16_t)scw}, cp = {(uint16_t)cw, (uint16_t)cw};
+            u32x4 blo, bhi;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const uint32_t x = ((L[k] >> sh) & 0x0f0f0f0fu) | (((H[k] >> (2u * cc)) & 0x03030303u) << 4);  // q, 0..63
+                const uint32_t t0 = as_u32(as_u16x2(__builtin_amdgcn_perm(0u, x, 0x0c010c00u)) * scp + cp);  // values 0, 1
+                const uint32_t t1 = as_u32(as_u16x2(__builtin_amdgcn_perm(0u, x, 0x0c030c02u)) * scp + cp);  // values 2, 3
+                blo[k] = __builtin_amdgcn_perm(t1, t0, 0x06040200u) ^ 0x80808080u;
+                bhi[k] = __builtin_amdgcn_perm(t1, t0, 0x07050301u);
+            }
+            const u32x4 act = *(const u32x4 *)(At + 16 + 32 * c + 16 * h);
+            shi = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&bhi, shi, 0, 0, 0);
+            slo = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&blo, slo, 0, 0, 0);
+        }
+    }
+    const float xd = h2f(dh);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
+        const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
+        sumf[i] = fmaf(xd * yd, (float)(256 * shi[i] + slo[i]), sumf[i]);  // sum += d_all*y.d*(isum - 32*isum_mins)
     }
 }
 
@@ -242,7 +302,10 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) 
         const uint8_t *buf = smem + (b & 1) * BUF;
         const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;          // this lane's activation column
         if (TYPE == Q6_K) {
-            q6_superblock(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
+            if (KQ_MMQ_Q6_VALU)
+                q6_superblock_valu(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
+            else
+                q6_superblock(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
             asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             continue;
         }

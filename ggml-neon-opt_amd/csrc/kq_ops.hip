@@ -580,10 +580,11 @@ constexpr int PROMPT_GMAX = 8;  // query heads per kv group handled by kq_attn_p
 #define KQ_PROMPT_DIAG 0  // timing-only builds: 1 no KQ dots, 2 no soft_max sums, 4 no KQV
 #endif
 
-// LDS: q16 [gsz][HD] | w [gsz][n_ctx] f32 | p16 [gsz][n_ctx] | scal [gsz][4] f32 |
-//      gsum [gsz][n_ctx/4] f64 (the KQV accumulators are reduced across lanes, not in LDS)
+// LDS: q16 [gsz][HD] | w [gsz][n_ctx] f32 | p16 [gsz][n_ctx] | scal [gsz][4] f32, with
+//      gsum [gsz][n_ctx/4] f64 over p16 (same bytes; read before p16 is written); the KQV
+//      accumulators are reduced across lanes, not in LDS
 size_t attn_prompt_group_lds(int hd, int n_ctx, int gsz) {
-    return (size_t)gsz * ((size_t)2 * hd + (size_t)n_ctx * 6 + 16 + (size_t)(n_ctx / 4) * 8);
+    return (size_t)gsz * ((size_t)2 * hd + (size_t)n_ctx * 6 + 16);
 }
 
 template <int HD>
@@ -606,7 +607,7 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
     float *w = (float *)(q16 + gsz * HD);                   // [gsz][nc]
     uint16_t *p16 = (uint16_t *)(w + gsz * nc);             // [gsz][nc]
     float *scal = (float *)(p16 + gsz * nc);                // [gsz][4]
-    double *gsum = (double *)(scal + 4 * gsz);              // [gsz][nc/4]
+    double *gsum = (double *)p16;                           // [gsz][nc/4], before p16
 
     for (int u = t; u < gsz * (HD / 2); u += 256) {  // rope(q) of the group's heads -> f16
         const int hh = u / (HD / 2), pr = u - hh * (HD / 2);

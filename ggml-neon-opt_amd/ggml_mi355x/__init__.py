@@ -315,7 +315,7 @@ def mul_mat(type_, w, K, x, out=None, workspace=None, stream=None):
     if M == 1 and x.data_ptr() % 16:
         ws = max(ws, K // QK_K * 304)  # Q8L activation blocks (kq_rows)
     if ws and (workspace is None or workspace.numel() < ws):
-        workspace = _workspace(ws, x.device)
+        workspace = _workspace(ws, x.device, stream)
     _check(lib().mi355x_mul_mat(type_, w.data_ptr(), K, N, w.stride(0), x.data_ptr(), M, x.stride(0) * 4,
                                 out.data_ptr(), out.stride(0) * 4,
                                 workspace.data_ptr() if ws else None, ws, _stream(stream)), "mi355x_mul_mat")
@@ -339,9 +339,11 @@ def mul_mat_q8(type_, w, K, q8, out=None, stream=None):
 _ws_cache = {}
 
 
-def _workspace(nbytes, device):
+def _workspace(nbytes, device, stream=None):
+    """Scratch for the quantized activation, one per (device, stream): launches on one
+    stream are ordered, those on different streams (other threads) may overlap."""
     torch = _torch()
-    key = str(device)
+    key = (str(device), _stream(stream).value or 0)
     buf = _ws_cache.get(key)
     if buf is None or buf.numel() < nbytes:
         buf = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
@@ -360,7 +362,7 @@ def gemv_fused(mats, x, stream=None, workspace=None):
     K = x.shape[-1]
     need = int(lib().mi355x_gemv_fused_workspace_size(K))
     if need and (workspace is None or workspace.numel() < need):
-        workspace = _workspace(need, x.device)
+        workspace = _workspace(need, x.device, stream)
     _check(lib().mi355x_gemv_fused(descs, n, x.data_ptr(), K, workspace.data_ptr() if need else None, need,
                                    _stream(stream)), "mi355x_gemv_fused")
 
@@ -406,7 +408,7 @@ def gemv_fused_ext(mats, x, prologue=PRO_NONE, x2=None, eps=0.0, residual=None, 
     ext.epi_y = epi_y.data_ptr() if epi_y is not None else None
     K = x.shape[-1]
     need = int(lib().mi355x_gemv_ext_workspace_size(K))
-    ws = _workspace(need, x.device)
+    ws = _workspace(need, x.device, stream)
     _check(lib().mi355x_gemv_fused_ext(descs, n, x.data_ptr(), K, ctypes.byref(ext), ws.data_ptr(), need,
                                        _stream(stream)), "mi355x_gemv_fused_ext")
 
