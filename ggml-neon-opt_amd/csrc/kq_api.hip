@@ -25,6 +25,7 @@ __global__ void kq_rows(const RowsArgs a);
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TYPE>
 __global__ void kq_mmq(const MmqArgs a);
+__global__ void kq_mmq_mixed(const MmqArgs a);
 template <int NWV, int CT>
 __global__ void kq_mmq_k4(const MmqArgs a);
 #ifndef KQ_K4_NWV
@@ -641,10 +642,17 @@ bool mmq_tile64(int type, int64_t N, int64_t M) {
 
 // Up to 4 matrices of one type on one Q8L activation in ONE 64 x 64-tile launch (a prompt
 // batch's q/k/v: the small k/v GEMMs no longer run as half-empty launches of their own).
-int launch_mmq_multi(int type, int n_mat, const void *const *w, const int64_t *N, const size_t *row_stride,
+// Mixed Q4_K / Q6_K matrices run on kq_mmq_mixed (each row tile its matrix's body).
+int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const int64_t *N, const size_t *row_stride,
                      float *const *y, const int64_t *y_col_stride, int64_t K, const uint8_t *xq, int64_t M,
                      hipStream_t stream) {
     if (n_mat < 1 || n_mat > 4) return MI355X_E_INVAL;
+    const int type = types[0];
+    bool mixed = false;
+    for (int d = 1; d < n_mat; ++d) mixed |= types[d] != type;
+    if (mixed)
+        for (int d = 0; d < n_mat; ++d)
+            if (types[d] != Q4_K && types[d] != Q6_K) return MI355X_E_INVAL;
     MmqArgs a;
     memset(&a, 0, sizeof(a));
     a.n_mat = n_mat;
@@ -661,8 +669,9 @@ int launch_mmq_multi(int type, int n_mat, const void *const *w, const int64_t *N
         a.mn_rows[d] = (int)N[d];
         a.my[d] = y[d];
         a.my_col_stride[d] = y_col_stride[d];
+        a.mtype[d] = types[d];
         tiles += (int)((N[d] + 63) / 64);
-        wbytes += (double)N[d] * a.nb * block_bytes(type);
+        wbytes += (double)N[d] * a.nb * block_bytes(types[d]);
         ybytes += (double)M * N[d] * 4.0;
     }
     a.tile0[n_mat] = tiles;
@@ -671,10 +680,12 @@ int launch_mmq_multi(int type, int n_mat, const void *const *w, const int64_t *N
     a.n_rows = a.mn_rows[0];
     a.y = a.my[0];
     a.y_col_stride = a.my_col_stride[0];
-    const void *fn = type == Q5_K ? (const void *)kq_mmq<Q5_K>
+    const void *fn = mixed          ? (const void *)kq_mmq_mixed
+                   : type == Q5_K ? (const void *)kq_mmq<Q5_K>
                    : type == Q6_K ? (const void *)kq_mmq<Q6_K>
                                   : (const void *)kq_mmq<Q4_K>;
-    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16;
+    const int ltype = mixed ? Q6_K : type;  // the larger LDS tile
+    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (ltype == Q6_K ? 224 : block_bytes(ltype))) + 16;
     const dim3 grid((unsigned)((M + 63) / 64), (unsigned)tiles, 1);
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
@@ -682,7 +693,7 @@ int launch_mmq_multi(int type, int n_mat, const void *const *w, const int64_t *N
     hipError_t e;
     if (timing_slot(stream, e0, e1)) {
         e = hipExtLaunchKernel(fn, grid, dim3(256), args, lds, stream, e0, e1, 0);
-        timing_log(std::string("kq::kq_mmq<") + std::to_string(type) + ">", wbytes + (double)M * a.nb * Q8L_STRIDE + ybytes,
+        timing_log(mixed ? std::string("kq::kq_mmq_mixed") : std::string("kq::kq_mmq<") + std::to_string(type) + ">", wbytes + (double)M * a.nb * Q8L_STRIDE + ybytes,
                    e0, e1);
     } else {
         e = hipLaunchKernel(fn, grid, dim3(256), args, lds, stream);

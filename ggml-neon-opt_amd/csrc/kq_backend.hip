@@ -261,6 +261,12 @@ bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
     return b->workspace_size >= mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], x->ne[1]);
 }
 
+// MUL_MATs that can share one tile-GEMM launch: one type, or Q4_K beside Q6_K (kq_mmq_mixed:
+// a prompt batch's q/k with the Q6_K attn_v of use_more_bits layers)
+bool multi_types_ok(int a, int b) {
+    return a == b || ((a == MI355X_TYPE_Q4_K || a == MI355X_TYPE_Q6_K) && (b == MI355X_TYPE_Q4_K || b == MI355X_TYPE_Q6_K));
+}
+
 std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const *nodes, int n, bool fuse) {
     std::vector<Launch> out;
     const std::vector<int> readers = fuse ? count_readers(nodes, n) : std::vector<int>(n, 0);
@@ -394,7 +400,8 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 int run = 1;
                 while (i + run < n && run < 4) {
                     const mi355x_tensor *u = nodes[i + run];
-                    if (u->op != MI355X_OP_MUL_MAT || u->src[1] != t->src[1] || u->src[0]->type != t->src[0]->type ||
+                    if (u->op != MI355X_OP_MUL_MAT || u->src[1] != t->src[1] ||
+                        !multi_types_ok(t->src[0]->type, u->src[0]->type) ||
                         u->src[0]->ne[0] != t->src[0]->ne[0] || !batched_mm_shares(b, u) ||
                         !kq::mmq_tile64(u->src[0]->type, u->src[0]->ne[1], u->src[1]->ne[1]))
                         break;
@@ -575,18 +582,20 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
                 q8.nb = x->nb[1];
             }
             const void *w[4];
+            int types[4];
             int64_t N[4], ycs[4];
             size_t rs[4];
             float *y[4];
             for (int k = 0; k < l.count; ++k) {
                 const mi355x_tensor *u = nodes[l.first + k];
                 w[k] = u->src[0]->data;
+                types[k] = u->src[0]->type;
                 N[k] = u->src[0]->ne[1];
                 rs[k] = u->src[0]->nb[1];
                 y[k] = (float *)u->data;
                 ycs[k] = (int64_t)(u->nb[1] / 4);
             }
-            rc = kq::launch_mmq_multi(t->src[0]->type, l.count, w, N, rs, y, ycs, K, (const uint8_t *)b->workspace, M,
+            rc = kq::launch_mmq_multi(types, l.count, w, N, rs, y, ycs, K, (const uint8_t *)b->workspace, M,
                                       b->stream);
             if (rc) return rc;
             const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;

@@ -213,6 +213,7 @@ struct MmqArgs {
     // the fields above only
     int n_mat;
     int tile0[5];
+    int mtype[4];  // kq_mmq_mixed: each matrix's type (Q4_K / Q6_K)
     const uint8_t *mw[4];
     int64_t mrow_stride[4];
     int mn_rows[4];

@@ -216,23 +216,14 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
     }
 }
 
-template <int TYPE>
-__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) {
-    MmqArgs a = a0;  // (the matrix of this row tile, below)
-    constexpr int BSZ = block_bytes(TYPE);
-    constexpr int NB_I = mmq_b_instr(TYPE);
-    constexpr int NW = mmq_nw(TYPE);
-    constexpr int BUF = mmq_buf(TYPE);
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 1, wn = wave >> 1;
-    const int r = lane & 31, h = lane >> 5;
-    // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (speed only,
-    // MI355X_MICROARCH.md), so the column tiles of one row tile go to blocks L, L + 8,
-    // L + 16, ... (one XCD): the weight tile is fetched into that XCD's L2 once and
-    // served from it to the others; the activation tiles fit every XCD's L2.
-    int tx = blockIdx.x, ty = blockIdx.y;
+// XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (speed only,
+// MI355X_MICROARCH.md), so the column tiles of one row tile go to blocks L, L + 8,
+// L + 16, ... (one XCD): the weight tile is fetched into that XCD's L2 once and
+// served from it to the others; the activation tiles fit every XCD's L2. With several
+// matrices on one activation, a gets this row tile's matrix d (returned).
+__device__ __forceinline__ int mmq_tile_of(const MmqArgs &a0, MmqArgs &a, int &tx, int &ty) {
+    tx = blockIdx.x;
+    ty = blockIdx.y;
     if (!(KQ_MMQ_DIAG & 16)) {
         const int gx = gridDim.x, L = blockIdx.y * gx + blockIdx.x;
         const int span = 8 * gx;                  // blocks per group of 8 row tiles
@@ -243,8 +234,8 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) 
             tx = in / 8;
         }
     }
+    int d = 0;
     if (a0.n_mat > 1) {  // several matrices on one activation: this row tile's matrix
-        int d = 0;
 #pragma unroll
         for (int k = 1; k < 4; ++k)
             if (k < a0.n_mat && ty >= a0.tile0[k]) d = k;
@@ -255,6 +246,21 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) 
         a.y_col_stride = a0.my_col_stride[d];
         ty -= a0.tile0[d];
     }
+    return d;
+}
+
+// One 64 x 64 output tile (4 waves of 32 x 32) over the whole K.
+template <int TYPE>
+__device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
+    constexpr int BSZ = block_bytes(TYPE);
+    constexpr int NB_I = mmq_b_instr(TYPE);
+    constexpr int NW = mmq_nw(TYPE);
+    constexpr int BUF = mmq_buf(TYPE);
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int wm = wave & 1, wn = wave >> 1;
+    const int r = lane & 31, h = lane >> 5;
     const int col0 = tx * MMQ_TILE, row0 = ty * MMQ_TILE;
     const int nb = a.nb;
 
@@ -428,6 +434,26 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) 
                 a.y[(int64_t)m * a.y_col_stride + n] = a.res ? sumf[i] + a.res[(int64_t)m * a.res_col_stride + n] : sumf[i];
         }
     }
+}
+
+template <int TYPE>
+__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) {
+    MmqArgs a = a0;
+    int tx, ty;
+    mmq_tile_of(a0, a, tx, ty);
+    mmq_tile<TYPE>(a, tx, ty);
+}
+
+// Q4_K and Q6_K matrices on one activation in one launch (a prompt batch's q/k with a
+// Q6_K attn_v): each row tile runs its matrix's kernel body (a0.mtype), LDS sized for Q6_K.
+__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq_mixed(const MmqArgs a0) {
+    MmqArgs a = a0;
+    int tx, ty;
+    const int d = mmq_tile_of(a0, a, tx, ty);
+    if (a0.mtype[d] == Q6_K)
+        mmq_tile<Q6_K>(a, tx, ty);
+    else
+        mmq_tile<Q4_K>(a, tx, ty);
 }
 
 // ------------------------------------------------------------ Q4_K, streamed operands
