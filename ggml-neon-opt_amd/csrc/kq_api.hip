@@ -595,7 +595,7 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
                                   : (const void *)kq_mmq<Q4_K>;
     // two superblock buffers: 64 Q8L columns + 64 weight rows (Q6_K: 224-B granule span), +16 B
     // for the Q6_K realign reads past the last row
-    size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16;
+    size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16 + MMQ_PF_LDS;
     dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64), 1);
     dim3 block(256);
     std::string name = std::string("kq::kq_mmq<") + std::to_string(type) + ">";
@@ -685,7 +685,7 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
                    : type == Q6_K ? (const void *)kq_mmq<Q6_K>
                                   : (const void *)kq_mmq<Q4_K>;
     const int ltype = mixed ? Q6_K : type;  // the larger LDS tile
-    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (ltype == Q6_K ? 224 : block_bytes(ltype))) + 16;
+    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (ltype == Q6_K ? 224 : block_bytes(ltype))) + 16 + MMQ_PF_LDS;
     const dim3 grid((unsigned)((M + 63) / 64), (unsigned)tiles, 1);
     allow_lds(fn, lds);
     hipEvent_t e0, e1;

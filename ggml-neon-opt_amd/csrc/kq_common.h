@@ -135,6 +135,10 @@ constexpr int ROWS_PRO_NONE = 0, ROWS_PRO_NORM = 1, ROWS_PRO_SWIGLU = 2;
 // LDS-DMA instructions. Ring depth per type keeps 6.8-8.5 KB in flight per wave,
 // ~80-100 KB per CU (measured ceiling: 2-3 KB steps, ~96 KB per CU, nt -> 7.1 TB/s).
 constexpr int ROWS_SB = 16;     // superblocks per step (4 lanes each)
+#ifndef KQ_MMQ_PF
+#define KQ_MMQ_PF 0  // kq_mmq tiles: L2 warm-up distance of the weight tile in superblocks (0 off; 2, 3 measured neutral to -5 %)
+#endif
+constexpr int MMQ_PF_LDS = KQ_MMQ_PF ? 1024 : 0;  // its scratch: 256 B per wave
 constexpr int Q8L_STRIDE = 304; // LDS/workspace Q8_K block: d @0, qs @16, bsums @272 (16-B aligned)
 constexpr int ROWS_RECS = 64;   // chain records per wave per batch (soft cap)
 __host__ __device__ constexpr int rows_gran(int type) { return block_bytes(type) + 1; }

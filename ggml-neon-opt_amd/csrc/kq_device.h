@@ -270,6 +270,12 @@ __device__ __forceinline__ void dma16(const void *src, LDS void *dst) {
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off" ::"s"(m0), "v"(src)
                  : "memory", "m0");
 }
+// One dword per lane (the 4-B form: 256 B per wave instruction).
+__device__ __forceinline__ void dma4(const void *src, LDS void *dst) {
+    const uint32_t m0 = (uint32_t)(uintptr_t)dst;
+    asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dword %1, off" ::"s"(m0), "v"(src)
+                 : "memory", "m0");
+}
 // Same, non-temporal (nt): for the once-read weight stream (measured on this part:
 // 6.2 -> 7.1 TB/s chip-wide, profiles/r01_lds_dma_stream_ceiling.txt).
 __device__ __forceinline__ void dma16_nt(const void *src, LDS void *dst) {

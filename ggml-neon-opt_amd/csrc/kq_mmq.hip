@@ -64,6 +64,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #else
 #define KQ_MMQ_WPE_ATTR
 #endif
+#ifndef KQ_MMQ_PIPE
+#define KQ_MMQ_PIPE 0  // experiment build: Q4_K tile loop software-pipelined (measured neutral, +88 VGPRs)
+#endif
 #ifndef KQ_MMQ_Q6_VALU
 #define KQ_MMQ_Q6_VALU 0  // experiment build: Q6_K group scales on VALU (round-2 kernel)
 #endif
@@ -289,18 +292,149 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 dma16(src, (LDS void *)(buf + MMQ_A_BYTES + 1024 * (t - MMQ_A_INSTR)));
             }
         }
+        if (KQ_MMQ_PF) {  // L2 warm-up of superblock b + KQ_MMQ_PF's weight tile: one dword per
+                          // 64-B piece of every row (LDS-DMA into a scratch area nobody reads)
+            int bp = b + KQ_MMQ_PF - 1;
+            bp = bp < nb ? bp : nb - 1;  // always one instruction: the vmcnt waits count it
+            const int t = threadIdx.x, part = t & 3;
+            int rw = row0 + (t >> 2);
+            rw = rw < a.n_rows ? rw : a.n_rows - 1;
+            const int off = part < 3 ? 64 * part : BSZ - 4;
+            dma4((const void *)((uintptr_t)(a.w + (int64_t)rw * a.row_stride + (int64_t)bp * BSZ + off) & ~(uintptr_t)3),
+                 (LDS void *)(smem + 2 * BUF + 16 + 256 * wave));
+        }
     };
+    constexpr int NWP = NW + (KQ_MMQ_PF ? 1 : 0);  // vm instructions per issue()
 
     f32x16 sumf;
 #pragma unroll
     for (int i = 0; i < 16; ++i) sumf[i] = 0.f;
 
     issue(0);
+    if constexpr (TYPE == Q4_K && KQ_MMQ_PIPE && !KQ_MMQ_DIAG && !KQ_MMQ_Q4_VALU) {
+        // Software-pipelined Q4_K loop: superblock b's MFMAs are issued before superblock
+        // b-1's fp32 chain runs, so the wave's VALU epilogue overlaps its own matrix-core
+        // work instead of waiting for it. Superblock b-1 carries its MFMA sums (two
+        // alternating accumulator sets) and its scalars (mins, column scales, d, dmin) in
+        // registers; each element's chain still runs superblock by superblock in order.
+        i32x16 s8a = {}, s1a = {}, s8b = {}, s1b = {};
+        f32x16 mins = {};
+        float yd[16];
+        float xd = 0.f, xdm = 0.f;
+        auto mfmas = [&](const uint8_t *buf, i32x16 &s8, i32x16 &s1) {
+            const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;
+            const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;
+            const u32x4 hdr = *(const u32x4 *)Bt;
+            const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
+            const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
+            const i32x16 zero = {};
+            s8 = zero;
+            s1 = zero;
+#pragma unroll
+            for (int jp = 0; jp < 4; ++jp) {
+                const u32x4 qv = *(const u32x4 *)(Bt + 16 + 32 * jp + 16 * h);
+                const u32x4 lo = qv & 0x0f0f0f0fu, hi = (qv >> 4) & 0x0f0f0f0fu;
+                const u32x4 alo = *(const u32x4 *)(At + 16 + 64 * jp + 16 * h);
+                const u32x4 ahi = *(const u32x4 *)(At + 48 + 64 * jp + 16 * h);
+                const uint32_t sw = jp < 2 ? s03 : s47;
+                const int sc_lo = (int)((sw >> (16u * (uint32_t)(jp & 1))) & 0xffu);
+                const int sc_hi = (int)((sw >> (16u * (uint32_t)(jp & 1) + 8u)) & 0xffu);
+                const u16x2 lh = {(uint16_t)(sc_lo >> 3), (uint16_t)(sc_lo >> 3)};
+                const u16x2 ll = {(uint16_t)(sc_lo & 7), (uint16_t)(sc_lo & 7)};
+                const u16x2 hh = {(uint16_t)(sc_hi >> 3), (uint16_t)(sc_hi >> 3)};
+                const u16x2 hl = {(uint16_t)(sc_hi & 7), (uint16_t)(sc_hi & 7)};
+                u32x4 b8lo, b1lo, b8hi, b1hi;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    b8lo[k] = as_u32(as_u16x2(lo[k]) * lh);
+                    b1lo[k] = as_u32(as_u16x2(lo[k]) * ll);
+                    b8hi[k] = as_u32(as_u16x2(hi[k]) * hh);
+                    b1hi[k] = as_u32(as_u16x2(hi[k]) * hl);
+                }
+                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b8lo, s8, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b1lo, s1, 0, 0, 0);
+                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b8hi, s8, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b1hi, s1, 0, 0, 0);
+            }
+        };
+        auto scalars = [&](const uint8_t *buf) {  // as the unpipelined loop below
+            const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;
+            const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;
+            const u32x4 hdr = *(const u32x4 *)Bt;
+            const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
+            const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
+            const u32x4 b0 = *(const u32x4 *)(At + 272), b1 = *(const u32x4 *)(At + 288);
+            const uint32_t bw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
+            f16x8 am, bm;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int bs = (int)(int16_t)(bw[j] & 0xffffu) + (int)(int16_t)(bw[j] >> 16);
+                am[j] = (_Float16)(h ? (bs >> 6) : (bs & 63));
+                const uint32_t mw = j < 4 ? m03 : m47;
+                const int mn = (int)((mw >> (8u * (uint32_t)(j & 3))) & 0xffu);
+                bm[j] = (_Float16)(h ? 64 * mn : mn);
+            }
+            const f32x16 zero = {};
+            mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
+            xd = h2f(hdr.x & 0xffffu);
+            xdm = h2f(hdr.x >> 16);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) yd[i] = *(const float *)(buf + (32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h) * Q8L_STRIDE);
+        };
+        auto epilogue = [&](const i32x16 &s8, const i32x16 &s1) {  // the reference's fp32 update
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                sumf[i] = fmaf(-mins[i], yd[i] * xdm, sumf[i]);
+                sumf[i] = fmaf((float)(8 * s8[i] + s1[i]), yd[i] * xd, sumf[i]);
+            }
+        };
+        auto land = [&](int b) {  // superblock b in LDS (and b+1 requested), every wave's part
+            if (b + 1 < nb) {
+                issue(b + 1);
+                vm_wait<NWP>();
+            } else {
+                vm_wait<0>();
+            }
+            asm volatile("s_barrier" ::: "memory");
+        };
+        auto release = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
+        land(0);
+        mfmas(smem, s8a, s1a);
+        scalars(smem);
+        release();
+        int b = 1;
+#pragma unroll 1
+        for (; b + 1 < nb; b += 2) {  // b into set B, b + 1 into set A
+            land(b);
+            const uint8_t *bufb = smem + (b & 1) * BUF;
+            mfmas(bufb, s8b, s1b);
+            epilogue(s8a, s1a);
+            scalars(bufb);
+            release();
+            land(b + 1);
+            const uint8_t *bufc = smem + ((b + 1) & 1) * BUF;
+            mfmas(bufc, s8a, s1a);
+            epilogue(s8b, s1b);
+            scalars(bufc);
+            release();
+        }
+        if (b < nb) {
+            land(b);
+            const uint8_t *bufb = smem + (b & 1) * BUF;
+            mfmas(bufb, s8b, s1b);
+            epilogue(s8a, s1a);
+            scalars(bufb);
+            release();
+            epilogue(s8b, s1b);
+        } else {
+            epilogue(s8a, s1a);
+        }
+    } else {
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
         if (b + 1 < nb) {
             issue(b + 1);
-            vm_wait<NW>();  // superblock b's DMAs (older than b+1's NW) have landed
+            vm_wait<NWP>();  // superblock b's DMAs (older than b+1's NW) have landed
         } else {
             vm_wait<0>();
         }
@@ -422,6 +556,8 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             }
         }
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer b&1 free for b+2
+    }
+
     }
 
     // ---- store: lane's weight row n, 16 activation columns
