@@ -22,6 +22,7 @@ __global__ void kq_gemv(const GemvArgs a);
 __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void kq_rows(const RowsArgs a);
+template <bool AM>
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TYPE>
 __global__ void kq_mmq(const MmqArgs a);
@@ -537,18 +538,19 @@ int launch_rows(const RowsPlan &pl, hipStream_t stream) {
 }
 
 int launch_quantize_q8L(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
-                        hipStream_t stream) {
+                        hipStream_t stream, bool mmq) {
+    const auto kern = mmq ? kq_quantize_q8L<true> : kq_quantize_q8L<false>;
     const int64_t nb = k / QK;
     const int64_t nblocks = nb * nrows;
     if (nblocks == 0) return MI355X_OK;
     const int64_t wgs = (nblocks + 15) / 16;
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
-        hipExtLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, e0, e1, 0, x,
+        hipExtLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, e0, e1, 0, x,
                               x_stride_floats, (uint8_t *)y, (int)nb, nblocks);
         timing_log("kq::kq_quantize_q8L", (double)nblocks * (QK * 4.0 + Q8L_STRIDE), e0, e1);
     } else {
-        hipLaunchKernelGGL(kq_quantize_q8L, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, x, x_stride_floats,
+        hipLaunchKernelGGL(kern, dim3((unsigned)wgs), dim3(WG_THREADS), 0, stream, x, x_stride_floats,
                            (uint8_t *)y, (int)nb, nblocks);
     }
     const hipError_t e = hipGetLastError();
@@ -1012,7 +1014,7 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
     if (mmq_applies(src0_type, src0, ne01, nb01, ne11) && ((uintptr_t)workspace & 15u) == 0) {
         if (!device_ok()) return MI355X_E_NODEVICE;
-        int rc = launch_quantize_q8L(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream);
+        int rc = launch_quantize_q8L(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream, true);
         if (rc) return rc;
         return launch_mmq(src0_type, src0, ne00, ne01, nb01, (const uint8_t *)workspace, ne11, dst,
                           (int64_t)(nb1 / 4), (hipStream_t)stream);

@@ -218,7 +218,7 @@ int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8, f
     const bool same = q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1];
     if (!same) {
         const int rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
-                                               b->stream);
+                                               b->stream, true);
         if (rc) {
             q8 = Q8State();
             return rc;
@@ -574,7 +574,7 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
             const int64_t K = t->src[0]->ne[0], M = x->ne[1];
             if (!(q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1])) {
                 rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
-                                             b->stream);
+                                             b->stream, true);
                 if (rc) return rc;
                 q8.src = x->data;
                 q8.k = K;

@@ -56,7 +56,7 @@ bool attn_prompt_q8_ok(const AttnArgs &a);  // the group kernel can write a.q8_o
 // prefill (ne11 >= 16) pieces, for the backend's shared-activation runs
 bool mmq_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M);
 int launch_quantize_q8L(const float *x, int64_t x_stride_floats, void *y, int64_t k, int64_t nrows,
-                        hipStream_t stream);
+                        hipStream_t stream, bool mmq = false);  // mmq: the prefill GEMMs' Q8L/mmq layout
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
                float *y, int64_t y_col_stride, hipStream_t stream, const float *res = nullptr,
                int64_t res_col_stride = 0);  // res: ADD epilogue

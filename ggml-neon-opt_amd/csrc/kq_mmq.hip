@@ -363,13 +363,10 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             const u32x4 hdr = *(const u32x4 *)Bt;
             const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
             const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
-            const u32x4 b0 = *(const u32x4 *)(At + 272), b1 = *(const u32x4 *)(At + 288);
-            const uint32_t bw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-            f16x8 am, bm;
+            const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
+            f16x8 bm;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int bs = (int)(int16_t)(bw[j] & 0xffffu) + (int)(int16_t)(bw[j] >> 16);
-                am[j] = (_Float16)(h ? (bs >> 6) : (bs & 63));
                 const uint32_t mw = j < 4 ? m03 : m47;
                 const int mn = (int)((mw >> (8u * (uint32_t)(j & 3))) & 0xffu);
                 bm[j] = (_Float16)(h ? 64 * mn : mn);
@@ -520,18 +517,15 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         }
         // summins = sum_j mn_j * bs_j exactly on one f16 MFMA 32x32x16 (bs_j = bsums[2j] +
         // bsums[2j+1] = 64*hi + lo, lo in 0..63): A = [lo_0..7 | hi_0..7] of the lane's
-        // activation column, B = [mn_0..7 | 64*mn_0..7] of its weight row; every product and
-        // partial sum is an integer below 2^24. (Four dependent f32 MFMAs 32x32x2 cost 256
+        // activation column (stored so by the quantizer: the Q8L/mmq layout), B = [mn_0..7 |
+        // 64*mn_0..7] of its weight row; every product and partial sum is an integer below 2^24. (Four dependent f32 MFMAs 32x32x2 cost 256
         // cycles per superblock against 32 for this one.)
         f32x16 mins;
         {
-            const u32x4 b0 = *(const u32x4 *)(At + 272), b1 = *(const u32x4 *)(At + 288);
-            const uint32_t bw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-            f16x8 am, bm;
+            const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
+            f16x8 bm;
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                const int bs = (int)(int16_t)(bw[j] & 0xffffu) + (int)(int16_t)(bw[j] >> 16);
-                am[j] = (_Float16)(h ? (bs >> 6) : (bs & 63));
                 const uint32_t mw = j < 4 ? m03 : m47;
                 const int mn = (int)((mw >> (8u * (uint32_t)(j & 3))) & 0xffu);
                 bm[j] = (_Float16)(h ? 64 * mn : mn);
@@ -744,14 +738,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
             const uint8_t *At = slot + (32 * c + r) * Q8L_STRIDE;
-            const u32x4 b0 = *(const u32x4 *)(At + 272), b1 = *(const u32x4 *)(At + 288);  // bsums[0..15]
-            const uint32_t bw[8] = {b0.x, b0.y, b0.z, b0.w, b1.x, b1.y, b1.z, b1.w};
-            f16x8 am;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {  // bs_j = bsums[2j] + bsums[2j+1] = 64*hi + lo
-                const int bs = (int)(int16_t)(bw[j] & 0xffffu) + (int)(int16_t)(bw[j] >> 16);
-                am[j] = (_Float16)(h ? (bs >> 6) : (bs & 63));
-            }
+            const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
             const f32x16 zero = {};
             const f32x16 mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
             const uint8_t *Ab = slot + 32 * c * Q8L_STRIDE;

@@ -719,7 +719,7 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
                 v[k] = u32x4{__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
             }
             const int64_t nbr = (int64_t)a.n_head * HD / QK;  // superblocks per row
-            quant16_store(v, l, a.q8_out + ((int64_t)i * nbr + (int64_t)g * nsb + rid) * Q8L_STRIDE);
+            quant16_store<true>(v, l, a.q8_out + ((int64_t)i * nbr + (int64_t)g * nsb + rid) * Q8L_STRIDE);
         }
     }
 }

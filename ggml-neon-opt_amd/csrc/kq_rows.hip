@@ -30,6 +30,8 @@
 namespace kq {
 
 // Q8L quantization of whole rows (K > 8192 path): 16 superblocks per workgroup.
+// AM: the prefill GEMMs' layout (quant16_store<true>: the mins operand in place of bsums).
+template <bool AM>
 __global__ void __launch_bounds__(WG_THREADS) kq_quantize_q8L(const float *__restrict__ x, int64_t x_stride,
                                                               uint8_t *__restrict__ y, int nb, int64_t nblocks) {
     const int lane = threadIdx.x & 63;
@@ -41,8 +43,10 @@ __global__ void __launch_bounds__(WG_THREADS) kq_quantize_q8L(const float *__res
     u32x4 v[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) v[k] = *(const u32x4 *)(xb + 4 * k);
-    quant16_store(v, lane & 15, y + bi * Q8L_STRIDE);
+    quant16_store<AM>(v, lane & 15, y + bi * Q8L_STRIDE);
 }
+template __global__ void kq_quantize_q8L<false>(const float *, int64_t, uint8_t *, int, int64_t);
+template __global__ void kq_quantize_q8L<true>(const float *, int64_t, uint8_t *, int, int64_t);
 
 // ------------------------------------------------------------ prefill prologues
 // The prompt graph's RMS_NORM -> MUL(norm weight) -> MUL_MATs and SWIGLU -> MUL_MAT:
@@ -100,7 +104,7 @@ __global__ void __launch_bounds__(256) kq_rms_norm_q8L(const float *__restrict__
             v[k].z = __float_as_uint((t.z * scale) * m.z);
             v[k].w = __float_as_uint((t.w * scale) * m.w);
         }
-        quant16_store(v, l, yq + (row * nb + b) * Q8L_STRIDE);
+        quant16_store<true>(v, l, yq + (row * nb + b) * Q8L_STRIDE);  // (prefill only: Q8L/mmq)
     }
 }
 
@@ -120,7 +124,7 @@ __global__ void __launch_bounds__(256) kq_swiglu_q8L(const float *__restrict__ g
         v[k].w = __float_as_uint(v_silu(gv.w) * uv.w);
     }
     (void)nb;
-    quant16_store(v, l, yq + bi * Q8L_STRIDE);
+    quant16_store<true>(v, l, yq + bi * Q8L_STRIDE);  // (prefill only: Q8L/mmq)
 }
 
 int launch_rms_norm_q8L(const float *x, const float *w, void *yq, int64_t n, int64_t nrows, float eps, hipStream_t s) {

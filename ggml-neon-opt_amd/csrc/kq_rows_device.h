@@ -30,7 +30,11 @@ __device__ __forceinline__ uint32_t qbyte(float iscale, float x) {
 // amax ignores NaN, max = first x with |x| == amax, iscale = -127/max (correctly
 // rounded), qs = MIN(127, nearest_int(fmaf(iscale, x, 1.5*2^23))) as int8,
 // bsums over the stored int8, d = 1/iscale; all-zero block -> zeros.
-// Writes the Q8L block (d @0, qs @16, bsums @272) at `qb`.
+// Writes the Q8L block (d @0, qs @16, bsums @272) at `qb`. AM (the prefill GEMMs' blocks,
+// "Q8L/mmq"): bytes 272..303 hold the f16 operand of kq_mmq's mins MFMA instead of the
+// bsums: bs_j = bsums[2j] + bsums[2j+1] = 64*hi + lo (lo in 0..63) as [lo_0..7 | hi_0..7],
+// integers exact in f16.
+template <bool AM = false>
 __device__ __forceinline__ void quant16_store(const u32x4 v[4], int l, uint8_t *qb) {
     float x[16];
 #pragma unroll
@@ -81,7 +85,15 @@ __device__ __forceinline__ void quant16_store(const u32x4 v[4], int l, uint8_t *
         d = 0.f;
     }
     *(u32x4 *)(qb + 16 + 16 * l) = q;
-    *(int16_t *)(qb + 272 + 2 * l) = (int16_t)bsum;
+    if (AM) {
+        const int bs = bsum + __builtin_amdgcn_update_dpp(bsum, bsum, 0xB1, 0xF, 0xF, false);  // lanes 2j, 2j+1
+        if (!(l & 1)) {
+            *(_Float16 *)(qb + 272 + l) = (_Float16)(bs & 63);
+            *(_Float16 *)(qb + 288 + l) = (_Float16)(bs >> 6);
+        }
+    } else {
+        *(int16_t *)(qb + 272 + 2 * l) = (int16_t)bsum;
+    }
     if (l == 0) *(float *)qb = d;
 }
 
