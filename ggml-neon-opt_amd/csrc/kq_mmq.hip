@@ -162,6 +162,29 @@ __device__ __forceinline__ void q6_superblock_valu(const MmqArgs &a, const uint8
     }
 }
 
+// B operand of the mins MFMA: [mn_0..7 | 64*mn_0..7] of the lane's row (h selects the half),
+// from the 6-bit mins bytes m03 / m47. Each byte pair becomes a 16-bit pair with a magic f16
+// exponent (v_perm with a constant byte): 0x64 -> 1024 + mn (ulp 1), 0x54 -> 64 + mn/16
+// (ulp 1/16); subtracting the magic and scaling by 1 or 1024 gives mn or 64*mn exactly.
+__device__ __forceinline__ f16x8 mins_operand(uint32_t m03, uint32_t m47, int h) {
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const uint32_t magic = h ? 0x54545454u : 0x64646464u;
+    const _Float16 base = h ? (_Float16)64.0f : (_Float16)1024.0f, mul = h ? (_Float16)1024.0f : (_Float16)1.0f;
+    const h2 nb2 = {(_Float16)-base, (_Float16)-base}, m2 = {mul, mul};
+    const uint32_t w[4] = {__builtin_amdgcn_perm(magic, m03, 0x04010400u), __builtin_amdgcn_perm(magic, m03, 0x04030402u),
+                           __builtin_amdgcn_perm(magic, m47, 0x04010400u), __builtin_amdgcn_perm(magic, m47, 0x04030402u)};
+    f16x8 r;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+        h2 v;
+        __builtin_memcpy(&v, &w[k], 4);
+        v = (v + nb2) * m2;
+        r[2 * k] = v[0];
+        r[2 * k + 1] = v[1];
+    }
+    return r;
+}
+
 // Q6_K superblock of one 32x32 tile: 8 chunks of 32 elements; a lane's 16 values of a
 // chunk are one 16-element scale group g (int8 scale sc). The scaled weight
 // W = sc * (q - 32) (|W| <= 4096) rides in the MFMA operands as two int8 bytes,
@@ -364,13 +387,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
             const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
             const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
-            f16x8 bm;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t mw = j < 4 ? m03 : m47;
-                const int mn = (int)((mw >> (8u * (uint32_t)(j & 3))) & 0xffu);
-                bm[j] = (_Float16)(h ? 64 * mn : mn);
-            }
+            const f16x8 bm = mins_operand(m03, m47, h);
             const f32x16 zero = {};
             mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
             xd = h2f(hdr.x & 0xffffu);
@@ -523,13 +540,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         f32x16 mins;
         {
             const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
-            f16x8 bm;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) {
-                const uint32_t mw = j < 4 ? m03 : m47;
-                const int mn = (int)((mw >> (8u * (uint32_t)(j & 3))) & 0xffu);
-                bm[j] = (_Float16)(h ? 64 * mn : mn);
-            }
+            const f16x8 bm = mins_operand(m03, m47, h);
             const f32x16 zero = {};
             mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
         }
@@ -727,13 +738,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
             }
         }
         // summins: B = [mn_0..7 | 64*mn_0..7] of the lane's row (h selects the half)
-        f16x8 bm;
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-            const uint32_t mw = j < 4 ? m03 : m47;
-            const int mn = (int)((mw >> (8u * (uint32_t)(j & 3))) & 0xffu);
-            bm[j] = (_Float16)(h ? 64 * mn : mn);
-        }
+        const f16x8 bm = mins_operand(m03, m47, h);
         const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16);
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
