@@ -343,7 +343,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         i32x16 s8a = {}, s1a = {}, s8b = {}, s1b = {};
         f32x16 mins = {};
         float yd[16];
-        float xd = 0.f, xdm = 0.f;
+        float xd = 0.f, xdm = 0.f, nxdm = 0.f;
         auto mfmas = [&](const uint8_t *buf, i32x16 &s8, i32x16 &s1) {
             const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;
             const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;
@@ -392,13 +392,14 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
             xd = h2f(hdr.x & 0xffffu);
             xdm = h2f(hdr.x >> 16);
+            nxdm = -xdm;
 #pragma unroll
             for (int i = 0; i < 16; ++i) yd[i] = *(const float *)(buf + (32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h) * Q8L_STRIDE);
         };
         auto epilogue = [&](const i32x16 &s8, const i32x16 &s1) {  // the reference's fp32 update
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                sumf[i] = fmaf(-mins[i], yd[i] * xdm, sumf[i]);
+                sumf[i] = fmaf(mins[i], yd[i] * nxdm, sumf[i]);  // = fmaf(-mins, yd*xdm, .) exactly
                 sumf[i] = fmaf((float)(8 * s8[i] + s1[i]), yd[i] * xd, sumf[i]);
             }
         };
@@ -545,7 +546,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
         }
         // the reference's fp32 update per element, superblock order
-        const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16);
+        const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16), nxdm = -xdm;
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
             const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
@@ -556,7 +557,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 const float t = fmaf(yd * xd, (float)sumi[i], -((yd * xdm) * mins[i]));
                 sumf[i] = sumf[i] + t;
             } else {
-                sumf[i] = fmaf(-mins[i], yd * xdm, sumf[i]);
+                sumf[i] = fmaf(mins[i], yd * nxdm, sumf[i]);  // = fmaf(-mins, yd*xdm, .) exactly
                 sumf[i] = fmaf((float)sumi[i], yd * xd, sumf[i]);
             }
         }
@@ -739,7 +740,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
         }
         // summins: B = [mn_0..7 | 64*mn_0..7] of the lane's row (h selects the half)
         const f16x8 bm = mins_operand(m03, m47, h);
-        const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16);
+        const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16), nxdm = -xdm;
 #pragma unroll
         for (int c = 0; c < CT; ++c) {
             const uint8_t *At = slot + (32 * c + r) * Q8L_STRIDE;
@@ -752,7 +753,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
                 const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
                 const float yd = *(const float *)(Ab + m * Q8L_STRIDE);
                 const int sumi = 8 * s8[c][i] + s1[c][i];
-                sumf[c][i] = fmaf(-mins[i], yd * xdm, sumf[c][i]);
+                sumf[c][i] = fmaf(mins[i], yd * nxdm, sumf[c][i]);  // = fmaf(-mins, yd*xdm, .) exactly
                 sumf[c][i] = fmaf((float)sumi, yd * xd, sumf[c][i]);
             }
         }
