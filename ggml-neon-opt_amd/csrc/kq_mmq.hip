@@ -162,6 +162,19 @@ __device__ __forceinline__ void q6_superblock_valu(const MmqArgs &a, const uint8
     }
 }
 
+// Scale-split multipliers of sub-blocks 2jp (lo nibbles) and 2jp+1 (hi nibbles) as 16-bit
+// pairs: sc = 8*sh + sl; sh / sl bytes of all four sub-blocks of a word split with two
+// masks, then one byte-broadcast permute per multiplier.
+struct SplitScales {
+    uint32_t sh03, sl03, sh47, sl47;
+};
+__device__ __forceinline__ SplitScales split_scales(uint32_t s03, uint32_t s47) {
+    return {(s03 >> 3) & 0x07070707u, s03 & 0x07070707u, (s47 >> 3) & 0x07070707u, s47 & 0x07070707u};
+}
+__device__ __forceinline__ uint32_t bcast16(uint32_t w, int k) {  // byte k of w in both 16-bit lanes
+    return __builtin_amdgcn_perm(0u, w, 0x0c000c00u + 0x00010001u * (uint32_t)k);
+}
+
 // B operand of the mins MFMA: [mn_0..7 | 64*mn_0..7] of the lane's row (h selects the half),
 // from the 6-bit mins bytes m03 / m47. Each byte pair becomes a 16-bit pair with a magic f16
 // exponent (v_perm with a constant byte): 0x64 -> 1024 + mn (ulp 1), 0x54 -> 64 + mn/16
@@ -350,6 +363,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             const u32x4 hdr = *(const u32x4 *)Bt;
             const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
             const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
+            const SplitScales ss = split_scales(s03, s47);
             const i32x16 zero = {};
             s8 = zero;
             s1 = zero;
@@ -359,13 +373,11 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 const u32x4 lo = qv & 0x0f0f0f0fu, hi = (qv >> 4) & 0x0f0f0f0fu;
                 const u32x4 alo = *(const u32x4 *)(At + 16 + 64 * jp + 16 * h);
                 const u32x4 ahi = *(const u32x4 *)(At + 48 + 64 * jp + 16 * h);
-                const uint32_t sw = jp < 2 ? s03 : s47;
-                const int sc_lo = (int)((sw >> (16u * (uint32_t)(jp & 1))) & 0xffu);
-                const int sc_hi = (int)((sw >> (16u * (uint32_t)(jp & 1) + 8u)) & 0xffu);
-                const u16x2 lh = {(uint16_t)(sc_lo >> 3), (uint16_t)(sc_lo >> 3)};
-                const u16x2 ll = {(uint16_t)(sc_lo & 7), (uint16_t)(sc_lo & 7)};
-                const u16x2 hh = {(uint16_t)(sc_hi >> 3), (uint16_t)(sc_hi >> 3)};
-                const u16x2 hl = {(uint16_t)(sc_hi & 7), (uint16_t)(sc_hi & 7)};
+                const int kb = 2 * (jp & 1);  // bytes of sub-blocks 2jp, 2jp+1 in their word
+                const u16x2 lh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb));
+                const u16x2 ll = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb));
+                const u16x2 hh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb + 1));
+                const u16x2 hl = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb + 1));
                 u32x4 b8lo, b1lo, b8hi, b1hi;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -470,6 +482,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
         const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
         const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
+        const SplitScales ss = split_scales(s03, s47);
         const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
         i32x16 sumi, s8 = {}, s1 = {};  // Q4_K: sumi = 8*s8 + s1 (scale split into 3-bit halves)
 #pragma unroll
@@ -502,10 +515,11 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 // packed 16-bit multiply scales two bytes per half without carries, so the
                 // per-sub-block scale rides in the MFMA operand and both sums accumulate
                 // across sub-blocks in the matrix core (exact int32).
-                const u16x2 lh = {(uint16_t)(sc_lo >> 3), (uint16_t)(sc_lo >> 3)};
-                const u16x2 ll = {(uint16_t)(sc_lo & 7), (uint16_t)(sc_lo & 7)};
-                const u16x2 hh = {(uint16_t)(sc_hi >> 3), (uint16_t)(sc_hi >> 3)};
-                const u16x2 hl = {(uint16_t)(sc_hi & 7), (uint16_t)(sc_hi & 7)};
+                const int kb = 2 * (jp & 1);  // bytes of sub-blocks 2jp, 2jp+1 in their word
+                const u16x2 lh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb));
+                const u16x2 ll = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb));
+                const u16x2 hh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb + 1));
+                const u16x2 hl = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb + 1));
                 u32x4 b8lo, b1lo, b8hi, b1hi;
 #pragma unroll
                 for (int k = 0; k < 4; ++k) {
@@ -702,6 +716,7 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
         const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
         const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
         const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
+        const SplitScales ss = split_scales(s03, s47);
         const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
         i32x16 s8[CT], s1[CT];
 #pragma unroll
@@ -712,13 +727,11 @@ __global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
         for (int jp = 0; jp < 4; ++jp) {
             const u32x4 qv = W[1 + jp];
             const u32x4 lo = qv & 0x0f0f0f0fu, hi = (qv >> 4) & 0x0f0f0f0fu;
-            const uint32_t sw = jp < 2 ? s03 : s47;
-            const int sc_lo = (int)((sw >> (16u * (uint32_t)(jp & 1))) & 0xffu);
-            const int sc_hi = (int)((sw >> (16u * (uint32_t)(jp & 1) + 8u)) & 0xffu);
-            const u16x2 lh = {(uint16_t)(sc_lo >> 3), (uint16_t)(sc_lo >> 3)};
-            const u16x2 ll = {(uint16_t)(sc_lo & 7), (uint16_t)(sc_lo & 7)};
-            const u16x2 hh = {(uint16_t)(sc_hi >> 3), (uint16_t)(sc_hi >> 3)};
-            const u16x2 hl = {(uint16_t)(sc_hi & 7), (uint16_t)(sc_hi & 7)};
+            const int kb = 2 * (jp & 1);  // bytes of sub-blocks 2jp, 2jp+1 in their word
+            const u16x2 lh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb));
+            const u16x2 ll = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb));
+            const u16x2 hh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb + 1));
+            const u16x2 hl = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb + 1));
             u32x4 b8lo, b1lo, b8hi, b1hi;
 #pragma unroll
             for (int k = 0; k < 4; ++k) {
