@@ -376,8 +376,18 @@ def prompt_impl(request):
     g.attn_prompt_impl(prev)
 
 
+@pytest.fixture(params=[0, 2], ids=["mmq_auto", "mmq_k4"])
+def prompt_mmq(request):
+    """The prompt's GEMMs on the default choice and with every Q4_K GEMM (single or
+    several matrices in one launch) on the streamed kernel kq_mmq_k4."""
+    import ggml_mi355x as g
+    prev = g.mmq_impl(request.param)
+    yield request.param
+    g.mmq_impl(prev)
+
+
 @pytest.mark.parametrize("hd", [64, 128])
-def test_llama_prompt_equals_tokens(dev, O, hd, prompt_impl):
+def test_llama_prompt_equals_tokens(dev, O, hd, prompt_impl, prompt_mmq):
     """A prompt batch through one graph (MUL_MAT at ne11 = T on the int8-MFMA GEMMs,
     batched norms, the prompt attention: all cells, then every query causally) gives the
     logits of its last token and the KV caches of decoding the tokens one by one, bit for
