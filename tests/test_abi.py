@@ -196,12 +196,15 @@ def test_hot_kernel_register_budgets(tmp_path):
         notes = subprocess.run([readelf, "--notes", str(p)], capture_output=True, text=True, check=True).stdout
         names = re.findall(r"\.name:\s+(\S+)", notes)
         vgprs = [int(v) for v in re.findall(r"\.vgpr_count:\s+(\d+)", notes)]
-        assert len(names) == len(vgprs)
-        for n, v in zip(names, vgprs):
+        spills = [int(v) for v in re.findall(r"\.vgpr_spill_count:\s+(\d+)", notes)]
+        assert len(names) == len(vgprs) == len(spills)
+        for n, v, sp in zip(names, vgprs, spills):
             for pat, budget in VGPR_BUDGET:
                 if re.match(pat, n):
                     seen[pat] += 1
-                    if v > budget:
-                        over.append((n, v, budget))
+                    # a spill can also move the destination of an in-flight inline-asm load
+                    # (the weight prefetches), not only cost time
+                    if v > budget or sp:
+                        over.append((n, v, budget, sp))
     assert all(seen.values()), f"budgeted kernels missing: {[p for p, c in seen.items() if not c]}"
     assert not over, f"kernels over their register budget: {over}"
