@@ -647,7 +647,7 @@ bool mmq_tile64(int type, int64_t N, int64_t M) {
 // Mixed Q4_K / Q6_K matrices run on kq_mmq_mixed (each row tile its matrix's body).
 int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const int64_t *N, const size_t *row_stride,
                      float *const *y, const int64_t *y_col_stride, int64_t K, const uint8_t *xq, int64_t M,
-                     hipStream_t stream) {
+                     hipStream_t stream, const MmqKv *kv) {
     if (n_mat < 1 || n_mat > 4) return MI355X_E_INVAL;
     const int type = types[0];
     bool mixed = false;
@@ -677,6 +677,15 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
         ybytes += (double)M * N[d] * 4.0;
     }
     a.tile0[n_mat] = tiles;
+    if (kv) {
+        for (int d = 0; d < n_mat; ++d) a.kv_kind[d] = kv->kind[d];
+        a.kv_pos = kv->pos;
+        a.kv_rope = kv->rope;
+        a.kv_k_cache = kv->k_cache;
+        a.kv_v_cache = kv->v_cache;
+        a.kv_n_ctx = kv->n_ctx;
+        a.kv_hd = kv->hd;
+    }
     a.w = a.mw[0];
     a.row_stride = a.mrow_stride[0];
     a.n_rows = a.mn_rows[0];

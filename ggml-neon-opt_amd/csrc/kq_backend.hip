@@ -530,30 +530,67 @@ bool attn_feeds_batched_mm(const mi355x_backend *b, const mi355x_tensor *t, cons
     return kq::attn_args_from(&d, a) == 0 && kq::attn_prompt_q8_ok(a);
 }
 
+// The kind-4 launch `l` holds the k and v MUL_MATs that the prompt ATTN_DECODE of `next`
+// reads (src[1], src[2]): its KV-cache cells can be stored by the GEMM's epilogue.
+bool kv_epilogue(mi355x_tensor *const *nodes, const Launch &l, const Launch &next, kq::MmqKv &kv) {
+    const mi355x_tensor *t = nodes[next.first];
+    if (next.kind != 0 || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] < 2) return false;
+    const int hd = t->op_params[2], n_head_kv = t->op_params[1];
+    if ((hd != 64 && hd != 128) || n_head_kv <= 0) return false;
+    const mi355x_tensor *kc = t->src[4], *vc = t->src[5];
+    if (((uintptr_t)kc->data & 15u) || ((uintptr_t)vc->data & 15u)) return false;
+    memset(&kv, 0, sizeof(kv));
+    int found = 0;
+    for (int k = 0; k < l.count; ++k) {
+        const mi355x_tensor *u = nodes[l.first + k];
+        const int role = u == t->src[1] ? 1 : u == t->src[2] ? 2 : 0;
+        if (!role) continue;
+        if (u->ne[0] != (int64_t)n_head_kv * hd || u->ne[1] != t->src[0]->ne[1]) return false;
+        kv.kind[k] = role;
+        found |= role;
+    }
+    if (found != 3) return false;
+    kv.pos = (const int32_t *)t->src[3]->data;
+    kv.rope = (const float *)t->src[6]->data;
+    kv.k_cache = (uint16_t *)kc->data;
+    kv.v_cache = (uint16_t *)vc->data;
+    kv.n_ctx = (int)kc->ne[1];
+    kv.hd = hd;
+    return true;
+}
+
 int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<Launch> &launches) {
     Q8State q8;
+    const mi355x_tensor *kv_done = nullptr;  // prompt ATTN whose KV cells a GEMM epilogue stored
     if (!kq::device_ok()) return MI355X_E_NODEVICE;
     for (size_t li = 0; li < launches.size(); ++li) {
         const Launch &l = launches[li];
         const mi355x_tensor *t = nodes[l.first];
         int rc;
-        if (l.kind == 0 && t->op == MI355X_OP_ATTN_DECODE && li + 1 < launches.size() &&
-            attn_feeds_batched_mm(b, t, launches[li + 1], nodes)) {
-            // prompt attention whose output only the next launch's GEMM reads (the o-proj):
-            // the group kernel also writes that GEMM's Q8L blocks, no kq_quantize_q8L launch
+        const bool q8_fuse = l.kind == 0 && t->op == MI355X_OP_ATTN_DECODE && li + 1 < launches.size() &&
+                             attn_feeds_batched_mm(b, t, launches[li + 1], nodes);
+        if (q8_fuse || (l.kind == 0 && t == kv_done)) {
+            // prompt attention: its KV cells already stored by the k/v GEMM's epilogue
+            // (kv_done), and/or its output only read by the next launch's GEMM (the o-proj),
+            // for which the group kernel also writes the Q8L blocks (no kq_quantize_q8L)
             mi355x_attn_desc d;
             attn_desc_of(t, d);
             d.rope_row = 0;
             kq::AttnArgs a;
             rc = kq::attn_args_from(&d, a);
             if (rc) return rc;
-            a.q8_out = (uint8_t *)b->workspace;
+            a.no_store = t == kv_done;
+            kv_done = nullptr;
+            if (q8_fuse) a.q8_out = (uint8_t *)b->workspace;
             rc = kq::launch_attn_prompt(a, (int)t->src[0]->ne[1], b->stream);
             if (rc) return rc;
-            q8.src = t->data;
-            q8.k = t->ne[0];
-            q8.m = t->ne[1];
-            q8.nb = t->nb[1];
+            q8 = Q8State();
+            if (q8_fuse) {
+                q8.src = t->data;
+                q8.k = t->ne[0];
+                q8.m = t->ne[1];
+                q8.nb = t->nb[1];
+            }
             continue;
         }
         if (l.kind == 2) {  // prefill prologue: the activation's Q8L blocks for the MUL_MATs after it
@@ -595,8 +632,34 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
                 y[k] = (float *)u->data;
                 ycs[k] = (int64_t)(u->nb[1] / 4);
             }
+            // the prompt attention right after, reading k and v of this group: its KV cells
+            // stored by this launch's epilogue (kq_kv_store's arithmetic), one launch fewer
+            kq::MmqKv kv;
+            const bool kv_fuse = li + 1 < launches.size() && kv_epilogue(nodes, l, launches[li + 1], kv);
+            if (kv_fuse) {  // k and v first: their row tiles (and the cache stores) start first
+                int order[4], no = 0;
+                for (int k = 0; k < l.count; ++k)
+                    if (kv.kind[k]) order[no++] = k;
+                for (int k = 0; k < l.count; ++k)
+                    if (!kv.kind[k]) order[no++] = k;
+                const void *w2[4];
+                int t2[4], kk2[4];
+                int64_t N2[4], ycs2[4];
+                size_t rs2[4];
+                float *y2[4];
+                for (int k = 0; k < l.count; ++k) {
+                    const int o = order[k];
+                    w2[k] = w[o], t2[k] = types[o], kk2[k] = kv.kind[o], N2[k] = N[o], ycs2[k] = ycs[o];
+                    rs2[k] = rs[o], y2[k] = y[o];
+                }
+                for (int k = 0; k < l.count; ++k) {
+                    w[k] = w2[k], types[k] = t2[k], kv.kind[k] = kk2[k], N[k] = N2[k], ycs[k] = ycs2[k];
+                    rs[k] = rs2[k], y[k] = y2[k];
+                }
+            }
             rc = kq::launch_mmq_multi(types, l.count, w, N, rs, y, ycs, K, (const uint8_t *)b->workspace, M,
-                                      b->stream);
+                                      b->stream, kv_fuse ? &kv : nullptr);
+            if (!rc && kv_fuse) kv_done = nodes[launches[li + 1].first];
             if (rc) return rc;
             const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;
             for (int k = 0; k < l.count; ++k) {  // an output over the quantized activation invalidates it

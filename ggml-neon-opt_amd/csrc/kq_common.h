@@ -194,6 +194,7 @@ struct AttnArgs {
     float scale;
     int diag;  // diagnostics only (MI355X_ATTN_DIAG): 1/2/3 stop after loads/KQ/soft_max, 4 empty
     int rope_row;  // rope_table holds only the row of *pos (no position-dependent load)
+    int no_store;     // prompt batch: the KV cells are already stored (the k/v GEMM's epilogue)
     uint8_t *q8_out;  // prompt batch (kq_attn_prompt_group): also the output rows as Q8L blocks
                       // for the next GEMM (row i's superblock b at (i*nb + b)*304), or null
 };
@@ -218,6 +219,13 @@ struct MmqArgs {
     int n_mat;
     int tile0[5];
     int mtype[4];  // kq_mmq_mixed: each matrix's type (Q4_K / Q6_K)
+    // KV-cache store epilogue of a prompt's k / v projections (kv_kind[d]: 1 k -> rope ->
+    // f16 cache rows, 2 v -> f16 transposed cache; 0 none); kv_cur: this tile's matrix
+    int kv_kind[4], kv_cur;
+    const int32_t *kv_pos;   // cell of each column (token)
+    const float *kv_rope;    // [n_ctx][head_dim/2][cos, sin]
+    uint16_t *kv_k_cache, *kv_v_cache;
+    int kv_n_ctx, kv_hd;
     const uint8_t *mw[4];
     int64_t mrow_stride[4];
     int mn_rows[4];

@@ -61,9 +61,18 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
                float *y, int64_t y_col_stride, hipStream_t stream, const float *res = nullptr,
                int64_t res_col_stride = 0);  // res: ADD epilogue
 bool mmq_tile64(int type, int64_t N, int64_t M);  // launch_mmq would use the 64 x 64 tile kernel
+// KV-cache store epilogue of launch_mmq_multi (a prompt's k / v projections): kind[d] 1 k,
+// 2 v, 0 none; the cells of kq_kv_store (rope(k) -> f16 rows, v -> f16 transposed)
+struct MmqKv {
+    int kind[4];
+    const int32_t *pos;
+    const float *rope;
+    uint16_t *k_cache, *v_cache;
+    int n_ctx, hd;
+};
 int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const int64_t *N, const size_t *row_stride,
                      float *const *y, const int64_t *y_col_stride, int64_t K, const uint8_t *xq, int64_t M,
-                     hipStream_t stream);  // types: Q4_K/Q6_K may mix (kq_mmq_mixed)
+                     hipStream_t stream, const MmqKv *kv = nullptr);  // types: Q4_K/Q6_K may mix (kq_mmq_mixed)
 // prefill prologues: rms_norm(x) * w -> Q8L, swiglu(g, u) -> Q8L (nrows rows of n)
 int launch_rms_norm_q8L(const float *x, const float *w, void *yq, int64_t n, int64_t nrows, float eps, hipStream_t s);
 int launch_swiglu_q8L(const float *g, const float *u, void *yq, int64_t n, int64_t nrows, hipStream_t s);

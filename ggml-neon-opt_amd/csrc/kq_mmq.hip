@@ -24,6 +24,7 @@
 //   f16 32x32x16: A[r][8h+j], B[8h+j][r], j<8; C/D (every dtype): col = r,
 //   row = (reg&3) + 8(reg>>2) + 4h.
 #include "kq_device.h"
+#include "kq_ops_device.h"
 
 // Timing-only ablations of kq_mmq<Q4_K>, compile time so the product kernel carries none of
 // them (as run-time branches they cost 40 VGPRs and a wave per SIMD): 1 no chain epilogue,
@@ -283,6 +284,7 @@ __device__ __forceinline__ int mmq_tile_of(const MmqArgs &a0, MmqArgs &a, int &t
         a.n_rows = a0.mn_rows[d];
         a.y = a0.my[d];
         a.y_col_stride = a0.my_col_stride[d];
+        a.kv_cur = a0.kv_kind[d];
         ty -= a0.tile0[d];
     }
     return d;
@@ -588,6 +590,25 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             const int m = col0 + 32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h;
             if (m < a.m_cols)
                 a.y[(int64_t)m * a.y_col_stride + n] = a.res ? sumf[i] + a.res[(int64_t)m * a.res_col_stride + n] : sumf[i];
+        }
+    }
+    if (a.kv_cur) {  // the prompt's KV-cache cells, as kq_kv_store computes them (kq_ops.hip)
+        const int hd = a.kv_hd;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int m = col0 + 32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h;
+            const float other = __shfl_xor(sumf[i], 1, 64);  // row n ^ 1: the rope partner
+            const int pos = m < a.m_cols ? a.kv_pos[m] : -1;
+            if (n >= a.n_rows || pos < 0 || pos >= a.kv_n_ctx) continue;  // no cell (its output is NaN)
+            if (a.kv_cur == 1) {
+                const int pr = (n % hd) >> 1;
+                const float *tc = a.kv_rope + (int64_t)pos * (hd / 2) * 2;
+                const bool odd = n & 1;
+                const float2 rk = rope_pair(odd ? other : sumf[i], odd ? sumf[i] : other, tc[2 * pr], tc[2 * pr + 1]);
+                a.kv_k_cache[(int64_t)pos * a.n_rows + n] = h2u(f2h_rne(odd ? rk.y : rk.x));
+            } else {
+                a.kv_v_cache[(int64_t)n * a.kv_n_ctx + pos] = h2u(f2h_rne(sumf[i]));
+            }
         }
     }
 }

@@ -851,7 +851,7 @@ int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
     const dim3 gg((unsigned)a.n_head_kv, (unsigned)n_tok);
     int rc;
     if (a.head_dim == 64) {
-        rc = timed_launch("kq::kq_kv_store<64>", 0.0, kq_kv_store<64>, gs, dim3(256), 0, s, a);
+        rc = a.no_store ? 0 : timed_launch("kq::kq_kv_store<64>", 0.0, kq_kv_store<64>, gs, dim3(256), 0, s, a);
         if (rc) return rc;
         if (group) {
             allow_lds((const void *)kq_attn_prompt_group<64>, glds);
@@ -860,7 +860,7 @@ int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
         allow_lds((const void *)kq_attn_prompt<64>, lds);
         return timed_launch("kq::kq_attn_prompt<64>", 0.0, kq_attn_prompt<64>, ga, dim3(256), lds, s, a);
     }
-    rc = timed_launch("kq::kq_kv_store<128>", 0.0, kq_kv_store<128>, gs, dim3(256), 0, s, a);
+    rc = a.no_store ? 0 : timed_launch("kq::kq_kv_store<128>", 0.0, kq_kv_store<128>, gs, dim3(256), 0, s, a);
     if (rc) return rc;
     if (group) {
         allow_lds((const void *)kq_attn_prompt_group<128>, glds);
@@ -1019,6 +1019,7 @@ int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a) {
     a.scale = d->scale;
     a.rope_row = d->rope_row ? 1 : 0;
     a.q8_out = nullptr;
+    a.no_store = 0;
     static const int diag = [] {
         const char *e = getenv("MI355X_ATTN_DIAG");
         return e ? atoi(e) : 0;
