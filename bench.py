@@ -822,7 +822,7 @@ def main():
         if roof is not None and not rowsplit:
             # HBM traffic of the same kernel from the committed rocprofv3 PMC pass of this
             # bench command (FETCH_SIZE x2 gfx950 correction), per launch
-            pname = "r02_token_summary.json" if isinstance(chain, Token) else "r01_chain_summary.json"
+            pname = "r02final_token_summary.json" if isinstance(chain, Token) else "r01_chain_summary.json"
             prof = os.path.join(ROOT, "profiles", pname)
             if not os.path.exists(prof) and isinstance(chain, Token):
                 pname = "r01_token_summary.json"
