@@ -542,9 +542,28 @@ def spawn_ranks(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + sys.argv[1:], env=env))
-    rcs = [p.wait() for p in procs]
-    bad = [rc for rc in rcs if rc != 0]
-    sys.exit(bad[0] if bad else 0)
+    # Poll every rank: when one fails (GPU fault, OOM) the others may wait forever in a
+    # gloo barrier or in an RCCL collective inside the replayed hipGraph, so end them and
+    # report the failing rank's status instead of blocking on them one by one.
+    while True:
+        rcs = [p.poll() for p in procs]
+        bad = [rc for rc in rcs if rc not in (None, 0)]
+        if bad:
+            for p in procs:
+                if p.poll() is None:
+                    p.terminate()
+            for p in procs:
+                try:
+                    p.wait(timeout=20)
+                except subprocess.TimeoutExpired:
+                    p.kill()
+                    p.wait()
+            print(json.dumps({"error": f"rank exited with status {bad[0]}", "statuses": [p.returncode for p in procs]}),
+                  file=sys.stderr)
+            sys.exit(bad[0] if bad[0] > 0 else 1)
+        if all(rc == 0 for rc in rcs):
+            sys.exit(0)
+        time.sleep(0.2)
 
 
 def tg_side(tk, steps, barrier):

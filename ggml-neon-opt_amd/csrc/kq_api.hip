@@ -865,6 +865,12 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
     return launch_gemv(pl, stream);
 }
 
+uint64_t api_selector_key() {
+    rows_enabled();  // resolve the environment defaults first
+    return (uint64_t)(uint32_t)(g_impl.load() + 1) | ((uint64_t)(uint32_t)g_rows_waves.load() << 8) |
+           ((uint64_t)(uint32_t)(mmq_impl() + 1) << 16);
+}
+
 }  // namespace kq
 
 using namespace kq;
@@ -940,13 +946,16 @@ ThreadCtx *thread_ctx(size_t need) {
 }
 
 // True when p is device-accessible memory of the current device (hipMalloc / managed).
+// A buffer of another GPU is foreign here: it is staged like host memory (a peer copy),
+// never read in place by a kernel of this device.
 bool on_device(const void *p) {
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, p) != hipSuccess) {
         (void)hipGetLastError();  // plain pageable host memory: not an error to keep
         return false;
     }
-    return at.type == hipMemoryTypeDevice || at.type == hipMemoryTypeManaged;
+    if (at.type == hipMemoryTypeManaged) return true;
+    return at.type == hipMemoryTypeDevice && at.device == current_device();
 }
 }  // namespace
 
@@ -962,13 +971,13 @@ void mi355x_quantize_row_q8_K(const float *x, void *y, int64_t k) {
     void *dy = y;
     uint8_t *stage = (uint8_t *)c->buf;
     if (!xd) {
-        if (hipMemcpyAsync(stage, x, xb, hipMemcpyHostToDevice, c->st) != hipSuccess) die(__func__, "copy in failed");
+        if (hipMemcpyAsync(stage, x, xb, hipMemcpyDefault, c->st) != hipSuccess) die(__func__, "copy in failed");
         dx = (const float *)stage;
         stage += (xb + 15) & ~(size_t)15;
     }
     if (!yd) dy = stage;
     if (mi355x_quantize_q8_K(dx, xb, dy, k, 1, c->st)) die(__func__, "launch failed");
-    if (!yd && hipMemcpyAsync(y, dy, yb, hipMemcpyDeviceToHost, c->st) != hipSuccess) die(__func__, "copy out failed");
+    if (!yd && hipMemcpyAsync(y, dy, yb, hipMemcpyDefault, c->st) != hipSuccess) die(__func__, "copy out failed");
     if (hipStreamSynchronize(c->st) != hipSuccess) die(__func__, "hipStreamSynchronize failed");
 }
 
@@ -1140,19 +1149,19 @@ static void vec_dot_dev(int type, const char *fn, int n, float *s, const void *v
     uint8_t *stage = (uint8_t *)c->buf;
     const void *dx = vx, *dy = vy;
     if (!xd) {
-        if (hipMemcpyAsync(stage, vx, wb, hipMemcpyHostToDevice, c->st) != hipSuccess) die(fn, "copy in failed");
+        if (hipMemcpyAsync(stage, vx, wb, hipMemcpyDefault, c->st) != hipSuccess) die(fn, "copy in failed");
         dx = stage;
         stage += (wb + 15) & ~(size_t)15;
     }
     if (!yd) {
-        if (hipMemcpyAsync(stage, vy, qb, hipMemcpyHostToDevice, c->st) != hipSuccess) die(fn, "copy in failed");
+        if (hipMemcpyAsync(stage, vy, qb, hipMemcpyDefault, c->st) != hipSuccess) die(fn, "copy in failed");
         dy = stage;
         stage += (qb + 15) & ~(size_t)15;
     }
     float *ds = sd ? s : (float *)stage;
     const int rc = mi355x_mul_mat_q8(type, dx, n, 1, wb, dy, 1, qb, ds, 4, c->st);
     if (rc) die(fn, "launch failed");
-    if (!sd && hipMemcpyAsync(s, ds, 4, hipMemcpyDeviceToHost, c->st) != hipSuccess) die(fn, "copy out failed");
+    if (!sd && hipMemcpyAsync(s, ds, 4, hipMemcpyDefault, c->st) != hipSuccess) die(fn, "copy out failed");
     if (hipStreamSynchronize(c->st) != hipSuccess) die(fn, "hipStreamSynchronize failed");
 }
 

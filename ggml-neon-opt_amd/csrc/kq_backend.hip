@@ -711,7 +711,12 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
 
 std::vector<uint64_t> graph_key_of(mi355x_tensor *const *nodes, int n_nodes) {
     std::vector<uint64_t> key;
-    key.reserve((size_t)n_nodes * 16);
+    key.reserve((size_t)n_nodes * 16 + 2);
+    // the plan captured under this key also depends on the process-wide kernel selectors
+    // (mmq_impl decides kind-4 batching and the KV-store epilogue, attn_prompt_impl the
+    // attention's Q8L output, ...): a changed selector must not replay the old graph
+    key.push_back(kq::api_selector_key());
+    key.push_back(kq::ops_selector_key());
     for (int i = 0; i < n_nodes; ++i) {
         const mi355x_tensor *t = nodes[i];
         key.push_back((uint64_t)(uintptr_t)t->data);

@@ -83,5 +83,9 @@ bool attn_group_ok(const AttnArgs &a, int nwaves);      // the one-workgroup-per
 size_t attn_group_bytes(const AttnArgs &a, int nwaves);  // its LDS
 // kq_api.hip
 void allow_lds(const void *fn, size_t lds);
+// Process-wide kernel selectors a captured launch plan depends on (gemv impl / waves,
+// mmq impl; attention decode / prompt impl), packed for the backend's graph key.
+uint64_t api_selector_key();
+uint64_t ops_selector_key();
 
 }  // namespace kq

@@ -27,7 +27,7 @@
 
 namespace {
 
-constexpr int kTypeF32 = MI355X_TYPE_F32, kTypeF16 = 1, kTypeI32 = 26;
+constexpr int kTypeF32 = MI355X_TYPE_F32, kTypeF16 = 1, kTypeI32 = 26, kTypeI64 = 27;
 
 float f_of(int32_t bits) {
     float f;
@@ -131,14 +131,29 @@ struct Lower {
 
     bool rope_ok(const mi355x_gtensor *r, int hd) const {
         if (!r || r->op != MI355X_GOP_ROPE || r->ne[2] < 1 || r->ne[3] != 1) return false;  // [hd, heads, tokens]
+        // freq_factors (src[2], Llama-3.1+ rope_freqs): the caller's table carries none
+        if (r->src[2]) return false;
         if (r->op_params[1] != hd || r->op_params[2] != 0) return false;   // n_dims, mode NORMAL
         if (f_of(r->op_params[5]) != opts->rope_freq_base || f_of(r->op_params[6]) != opts->rope_freq_scale)
             return false;
         return f_of(r->op_params[7]) == 0.0f && f_of(r->op_params[8]) == 1.0f;  // ext_factor, attn_factor
     }
 
-    // The attention block ending at CONT node `c` -> one ATTN_DECODE.
+    // A SET_ROWS index operand: an I32/I64 leaf of `n` entries (its contents live on the
+    // device; what they hold is the adapter's cells_eq_pos promise).
+    static bool idx_ok(const mi355x_gtensor *t, int64_t n) {
+        const mi355x_gtensor *r = root(t);
+        return r && r->op == MI355X_GOP_NONE && (t->type == kTypeI32 || t->type == kTypeI64) && t->ne[0] == n &&
+               t->ne[1] == 1 && t->ne[2] == 1 && t->ne[3] == 1;
+    }
+
+    // The attention block ending at CONT node `c` -> one ATTN_DECODE. ATTN_DECODE writes
+    // each token's K/V at cell == its position and attends causally over [0, pos]; that
+    // is the block's meaning only under the adapter's cells_eq_pos promise (one sequence,
+    // k_idxs == v_idxs cells == inp_pos, causal mask, views from cell 0), so without it
+    // the block is not lowered.
     bool attention(const mi355x_gtensor *c) {
+        if (!opts->cells_eq_pos) return false;
         const mi355x_gtensor *p = c->src[0];
         if (!p || p->op != MI355X_GOP_PERMUTE) return false;
         const mi355x_gtensor *kqv = root(p->src[0]);
@@ -169,6 +184,10 @@ struct Lower {
         if (nkv <= 0 || nh % nkv) return false;
         const int64_t T = rq->ne[2];  // tokens of the batch (1: a decode token; > 1: a prompt)
         if (rk->ne[2] != T) return false;
+        // one K row per token; the transposed V store scatters one index per element
+        if (!idx_ok(sk->src[1], T) || !idx_ok(sv->src[1], (int64_t)nkv * hd * T)) return false;
+        // the KQ / KQV operands are views of the caches from cell 0
+        if (kq->src[0]->view_offs != 0 || kqv->src[0]->view_offs != 0) return false;
         const mi355x_gtensor *qmm = root(rq->src[0]), *kmm = root(rk->src[0]), *vmm = root(sv->src[0]);
         if (!qmm || !kmm || !vmm || qmm->op != MI355X_GOP_MUL_MAT || kmm->op != MI355X_GOP_MUL_MAT ||
             vmm->op != MI355X_GOP_MUL_MAT)

@@ -880,6 +880,10 @@ int check_attn(const AttnArgs &a) {
     return MI355X_OK;
 }
 
+uint64_t ops_selector_key() {
+    return (uint64_t)(uint32_t)attn_impl() | ((uint64_t)(uint32_t)g_prompt_impl.load() << 8);
+}
+
 }  // namespace kq
 
 using namespace kq;

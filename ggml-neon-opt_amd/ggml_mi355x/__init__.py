@@ -25,7 +25,7 @@ MAX_FUSED = 4
 OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROPE, OP_ATTN_DECODE, OP_ALL_GATHER = range(10)
 MAX_SRC = 8
 FLAG_OUTPUT = 1
-E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_TIMEOUT, E_COMM = 0, -1, -2, -3, -4, -5, -6
+E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM = 0, -1, -2, -3, -4, -6
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 ATTN_GROUP, ATTN_HEAD = 0, 1
@@ -94,7 +94,7 @@ GTensor._fields_ = [("type", ctypes.c_int), ("op", ctypes.c_int), ("ne", ctypes.
 
 class LowerOpts(ctypes.Structure):
     _fields_ = [("rope_table", ctypes.c_void_p), ("rope_n_pos", ctypes.c_int), ("rope_freq_base", ctypes.c_float),
-                ("rope_freq_scale", ctypes.c_float)]
+                ("rope_freq_scale", ctypes.c_float), ("cells_eq_pos", ctypes.c_int)]
 
 
 (GOP_NONE, GOP_GET_ROWS, GOP_RMS_NORM, GOP_MUL, GOP_ADD, GOP_MUL_MAT, GOP_ROPE, GOP_SET_ROWS, GOP_SOFT_MAX, GOP_GLU,
@@ -598,16 +598,19 @@ class Backend:
             pass
 
 
-def lower_ggml_graph(gnodes, rope_table_ptr, rope_n_pos, freq_base, freq_scale=1.0, arena_cap=None):
+def lower_ggml_graph(gnodes, rope_table_ptr, rope_n_pos, freq_base, freq_scale=1.0, arena_cap=None,
+                     cells_eq_pos=True):
     """mi355x_lower_ggml_graph over a list of GTensor nodes (graph order). Returns
-    (status, [Tensor node list], arena) — the arena keeps the nodes alive."""
+    (status, [Tensor node list], arena) — the arena keeps the nodes alive.
+    cells_eq_pos: the adapter's promise (mi355x_lower_opts) that the batch is one
+    sequence whose KV cells equal its positions under a causal mask."""
     n = len(gnodes)
     arr = (ctypes.POINTER(GTensor) * max(1, n))(*[ctypes.pointer(t) for t in gnodes])
     cap = arena_cap or (4 * n + 64)
     arena = (Tensor * cap)()
     out = (ctypes.POINTER(Tensor) * cap)()
     nn = ctypes.c_int(0)
-    opts = LowerOpts(rope_table_ptr, rope_n_pos, freq_base, freq_scale)
+    opts = LowerOpts(rope_table_ptr, rope_n_pos, freq_base, freq_scale, 1 if cells_eq_pos else 0)
     rc = int(lib().mi355x_lower_ggml_graph(arr, n, ctypes.byref(opts), arena, cap, out, cap, ctypes.byref(nn)))
     return rc, [out[i].contents for i in range(nn.value)], (arena, out)
 

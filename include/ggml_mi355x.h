@@ -89,7 +89,6 @@ enum mi355x_status {
     MI355X_E_UNSUPPORTED = -2, /* combination not implemented on this device   */
     MI355X_E_WORKSPACE  = -3,  /* workspace missing or too small               */
     MI355X_E_NODEVICE   = -4,  /* no gfx950 device / HIP runtime unavailable   */
-    MI355X_E_TIMEOUT    = -5,  /* an overlapped launch's activation hand-off timed out */
     MI355X_E_COMM       = -6,  /* RCCL missing / communicator error            */
 };
 
@@ -443,6 +442,14 @@ typedef struct {
     void *rope_table;               /* f32 [head_dim, n_pos] from mi355x_rope_table  */
     int rope_n_pos;                 /* its rows (>= the KV cache size)           */
     float rope_freq_base, rope_freq_scale; /* the table's parameters (checked against ROPE) */
+    int cells_eq_pos;               /* the adapter's promise, checked on the host before the
+                                     * call: ONE sequence, every token's K/V cell index
+                                     * (SET_ROWS k_idxs / v_idxs) equals its position
+                                     * (inp_pos), the mask is the causal mask over cells
+                                     * [0, pos] and the KQ / KQV views start at cell 0.
+                                     * ATTN_DECODE writes cell == pos and attends over
+                                     * [0, pos]; with 0 here attention blocks are not
+                                     * lowered (MI355X_E_UNSUPPORTED). */
 } mi355x_lower_opts;
 /* Lowers `n` ggml nodes (graph order) into backend nodes. Tensors are written into
  * `arena` (cap entries: nodes and the leaf mirrors they reference); `nodes_out`

@@ -102,6 +102,48 @@ def test_lowering_rejects_what_it_cannot_run():
     assert g.lower_ggml_graph(G.nodes, dec.table.data_ptr(), 32, hp["freq_base"], arena_cap=8)[0] == g.E_WORKSPACE
 
 
+def test_lowering_rejects_attention_it_would_misplace():
+    """ATTN_DECODE writes cell == pos and attends causally over [0, pos]. The lowering
+    cannot read the device-resident k_idxs / mask, so it lowers an attention block only
+    under the adapter's cells_eq_pos promise (one sequence, k_idxs == inp_pos, causal
+    mask), and refuses what the table cannot express: rope freq_factors (Llama-3.1+
+    rope_freqs, ROPE src[2]), index operands of the wrong shape, KQ views not at cell 0."""
+    hp = hparams(512, 1, 8, 2, 768, 1024)
+    wt, dec = _describe(hp, 32)
+    L = _leaves(hp, wt, dec)
+    tab = dec.table.data_ptr()
+
+    def lower(mutate, **kw):
+        G = GG.llama_decode_graph(hp, L, 32)
+        mutate(G)
+        return g.lower_ggml_graph(G.nodes, tab, 32, hp["freq_base"], **kw)[0]
+
+    def nodes(G, op):
+        return [t for t in G.nodes if t.op == op]
+
+    assert lower(lambda G: None) == 0
+    # several sequences / cells != positions (seq_rm, defrag, context shift): no promise
+    assert lower(lambda G: None, cells_eq_pos=False) == g.E_UNSUPPORTED
+    # rope with freq_factors on either the Q or the K rope
+    ff = GG.Graph().leaf(GG.F32, [hp["head_dim"] // 2], 0x2000, name="rope_freqs")
+    import ctypes
+    for which in (0, 1):
+        assert lower(lambda G: nodes(G, g.GOP_ROPE)[which].src.__setitem__(2, ctypes.pointer(ff))) == g.E_UNSUPPORTED
+    # a K index operand that is not one row per token
+    bad_idx = GG.Graph().leaf(GG.I64, [2], 0x1000, name="k_idxs")
+    assert lower(lambda G: nodes(G, g.GOP_SET_ROWS)[0].src.__setitem__(1, ctypes.pointer(bad_idx))) == g.E_UNSUPPORTED
+    # f32 indices are not indices
+    f_idx = GG.Graph().leaf(GG.F32, [1], 0x1000, name="k_idxs")
+    assert lower(lambda G: nodes(G, g.GOP_SET_ROWS)[0].src.__setitem__(1, ctypes.pointer(f_idx))) == g.E_UNSUPPORTED
+
+    # a KQ view that starts past cell 0
+    def shift_view(G):
+        kq = next(t for t in G.nodes if t.op == g.GOP_MUL_MAT and t.name == b"kq")
+        kq.src[0].contents.view_offs = 64
+
+    assert lower(shift_view) == g.E_UNSUPPORTED
+
+
 def test_lowering_supports_every_lowered_node():
     """Every node the lowering emits passes the backend's supports_op."""
     hp = hparams(512, 2, 8, 2, 768, 1024)
