@@ -22,6 +22,19 @@
 // waves 1-3 through exact LDS records).
 #include "kq_device.h"
 
+// Diagnostics (timing only: MI355X_GEMV_DIAG bits, per-wave stamps) exist only in
+// experiment builds (-DKQ_GEMV_DIAG=1); in the product build they compile out.
+#ifndef KQ_GEMV_DIAG
+#define KQ_GEMV_DIAG 0
+#endif
+#if KQ_GEMV_DIAG
+#define GDIAG(a) ((a).diag)
+#define GSTAMPS(a) ((a).stamps)
+#else
+#define GDIAG(a) 0
+#define GSTAMPS(a) ((uint64_t *)nullptr)
+#endif
+
 namespace kq {
 
 // ------------------------------------------------------------------ Q8_K quantize kernel
@@ -122,8 +135,8 @@ struct TaskLane {
 template <int NCOL, bool FUSEDQ, bool DEBUG, int TMASK>
 __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
-    if (a.diag & 2) return;  // diagnostics: empty launch (same grid / LDS)
+    const uint64_t st0 = GSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (GDIAG(a) & 2) return;  // diagnostics: empty launch (same grid / LDS)
     const int nb = a.nb, D = a.ring;
     constexpr int SLOT = slot_bytes(TMASK);
     const LdsLayout L = lds_layout(NCOL, nb, a.out_per_wg, FUSEDQ, SLOT, D);
@@ -212,7 +225,7 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
         const int type = TMASK == 1 ? Q4_K : TMASK == 4 ? Q6_K : ct.type;
         const uint8_t *slot = cslot;
         cslot = cslot + SLOT == ring_end ? ring : cslot + SLOT;
-        if (!(a.diag & 8)) {  // diagnostics bit 3: stream weights only, no arithmetic
+        if (!(GDIAG(a) & 8)) {  // diagnostics bit 3: stream weights only, no arithmetic
         uint32_t sh = 0;
         if (type == Q6_K) sh = (uint32_t)((uintptr_t)(ct.crow + (int64_t)blk * 210) & 15u);
         Regs rr;
@@ -251,7 +264,7 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     it.load<TMASK>(a, tfirst, lane);
     ct = it;
     uint64_t sa = 0, sb = 0, sc = 0;
-    if (a.stamps) sa = __builtin_amdgcn_s_memrealtime();
+    if (GSTAMPS(a)) sa = __builtin_amdgcn_s_memrealtime();
     if (FUSEDQ) {
         const float *xc = a.x + (int64_t)col0 * a.x_col_stride + (int64_t)lo * QK;
         for (int i = 0; i < S; ++i) dma16(xc + (int64_t)i * QK + 4 * lane, (LDS void *)(act + 1024 * i));
@@ -268,9 +281,9 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     }
     const int pre = Q < D ? Q : D;
     for (int j = 0; j < pre; ++j) issue();
-    if (a.stamps) sb = __builtin_amdgcn_s_memrealtime();
+    if (GSTAMPS(a)) sb = __builtin_amdgcn_s_memrealtime();
     vm_wait_steps(pre);  // activation DMAs are older than the ring's 2*pre
-    if (a.stamps) sc = __builtin_amdgcn_s_memrealtime();
+    if (GSTAMPS(a)) sc = __builtin_amdgcn_s_memrealtime();
     if (FUSEDQ) {
         // quantize in place: block i's f32 staging [1024i, 1024i+1024) -> raw Q8_K [292i, 292i+292)
 #pragma unroll 1
@@ -285,11 +298,11 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     }
     wave_lds_fence();  // this wave's staged activations before its own reads
     uint64_t st1 = 0, st2 = 0;
-    if (a.stamps) {
+    if (GSTAMPS(a)) {
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         st1 = __builtin_amdgcn_s_memrealtime();
     }
-    if (a.diag & 1) return;  // diagnostics: prologue only
+    if (GDIAG(a) & 1) return;  // diagnostics: prologue only
 
     // ---- main loop: wait for step q's slot, compute it, refill the slot with step q+D
     if (S > 0) {
@@ -303,7 +316,7 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
     } else {
         for (int k = 0; k < my_tasks; ++k) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     }
-    if (a.stamps) st2 = __builtin_amdgcn_s_memrealtime();
+    if (GSTAMPS(a)) st2 = __builtin_amdgcn_s_memrealtime();
 
     // ---- flush wave 0's staged results: task k -> rows row0..row0+7, NCOL columns
     if (!DEBUG && wave == 0 && my_tasks > 0) {
@@ -315,17 +328,17 @@ __global__ void __launch_bounds__(WG_THREADS) kq_gemv(const GemvArgs a) {
                 a.y[si.m][(int64_t)(col0 + c) * a.y_col_stride[si.m] + si.row0 + r] = outs[k * NCOL * 8 + lane];
         }
     }
-    if (a.stamps) {
+    if (GSTAMPS(a)) {
         const int64_t o = ((int64_t)blockIdx.x * WAVES_PER_WG + wave) * 8;
         if (lane == 0 && o + 7 < a.stamps_cap) {
             const uint64_t st3 = __builtin_amdgcn_s_memrealtime();
-            a.stamps[o] = st0;
-            a.stamps[o + 1] = st1;
-            a.stamps[o + 2] = st2;
-            a.stamps[o + 3] = st3;
-            a.stamps[o + 4] = sa;
-            a.stamps[o + 5] = sb;
-            a.stamps[o + 6] = sc;
+            GSTAMPS(a)[o] = st0;
+            GSTAMPS(a)[o + 1] = st1;
+            GSTAMPS(a)[o + 2] = st2;
+            GSTAMPS(a)[o + 3] = st3;
+            GSTAMPS(a)[o + 4] = sa;
+            GSTAMPS(a)[o + 5] = sb;
+            GSTAMPS(a)[o + 6] = sc;
         }
     }
 }

@@ -27,6 +27,21 @@
 #include "kq_ops_device.h"
 #include "kq_rows_device.h"
 
+// Diagnostics (timing only: MI355X_GEMV_DIAG bits, per-wave s_memrealtime stamps) exist
+// only in experiment builds: make variant NAME=rdiag VFLAGS=-DKQ_ROWS_DIAG=1. In the
+// product build RDIAG / RSTAMPS are constants and every diagnostic branch compiles out
+// (run-time diag branches cost kq_mmq 40 VGPRs).
+#ifndef KQ_ROWS_DIAG
+#define KQ_ROWS_DIAG 0
+#endif
+#if KQ_ROWS_DIAG
+#define RDIAG(a) ((a).diag)
+#define RSTAMPS(a) ((a).stamps)
+#else
+#define RDIAG(a) 0
+#define RSTAMPS(a) ((uint64_t *)nullptr)
+#endif
+
 namespace kq {
 
 // Q8L quantization of whole rows (K > 8192 path): 16 superblocks per workgroup.
@@ -230,7 +245,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 #pragma unroll
                 for (int k = 0; k < 4; ++k) xv[i][k] = gload16_asm(xp + 4 * k);
                 if (PRO != ROWS_PRO_NONE) {  // (diag bit 4: read x again instead of x2, timing only)
-                    const float *x2p = ((a.diag & 16) ? a.x : a.x2) + (int64_t)b * QK + 16 * (lane & 15);
+                    const float *x2p = ((RDIAG(a) & 16) ? a.x : a.x2) + (int64_t)b * QK + 16 * (lane & 15);
 #pragma unroll
                     for (int k = 0; k < 4; ++k) x2v[i][k] = gload16_asm(x2p + 4 * k);
                 }
@@ -262,7 +277,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 #pragma unroll
                 for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(x2v[i][k]));
         }
-        if (a.diag & 32) {  // diagnostics (timing only): skip the transform
+        if (RDIAG(a) & 32) {  // diagnostics (timing only): skip the transform
         } else if (pro == ROWS_PRO_SWIGLU) {  // ggml_vec_swiglu_f32: silu(gate) * up
 #pragma unroll
             for (int i = 0; i < ROWS_QPASS; ++i)
@@ -303,16 +318,16 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 #pragma unroll
                     for (int k = 0; k < 4; ++k) xv[i][k] = normmul4(xv[i][k], x2v[i][k], scale);
         }
-        if (a.stamps) sx = __builtin_amdgcn_s_memrealtime();
+        if (RSTAMPS(a)) sx = __builtin_amdgcn_s_memrealtime();
 #pragma unroll 1
         for (int i = 0; i < qiters; ++i) {  // one copy of the quantizer; pick the pass's registers
             u32x4 cur[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) cur[k] = i == 0 ? xv[0][k] : i == 1 ? xv[1][k] : xv[2][k];
             const int b = PASS * i + 4 * wave + (lane >> 4);
-            if (b < nb && !(a.diag & 64)) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * b);  // (diag 64: timing only)
+            if (b < nb && !(RDIAG(a) & 64)) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * b);  // (diag 64: timing only)
         }
-        if (a.stamps) {
+        if (RSTAMPS(a)) {
             asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
             sq = __builtin_amdgcn_s_memrealtime();
         }
@@ -327,7 +342,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     }
     while (it_ < D && it_ < T) issue();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // Q8_K row complete (no vmcnt drain)
-    const uint64_t st1 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t st1 = RSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
 
     // ---- main loop
     int io = q, rr = 0;  // quad's (block, row-in-batch) of superblock 16t+q
@@ -348,7 +363,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         } else {
             vm_wait_k<NI>(T - t - 1);
         }
-        if (!(a.diag & 8) && ROWS_SB * t + q < G) {
+        if (!(RDIAG(a) & 8) && ROWS_SB * t + q < G) {
             const uint8_t *blk = cslot + mis + q * BSZ;
             const uint8_t *ab = actq + io * Q8L_STRIDE;
             QuadOut r = TYPE == Q4_K ? quad_q4K(blk, ab, s) : TYPE == Q5_K ? quad_q5K(blk, ab, s) : quad_q6K(blk, ab, s);
@@ -385,7 +400,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             }
         }
         if (it_ < T) issue();
-        if (a.stamps && t == 0) sf = __builtin_amdgcn_s_memrealtime();
+        if (RSTAMPS(a) && t == 0) sf = __builtin_amdgcn_s_memrealtime();
         if (ROWS_SB * (t + 1) >= bend) {  // batch complete: replay its rows' chains, lane r <-> row r
             wave_lds_fence();
             const int nr = bR < ww.nrows - brow ? bR : ww.nrows - brow;
@@ -402,7 +417,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             wave_lds_fence();
         }
     }
-    const uint64_t st2 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    const uint64_t st2 = RSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
     if (pf_on) {  // every touch has landed (they are older than step pre0): release the register
         asm volatile("" ::"v"(pf_sink));
     }
@@ -425,7 +440,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     // ---- SWIGLU epilogue (the GLU node after the gate/up MUL_MATs): up wave and its
     // gate partner own the same rows in this workgroup; both results are staged in LDS.
     // Same arithmetic as kq_swiglu (ggml_vec_swiglu_f32: NEON body, libm tail).
-    if (a.epi && !(a.diag & 128)) {  // uniform over the grid: every wave of the workgroup reaches the barrier (diag 128: timing only)
+    if (a.epi && !(RDIAG(a) & 128)) {  // uniform over the grid: every wave of the workgroup reaches the barrier (diag 128: timing only)
         asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
         if (ww.m == 1 && ww.nrows > 0) {
             const float *gouts = (const float *)(smem + L.outs + (wave - a.epi_wave_off) * L.outs_stride);
@@ -438,16 +453,16 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
                 }
         }
     }
-    if (a.stamps) {
+    if (RSTAMPS(a)) {
         const int64_t o = ((int64_t)blockIdx.x * ROWS_WAVES + wave) * 8;  // stamp slots sized for the most waves
         if (lane == 0 && o + 7 < a.stamps_cap) {
-            a.stamps[o] = st0;
-            a.stamps[o + 1] = st1;
-            a.stamps[o + 2] = st2;
-            a.stamps[o + 3] = __builtin_amdgcn_s_memrealtime();
-            a.stamps[o + 4] = sx;
-            a.stamps[o + 5] = sq;
-            a.stamps[o + 6] = sf;
+            RSTAMPS(a)[o] = st0;
+            RSTAMPS(a)[o + 1] = st1;
+            RSTAMPS(a)[o + 2] = st2;
+            RSTAMPS(a)[o + 3] = __builtin_amdgcn_s_memrealtime();
+            RSTAMPS(a)[o + 4] = sx;
+            RSTAMPS(a)[o + 5] = sq;
+            RSTAMPS(a)[o + 6] = sf;
         }
     }
 }
@@ -455,8 +470,8 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
 template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void __launch_bounds__(ROWS_WAVES * 64) kq_rows(const RowsArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    if (a.diag & 256) return;  // diagnostics (timing only): empty launch
-    const uint64_t st0 = a.stamps ? __builtin_amdgcn_s_memrealtime() : 0;
+    if (RDIAG(a) & 256) return;  // diagnostics (timing only): empty launch
+    const uint64_t st0 = RSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const RowsLayout L = rows_layout(a.nb, TMASK, a.bR, a.rpw, __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6)));

@@ -69,6 +69,8 @@ if __name__ == "__main__":
                 env["MI355X_GEMV_WPC"] = kv[4:]
             elif kv.startswith("lib="):
                 env["MI355X_LIB"] = os.path.join(ROOT, kv[4:])
+        if mode in ("prologue", "empty", "quantonly", "dmaonly"):  # diagnostics: compile-time build only
+            env.setdefault("MI355X_LIB", os.path.join(ROOT, "ggml-neon-opt_amd/lib/variants/libdiag.so"))
         if mode == "prologue":
             env["MI355X_GEMV_DIAG"] = "1"
         elif mode == "empty":

@@ -5,6 +5,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "ggml-neon-opt_amd")]
+# stamps exist only in the diagnostic build:
+#   make -C ggml-neon-opt_amd variant NAME=diag VFLAGS="-DKQ_ROWS_DIAG=1 -DKQ_GEMV_DIAG=1"
+os.environ.setdefault("MI355X_LIB", os.path.join(ROOT, "ggml-neon-opt_amd/lib/variants/libdiag.so"))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
