@@ -413,7 +413,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
         a.y[i] = d[i].y;
     }
     {
-        static int diag = -1, pre_env = -1, pf_env = -1;
+        static int diag = -1, pre_env = -1, pf_env = -1, xm_env = -1;
         if (diag < 0) {
             const char *e = getenv("MI355X_GEMV_DIAG");
             diag = e ? atoi(e) : 0;
@@ -421,8 +421,11 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
             pre_env = e ? atoi(e) : 1;
             e = getenv("MI355X_GEMV_PF");
             pf_env = e ? atoi(e) : 0;
+            e = getenv("MI355X_GEMV_XMODE");
+            xm_env = e ? atoi(e) & 7 : 0;
         }
         a.pf = pf_env;
+        a.xmode = xm_env;
         a.diag = diag;
         // weight steps issued before the activation is quantized. One: a deeper early burst
         // delays the activation loads queued behind it. Alone, K = 2048 GEMVs ran 5-9 %

@@ -104,6 +104,7 @@ struct RowsArgs {
     int pre0;         // weight steps issued before the activation is quantized
     int pf;           // L2 prefetch on/off (ROWS_PF 4-KB touches of the stream past the ring)
     int bR;           // rows per chain batch (bR*nb % 16 == 0 unless bR >= rpw)
+    int xmode;        // fused-quantization prologue: ROWS_X_* bits
     int diag;         // diagnostics (timing only): bit3 stream weights only, 16/32 prologue, 64 no quantization, 128 no SWIGLU epilogue, 256 empty launch
     int wave_prefix[MI355X_MAX_FUSED + 1];
     int rbase[MI355X_MAX_FUSED];
@@ -128,6 +129,14 @@ struct RowsArgs {
     float *epi_y;
 };
 constexpr int ROWS_PRO_NONE = 0, ROWS_PRO_NORM = 1, ROWS_PRO_SWIGLU = 2;
+// Prologue of the fused quantization (a.xmode bits):
+//  ROWS_X_ROT   workgroup b visits the activation's superblocks from b mod nb on, so the
+//               256 workgroups do not all read the same L2 lines at the same moment;
+//  ROWS_X_BAR   a workgroup barrier between every wave's activation loads and the first
+//               weight DMA (the activation requests are queued ahead of the stream's);
+//  ROWS_X_PIPE  pass i is transformed and quantized as soon as ITS loads landed, while
+//               the later passes (and the weight steps) are still in flight.
+constexpr int ROWS_X_ROT = 1, ROWS_X_BAR = 2, ROWS_X_PIPE = 4;
 
 // One step = 16 consecutive superblocks of a wave's row stream (2304 / 2816 / 3360
 // B), fetched as 16-B granules from the 16-B boundary below them (+1 granule of

@@ -42,6 +42,10 @@
 #define RSTAMPS(a) ((uint64_t *)nullptr)
 #endif
 
+#ifndef KQ_ROWS_XMODE
+#define KQ_ROWS_XMODE 0  // fused-quantization prologue (ROWS_X_* bits); -1: a.xmode at run time
+#endif
+
 namespace kq {
 
 // Q8L quantization of whole rows (K > 8192 path): 16 superblocks per workgroup.
@@ -232,15 +236,29 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     uint64_t sx = 0, sq = 0, sf = 0;  // diagnostics: x landed, quantized, first step computed
     if (FUSEDQ) {
         const int PASS = 4 * nwv;  // superblocks per workgroup pass
+        // KQ_ROWS_XMODE >= 0: the prologue fixed at compile time (experiment builds)
+        const int xm = KQ_ROWS_XMODE >= 0 ? KQ_ROWS_XMODE : a.xmode;
         u32x4 xv[ROWS_QPASS][4] = {};
         u32x4 x2v[ROWS_QPASS][4] = {};  // norm weight / up, same elements as xv
         const int qiters = (nb + PASS - 1) / PASS;
+        // passes this wave loads (wave-uniform): pass i while slot 4*wave of it lies in the row
+        int qw = 0;
+#pragma unroll
+        for (int i = 0; i < ROWS_QPASS; ++i) qw += (i < qiters && PASS * i + 4 * wave < nb) ? 1 : 0;
+        // slot j of the passes -> superblock: rotated by the workgroup (ROWS_X_ROT) so the
+        // grid does not read the activation's lines in one order; slots past the row read
+        // superblock nb-1's place and store nothing
+        const int rot = (xm & ROWS_X_ROT) ? (int)(blockIdx.x % (unsigned)nb) : 0;
+        auto sbk = [&](int j) {
+            int b = (j < nb ? j : nb - 1) + rot;
+            return b >= nb ? b - nb : b;
+        };
         constexpr int pro = PRO;
+        constexpr int PL = PRO != ROWS_PRO_NONE ? 8 : 4;  // loads per pass
 #pragma unroll
         for (int i = 0; i < ROWS_QPASS; ++i) {
-            if (i < qiters && PASS * i + 4 * wave < nb) {  // waves past the row load nothing
-                int b = PASS * i + 4 * wave + (lane >> 4);
-                b = b < nb ? b : nb - 1;
+            if (i < qw) {  // waves past the row load nothing
+                const int b = sbk(PASS * i + 4 * wave + (lane >> 4));
                 const float *xp = a.x + (int64_t)b * QK + 16 * (lane & 15);
 #pragma unroll
                 for (int k = 0; k < 4; ++k) xv[i][k] = gload16_asm(xp + 4 * k);
@@ -258,78 +276,102 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         // compiler sees dead is reused while the load is in flight: a build with that branch
         // compiled out faulted (profiles/r02_attn_epilogue_rejected.md).
         rv = gload4_asm(res_p && ww.nrows > 0 ? res_p + ww.r0 + (lane < ww.nrows ? lane : 0) : a.x);
+        // ROWS_X_BAR: every wave's activation requests are queued before any weight DMA of
+        // the workgroup (uniform: every wave of the workgroup runs the prologue)
+        if (xm & ROWS_X_BAR) asm volatile("s_barrier" ::: "memory");
         for (int j = 0; j < pre0; ++j) issue();
         if (pf_on) {  // L2 prefetch of the stream just past the ring (younger than the pre0 steps)
             const uint8_t *p = s16 + (int64_t)D * (ROWS_SB * BSZ) + 64 * lane;
 #pragma unroll
             for (int i = 0; i < ROWS_PF; ++i) l2_touch(p + 4096 * i < last16 ? p + 4096 * i : last16, pf_sink);
-            vm_wait_kp<NI, ROWS_PF>(pre0);  // the activation loads are older than both
-        } else {
-            vm_wait_k<NI>(pre0);  // the activation loads are older than pre0 weight steps
         }
-        // the loads above are invisible to the compiler: pin their registers past the wait
-        asm volatile("" : "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[1][0]),
-                     "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]), "+v"(xv[2][0]), "+v"(xv[2][1]), "+v"(xv[2][2]),
-                     "+v"(xv[2][3]));
-        if (pro != ROWS_PRO_NONE) {
+        // vector-memory operations younger than the last pass's activation loads
+        const int tail = 1 + NI * pre0 + (pf_on ? ROWS_PF : 0);
+        // the asm loads are invisible to the compiler: pin their registers past each wait
+        auto pin = [&]() {
+            asm volatile("" : "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[1][0]),
+                         "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]), "+v"(xv[2][0]), "+v"(xv[2][1]),
+                         "+v"(xv[2][2]), "+v"(xv[2][3]));
+            if (pro != ROWS_PRO_NONE) {
 #pragma unroll
-            for (int i = 0; i < ROWS_QPASS; ++i)
+                for (int i = 0; i < ROWS_QPASS; ++i)
 #pragma unroll
-                for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(x2v[i][k]));
-        }
-        if (RDIAG(a) & 32) {  // diagnostics (timing only): skip the transform
-        } else if (pro == ROWS_PRO_SWIGLU) {  // ggml_vec_swiglu_f32: silu(gate) * up
-#pragma unroll
-            for (int i = 0; i < ROWS_QPASS; ++i)
-                if (i < qiters)
-#pragma unroll
-                    for (int k = 0; k < 4; ++k) xv[i][k] = swiglu4(xv[i][k], x2v[i][k]);
-        } else if (pro == ROWS_PRO_NORM) {  // rms_norm then MUL by the norm weight
-            double *sums = (double *)(smem + L.sums);
+                    for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(x2v[i][k]));
+            }
+        };
+        if (pro != ROWS_PRO_NORM && (xm & ROWS_X_PIPE)) {
+            // pass by pass: pass i's transform + quantization overlap the later passes' loads
 #pragma unroll
             for (int i = 0; i < ROWS_QPASS; ++i) {
-                if (i < qiters && PASS * i + 4 * wave < nb) {  // wave-uniform: this wave holds x of the pass
-                    const int b = PASS * i + 4 * wave + (lane >> 4);
-                    double sq = 0.0;
-                    if (b < nb) {
-                        float v[16];
+                if (i < qw) {
+                    vm_wait_dyn((qw - 1 - i) * PL + tail);
+                    pin();
+                    if (pro == ROWS_PRO_SWIGLU && !(RDIAG(a) & 32)) {  // ggml_vec_swiglu_f32: silu(gate) * up
 #pragma unroll
-                        for (int k = 0; k < 4; ++k) {
-                            v[4 * k] = __uint_as_float(xv[i][k].x), v[4 * k + 1] = __uint_as_float(xv[i][k].y);
-                            v[4 * k + 2] = __uint_as_float(xv[i][k].z), v[4 * k + 3] = __uint_as_float(xv[i][k].w);
-                        }
-                        sq = sumsq16(v);
+                        for (int k = 0; k < 4; ++k) xv[i][k] = swiglu4(xv[i][k], x2v[i][k]);
                     }
-                    sq = row16_sum(sq);  // DPP, every lane of the wave active
-                    if (b < nb && (lane & 15) == 0) sums[b] = sq;
+                    const int j = PASS * i + 4 * wave + (lane >> 4);
+                    if (j < nb && !(RDIAG(a) & 64)) quant16_store(xv[i], lane & 15, smem + L.act + Q8L_STRIDE * sbk(j));
                 }
             }
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            double tot = seq_sum_lanes(sums, nb, lane);  // superblocks in order
-            // workgroup-uniform (every wave sums the same LDS values): the rare rows whose
-            // float mean could depend on the order are summed in ggml's order (each wave)
-            if (rms_mean_ambiguous(div_by_count(tot, (int64_t)nb * QK), (int64_t)nb * QK))
-                tot = seq_sumsq_wave(a.x, (int64_t)nb * QK, lane);
-            const float mean = (float)div_by_count(tot, (int64_t)nb * QK);
-            const float scale = 1.0f / sqrtf(mean + a.eps);
+            if (RSTAMPS(a)) sx = sq = __builtin_amdgcn_s_memrealtime();
+        } else {
+            vm_wait_dyn(tail);  // every pass landed
+            pin();
+            if (RDIAG(a) & 32) {  // diagnostics (timing only): skip the transform
+            } else if (pro == ROWS_PRO_SWIGLU) {  // ggml_vec_swiglu_f32: silu(gate) * up
 #pragma unroll
-            for (int i = 0; i < ROWS_QPASS; ++i)
-                if (i < qiters)
+                for (int i = 0; i < ROWS_QPASS; ++i)
+                    if (i < qw)
 #pragma unroll
-                    for (int k = 0; k < 4; ++k) xv[i][k] = normmul4(xv[i][k], x2v[i][k], scale);
-        }
-        if (RSTAMPS(a)) sx = __builtin_amdgcn_s_memrealtime();
+                        for (int k = 0; k < 4; ++k) xv[i][k] = swiglu4(xv[i][k], x2v[i][k]);
+            } else if (pro == ROWS_PRO_NORM) {  // rms_norm then MUL by the norm weight
+                double *sums = (double *)(smem + L.sums);
+#pragma unroll
+                for (int i = 0; i < ROWS_QPASS; ++i) {
+                    if (i < qw) {  // wave-uniform: this wave holds x of the pass
+                        const int j = PASS * i + 4 * wave + (lane >> 4);
+                        double sq = 0.0;
+                        if (j < nb) {
+                            float v[16];
+#pragma unroll
+                            for (int k = 0; k < 4; ++k) {
+                                v[4 * k] = __uint_as_float(xv[i][k].x), v[4 * k + 1] = __uint_as_float(xv[i][k].y);
+                                v[4 * k + 2] = __uint_as_float(xv[i][k].z), v[4 * k + 3] = __uint_as_float(xv[i][k].w);
+                            }
+                            sq = sumsq16(v);
+                        }
+                        sq = row16_sum(sq);  // DPP, every lane of the wave active
+                        if (j < nb && (lane & 15) == 0) sums[sbk(j)] = sq;
+                    }
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+                double tot = seq_sum_lanes(sums, nb, lane);  // superblocks in order
+                // workgroup-uniform (every wave sums the same LDS values): the rare rows whose
+                // float mean could depend on the order are summed in ggml's order (each wave)
+                if (rms_mean_ambiguous(div_by_count(tot, (int64_t)nb * QK), (int64_t)nb * QK))
+                    tot = seq_sumsq_wave(a.x, (int64_t)nb * QK, lane);
+                const float mean = (float)div_by_count(tot, (int64_t)nb * QK);
+                const float scale = 1.0f / sqrtf(mean + a.eps);
+#pragma unroll
+                for (int i = 0; i < ROWS_QPASS; ++i)
+                    if (i < qw)
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) xv[i][k] = normmul4(xv[i][k], x2v[i][k], scale);
+            }
+            if (RSTAMPS(a)) sx = __builtin_amdgcn_s_memrealtime();
 #pragma unroll 1
-        for (int i = 0; i < qiters; ++i) {  // one copy of the quantizer; pick the pass's registers
-            u32x4 cur[4];
+            for (int i = 0; i < qw; ++i) {  // one copy of the quantizer; pick the pass's registers
+                u32x4 cur[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) cur[k] = i == 0 ? xv[0][k] : i == 1 ? xv[1][k] : xv[2][k];
-            const int b = PASS * i + 4 * wave + (lane >> 4);
-            if (b < nb && !(RDIAG(a) & 64)) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * b);  // (diag 64: timing only)
-        }
-        if (RSTAMPS(a)) {
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-            sq = __builtin_amdgcn_s_memrealtime();
+                for (int k = 0; k < 4; ++k) cur[k] = i == 0 ? xv[0][k] : i == 1 ? xv[1][k] : xv[2][k];
+                const int j = PASS * i + 4 * wave + (lane >> 4);
+                if (j < nb && !(RDIAG(a) & 64)) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * sbk(j));  // (diag 64: timing only)
+            }
+            if (RSTAMPS(a)) {
+                asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+                sq = __builtin_amdgcn_s_memrealtime();
+            }
         }
     } else {
         const int ng = nb * (Q8L_STRIDE / 16);

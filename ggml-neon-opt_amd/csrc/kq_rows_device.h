@@ -253,6 +253,24 @@ __device__ __forceinline__ void vm_wait_kp(int k) {
     else vm_wait<P>();
 }
 
+// s_waitcnt vmcnt(n) for a run-time, wave-uniform n (a scalar branch per case); above
+// the table's range it waits for the table's largest count, a stronger wait.
+__device__ __forceinline__ void vm_wait_dyn(int n) {
+#define KQ_VMW_CASE(N) \
+    case N: vm_wait<N>(); break;
+    switch (n < 0 ? 0 : n) {
+        KQ_VMW_CASE(0) KQ_VMW_CASE(1) KQ_VMW_CASE(2) KQ_VMW_CASE(3) KQ_VMW_CASE(4) KQ_VMW_CASE(5) KQ_VMW_CASE(6)
+        KQ_VMW_CASE(7) KQ_VMW_CASE(8) KQ_VMW_CASE(9) KQ_VMW_CASE(10) KQ_VMW_CASE(11) KQ_VMW_CASE(12)
+        KQ_VMW_CASE(13) KQ_VMW_CASE(14) KQ_VMW_CASE(15) KQ_VMW_CASE(16) KQ_VMW_CASE(17) KQ_VMW_CASE(18)
+        KQ_VMW_CASE(19) KQ_VMW_CASE(20) KQ_VMW_CASE(21) KQ_VMW_CASE(22) KQ_VMW_CASE(23) KQ_VMW_CASE(24)
+        KQ_VMW_CASE(25) KQ_VMW_CASE(26) KQ_VMW_CASE(27) KQ_VMW_CASE(28) KQ_VMW_CASE(29) KQ_VMW_CASE(30)
+        KQ_VMW_CASE(31) KQ_VMW_CASE(32) KQ_VMW_CASE(33) KQ_VMW_CASE(34) KQ_VMW_CASE(35) KQ_VMW_CASE(36)
+        KQ_VMW_CASE(37) KQ_VMW_CASE(38) KQ_VMW_CASE(39) KQ_VMW_CASE(40)
+        default: vm_wait<40>(); break;
+    }
+#undef KQ_VMW_CASE
+}
+
 // One L2 prefetch touch: a dword load per lane into a register reserved for it
 // (tied in/out, so every touch reuses it and nothing else is allocated there while
 // the loads are in flight); the caller consumes `sink` after its covering wait.
