@@ -248,13 +248,16 @@ def timed_kernel_stats(be, chain, tokens):
         assert rc == 0, rc
     rows = g.timing_read()
     g.timing_enable(False)
-    per = {}
+    per, kinds = {}, {}
     for name, nbytes, ms in rows:
-        d = per.setdefault(name, {"launches": 0, "bytes": 0.0, "ms": 0.0})
-        d["launches"] += 1
-        d["bytes"] += nbytes
-        d["ms"] += ms
-    return per
+        # by kernel name, and by launch kind (name + algorithmic bytes: the q/k/v and the
+        # gate/up launches of one kernel instantiation differ 4.4x in size)
+        for key, tab in ((name, per), (f"{name} @ {nbytes / 1e6:.3f} MB", kinds)):
+            d = tab.setdefault(key, {"launches": 0, "bytes": 0.0, "ms": 0.0, "kernel": name})
+            d["launches"] += 1
+            d["bytes"] += nbytes
+            d["ms"] += ms
+    return per, kinds
 
 
 def large_gemv(dev, reps=20):
@@ -437,6 +440,22 @@ def host_cpu():
     return model, os.cpu_count() or 1, aff
 
 
+def physical_cores():
+    """Physical cores among the CPUs of this process's affinity (SMT siblings once)."""
+    try:
+        cpus = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        return os.cpu_count() or 1
+    cores = set()
+    for c in cpus:
+        try:
+            with open(f"/sys/devices/system/cpu/cpu{c}/topology/thread_siblings_list") as f:
+                cores.add(f.read().strip())
+        except OSError:
+            cores.add(str(c))
+    return max(1, len(cores))
+
+
 def cpu_baseline_token(tk, seconds):
     """The oracle's restated llm_build_llama token (ggml-cpu semantics op by op: the
     matmuls through the restated ggml_compute_forward_mul_mat — quantize_row_q8_K_ref,
@@ -483,17 +502,26 @@ def cpu_baseline_token(tk, seconds):
                 break
         return tokens, el
 
-    n1, e1 = leg(1, seconds / 2)
-    nn, en = leg(threads_n, seconds / 2)
+    phys = physical_cores()
+    n1, e1 = leg(1, seconds * 0.4)
+    nn, en = leg(threads_n, seconds * 0.35)
+    legs = {"t1": {"tok_s": round(n1 / e1, 3), "tokens": n1, "seconds": round(e1, 2)},
+            f"t{threads_n}": {"tok_s": round(nn / en, 3), "tokens": nn, "seconds": round(en, 2)}}
+    if phys > threads_n:  # the affinity's physical cores, one thread each (a short leg)
+        npn, epn = leg(phys, seconds * 0.25)
+        legs[f"t{phys}"] = {"tok_s": round(npn / epn, 3), "tokens": npn, "seconds": round(epn, 2),
+                            "note": "one thread per physical core of the process's affinity (shared host)"}
     return {"value": round(nn / en, 3), "unit": "tok/s", "cores": threads_n, "kind": "port",
-            "legs": {"t1": {"tok_s": round(n1 / e1, 3), "tokens": n1, "seconds": round(e1, 2)},
-                     f"t{threads_n}": {"tok_s": round(nn / en, 3), "tokens": nn, "seconds": round(en, 2)}},
-            "host_cpu": model_name, "host_logical_cpus": ncpu, "affinity_cpus": aff,
+            "legs": legs, "host_cpu": model_name, "host_logical_cpus": ncpu, "affinity_cpus": aff,
+            "affinity_physical_cores": phys,
+            "thread_cap": f"value is the -t {threads_n} leg: min(16, affinity) threads, the GPU box's CPU share "
+                          f"per GPU; the -t {phys} leg uses every physical core of the affinity",
             "sample": f"tokens 0..n-1 from an empty KV cache of the full {tk.model} Q4_K_M decode graph through "
                       f"the oracle's restated llm_build_llama / ggml-cpu ops (mul_mat: quantize_row_q8_K_ref + "
                       f"NEON-order vec_dot with AVX2 integer parts, bit-identical to the scalar restatement, "
-                      f"persistent pool); legs -t 1 ({n1} tokens, {e1:.1f} s) and -t {threads_n} ({nn} tokens, "
-                      f"{en:.1f} s); value is the -t {threads_n} leg"}
+                      f"persistent pool); legs -t 1 ({n1} tokens, {e1:.1f} s), -t {threads_n} ({nn} tokens, "
+                      f"{en:.1f} s)" + (f", -t {phys}" if phys > threads_n else "") +
+                      f"; value is the -t {threads_n} leg"}
 
 
 def cpu_baseline(chain, seconds):
@@ -816,7 +844,7 @@ def main():
         chain.dec.reset()
         torch.cuda.synchronize()
         barrier()
-    per = timed_kernel_stats(be, chain, tokens=4)
+    per, kinds = timed_kernel_stats(be, chain, tokens=4)
     tg = tg_side(chain, args.tg, barrier) if isinstance(chain, Token) and args.tg > 0 else None
     reps = None
     if isinstance(chain, Token) and rowsplit and world > 1:
@@ -827,35 +855,41 @@ def main():
 
     result = None
     if rank == 0:
-        # roofline of the dominant GEMV kernel, from per-launch kernel timestamps
+        # roofline of the dominant GEMV LAUNCH KIND (kernel + bytes per launch, so the q/k/v
+        # and gate/up launches of one instantiation are not averaged), from per-launch
+        # kernel timestamps (hipExtLaunchKernelGGL events on the launch stream)
         roof = None
-        gemv = {k: v for k, v in per.items() if "kq_rows" in k or "kq_gemv" in k}
+        gemv = {k: v for k, v in kinds.items() if "kq_rows" in k or "kq_gemv" in k}
         if gemv:
             dom = max(gemv, key=lambda k: gemv[k]["ms"])
-            d = per[dom]
+            d = kinds[dom]
             ach = d["bytes"] / (d["ms"] * 1e-3) / 1e9
             roof = {"bound": "hbm", "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": dom,
-                    "launches": d["launches"], "bytes_per_launch": d["bytes"] / d["launches"],
-                    "us_per_launch": d["ms"] * 1e3 / d["launches"]}
-        if roof is not None and not rowsplit:
-            # HBM traffic of the same kernel from the committed rocprofv3 PMC pass of this
-            # bench command (FETCH_SIZE x2 gfx950 correction), per launch
-            pname = "r02final_token_summary.json" if isinstance(chain, Token) else "r01_chain_summary.json"
-            prof = os.path.join(ROOT, "profiles", pname)
-            if not os.path.exists(prof) and isinstance(chain, Token):
-                pname = "r01_token_summary.json"
-                prof = os.path.join(ROOT, "profiles", pname)
+                    "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None, "kernel": d["kernel"],
+                    "launch_kind": dom, "launches": d["launches"], "bytes_per_launch": d["bytes"] / d["launches"],
+                    "us_per_launch": round(d["ms"] * 1e3 / d["launches"], 3)}
+        if roof is not None and not rowsplit and isinstance(chain, Token):
+            # the same launch kind from the committed rocprofv3 passes of this bench command:
+            # graph-replayed duration (kernel trace) and HBM read (FETCH_SIZE x2, the gfx950
+            # correction), per launch; frac_rocprof = the roofline at the replayed duration
+            prof = os.path.join(ROOT, "profiles", "r03_token_summary.json")
             if os.path.exists(prof):
                 with open(prof) as f:
-                    pk = json.load(f).get("by_kernel", {}).get(roof["kernel"])
-                if pk and pk.get("hbm_read_per_launch"):
-                    roof["traffic"] = round(pk["hbm_read_per_launch"], 0)
+                    pk = json.load(f).get("by_kind", {}).get(roof["launch_kind"])
+                if pk:
+                    roof["traffic"] = round(pk["hbm_read_per_launch"], 0) if pk.get("hbm_read_per_launch") else None
                     roof["traffic_unit"] = "bytes/launch (HBM read, rocprofv3 FETCH_SIZE x2)"
-                    roof["traffic_source"] = "profiles/" + pname
-                    roof["rocprof_us_per_launch"] = round(pk["us_per_launch"], 2)
+                    roof["rocprof_source"] = "profiles/r03_token_summary.json"
+                    roof["rocprof_us_per_launch"] = round(pk["us_per_launch"], 3)
+                    ach_r = roof["bytes_per_launch"] / (pk["us_per_launch"] * 1e-6) / 1e9
+                    roof["frac_rocprof"] = round(ach_r / HBM_PEAK_GBS, 4)
         kernels = {k: {"launches": v["launches"], "us_per_launch": round(v["ms"] * 1e3 / v["launches"], 2),
                        "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1)} for k, v in per.items()}
+        launch_kinds = {k: {"launches": v["launches"], "MB_per_launch": round(v["bytes"] / v["launches"] / 1e6, 3),
+                            "us_per_launch": round(v["ms"] * 1e3 / v["launches"], 2),
+                            "GBps": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9, 1),
+                            "frac": round(v["bytes"] / (v["ms"] * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
+                        for k, v in kinds.items() if v["bytes"] > 0}
         side = None
         if isinstance(chain, Token) and not args.no_chain and world == 1:
             side = chain_side(args.model, dev, be)
@@ -909,7 +943,7 @@ def main():
             # the whole token (every launch, gap and gather included) against the HBM roofline, per GPU
             "token_hbm_frac": round(per_gpu_rate * local_bytes / 1e9 / HBM_PEAK_GBS, 4),
             "roofline": roof,
-            "kernels": kernels,
+            "kernels": kernels, "launch_kinds": launch_kinds,
             "tg128": tg,
             "gemv_large": large,
             "prefill_pp512": prefill,
