@@ -248,6 +248,10 @@ def timed_kernel_stats(be, chain, tokens):
         assert rc == 0, rc
     rows = g.timing_read()
     g.timing_enable(False)
+    if os.environ.get("BENCH_KINDS_OUT") and tokens > 0:  # launch kinds of one token, in order (profiles)
+        n = len(rows) // tokens
+        with open(os.environ["BENCH_KINDS_OUT"], "w") as f:
+            json.dump([f"{name} @ {nbytes / 1e6:.3f} MB" for name, nbytes, _ in rows[:n]], f)
     per, kinds = {}, {}
     for name, nbytes, ms in rows:
         # by kernel name, and by launch kind (name + algorithmic bytes: the q/k/v and the
@@ -440,6 +444,25 @@ def host_cpu():
     return model, os.cpu_count() or 1, aff
 
 
+def cpu_quota():
+    """CPUs this process's cgroup may use (cgroup v2 cpu.max quota / period), or None."""
+    for path in ("/sys/fs/cgroup/cpu.max",):
+        try:
+            with open(path) as f:
+                q, per = f.read().split()[:2]
+            return None if q == "max" else int(q) / int(per)
+        except (OSError, ValueError):
+            pass
+    try:  # cgroup v1
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_quota_us") as f:
+            q = int(f.read())
+        with open("/sys/fs/cgroup/cpu/cpu.cfs_period_us") as f:
+            per = int(f.read())
+        return None if q <= 0 else q / per
+    except (OSError, ValueError):
+        return None
+
+
 def physical_cores():
     """Physical cores among the CPUs of this process's affinity (SMT siblings once)."""
     try:
@@ -503,17 +526,23 @@ def cpu_baseline_token(tk, seconds):
         return tokens, el
 
     phys = physical_cores()
+    quota = cpu_quota()
     n1, e1 = leg(1, seconds * 0.4)
     nn, en = leg(threads_n, seconds * 0.35)
     legs = {"t1": {"tok_s": round(n1 / e1, 3), "tokens": n1, "seconds": round(e1, 2)},
             f"t{threads_n}": {"tok_s": round(nn / en, 3), "tokens": nn, "seconds": round(en, 2)}}
-    if phys > threads_n:  # the affinity's physical cores, one thread each (a short leg)
+    if phys > threads_n and (quota is None or quota >= phys):  # one thread per physical core (a short leg)
         npn, epn = leg(phys, seconds * 0.25)
         legs[f"t{phys}"] = {"tok_s": round(npn / epn, 3), "tokens": npn, "seconds": round(epn, 2),
-                            "note": "one thread per physical core of the process's affinity (shared host)"}
+                            "note": "one thread per physical core of the process's affinity"}
+    elif phys > threads_n:
+        # a cgroup CPU quota below the core count: that many spinning workers time-slice on
+        # the quota's CPUs (measured: 0.29 tok/s at -t 128 on a 16-CPU quota), so the leg
+        # would time the scheduler, not ggml-cpu
+        legs[f"t{phys}"] = {"skipped": f"cgroup CPU quota {quota:g} CPUs < {phys} physical cores"}
     return {"value": round(nn / en, 3), "unit": "tok/s", "cores": threads_n, "kind": "port",
             "legs": legs, "host_cpu": model_name, "host_logical_cpus": ncpu, "affinity_cpus": aff,
-            "affinity_physical_cores": phys,
+            "affinity_physical_cores": phys, "cgroup_cpu_quota": quota,
             "thread_cap": f"value is the -t {threads_n} leg: min(16, affinity) threads, the GPU box's CPU share "
                           f"per GPU; the -t {phys} leg uses every physical core of the affinity",
             "sample": f"tokens 0..n-1 from an empty KV cache of the full {tk.model} Q4_K_M decode graph through "

@@ -42,6 +42,7 @@ def main():
     ap.add_argument("--pmc-warmup", type=int, default=None, help="PMC passes: warmup tokens (default: --warmup)")
     ap.add_argument("--pmc-steps", type=int, default=None, help="PMC passes: timed tokens (default: --steps)")
     ap.add_argument("--bench-json", default=None, help="bench JSON line (for the algorithmic bytes)")
+    ap.add_argument("--kinds", default=None, help="bench BENCH_KINDS_OUT file: launch kind of every position")
     a = ap.parse_args()
     L, W, K = a.launches, a.warmup, a.steps
     PW = a.warmup if a.pmc_warmup is None else a.pmc_warmup
@@ -84,13 +85,33 @@ def main():
     for k in by_kernel.values():
         k["us_per_launch"] = k["us_per_token"] / k["launches_per_token"]
         k["hbm_read_per_launch"] = k["hbm_read_per_token"] / k["launches_per_token"]
+    by_kind = {}
+    if a.kinds:  # launch kinds (kernel @ algorithmic MB per launch), as bench.py's roofline keys them
+        with open(a.kinds) as f:
+            kinds = json.load(f)
+        assert len(kinds) == L, (len(kinds), L)
+        for e, kname in zip(per_pos, kinds):
+            assert kname.startswith(e["kernel"]), (kname, e["kernel"])
+            e["kind"] = kname
+            k = by_kind.setdefault(kname, {"launches_per_token": 0, "us_per_token": 0.0, "hbm_read_per_token": 0.0,
+                                           "MB_per_launch": float(kname.split(" @ ")[1].split()[0])})
+            k["launches_per_token"] += 1
+            k["us_per_token"] += e["us_mean"]
+            k["hbm_read_per_token"] += e.get("hbm_read_bytes", 0.0)
+        for k in by_kind.values():
+            k["us_per_launch"] = k["us_per_token"] / k["launches_per_token"]
+            k["hbm_read_per_launch"] = k["hbm_read_per_token"] / k["launches_per_token"]
+            k["GBps"] = k["MB_per_launch"] * 1e6 / (k["us_per_launch"] * 1e-6) / 1e9
+            k["frac"] = k["GBps"] / 8000.0
+            k["traffic_over_algorithmic"] = (k["hbm_read_per_launch"] / (k["MB_per_launch"] * 1e6)
+                                             if k["MB_per_launch"] > 0 and fetch else None)
     span = (int(timed[-1]["End_Timestamp"]) - int(timed[0]["Start_Timestamp"])) / 1e3 / K
     busy = sum(dur(r) for r in timed) / 1e3 / K * 1e3
     out = {"source": a.src, "warmup": W, "steps": K, "launches_per_token": L,
            "token_span_us": span, "kernel_busy_us_per_token": busy,
            "hbm_read_MB_per_token": sum(e.get("hbm_read_bytes", 0) for e in per_pos) / 1e6 if fetch else None,
            "hbm_write_MB_per_token": sum(e.get("hbm_write_bytes", 0) for e in per_pos) / 1e6 if write else None,
-           "by_kernel": by_kernel, "per_position": per_pos}
+           "by_kernel": by_kernel, "by_kind": by_kind, "per_position": per_pos}
     if a.bench_json:
         with open(a.bench_json) as f:
             out["bench"] = json.loads([ln for ln in f if ln.startswith("{")][-1])
@@ -108,6 +129,14 @@ def main():
         for name, k in sorted(by_kernel.items(), key=lambda kv: -kv[1]["us_per_token"]):
             f.write(f"| `{name}` | {k['launches_per_token']} | {k['us_per_launch']:.2f} | "
                     f"{k['hbm_read_per_launch'] / 1e6:.2f} |\n")
+        if by_kind:
+            f.write("\n| launch kind (kernel @ algorithmic MB) | launches/token | us/launch (replayed) | GB/s | "
+                    "frac of 8 TB/s | HBM read/launch (MB) | read / algorithmic |\n|---|---|---|---|---|---|---|\n")
+            for name, k in sorted(by_kind.items(), key=lambda kv: -kv[1]["us_per_token"]):
+                ratio = k["traffic_over_algorithmic"]
+                f.write(f"| `{name}` | {k['launches_per_token']} | {k['us_per_launch']:.2f} | {k['GBps']:.0f} | "
+                        f"{k['frac']:.3f} | {k['hbm_read_per_launch'] / 1e6:.2f} | "
+                        f"{'' if ratio is None else f'{ratio:.2f}'} |\n")
         f.write("\n| pos | kernel | grid | LDS | us (mean) | HBM read (MB) |\n|---|---|---|---|---|---|\n")
         for e in per_pos[:8] + per_pos[-1:]:
             f.write(f"| {e['pos']} | `{e['kernel']}` | {e['grid']} | {e['lds']} | {e['us_mean']:.2f} | "
