@@ -65,6 +65,8 @@ struct Rccl {
     ncclResult_t (*comm_init_rank)(ncclComm_t *, int, ncclUniqueId, int) = nullptr;
     ncclResult_t (*comm_destroy)(ncclComm_t) = nullptr;
     ncclResult_t (*all_gather)(const void *, void *, size_t, ncclDataType_t, ncclComm_t, hipStream_t) = nullptr;
+    ncclResult_t (*all_reduce)(const void *, void *, size_t, ncclDataType_t, ncclRedOp_t, ncclComm_t,
+                               hipStream_t) = nullptr;
     const char *(*error_string)(ncclResult_t) = nullptr;
 };
 
@@ -84,8 +86,9 @@ Rccl &rccl() {
     r.comm_init_rank = (decltype(r.comm_init_rank))dlsym(h, "ncclCommInitRank");
     r.comm_destroy = (decltype(r.comm_destroy))dlsym(h, "ncclCommDestroy");
     r.all_gather = (decltype(r.all_gather))dlsym(h, "ncclAllGather");
+    r.all_reduce = (decltype(r.all_reduce))dlsym(h, "ncclAllReduce");
     r.error_string = (decltype(r.error_string))dlsym(h, "ncclGetErrorString");
-    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.error_string;
+    r.ok = r.get_unique_id && r.comm_init_rank && r.comm_destroy && r.all_gather && r.all_reduce && r.error_string;
     return r;
 }
 
@@ -497,6 +500,17 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
             }
             return 0;
         }
+        case MI355X_OP_ALL_REDUCE: {
+            if (!b->comm && b->loop_world > 0) return 0;  // emulated rank: the caller's reduced vector stays
+            if (!b->comm || nelem(t) != nelem(t->src[0])) return MI355X_E_COMM;
+            const ncclResult_t r = rccl().all_reduce(t->src[0]->data, t->data, (size_t)nelem(t), ncclFloat32, ncclSum,
+                                                     b->comm, st);
+            if (r != ncclSuccess) {
+                fprintf(stderr, "ggml_mi355x: ncclAllReduce: %s\n", rccl().error_string(r));
+                return MI355X_E_COMM;
+            }
+            return 0;
+        }
         case MI355X_OP_ATTN_DECODE: {
             mi355x_attn_desc a;
             attn_desc_of(t, a);
@@ -862,6 +876,9 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
             // a packed f32 slice gathered into a packed f32 vector (world known at compute time)
             return contig_f32(op) && contig_f32(op->src[0]) && op->ne[1] == 1 && op->src[0]->ne[1] == 1 &&
                    op->src[0]->ne[0] > 0 && op->ne[0] % op->src[0]->ne[0] == 0;
+        case MI355X_OP_ALL_REDUCE:
+            // a packed f32 partial summed over the ranks into a packed f32 vector of the same length
+            return contig_f32(op) && contig_f32(op->src[0]) && nelem(op) == nelem(op->src[0]) && nelem(op) > 0;
         case MI355X_OP_ATTN_DECODE: {
             for (int s = 0; s < 7; ++s)
                 if (!op->src[s] || !op->src[s]->data) return 0;

@@ -22,7 +22,8 @@ QK_K = 256
 BLOCK_BYTES = {TYPE_Q4_K: 144, TYPE_Q5_K: 176, TYPE_Q6_K: 210, TYPE_Q8_K: 292}
 TYPE_NAMES = {TYPE_Q4_K: "q4_K", TYPE_Q5_K: "q5_K", TYPE_Q6_K: "q6_K", TYPE_Q8_K: "q8_K", TYPE_F32: "f32"}
 MAX_FUSED = 4
-OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROPE, OP_ATTN_DECODE, OP_ALL_GATHER = range(10)
+OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROPE, OP_ATTN_DECODE, OP_ALL_GATHER, \
+    OP_ALL_REDUCE = range(11)
 MAX_SRC = 8
 FLAG_OUTPUT = 1
 E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM = 0, -1, -2, -3, -4, -6

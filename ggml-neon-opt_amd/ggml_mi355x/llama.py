@@ -20,7 +20,8 @@ from __future__ import annotations
 
 import ctypes
 
-from . import (FLAG_OUTPUT, OP_ADD, OP_ALL_GATHER, OP_ATTN_DECODE, OP_GET_ROWS, OP_MUL, OP_MUL_MAT, OP_RMS_NORM,
+from . import (FLAG_OUTPUT, OP_ADD, OP_ALL_GATHER, OP_ALL_REDUCE, OP_ATTN_DECODE, OP_GET_ROWS, OP_MUL, OP_MUL_MAT,
+               OP_RMS_NORM,
                OP_SWIGLU, TYPE_F16, TYPE_F32, TYPE_I32, Backend, Mi355xError, f32_bits, make_tensor, rope_table)
 
 def torch_tensor(values):
@@ -72,6 +73,8 @@ class LlamaDecoder:
             nh, nkv = split.n_head, split.n_head_kv  # this rank's heads
         kvw = nkv * hd
         self.gathers = []  # (node output buffer) of every ALL_GATHER, in graph order
+        self.reduces = []  # (input partial, output) buffers of every ALL_REDUCE (split mode "reduce")
+        reduce_mode = split is not None and split.mode == "reduce"
         f32 = torch.float32
 
         def buf(n, dtype=f32):
@@ -124,6 +127,12 @@ class LlamaDecoder:
             self.gathers.append(b)
             return full, b
 
+        def allreduce(part, part_buf):
+            """ALL_REDUCE(sum) of a K-split stage's partial (reduce mode)."""
+            full, b = node(OP_ALL_REDUCE, part.ne[0], [part])
+            self.reduces.append((part_buf, b))
+            return full, b
+
         def rows_view(t_buf, lo, n):
             """The rows [lo, lo+n) of a full f32 vector (the residual of a local slice)."""
             return leaf(t_buf[lo:lo + n], TYPE_F32, n)
@@ -152,23 +161,41 @@ class LlamaDecoder:
             kc = leaf(self.k_cache[i], TYPE_F16, kvw, n_ctx)
             vc = leaf(self.v_cache[i], TYPE_F16, n_ctx, kvw)
             att, _ = node(OP_ATTN_DECODE, nh * hd, [q, k, v, pos, kc, vc, tab], [nh, nkv, hd, scale])
-            att, _ = gather(att, nh * hd)
-            o = mm(p + "attn_output", att)
-            res = x if split is None else rows_view(xb, r_e0, El)
-            ffn_inp, fb = node(OP_ADD, El, [o, res])
-            ffn_inp, fbg = gather(ffn_inp, El)
-            fb = fbg if fbg is not None else fb
+            if reduce_mode:
+                # K-split attn_output over the rank's heads; the residual rides on rank 0's
+                # partial, so the ALL_REDUCE delivers mul_mat + x
+                o = mm(p + "attn_output", att)
+                if split.rank == 0:
+                    o, ob = node(OP_ADD, E, [o, x])
+                else:
+                    ob = self._bufs[-1]
+                ffn_inp, fb = allreduce(o, ob)
+            else:
+                att, _ = gather(att, nh * hd)
+                o = mm(p + "attn_output", att)
+                res = x if split is None else rows_view(xb, r_e0, El)
+                ffn_inp, fb = node(OP_ADD, El, [o, res])
+                ffn_inp, fbg = gather(ffn_inp, El)
+                fb = fbg if fbg is not None else fb
             n2, _ = node(OP_RMS_NORM, E, [ffn_inp], eps_bits)
             m2, _ = node(OP_MUL, E, [n2, leaf(weights[p + "ffn_norm"], TYPE_F32, E)])
             gt = mm(p + "ffn_gate", m2)
             up = mm(p + "ffn_up", m2)
             glu, _ = node(OP_SWIGLU, gt.ne[0], [gt, up])
-            glu, _ = gather(glu, F // world)
-            dn = mm(p + "ffn_down", glu)
-            res = ffn_inp if split is None else rows_view(fb, r_e0, El)
-            x, xb = node(OP_ADD, El, [dn, res])
-            x, xbg = gather(x, El)
-            xb = xbg if xbg is not None else xb
+            if reduce_mode:  # the rank's ffn rows are its K slice of ffn_down
+                dn = mm(p + "ffn_down", glu)
+                if split.rank == 0:
+                    dn, db = node(OP_ADD, E, [dn, ffn_inp])
+                else:
+                    db = self._bufs[-1]
+                x, xb = allreduce(dn, db)
+            else:
+                glu, _ = gather(glu, F // world)
+                dn = mm(p + "ffn_down", glu)
+                res = ffn_inp if split is None else rows_view(fb, r_e0, El)
+                x, xb = node(OP_ADD, El, [dn, res])
+                x, xbg = gather(x, El)
+                xb = xbg if xbg is not None else xb
             self.last_hidden = xb
         n3, _ = node(OP_RMS_NORM, E, [x], eps_bits)
         m3, _ = node(OP_MUL, E, [n3, leaf(weights["output_norm"], TYPE_F32, E)])

@@ -354,11 +354,18 @@ int mi355x_attn_prompt_impl(int impl);
  *                one RCCL ncclAllGather over xGMI on the backend stream (captured in the
  *                hipGraph). Needs mi355x_backend_set_comm; the exchange step of the
  *                row split (weight rows of one matrix across the GPUs,
- *                the reference's per-thread row split README.md:125-131 across devices). */
+ *                the reference's per-thread row split README.md:125-131 across devices).
+ *   ALL_REDUCE   src0 f32 [n] (this rank's PARTIAL output of a K-split MUL_MAT: the
+ *                reference's fp32 chain over the rank's superblock range of K) -> f32 [n]
+ *                the sum over ranks, one RCCL ncclAllReduce(sum) on the backend stream
+ *                (captured in the hipGraph). The exchange step of the K-split ("Megatron")
+ *                pairing of SURVEY.md §8e: o-proj and ffn_down split along K at 256-element
+ *                superblock boundaries, 2 collectives per layer. The sum re-associates the
+ *                row's fp32 chain: within SURVEY.md §8c's fp32 bound, not bit-exact. */
 enum mi355x_op {
     MI355X_OP_NONE = 0, MI355X_OP_MUL_MAT = 1, MI355X_OP_GET_ROWS = 2, MI355X_OP_RMS_NORM = 3,
     MI355X_OP_MUL = 4, MI355X_OP_ADD = 5, MI355X_OP_SWIGLU = 6, MI355X_OP_ROPE = 7,
-    MI355X_OP_ATTN_DECODE = 8, MI355X_OP_ALL_GATHER = 9,
+    MI355X_OP_ATTN_DECODE = 8, MI355X_OP_ALL_GATHER = 9, MI355X_OP_ALL_REDUCE = 10,
 };
 #define MI355X_MAX_SRC 8
 #define MI355X_TENSOR_FLAG_OUTPUT 1  /* read by the caller after graph_compute: never elided by fusion */
@@ -473,7 +480,9 @@ int mi355x_backend_set_comm(mi355x_backend_t backend, int rank, int world,
 int mi355x_backend_comm_world(mi355x_backend_t backend);         /* 0 if no communicator */
 /* Test emulation of ONE rank of a world on a single GPU, without a communicator:
  * ALL_GATHER then copies this rank's slice to offset rank*n of its output and leaves
- * the other ranks' parts as the caller put them. world = 0 turns it off. */
+ * the other ranks' parts as the caller put them; ALL_REDUCE leaves its output as the
+ * caller put it (the reduced vector the other ranks would deliver; the rank's partial
+ * stays readable in its source node). world = 0 turns it off. */
 int mi355x_backend_set_comm_loopback(mi355x_backend_t backend, int rank, int world);
 
 /* ------------------------------------------------ GGUF model files (host) */

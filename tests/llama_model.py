@@ -9,9 +9,9 @@ from __future__ import annotations
 
 import numpy as np
 
-Q4_K, Q6_K = 12, 14
-W2 = {Q4_K: 66727.0, Q6_K: 1.865e6}
-BB = {Q4_K: 144, Q6_K: 210}
+Q4_K, Q5_K, Q6_K = 12, 13, 14
+W2 = {Q4_K: 66727.0, Q5_K: 277630.0, Q6_K: 1.865e6}
+BB = {Q4_K: 144, Q5_K: 176, Q6_K: 210}
 
 
 def use_more_bits(i, n):
@@ -27,8 +27,8 @@ def kquant(rng, type_, N, K, rms_keep=True):
     else:
         d = rng.uniform(2.0 ** -14, 2.0 ** -6, size=(N, nb))
     dh = d.astype(np.float16).view(np.uint8).reshape(N, nb, 2)
-    if type_ == Q4_K:
-        dmin = (d * 7.5) if rms_keep else rng.uniform(2.0 ** -14, 2.0 ** -6, size=(N, nb))
+    if type_ in (Q4_K, Q5_K):
+        dmin = (d * (7.5 if type_ == Q4_K else 15.5)) if rms_keep else rng.uniform(2.0 ** -14, 2.0 ** -6, size=(N, nb))
         raw[..., 0:2] = dh
         raw[..., 2:4] = dmin.astype(np.float16).view(np.uint8).reshape(N, nb, 2)
     else:
@@ -36,8 +36,10 @@ def kquant(rng, type_, N, K, rms_keep=True):
     return raw.reshape(N, nb * B)
 
 
-def build(hp, seed=0):
-    """Host weights: dict name -> (type, uint8 array) for matrices, f32 arrays for norms."""
+def build(hp, seed=0, v_type=Q4_K):
+    """Host weights: dict name -> (type, uint8 array) for matrices, f32 arrays for norms.
+    v_type: attn_v outside the use_more_bits layers (Q4_K; Q5_K in Llama-3-70B's
+    Q4_K_M mix)."""
     rng = np.random.default_rng(seed)
     E, F, V, L = hp["n_embd"], hp["n_ff"], hp["n_vocab"], hp["n_layer"]
     kvw = hp["n_head_kv"] * hp["head_dim"]
@@ -51,7 +53,8 @@ def build(hp, seed=0):
         w[p + "ffn_norm"] = rng.uniform(0.8, 1.2, E).astype(np.float32)
         w[p + "attn_q"] = (Q4_K, kquant(rng, Q4_K, E, E))
         w[p + "attn_k"] = (Q4_K, kquant(rng, Q4_K, kvw, E))
-        w[p + "attn_v"] = (Q6_K if mb else Q4_K, kquant(rng, Q6_K if mb else Q4_K, kvw, E))
+        vt = Q6_K if mb else v_type
+        w[p + "attn_v"] = (vt, kquant(rng, vt, kvw, E))
         w[p + "attn_output"] = (Q4_K, kquant(rng, Q4_K, E, E))
         w[p + "ffn_gate"] = (Q4_K, kquant(rng, Q4_K, F, E))
         w[p + "ffn_up"] = (Q4_K, kquant(rng, Q4_K, F, E))
