@@ -33,9 +33,13 @@ the oracle's restated ggml-cpu token on this host's cores, a bounded sample.
 
 Multi-GPU (--gpus N under torch.distributed.run): every rank decodes its own
 token stream with its own copy of the weights ("replicas", weak scaling); value
-is the aggregate tokens/s = N*K / max-over-ranks time. `--mode rowsplit` instead
-splits every weight matrix's rows over the ranks and all-gathers each stage's
-output with RCCL (the north_star's row-split path; see DESIGN.md for when it pays).
+is the aggregate tokens/s = N*K / max-over-ranks time. Beside it the line carries the
+north_star's row-split path for TinyLlama and Llama-3-70B in both exchange schedules
+("rowsplit": gather = every matrix by rows + one RCCL all-gather per stage; reduce =
+attn_output / ffn_down split along K + one RCCL all-reduce per K-split stage, 2 per
+layer), and "collectives_us", the per-collective cost of those exchanges on the job's
+ranks. `--mode rowsplit` / `rowsplit-reduce` make one of the splits the headline
+(strong scaling). DESIGN.md §6 has the budget of when a split pays.
 """
 from __future__ import annotations
 
@@ -209,7 +213,7 @@ class Token:
         h = HPARAMS[model]
         self.hp = hparams(m["E"], m["L"], h["n_head"], h["n_head_kv"], m["FF"], m["V"], freq_base=h["freq_base"])
         self.model = model
-        self.split = TokenSplit(self.hp, *split) if split is not None else None  # (world, rank)
+        self.split = TokenSplit(self.hp, *split) if split is not None else None  # (world, rank[, mode])
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed)
         self.stages = q4km_chain(model)
@@ -218,6 +222,10 @@ class Token:
         for stage in self.stages:
             for name, typ, K, N in stage:
                 r0, r1 = self.split.rows_of(name) if self.split is not None else (0, N)
+                base = name.split(".")[-1]
+                if self.split is not None and base in self.split.cols:  # reduce mode: the rank's K slice
+                    c0, c1 = self.split.cols[base]
+                    K = 256 * (c1 - c0)
                 w[name] = (typ, random_kquant(typ, r1 - r0, K, gen, dev, rms_keep=True))
                 self.bytes_per_token += w[name][1].numel()
         w["token_embd"] = (g.TYPE_Q4_K, random_kquant(g.TYPE_Q4_K, m["V"], m["E"], gen, dev))
@@ -234,7 +242,7 @@ class Token:
 
     def launches(self):
         n = 5 * self.hp["n_layer"] + 2
-        return n + (4 * self.hp["n_layer"] + 1 if self.split is not None else 0)
+        return n + (self.split.collectives_per_token() if self.split is not None else 0)
 
 
 def timed_kernel_stats(be, chain, tokens):
@@ -701,19 +709,24 @@ def replicas_side(model, dev, world, rank, local, barrier, steps=64, warmup=8):
     return out
 
 
-def split_model_side(model, dev, world, rank, local, barrier, steps=16, warmup=4):
-    """BASELINE config 4 on the same executor: `model`'s full decode token row-split over
-    the job's ranks (every rank its rows and heads, one RCCL ALL_GATHER node per stage,
-    DESIGN.md section 6) or, at one rank, on one GPU without communicator — the scaling
-    run's reference point. `steps` tokens from an empty KV cache, hipGraph replay, the
-    wall time of the slowest rank. Collective: every rank calls it."""
+def split_model_side(model, dev, world, rank, local, barrier, steps=16, warmup=4, mode="gather"):
+    """BASELINE config 4 on the same executor: `model`'s full decode token split over the
+    job's ranks — mode "gather" (every matrix by output rows, one RCCL ALL_GATHER node
+    per stage, bit-exact) or "reduce" (attn_output / ffn_down split along K, one RCCL
+    ALL_REDUCE per K-split stage: 2 per layer), DESIGN.md section 6 — or, at one rank,
+    on one GPU without communicator: the scaling run's reference point. `steps` tokens
+    from an empty KV cache, hipGraph replay, the wall time of the slowest rank.
+    Collective: every rank calls it."""
     be = g.Backend(local)
     if world > 1:
         err = connect(be, world, rank)
         if err is not None:
-            return {"model": model, "parallelism": f"rowsplit{world}", "error": err}
+            return {"model": model, "parallelism": f"rowsplit-{mode}{world}", "error": err}
     n_ctx = max(128, (max(steps, warmup) + 31) // 32 * 32)
-    tk = Token(model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank) if world > 1 else None)
+    try:
+        tk = Token(model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank, mode) if world > 1 else None)
+    except ValueError as e:  # a split the plan cannot express (e.g. reduce mode's superblock grid)
+        return {"model": model, "parallelism": f"rowsplit-{mode}{world}", "error": str(e)}
     for i in range(warmup):
         tk.dec.step(tk.tokens[i], i)
     be.synchronize()
@@ -733,13 +746,68 @@ def split_model_side(model, dev, world, rank, local, barrier, steps=16, warmup=4
         el = float(t.item())
     ms = el / steps * 1e3
     local_bytes = tk.bytes_per_token
-    out = {"model": model, "parallelism": f"rowsplit{world}" if world > 1 else "1 GPU", "tg_steps": steps,
+    full_bytes = sum(N * (K // 256) * g.BLOCK_BYTES[typ] for st in q4km_chain(model) for _, typ, K, N in st)
+    out = {"model": model, "parallelism": f"rowsplit-{mode}{world}" if world > 1 else "1 GPU", "tg_steps": steps,
            "tok_s": round(steps / el, 2), "ms_per_token": round(ms, 3),
-           "weights_MB_per_token": round(local_bytes * world / 1e6, 1) if world > 1 else round(local_bytes / 1e6, 1),
+           "weights_MB_per_token": round(full_bytes / 1e6, 1),
            "weights_MB_per_token_per_gpu": round(local_bytes / 1e6, 1),
            "token_hbm_frac": round(local_bytes / (ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
-           "launches_per_token": tk.launches()}
+           "launches_per_token": tk.launches(),
+           "collectives_per_token": tk.split.collectives_per_token() if tk.split is not None else 0}
     del tk, be
+    torch.cuda.empty_cache()
+    return out
+
+
+def collective_side(dev, world, rank, local, barrier, n_chain=64, reps=20):
+    """Per-collective cost on this job's ranks (the worksheet input of DESIGN.md §6):
+    chains of `n_chain` dependent ALL_REDUCE / ALL_GATHER nodes of the decode token's
+    message sizes (TinyLlama / Llama-3-70B hidden vectors: 2048 / 8192 f32), replayed from
+    one hipGraph as the token's collectives are; us per collective, slowest rank.
+    Collective: every rank calls it (at one rank: a 1-rank RCCL communicator)."""
+    from ggml_mi355x import OP_ALL_GATHER, OP_ALL_REDUCE, make_tensor
+    be = g.Backend(local)
+    err = connect(be, world, rank)
+    if err is not None:
+        return {"error": err}
+    out = {"world": world}
+    st = torch.cuda.ExternalStream(be.stream)
+    for label, op, n in (("all_reduce_8KB", OP_ALL_REDUCE, 2048), ("all_reduce_32KB", OP_ALL_REDUCE, 8192),
+                         ("all_gather_8KB", OP_ALL_GATHER, 2048), ("all_gather_32KB", OP_ALL_GATHER, 8192)):
+        if op == OP_ALL_GATHER and n % world:
+            continue
+        n_in = n if op == OP_ALL_REDUCE else n // world
+        bufs = [torch.zeros(n, device=dev) for _ in range(n_chain + 1)]
+        keep, nodes = [], []
+        prev = make_tensor(g.TYPE_F32, n_in, 1, bufs[0].data_ptr())
+        keep.append(prev)
+        for k in range(n_chain):  # node k reads node k-1's output (its first n_in floats)
+            t = make_tensor(g.TYPE_F32, n, 1, bufs[k + 1].data_ptr(), op=op, srcs=[prev])
+            keep.append(t)
+            nodes.append(t)
+            prev = make_tensor(g.TYPE_F32, n_in, 1, bufs[k + 1].data_ptr())
+            keep.append(prev)
+        rc = be.graph_compute(nodes, use_graph=True)  # capture + warm-up replay
+        if rc != 0:
+            out[label] = {"error": rc}
+            continue
+        be.synchronize()
+        barrier()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for _ in range(reps):
+            be.graph_compute(nodes, use_graph=True)
+        e1.record(st)
+        be.synchronize()
+        us = e0.elapsed_time(e1) * 1e3 / (reps * n_chain)
+        if world > 1:
+            import torch.distributed as dist
+            t = torch.tensor([us], dtype=torch.float64)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            us = float(t.item())
+        out[label] = round(us, 2)
+        barrier()
+    del be
     torch.cuda.empty_cache()
     return out
 
@@ -750,10 +818,12 @@ def main():
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--model", default="tinyllama-1.1b", choices=sorted(MODELS))
-    ap.add_argument("--mode", default=None, choices=["rowsplit", "replicas"],
-                    help="N > 1: rowsplit (default; the decode token's weight rows split over the GPUs, one "
-                         "RCCL all-gather per stage, one token stream: strong scaling) or replicas (an "
-                         "independent token stream per GPU: weak scaling)")
+    ap.add_argument("--mode", default="replicas", choices=["replicas", "rowsplit", "rowsplit-reduce"],
+                    help="the headline at N GPUs: replicas (default: an independent token stream per GPU, "
+                         "weak scaling), rowsplit (one token stream, the weight rows split over the GPUs, one "
+                         "RCCL all-gather per stage: strong scaling) or rowsplit-reduce (one stream, "
+                         "attn_output / ffn_down split along K, one RCCL all-reduce per K-split stage). At N > 1 "
+                         "the line carries both row splits of TinyLlama and Llama-3-70B beside the headline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true")
@@ -769,6 +839,7 @@ def main():
     ap.add_argument("--no-chain", action="store_true", help="token workload: skip the matmul-chain side figure")
     ap.add_argument("--no-8b", action="store_true", help="skip the Llama-3-8B side figure (configs 3 and 5)")
     ap.add_argument("--tg", type=int, default=128, help="tokens of the tg side figure (0: skip)")
+    ap.add_argument("--no-collectives", action="store_true", help="skip the per-collective RCCL timing")
     ap.add_argument("--no-70b", action="store_true",
                     help="skip the Llama-3-70B side figure (config 4: row split over the job's GPUs, 1 GPU at N = 1)")
     args = ap.parse_args()
@@ -780,8 +851,8 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    mode = args.mode or ("rowsplit" if world > 1 else "replicas")
-    if mode == "rowsplit" and args.workload != "token":
+    mode = args.mode
+    if mode != "replicas" and args.workload != "token":
         raise SystemExit("bench: the row split runs the decode token workload")
     if world > 1:
         # control plane only (barriers, the RCCL id, the max over ranks): gloo on the host;
@@ -805,7 +876,8 @@ def main():
     if args.gguf:
         from ggml_mi355x.gguf import GGUFFile
         gguf = GGUFFile(args.gguf)
-    rowsplit = mode == "rowsplit"  # (--mode rowsplit at N = 1: the same graph, gathers over a 1-rank RCCL comm)
+    rowsplit = mode != "replicas"  # (--mode rowsplit* at N = 1: the same graph, collectives over a 1-rank RCCL comm)
+    split_mode = "reduce" if mode == "rowsplit-reduce" else "gather"
     comm_error = None
     if args.workload == "token":
         be = g.Backend(local)
@@ -817,7 +889,7 @@ def main():
                 rowsplit = False
                 be = g.Backend(local)
         n_ctx = max(128, (max(args.steps, args.warmup, args.tg) + 31) // 32 * 32)
-        chain = Token(args.model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank) if rowsplit else None)
+        chain = Token(args.model, dev, 0x51A7 + rank, be, n_ctx, split=(world, rank, split_mode) if rowsplit else None)
         stream = torch.cuda.ExternalStream(be.stream)
         use_graph = not args.no_graph
         pos = [0]
@@ -878,9 +950,23 @@ def main():
     reps = None
     if isinstance(chain, Token) and rowsplit and world > 1:
         reps = replicas_side(args.model, dev, world, rank, local, barrier)
+    splits = None  # N > 1: both row-split schedules of the headline model, one token stream each
+    if isinstance(chain, Token) and world > 1:
+        splits = {m: split_model_side(args.model, dev, world, rank, local, barrier, steps=32, warmup=4, mode=m)
+                  for m in ("gather", "reduce")}
     l70 = None
     if isinstance(chain, Token) and not args.no_70b and args.model != "llama-3-70b":
-        l70 = split_model_side("llama-3-70b", dev, world, rank, local, barrier)
+        if world > 1:
+            l70 = {m: split_model_side("llama-3-70b", dev, world, rank, local, barrier, mode=m)
+                   for m in ("gather", "reduce")}
+        else:
+            l70 = split_model_side("llama-3-70b", dev, world, rank, local, barrier)
+    colls = None
+    if isinstance(chain, Token) and not args.no_collectives:
+        try:
+            colls = collective_side(dev, world, rank, local, barrier)
+        except Exception as e:  # noqa: BLE001 - a side figure; reported in the line
+            colls = {"error": f"{type(e).__name__}: {e}"}
 
     result = None
     if rank == 0:
@@ -942,7 +1028,8 @@ def main():
         if isinstance(chain, Token):
             executor = ("LlamaDecoder -> mi355x_backend_graph_compute: node fusion (norm/swiglu GEMV prologues, "
                         "residual/swiglu epilogues), kq_rows + kq_attn_decode" +
-                        (", RCCL ncclAllGather per stage (row split)" if rowsplit else "") + ", " +
+                        ((", RCCL ncclAllReduce per K-split stage (row split, reduce)" if split_mode == "reduce" else
+                          ", RCCL ncclAllGather per stage (row split)") if rowsplit else "") + ", " +
                         ("hipGraph replay" if not args.no_graph else "eager"))
         else:
             executor = f"{'kq_gemv' if args.impl == 'tasks' else 'kq_rows'}: 1 launch per stage" + \
@@ -965,7 +1052,7 @@ def main():
                        "weights_MB_per_token_per_gpu": round(local_bytes / 1e6, 1),
                        "stages_per_token": chain.launches(),
                        "executor": executor,
-                       "parallelism": (f"rowsplit{world}" if rowsplit else f"replicas x{world}"),
+                       "parallelism": (f"rowsplit-{split_mode}{world}" if rowsplit else f"replicas x{world}"),
                        "hipgraph": not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
             "effective_GBps": round(per_gpu_rate * local_bytes / 1e9, 1),
@@ -981,6 +1068,8 @@ def main():
             "llama3_8b": l3,
             "llama3_70b": l70,
             "replicas": reps,
+            "rowsplit": splits,
+            "collectives_us": colls,
             "rowsplit_error": comm_error,
             "cpu_baseline": cpu,
         }

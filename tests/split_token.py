@@ -75,7 +75,7 @@ def split_decode_token(lmodel, split, token, pos, cache, gather, n_threads=2, fu
 
 
 
-def _ksplit_gen(lmodel, split, token, pos, cache, n_threads, full_trace):
+def _ksplit_gen(lmodel, split, token, pos, cache, n_threads, full_trace, variant="neon"):
     """Reduce mode (TokenSplit(mode="reduce"), the K-split Megatron pairing) as a
     generator that yields ("reduce" | "gather", local f32 vector) at every collective and
     receives the exchanged vector: the rank's q/k/v heads and attention, its K slice of
@@ -90,27 +90,27 @@ def _ksplit_gen(lmodel, split, token, pos, cache, n_threads, full_trace):
     scale = np.float32(1.0) / np.sqrt(np.float32(hd))
     for li, L in enumerate(lmodel["layers"]):
         cur = OO.mul(OO.rms_norm(x, eps), L["attn_norm"])
-        q = KO.mul_mat(L["wq"][0], L["wq"][1], cur, n_threads)[0]
-        k = KO.mul_mat(L["wk"][0], L["wk"][1], cur, n_threads)[0]
-        v = KO.mul_mat(L["wv"][0], L["wv"][1], cur, n_threads)[0]
+        q = KO.mul_mat(L["wq"][0], L["wq"][1], cur, n_threads, variant)[0]
+        k = KO.mul_mat(L["wk"][0], L["wk"][1], cur, n_threads, variant)[0]
+        v = KO.mul_mat(L["wv"][0], L["wv"][1], cur, n_threads, variant)[0]
         q = OO.rope(q, hd, hd, pos, table)
         k = OO.rope(k, hd, hd, pos, table)
         kc, vc = cache[li]
         att = OO.attn_decode(q, k, v, kc, vc, pos, split.n_head, split.n_head_kv, hd, float(scale))
-        o = KO.mul_mat(L["wo"][0], L["wo"][1], att, n_threads)[0]
+        o = KO.mul_mat(L["wo"][0], L["wo"][1], att, n_threads, variant)[0]
         po = OO.add(o, x) if split.rank == 0 else o
         ffn_inp = yield ("reduce", po)
         cur = OO.mul(OO.rms_norm(ffn_inp, eps), L["ffn_norm"])
-        g = KO.mul_mat(L["w_gate"][0], L["w_gate"][1], cur, n_threads)[0]
-        u = KO.mul_mat(L["w_up"][0], L["w_up"][1], cur, n_threads)[0]
+        g = KO.mul_mat(L["w_gate"][0], L["w_gate"][1], cur, n_threads, variant)[0]
+        u = KO.mul_mat(L["w_up"][0], L["w_up"][1], cur, n_threads, variant)[0]
         glu = OO.swiglu(g, u)
-        dn = KO.mul_mat(L["w_down"][0], L["w_down"][1], glu, n_threads)[0]
+        dn = KO.mul_mat(L["w_down"][0], L["w_down"][1], glu, n_threads, variant)[0]
         pd = OO.add(dn, ffn_inp) if split.rank == 0 else dn
         x = yield ("reduce", pd)
         if full_trace is not None:
             full_trace.append({"att": att, "p_ffn_inp": po, "ffn_inp": ffn_inp, "glu": glu, "p_x": pd, "x": x})
     cur = OO.mul(OO.rms_norm(x, eps), lmodel["output_norm"])
-    lg = KO.mul_mat(lmodel["output"][0], lmodel["output"][1], cur, n_threads)[0]
+    lg = KO.mul_mat(lmodel["output"][0], lmodel["output"][1], cur, n_threads, variant)[0]
     return (yield ("gather", lg))
 
 
@@ -134,7 +134,7 @@ def rank_ordered_sum(parts):
     return acc
 
 
-def ksplit_reference(model, hp, world, tokens, n_ctx, n_threads=2):
+def ksplit_reference(model, hp, world, tokens, n_ctx, n_threads=2, variant="neon"):
     """Every rank of a reduce-mode split in one process, in lock step, the all-reduce a
     rank-ordered f32 sum: the restatement the per-rank GPU emulation is checked against
     bit for bit. Returns per token (logits, traces[rank] -> per layer dict)."""
@@ -145,7 +145,8 @@ def ksplit_reference(model, hp, world, tokens, n_ctx, n_threads=2):
     out = []
     for pos, tok in enumerate(tokens):
         traces = [[] for _ in range(world)]
-        gens = [_ksplit_gen(lms[r], splits[r], tok, pos, caches[r], n_threads, traces[r]) for r in range(world)]
+        gens = [_ksplit_gen(lms[r], splits[r], tok, pos, caches[r], n_threads, traces[r], variant)
+                for r in range(world)]
         reqs = [next(gen) for gen in gens]
         while True:
             kinds = {k for k, _ in reqs}
