@@ -95,6 +95,7 @@ def _run_gather_ranks(dev, hp, w, ref, world, rank):
         b.synchronize()
         for i, (buf, v) in enumerate(zip(dec.gathers, full)):
             got = buf.cpu().numpy()
+            assert np.isfinite(got).all()
             assert bits_equal(got, v), (world, rank, p, i, first_mismatch(got, v))
     torch.cuda.synchronize()
     b.close()
@@ -121,6 +122,7 @@ def _run_reduce_ranks(dev, hp, w, kref, world, rank):
             got = pb.cpu().numpy()
             assert bits_equal(got, v), (world, rank, p, i, first_mismatch(got, v))
         got = dec.gathers[0].cpu().numpy()
+        assert np.isfinite(got).all() and np.abs(got).max() > 0
         assert bits_equal(got, logits), (world, rank, p, first_mismatch(got, logits))
     torch.cuda.synchronize()
     b.close()
@@ -205,6 +207,7 @@ def test_rowsplit_reduce_world1_rccl(dev, O, w_tl, use_graph):
         dec.step(tok, p, use_graph=use_graph)
         b.synchronize()
         got = dec.logits.cpu().numpy()
+        assert np.isfinite(got).all() and np.abs(got).max() > 0
         assert bits_equal(got, logits), (p, first_mismatch(got, logits))
         for li in range(hp["n_layer"]):
             for j, k in enumerate(("ffn_inp", "x")):
@@ -239,6 +242,7 @@ def test_prompt_512_equals_tokens(dev, O, width):
     lg = dec.prompt(tokens, 0)
     b.synchronize()
     got = lg.cpu().numpy().copy()
+    assert np.isfinite(got).all() and np.abs(got).max() > 0
     kc = [c.clone() for c in dec.k_cache]
     vc = [c.clone() for c in dec.v_cache]
     dec.reset()
