@@ -840,6 +840,8 @@ def main():
     ap.add_argument("--no-8b", action="store_true", help="skip the Llama-3-8B side figure (configs 3 and 5)")
     ap.add_argument("--tg", type=int, default=128, help="tokens of the tg side figure (0: skip)")
     ap.add_argument("--no-collectives", action="store_true", help="skip the per-collective RCCL timing")
+    ap.add_argument("--no-device-warmup", action="store_true",
+                    help="skip the ~0.3 s untimed device warm-up before the warmup steps")
     ap.add_argument("--no-70b", action="store_true",
                     help="skip the Llama-3-70B side figure (config 4: row split over the job's GPUs, 1 GPU at N = 1)")
     args = ap.parse_args()
@@ -909,6 +911,19 @@ def main():
             if rc != 0:
                 raise RuntimeError(f"graph_compute failed: {rc}")
 
+    # Device warm-up first (untimed, not a step of the run): on a fresh box the first few ms
+    # of decode ran ~6 % slower than steady state (clocks leaving idle: 0.691 against
+    # 0.656 ms/token in one process, gpurun_out r03c), which --warmup 5 (~3.5 ms of tokens)
+    # does not cover. Decode 384 tokens from position 0 (cache reset after); then the W
+    # warmup steps and the K timed steps of the contract, from an empty cache. A fixed
+    # count, not a time: at N > 1 every rank must run the same collectives.
+    if isinstance(chain, Token) and not args.no_device_warmup:
+        for _ in range(12):  # 12 x 32 tokens (~0.25 s of TinyLlama decode)
+            for i in range(min(32, chain.n_ctx)):
+                chain.dec.step(chain.tokens[i], i, use_graph=use_graph)
+            be.synchronize()
+        chain.dec.reset()
+        torch.cuda.synchronize()
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize()
