@@ -27,17 +27,6 @@ __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, in
 template <int TYPE>
 __global__ void kq_mmq(const MmqArgs a);
 __global__ void kq_mmq_mixed(const MmqArgs a);
-template <int NWV, int CT>
-__global__ void kq_mmq_k4(const MmqArgs a);
-#ifndef KQ_K4_NWV
-#define KQ_K4_NWV 8  // waves of the kq_mmq_k4 instantiation (experiment builds: kq_mmq.hip)
-#endif
-#ifndef KQ_K4_CT
-#define KQ_K4_CT 2
-#endif
-#ifndef KQ_K4_DEPTH
-#define KQ_K4_DEPTH 4
-#endif
 
 namespace {
 
@@ -563,15 +552,17 @@ int launch_quantize_q8L(const float *x, int64_t x_stride_floats, void *y, int64_
 // ------------------------------------------------------------ batched MFMA path
 constexpr int64_t kMmqMinCols = 16;  // below this the NCOL GEMV streams the weights fewer times
 
-// Prefill kernel selector (mi355x_mmq_impl): -1 until first read from MI355X_MMQ_IMPL
-// (tile64 / k4: A/B runs and parity of every variant).
+// Prefill kernel selector (mi355x_mmq_impl): -1 until first read from MI355X_MMQ_IMPL.
+// Round 3 removed the streamed Q4_K kernel (kq_mmq_k4): equal to the 64 x 64 tiles
+// within the box spread at pp512, 17-40 % slower on every shape forced onto it
+// (profiles/r02_mmq_impl_ab.txt); AUTO and TILE64 now both select the 64 x 64 tiles.
 std::atomic<int> g_mmq_impl{-1};
 int mmq_impl() {
     int v = g_mmq_impl.load();
     if (v < 0) {
         const char *e = getenv("MI355X_MMQ_IMPL");
         int x = MI355X_MMQ_AUTO;
-        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : strcmp(e, "k4") == 0 ? MI355X_MMQ_K4 : x;
+        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : x;
         int expect = -1;
         g_mmq_impl.compare_exchange_strong(expect, x);
         v = g_mmq_impl.load();
@@ -604,21 +595,6 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64), 1);
     dim3 block(256);
     std::string name = std::string("kq::kq_mmq<") + std::to_string(type) + ">";
-    if (type == Q4_K) {
-        // streamed Q4_K kernel (kq_mmq.hip kq_mmq_k4<8, 2>: 256 weight rows x 64 columns per
-        // workgroup) where its grid fills most of the chip; measured ~7 % faster there and
-        // slower on half-empty grids (profiles/r02_prefill_ablation.md)
-        const int impl = mmq_impl();
-        constexpr int RT = 32 * KQ_K4_NWV, CT = 32 * KQ_K4_CT;  // weight rows / columns per workgroup
-        const int64_t g82 = ((N + RT - 1) / RT) * ((M + CT - 1) / CT) * RT * CT / (256 * 64);
-        if (impl == MI355X_MMQ_K4 || (impl == MI355X_MMQ_AUTO && g82 >= 160)) {
-            fn = (const void *)kq_mmq_k4<KQ_K4_NWV, KQ_K4_CT>;
-            lds = (size_t)KQ_K4_DEPTH * CT * Q8L_STRIDE;
-            grid = dim3((unsigned)((M + CT - 1) / CT), (unsigned)((N + RT - 1) / RT), 1);
-            block = dim3(64 * KQ_K4_NWV);
-            name = KQ_K4_NWV == 8 && KQ_K4_CT == 2 ? "kq::kq_mmq_k4<8, 2>" : "kq::kq_mmq_k4<NWV, CT>";
-        }
-    }
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
     const bool timed = timing_slot(stream, e0, e1);
@@ -636,13 +612,11 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     return e == hipSuccess ? MI355X_OK : (int)e;
 }
 
-// Whether launch_mmq would run this GEMM on the 64 x 64 tile kernel (not kq_mmq_k4).
+// Whether launch_mmq would run this GEMM on the 64 x 64 tile kernel: every GEMM since the
+// streamed kernel was removed (kept as the backend's batching test).
 bool mmq_tile64(int type, int64_t N, int64_t M) {
-    if (type != Q4_K) return true;
-    const int impl = mmq_impl();
-    constexpr int RT = 32 * KQ_K4_NWV, CT = 32 * KQ_K4_CT;
-    const int64_t g82 = ((N + RT - 1) / RT) * ((M + CT - 1) / CT) * RT * CT / (256 * 64);
-    return !(impl == MI355X_MMQ_K4 || (impl == MI355X_MMQ_AUTO && g82 >= 160));
+    (void)type, (void)N, (void)M;
+    return true;
 }
 
 // Up to 4 matrices of one type on one Q8L activation in ONE 64 x 64-tile launch (a prompt
@@ -1100,7 +1074,7 @@ int mi355x_gemv_impl(int impl) {
 }
 
 int mi355x_mmq_impl(int impl) {
-    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_K4) return MI355X_E_INVAL;
+    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE64) return MI355X_E_INVAL;
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
     return prev;

@@ -37,20 +37,6 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #endif
 // Experiment build: Q4_K with unsplit operands (one int8 MFMA per sub-block, the scale
 // applied on VALU as for Q5_K) instead of the scale split (two MFMAs per sub-block).
-// kq_mmq_k4 experiment builds: KQ_K4_DIAG 1 compute only (no loads), 2 data movement only;
-// KQ_K4_NWV waves per workgroup of the launched instantiation (32 weight rows each).
-#ifndef KQ_K4_DIAG
-#define KQ_K4_DIAG 0
-#endif
-#ifndef KQ_K4_NWV
-#define KQ_K4_NWV 8
-#endif
-#ifndef KQ_K4_CT
-#define KQ_K4_CT 2  // 32-column MFMA tiles per wave (one scale-split weight operand feeds them all)
-#endif
-#ifndef KQ_K4_DEPTH
-#define KQ_K4_DEPTH 4
-#endif
 // Q6_K chunk loop unrolled by 2 and kq_mmq held to 2 waves per SIMD: fully unrolled, the
 // compiler kept every chunk's MFMA results live (376 VGPRs, one wave per SIMD); now 146
 // and Q6_K prefill 23-29 % faster, Q5_K 4 % (profiles/r02_prefill_ablation.md).
@@ -633,194 +619,6 @@ __global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq_mixed(const MmqArg
         mmq_tile<Q4_K>(a, tx, ty);
 }
 
-// ------------------------------------------------------------ Q4_K, streamed operands
-// kq_mmq_k4<NWV, CT>: the same per-element numerics as kq_mmq<Q4_K> (sumi = 8*S8 + S1 on
-// the matrix core, the reference's two fmaf per superblock in order), with the data
-// movement rebuilt after an ablation showed kq_mmq bound by its LDS fill, not by compute
-// (profiles/r02_prefill_ablation.md): 64 x 64 tiles re-read ~0.8 GB through one
-// superblock in flight per workgroup.
-//  * a wave owns 32 weight rows x 32*CT activation columns: each lane loads its own
-//    weight row straight into registers (5 x 16 B per superblock, asm loads 2
-//    superblocks ahead, no LDS), so one scale-split operand feeds CT MFMA tiles;
-//  * the workgroup's 32*CT activation columns (Q8L blocks) stream through a 4-slot LDS
-//    ring by LDS-DMA, 3 superblocks in flight, one barrier per superblock;
-//  * summins = sum_j mn_j * bs_j exactly on one f16 MFMA 32x32x16 per tile: bs_j =
-//    64*hi + lo (lo in 0..63) so A = [lo_0..7 | hi_0..7], B = [mn_0..7 | 64*mn_0..7]; every
-//    product and partial sum is an integer below 2^24 (exact in the f32 accumulator);
-//  * tile order: the column tiles of 8 consecutive row tiles go to one XCD (speed only).
-// Constant vmcnt: every wave issues NA DMA and 5 weight loads per superblock step
-// (indices past the last superblock re-fetch it into a free slot / register set).
-__device__ __forceinline__ u32x4 ld16_asm(const uint8_t *p) {
-    u32x4 v;
-    asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
-    return v;
-}
-
-template <int NWV, int CT>
-struct K4Cfg {
-    static constexpr int COLS = 32 * CT;
-    static constexpr int SLOT = COLS * Q8L_STRIDE;         // 9728 / 19456 B
-    static constexpr int GRAN = SLOT / 16;                 // 608 / 1216 granules
-    static constexpr int AINS = (GRAN + 63) / 64;          // 10 / 19 DMA instructions
-    static constexpr int NA = (AINS + NWV - 1) / NWV;      // per wave and step
-    static constexpr int DEPTH = KQ_K4_DEPTH;
-    static_assert(DEPTH >= 4, "step b issues dma(b + 3) into slot (b + 3) % DEPTH while slot b is read");
-    static constexpr int LDS_BYTES = DEPTH * SLOT;
-};
-
-template <int NWV, int CT>
-__global__ void __launch_bounds__(NWV * 64) kq_mmq_k4(const MmqArgs a) {
-    using C = K4Cfg<NWV, CT>;
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int r = lane & 31, h = lane >> 5;
-    int tx = blockIdx.x, ty = blockIdx.y;
-    {
-        const int gx = gridDim.x, L = blockIdx.y * gx + blockIdx.x;
-        const int span = 8 * gx, grp = L / span, in = L - grp * span;
-        if (gridDim.y - 8 * grp >= 8) {
-            ty = 8 * grp + in % 8;
-            tx = in / 8;
-        }
-    }
-    const int col0 = tx * C::COLS, row0 = ty * 32 * NWV;
-    const int nb = a.nb;
-    const int n = row0 + 32 * wave + r;                    // this lane's weight row
-    const uint8_t *wrow = a.w + (int64_t)(n < a.n_rows ? n : a.n_rows - 1) * a.row_stride;
-
-    auto dma = [&](int b) {  // superblock min(b, nb-1) of the column tile into slot b % DEPTH
-        if (KQ_K4_DIAG & 1) return;  // timing only: no data movement
-        const int bb = b < nb ? b : nb - 1;
-        uint8_t *slot = smem + (b % C::DEPTH) * C::SLOT;
-#pragma unroll
-        for (int s = 0; s < C::NA; ++s) {
-            int t = wave + NWV * s;
-            t = t < C::AINS ? t : C::AINS - 1;  // pad: repeat the last instruction
-            const int g = 64 * t + lane;
-            if (g < C::GRAN) {
-                int c = g / (Q8L_STRIDE / 16);
-                const int piece = g - c * (Q8L_STRIDE / 16);
-                c = col0 + c < a.m_cols ? col0 + c : a.m_cols - 1;
-                dma16(a.xq + (int64_t)c * a.xq_col_stride + (int64_t)bb * Q8L_STRIDE + 16 * piece,
-                      (LDS void *)(slot + 1024 * t));
-            }
-        }
-    };
-    auto wload = [&](int b, u32x4 (&W)[5]) {  // header + this lane's qs half of each sub-block pair
-        if (KQ_K4_DIAG & 1) return;
-        const uint8_t *blk = wrow + (int64_t)(b < nb ? b : nb - 1) * 144;
-        W[0] = ld16_asm(blk);
-#pragma unroll
-        for (int jp = 0; jp < 4; ++jp) W[1 + jp] = ld16_asm(blk + 16 + 32 * jp + 16 * h);
-    };
-
-    f32x16 sumf[CT];
-#pragma unroll
-    for (int c = 0; c < CT; ++c)
-#pragma unroll
-        for (int i = 0; i < 16; ++i) sumf[c][i] = 0.f;
-    u32x4 W0[5], W1[5], W2[5];
-
-    auto step = [&](int b, u32x4 (&W)[5], u32x4 (&Wn)[5]) {
-        // superblock b: its slot (issued 3 steps ago) and W (2 steps ago) have landed once
-        // at most the younger step's NA DMAs + 5 loads are outstanding
-        vm_wait<C::NA + 5>();
-#pragma unroll
-        for (int k = 0; k < 5; ++k) asm volatile("" : "+v"(W[k]));
-        asm volatile("s_barrier" ::: "memory");  // every wave's part of the slot; slot b-1 free
-        dma(b + 3);
-        wload(b + 2, Wn);
-        if (KQ_K4_DIAG & 2) return;  // timing only: data movement and barriers, no compute
-        const uint8_t *slot = smem + (b % C::DEPTH) * C::SLOT;
-        const u32x4 hdr = W[0];
-        const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
-        const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
-        const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
-        const SplitScales ss = split_scales(s03, s47);
-        const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
-        i32x16 s8[CT], s1[CT];
-#pragma unroll
-        for (int c = 0; c < CT; ++c)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) s8[c][i] = s1[c][i] = 0;
-#pragma unroll
-        for (int jp = 0; jp < 4; ++jp) {
-            const u32x4 qv = W[1 + jp];
-            const u32x4 lo = qv & 0x0f0f0f0fu, hi = (qv >> 4) & 0x0f0f0f0fu;
-            const int kb = 2 * (jp & 1);  // bytes of sub-blocks 2jp, 2jp+1 in their word
-            const u16x2 lh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb));
-            const u16x2 ll = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb));
-            const u16x2 hh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb + 1));
-            const u16x2 hl = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb + 1));
-            u32x4 b8lo, b1lo, b8hi, b1hi;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                b8lo[k] = as_u32(as_u16x2(lo[k]) * lh);
-                b1lo[k] = as_u32(as_u16x2(lo[k]) * ll);
-                b8hi[k] = as_u32(as_u16x2(hi[k]) * hh);
-                b1hi[k] = as_u32(as_u16x2(hi[k]) * hl);
-            }
-#pragma unroll
-            for (int c = 0; c < CT; ++c) {
-                const uint8_t *At = slot + (32 * c + r) * Q8L_STRIDE;
-                const u32x4 alo = *(const u32x4 *)(At + 16 + 64 * jp + 16 * h);
-                const u32x4 ahi = *(const u32x4 *)(At + 48 + 64 * jp + 16 * h);
-                s8[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b8lo, s8[c], 0, 0, 0);
-                s1[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b1lo, s1[c], 0, 0, 0);
-                s8[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b8hi, s8[c], 0, 0, 0);
-                s1[c] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b1hi, s1[c], 0, 0, 0);
-            }
-        }
-        // summins: B = [mn_0..7 | 64*mn_0..7] of the lane's row (h selects the half)
-        const f16x8 bm = mins_operand(m03, m47, h);
-        const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16), nxdm = -xdm;
-#pragma unroll
-        for (int c = 0; c < CT; ++c) {
-            const uint8_t *At = slot + (32 * c + r) * Q8L_STRIDE;
-            const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
-            const f32x16 zero = {};
-            const f32x16 mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
-            const uint8_t *Ab = slot + 32 * c * Q8L_STRIDE;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
-                const float yd = *(const float *)(Ab + m * Q8L_STRIDE);
-                const int sumi = 8 * s8[c][i] + s1[c][i];
-                sumf[c][i] = fmaf(mins[i], yd * nxdm, sumf[c][i]);  // = fmaf(-mins, yd*xdm, .) exactly
-                sumf[c][i] = fmaf((float)sumi, yd * xd, sumf[c][i]);
-            }
-        }
-    };
-
-    // prologue: the steps -3, -2, -1 of the issue pattern (slot 0 | slot 1 + W(0) | slot 2 + W(1))
-    dma(0);
-    dma(1);
-    wload(0, W0);
-    dma(2);
-    wload(1, W1);
-#pragma unroll 1
-    for (int b = 0; b < nb; b += 3) {
-        step(b, W0, W2);
-        if (b + 1 < nb) step(b + 1, W1, W0);
-        if (b + 2 < nb) step(b + 2, W2, W1);
-    }
-    vm_wait<0>();  // the re-fetches past the end: no LDS-DMA may land after the workgroup exits
-
-    if (n < a.n_rows) {
-#pragma unroll
-        for (int c = 0; c < CT; ++c)
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                const int m = col0 + 32 * c + (i & 3) + 8 * (i >> 2) + 4 * h;
-                if (m < a.m_cols)
-                    a.y[(int64_t)m * a.y_col_stride + n] =
-                        a.res ? sumf[c][i] + a.res[(int64_t)m * a.res_col_stride + n] : sumf[c][i];
-            }
-    }
-}
-
-template __global__ void kq_mmq_k4<KQ_K4_NWV, KQ_K4_CT>(const MmqArgs a);
 
 template __global__ void kq_mmq<Q4_K>(const MmqArgs a);
 template __global__ void kq_mmq<Q5_K>(const MmqArgs a);

@@ -45,6 +45,19 @@
 #ifndef KQ_ROWS_XMODE
 #define KQ_ROWS_XMODE 0  // fused-quantization prologue (ROWS_X_* bits); -1: a.xmode at run time
 #endif
+// Weight steps issued before the activation wait, and the L2 prefetch touches past the
+// ring: compile-time (-1: from RowsArgs at run time, the experiment knobs
+// MI355X_GEMV_PRE0 / MI355X_GEMV_PF). Constants make every s_waitcnt that covers an
+// inline-asm activation load a constant on each path, which tools/vmem_lint.py checks.
+#ifndef KQ_ROWS_PRE0
+#define KQ_ROWS_PRE0 1
+#endif
+#ifndef KQ_ROWS_L2PF
+#define KQ_ROWS_L2PF 0
+#endif
+#ifndef KQ_ROWS_LINT_BREAK
+#define KQ_ROWS_LINT_BREAK 0  // 1: drop the activation wait (a lint self-test build, never run)
+#endif
 
 namespace kq {
 
@@ -205,7 +218,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         G > 0 ? (const uint8_t *)((uintptr_t)(src + (int64_t)G * BSZ - 1) & ~(uintptr_t)15) : s16;
 
     // L2 prefetch (uniform per wave): only streams longer than the ring, fused path
-    const bool pf_on = FUSEDQ && a.pf && T > D + 1;
+    const bool pf_on = FUSEDQ && (KQ_ROWS_L2PF < 0 ? a.pf != 0 : KQ_ROWS_L2PF != 0) && T > D + 1;
     uint32_t pf_sink = 0;
     uint8_t *islot = ring;
     int it_ = 0;  // next step to issue
@@ -231,8 +244,10 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     uint32_t rv = 0;  // residual of the fused ADD for row r0 + lane (first 64 rows)
 
     // ---- prologue: activation loads, pre0 weight steps, quantize, then the rest of the ring
-    const int pre_cap = a.pre0 < D ? a.pre0 : D;  // never more than the ring holds
-    const int pre0 = T < pre_cap ? T : pre_cap;     // 0..3
+    const int pre_req = KQ_ROWS_PRE0 < 0 ? a.pre0 : KQ_ROWS_PRE0;
+    const int pre_cap = pre_req < D ? pre_req : D;  // never more than the ring holds
+    // min(T, pre_cap) written so that the compiler sees 0 <= pre0 <= pre_cap (T >= 0)
+    const int pre0 = T >= pre_cap ? pre_cap : (T > 0 ? T : 0);
     uint64_t sx = 0, sq = 0, sf = 0;  // diagnostics: x landed, quantized, first step computed
     if (FUSEDQ) {
         const int PASS = 4 * nwv;  // superblocks per workgroup pass
@@ -279,6 +294,17 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
         // ROWS_X_BAR: every wave's activation requests are queued before any weight DMA of
         // the workgroup (uniform: every wave of the workgroup runs the prologue)
         if (xm & ROWS_X_BAR) asm volatile("s_barrier" ::: "memory");
+        // The product build (one step ahead, no prefetch touches) issues exactly one step's
+        // DMA instructions on every path: a wave without rows (T == 0) issues them from the
+        // activation (valid memory, into a ring slot it never reads), so the one constant
+        // wait below covers the activation loads on every path (tools/vmem_lint.py).
+        constexpr bool kConstPre = KQ_ROWS_PRE0 == 1 && KQ_ROWS_L2PF == 0;
+        if (kConstPre && T == 0) {
+            const uint8_t *xb = (const uint8_t *)a.x + 16 * lane;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+                if (i + 1 < NI || lane < GRAN - 64 * (NI - 1)) dma16_nt(xb, (LDS void *)(islot + 1024 * i));
+        }
         for (int j = 0; j < pre0; ++j) issue();
         if (pf_on) {  // L2 prefetch of the stream just past the ring (younger than the pre0 steps)
             const uint8_t *p = s16 + (int64_t)D * (ROWS_SB * BSZ) + 64 * lane;
@@ -316,7 +342,15 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             }
             if (RSTAMPS(a)) sx = sq = __builtin_amdgcn_s_memrealtime();
         } else {
-            vm_wait_dyn(tail);  // every pass landed
+            // every pass landed: all but the pre0 weight steps (and prefetch touches); with
+            // compile-time pre0 / prefetch a constant per path
+            if (KQ_ROWS_LINT_BREAK) {
+                // deliberately broken build (tests/test_abi.py: the ISA lint must flag it): no wait
+            } else if (kConstPre) {
+                vm_wait<NI>();  // all but the one step's DMA instructions (fewer if predicated off: a stronger wait)
+            } else {
+                vm_wait_dyn(tail);
+            }
             pin();
             if (RDIAG(a) & 32) {  // diagnostics (timing only): skip the transform
             } else if (pro == ROWS_PRO_SWIGLU) {  // ggml_vec_swiglu_f32: silu(gate) * up

@@ -376,10 +376,10 @@ def prompt_impl(request):
     g.attn_prompt_impl(prev)
 
 
-@pytest.fixture(params=[0, 2], ids=["mmq_auto", "mmq_k4"])
+@pytest.fixture(params=[0], ids=["mmq_auto"])
 def prompt_mmq(request):
-    """The prompt's GEMMs on the default choice and with every Q4_K GEMM (single or
-    several matrices in one launch) on the streamed kernel kq_mmq_k4."""
+    """The prompt's GEMMs on the default choice (the 64 x 64-tile kernel; the streamed
+    Q4_K kernel was removed in round 3)."""
     import ggml_mi355x as g
     prev = g.mmq_impl(request.param)
     yield request.param

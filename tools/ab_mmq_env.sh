@@ -7,7 +7,7 @@ mkdir -p gpurun_out
 OUT=gpurun_out/ab_mmq.log
 : > $OUT
 for round in $(seq ${ROUNDS:-2}); do
-  for E in "" "MI355X_MMQ_IMPL=k4" "MI355X_MMQ_IMPL=tile64"; do
+  for E in "" "MI355X_MMQ_IMPL=tile64"; do
     env $E timeout -k 10 300 python bench.py --steps 8 --warmup 2 --no-cpu-baseline --no-large --no-chain --no-70b --tg 0 > gpurun_out/ab_mmq_one.json 2>/dev/null || exit $?
     python - "$E" >> $OUT <<'PY' || exit $?
 import json, sys
