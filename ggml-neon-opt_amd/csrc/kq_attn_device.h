@@ -225,7 +225,7 @@ __device__ void attn_group(const AttnArgs &a, int g, uint8_t *base, int wave, in
             }
         }
         wave_lds_fence();
-        const double sum = seq_sum_lds(gsum, n_kv / 4);  // the sequential double sum, in order
+        const double sum = softmax_group_sum(gsum, n_kv / 4, lane);  // ggml's in-order sum (a tree where exact)
         const float inv = (float)(1.0 / sum);
         for (int c = lane; c < n_kv; c += 64) p16[c] = h2u(f2h_rne(w[c] * inv));
         wave_lds_fence();

@@ -206,6 +206,16 @@ __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, floa
 //  4. kqv[d] = vec_dot_f16(v_cache[g*hd+d][0..n_kv), p16): thread (d, j) runs
 //     accumulator j (8 lanes) over cells 32it+8j+l, then the f16 reduce tree.
 // A position outside the cache fails loudly: NaN output, caches untouched.
+// Timing diagnostics (MI355X_ATTN_DIAG stops) only in experiment builds
+// (make variant-ops NAME=adiag VFLAGS=-DKQ_ATTN_DIAG=1); the product kernel has none.
+#ifndef KQ_ATTN_DIAG
+#define KQ_ATTN_DIAG 0
+#endif
+#if KQ_ATTN_DIAG
+#define ADIAG(a) ((a).diag)
+#else
+#define ADIAG(a) 0
+#endif
 template <int HD>
 __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     static_assert(HD == 64 || HD == 128, "head_dim");
@@ -222,7 +232,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     const int g = h / gsz;
     const int kvw = a.n_head_kv * HD;
     const int t = threadIdx.x;
-    if (a.diag == 4) return;  // diagnostics (MI355X_ATTN_DIAG): empty launch
+    if (ADIAG(a) == 4) return;  // diagnostics (MI355X_ATTN_DIAG): empty launch
 
     // ---- 0. position-independent loads, issued with the position
     const int pos_in = *a.pos;
@@ -243,7 +253,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         x0 = a.v[(int64_t)g * HD + (t - HD / 2)];
     }
     uint4 kpre[KV4] = {};
-    if (t < a.n_ctx && a.diag != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
+    if (t < a.n_ctx && ADIAG(a) != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
         const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)t * kvw + (int64_t)g * HD);
 #pragma unroll
         for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
@@ -255,7 +265,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx + 8 * j;
 #pragma unroll
         for (int it = 0; it < VPF; ++it)
-            if (32 * it < a.n_ctx && a.diag != 5) vpre[ii][it] = *(const uint4 *)(vr + 32 * it);
+            if (32 * it < a.n_ctx && ADIAG(a) != 5) vpre[ii][it] = *(const uint4 *)(vr + 32 * it);
     }
 
     const bool bad = pos_in < 0 || pos_in >= a.n_ctx;  // no cache cell for this position
@@ -294,7 +304,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         if (writer) a.v_cache[(int64_t)(g * HD + d) * a.n_ctx + pos] = vv;
     }
     __syncthreads();
-    if (a.diag == 1 || a.diag == 5) {  // diagnostics: stop after the loads and rope
+    if (ADIAG(a) == 1 || ADIAG(a) == 5) {  // diagnostics: stop after the loads and rope
         if (t < HD) a.out[(int64_t)h * HD + t] = x0 + __uint_as_float(kpre[0].x ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
         return;
     }
@@ -316,7 +326,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         const float wmx = wave_fmax(sc);  // max (order-free): per wave, then over the 4 waves
         if ((t & 63) == 0) scal[t >> 6] = wmx;
         __syncthreads();
-        if (a.diag == 2) {  // diagnostics: stop after KQ
+        if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
             if (t < HD) a.out[(int64_t)h * HD + t] = sc + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
@@ -327,12 +337,13 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         const float g4 = s01 + dpp_mov_f32<0x4E>(s01);  // lane 4g: (e0 + e1) + (e2 + e3)
         if ((t & 3) == 0 && c < n_kv) gsum[t >> 2] = (double)g4;
         __syncthreads();
-        // every thread runs the same in-order double sum (no barrier to publish it)
-        const double sum = seq_sum_lds(gsum, n_kv / 4);
+        // every wave computes the same sum (no barrier to publish it): ggml's in-order double
+        // sum, as a tree where that is exact (softmax_group_sum)
+        const double sum = softmax_group_sum(gsum, n_kv / 4, t & 63);
         const float inv = (float)(1.0 / sum);
         if (c < n_kv) p16[c] = h2u(f2h_rne(ec * inv));
         __syncthreads();
-        if (a.diag == 3) {  // diagnostics: stop after soft_max
+        if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
             if (t < HD) a.out[(int64_t)h * HD + t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
@@ -358,7 +369,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
             w[c] = s;
         }
         __syncthreads();
-        if (a.diag == 2) {  // diagnostics: stop after KQ
+        if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
             if (t < HD) a.out[(int64_t)h * HD + t] = w[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
@@ -384,17 +395,16 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
             gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));  // the vaddvq group sum, in parallel
         }
         __syncthreads();
-        if (t == 0) {  // the sequential double sum over the groups, in order: only the
-                       // dependent f64 adds stay serial, fed by 16-B LDS reads 8 groups ahead
-            double sum = seq_sum_lds(gsum, n_kv / 4);
+        if (t < 64) {  // ggml's in-order double sum over the groups (a tree where exact)
+            double sum = softmax_group_sum(gsum, n_kv / 4, t);
             sum = 1.0 / sum;
-            scal[1] = (float)sum;
+            if (t == 0) scal[1] = (float)sum;
         }
         __syncthreads();
         const float inv = scal[1];
         for (int c = t; c < n_kv; c += 256) p16[c] = h2u(f2h_rne(w[c] * inv));
         __syncthreads();
-        if (a.diag == 3) {  // diagnostics: stop after soft_max
+        if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
             if (t < HD) a.out[(int64_t)h * HD + t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
@@ -540,7 +550,10 @@ __global__ void __launch_bounds__(256) kq_attn_prompt(const AttnArgs a) {
         gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));
     }
     __syncthreads();
-    if (t == 0) scal[1] = (float)(1.0 / seq_sum_lds(gsum, n_kv / 4));
+    if (t < 64) {  // ggml's in-order double sum (a tree where exact: softmax_group_sum)
+        const float inv = (float)(1.0 / softmax_group_sum(gsum, n_kv / 4, t));
+        if (t == 0) scal[1] = inv;
+    }
     __syncthreads();
     const float inv = scal[1];
     for (int c = t; c < n_kv; c += 256) p16[c] = h2u(f2h_rne(w[c] * inv));
@@ -660,8 +673,14 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
         gsum[hh * (nc / 4) + gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));
     }
     __syncthreads();
-    if (t < gsz)  // the in-order double sums: lane hh of wave 0 runs head hh's, all heads at once
-        scal[4 * t + 1] = (KQ_PROMPT_DIAG & 2) ? (float)gsum[t * (nc / 4)] : (float)(1.0 / seq_sum_lds(gsum + t * (nc / 4), ng));
+    if (KQ_PROMPT_DIAG & 2) {
+        if (t < gsz) scal[4 * t + 1] = (float)gsum[t * (nc / 4)];
+    } else if (t < 64 * (gsz < 4 ? gsz : 4)) {  // ggml's in-order double sums (trees where exact), a wave per head
+        for (int hh = t >> 6; hh < gsz; hh += 4) {
+            const float inv = (float)(1.0 / softmax_group_sum(gsum + hh * (nc / 4), ng, t & 63));
+            if ((t & 63) == 0) scal[4 * hh + 1] = inv;
+        }
+    }
     __syncthreads();
     for (int u = t; u < gsz * n_kv; u += 256) {
         const int hh = u / n_kv, c = u - hh * n_kv;

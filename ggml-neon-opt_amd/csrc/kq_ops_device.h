@@ -279,4 +279,33 @@ __device__ __forceinline__ double seq_sum_lds(const double *p, int n) {
     return sum;
 }
 
+// soft_max's double sum of the n vaddvq group sums g[0..n) (LDS doubles, each a float
+// (e0 + e1) + (e2 + e3) >= 0, e <= 1: every g <= 4), with the bits of ggml's in-order
+// `sum += (ggml_float)g` (ggml_vec_soft_max_f32), computed by one whole wave.
+// Every nonzero float g is a multiple of 2^(e(g) - 23) (e: its unbiased exponent), so
+// every partial sum of such terms, in ANY order, is a multiple of 2^(e_min - 23) no
+// larger than 4n: exactly representable in double while 4n < 2^(e_min + 30), i.e.
+// e_min >= floor(log2(4n)) - 29 (n_kv 128: g >= 2^-22). Then the in-order sum never
+// rounds and equals the exact sum, which a tree over the wave computes in 6 steps
+// instead of n dependent f64 adds; any smaller, subnormal or non-finite g (a very
+// peaked soft_max) takes the in-order sum itself.
+__device__ __forceinline__ double softmax_group_sum(const double *g, int n, int lane) {
+    if (n <= 0) return 0.0;
+    const int thr = (31 - __builtin_clz((unsigned)(4 * n))) - 29;
+    double part = 0.0;
+    bool ok = true;
+    for (int i = lane; i < n; i += 64) {
+        const double v = g[i];
+        const int ef = (__float_as_int((float)v) >> 23) & 0xff;  // (float)v is exact: v holds a float
+        ok = ok && (v == 0.0 || (ef != 0 && ef != 255 && ef - 127 >= thr));
+        part += v;  // exact when ok (a subset's sum)
+    }
+    if (__all(ok)) {
+#pragma unroll
+        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+        return part;
+    }
+    return seq_sum_lds(g, n);
+}
+
 }  // namespace kq

@@ -144,6 +144,35 @@ def test_attn_decode_sequence(dev, O, attn_impl, hd, nh, nkv, n_ctx, rope_row):
     assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
 
 
+@pytest.mark.parametrize("qscale", [0.05, 2.0, 40.0], ids=["flat", "normal", "peaked"])
+def test_attn_softmax_sum_tree_and_fallback(dev, O, attn_impl, qscale):
+    """soft_max's double sum runs as a wave tree where every partial sum is exact (then it
+    equals ggml's in-order sum bit for bit) and in order otherwise: flat scores (every
+    group sum ~4, the tree), N(0, 2) scores, and very peaked ones (group sums far below
+    2^-22: the in-order path). Positions up to 511 (n_kv 512, the > 256-cell path too)."""
+    import torch
+    import ggml_mi355x as g
+    hd, nh, nkv, n_ctx = 64, 8, 2, 512
+    rng = np.random.default_rng(int(qscale * 100))
+    kvw = nkv * hd
+    tab = g.rope_table(n_ctx, hd, 10000.0, 1.0, device=dev)
+    tref = O.rope_table(n_ctx, hd, 10000.0)
+    kc = torch.zeros((n_ctx, kvw), dtype=torch.int16, device=dev)
+    vc = torch.zeros((kvw, n_ctx), dtype=torch.int16, device=dev)
+    kc_ref = np.zeros((n_ctx, kvw), np.uint16)
+    vc_ref = np.zeros((kvw, n_ctx), np.uint16)
+    scale = float(np.float32(1.0) / np.sqrt(np.float32(hd)))
+    for p in list(range(0, 300)) + [383, 384, 511]:
+        q = (rng.standard_normal(nh * hd) * qscale).astype(np.float32)
+        k = rng.standard_normal(kvw).astype(np.float32)
+        v = rng.standard_normal(kvw).astype(np.float32)
+        pos = torch.tensor([p], dtype=torch.int32, device=dev)
+        got = g.attn_decode(t(q, dev), t(k, dev), t(v, dev), pos, tab, kc, vc, nh, nkv, hd, scale).cpu().numpy()
+        ref = O.attn_decode(O.rope(q, hd, hd, p, tref), O.rope(k, hd, hd, p, tref), v, kc_ref, vc_ref, p, nh, nkv,
+                            hd, scale)
+        assert bits_equal(got, ref), (p, first_mismatch(got, ref))
+
+
 def test_attn_decode_rejects_bad_position(dev, attn_impl):
     """A position outside the cache never computes silently: NaN output, caches untouched."""
     import torch

@@ -240,3 +240,36 @@ def test_fast_attention_matches_restatement(pos, n_threads):
     b = O.attn_decode(q, k, v, kc2, vc2, pos, nh, nkv, hd, 0.125, fast_threads=n_threads)
     assert (a.view(np.uint32) == b.view(np.uint32)).all()
     assert (kc == kc2).all() and (vc == vc2).all()
+
+
+def test_softmax_group_sum_exactness_argument():
+    """The argument behind softmax_group_sum (kq_ops_device.h): when every nonzero float
+    group sum g <= 4 of n terms has exponent >= floor(log2(4n)) - 29, ggml's in-order
+    double sum never rounds, so any order (the GPU's wave tree) gives the same bits;
+    below the threshold the orders can differ (hence the in-order fallback)."""
+    import math
+    rng = np.random.default_rng(7)
+    for n in (8, 32, 64, 128, 2048):
+        thr = int(math.floor(math.log2(4 * n))) - 29
+        for trial in range(200):
+            ex = rng.integers(thr, 3, size=n)
+            g = (rng.uniform(1, 2, size=n) * np.exp2(ex.astype(np.float64))).astype(np.float32)
+            g = np.minimum(g, np.float32(4.0))
+            g[rng.random(n) < 0.2] = 0
+            d = g.astype(np.float64)
+            seq = 0.0
+            for v in d:
+                seq += v
+            assert seq == math.fsum(d)  # exact: equals the exactly rounded (here: exact) sum
+            perm = rng.permutation(n)
+            tree = d[perm].copy()
+            while len(tree) > 1:
+                if len(tree) % 2:
+                    tree = np.append(tree, 0.0)
+                tree = tree[0::2] + tree[1::2]
+            assert tree[0] == seq
+    # below the threshold the orders do differ: 1 + 2^-53 + 2^-53 rounds twice in order
+    # ((1 + 2^-53) ties to 1), once as (2^-53 + 2^-53) + 1
+    d = np.array([1.0, 2.0 ** -53, 2.0 ** -53], np.float64)
+    seq = (d[0] + d[1]) + d[2]
+    assert seq != d[0] + (d[1] + d[2])
