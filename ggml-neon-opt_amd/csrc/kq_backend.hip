@@ -37,6 +37,7 @@ struct mi355x_backend {
     std::vector<Captured> graphs;
     bool fuse = true;
     ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
+    bool loop_nocopy = false;   // emulated rank, timing only (MI355X_LOOPBACK_NOCOPY)
     int rank = 0, world = 0;
     int loop_rank = -1, loop_world = 0;  // single-GPU emulation of one rank (tests)
 };
@@ -486,6 +487,7 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
         case MI355X_OP_ALL_GATHER: {
             if (!b->comm && b->loop_world > 0) {  // emulated rank: own slice into place, the rest untouched
                 if (nelem(t) != nelem(t->src[0]) * b->loop_world) return MI355X_E_COMM;
+                if (b->loop_nocopy) return 0;  // (timing of a rank's compute alone: tools/split_budget.py)
                 const size_t n = (size_t)nelem(t->src[0]) * 4;
                 const hipError_t e = hipMemcpyAsync((char *)t->data + (size_t)b->loop_rank * n, t->src[0]->data, n,
                                                     hipMemcpyDeviceToDevice, st);
@@ -967,6 +969,10 @@ int mi355x_backend_set_comm_loopback(mi355x_backend_t b, int rank, int world) {
     drop_graph(b);
     b->loop_rank = world > 0 ? rank : -1;
     b->loop_world = world;
+    // timing only: emulated ALL_GATHERs skip their own-slice copy, so a token's time is the
+    // rank's compute alone (the gathered vectors are then stale: never for parity runs)
+    const char *e = getenv("MI355X_LOOPBACK_NOCOPY");
+    b->loop_nocopy = e && atoi(e) != 0;
     return MI355X_OK;
 }
 
