@@ -446,7 +446,14 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
         return e ? atoi(e) : 0;
     }();
     if (wpc_env > 0 && wpc_env < waves_per_cu) waves_per_cu = wpc_env;
-    const int64_t cap = (int64_t)num_cus() * waves_per_cu;
+    // workgroups: one per CU; an A/B knob caps it for small launches (MI355X_GEMV_SMALL_WG)
+    static const int small_wg_env = [] {
+        const char *e = getenv("MI355X_GEMV_SMALL_WG");
+        return e ? atoi(e) : 0;
+    }();
+    int64_t n_wg = num_cus();
+    if (small_wg_env > 0 && bytes_total * nb < small_bytes && small_wg_env < n_wg) n_wg = small_wg_env;
+    const int64_t cap = n_wg * waves_per_cu;
     int64_t wv[MI355X_MAX_FUSED] = {0, 0, 0, 0};
     int64_t waves = 0;
     for (int i = 0; i < n_desc; ++i) {
@@ -494,7 +501,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     const RowsLayout L = rows_layout((int)nb, tmask, a.bR, a.rpw, pl.nwv);
     if ((size_t)L.total > kMaxLds) return MI355X_E_UNSUPPORTED;
     pl.lds = (size_t)L.total;
-    const int64_t grid = waves < num_cus() ? waves : num_cus();
+    const int64_t grid = waves < n_wg ? waves : n_wg;
     pl.grid = dim3((unsigned)(grid > 0 ? grid : 1), 1, 1);
     return MI355X_OK;
 }

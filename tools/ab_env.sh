@@ -8,7 +8,7 @@ OUT=gpurun_out/ab_env.log
 : > $OUT
 for round in $(seq ${ROUNDS:-2}); do
   for E in "$@"; do
-    env $E timeout -k 10 200 python bench.py --steps 64 --warmup 8 --no-cpu-baseline --no-large --no-prefill --no-8b --no-70b --no-chain --tg 0 ${BENCH_ARGS:-} > gpurun_out/ab_one.json 2>/dev/null || exit $?
+    env $E timeout -k 10 200 python bench.py --steps 64 --warmup 8 --no-cpu-baseline --no-large --no-prefill --no-8b --no-70b --no-chain --no-collectives --tg 0 ${BENCH_ARGS:-} > gpurun_out/ab_one.json 2>/dev/null || exit $?
     python - "$E" >> $OUT <<'PY' || exit $?
 import json, sys
 d = json.loads(open("gpurun_out/ab_one.json").read().strip().splitlines()[-1])
