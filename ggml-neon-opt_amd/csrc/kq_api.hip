@@ -24,8 +24,9 @@ template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void kq_rows(const RowsArgs a);
 template <bool AM>
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
-template <int TYPE>
+template <int TYPE, int RT>
 __global__ void kq_mmq(const MmqArgs a);
+template <int RT>
 __global__ void kq_mmq_mixed(const MmqArgs a);
 
 namespace {
@@ -569,12 +570,35 @@ int mmq_impl() {
     if (v < 0) {
         const char *e = getenv("MI355X_MMQ_IMPL");
         int x = MI355X_MMQ_AUTO;
-        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : x;
+        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : strcmp(e, "tile128") == 0 ? MI355X_MMQ_TILE128 : x;
         int expect = -1;
         g_mmq_impl.compare_exchange_strong(expect, x);
         v = g_mmq_impl.load();
     }
     return v;
+}
+
+// Weight rows per prefill workgroup (kq_mmq's RT): 64 (4 waves) or 128 (8 waves, the
+// activation tile fetched once per 128 rows).
+int mmq_rows() {
+    const int impl = mmq_impl();
+    return impl == MI355X_MMQ_TILE128 ? 128 : 64;
+}
+const void *mmq_fn(int type, bool mixed, int rt) {
+    if (rt == 128)
+        return mixed          ? (const void *)kq_mmq_mixed<128>
+             : type == Q5_K ? (const void *)kq_mmq<Q5_K, 128>
+             : type == Q6_K ? (const void *)kq_mmq<Q6_K, 128>
+                            : (const void *)kq_mmq<Q4_K, 128>;
+    return mixed          ? (const void *)kq_mmq_mixed<64>
+         : type == Q5_K ? (const void *)kq_mmq<Q5_K, 64>
+         : type == Q6_K ? (const void *)kq_mmq<Q6_K, 64>
+                        : (const void *)kq_mmq<Q4_K, 64>;
+}
+// two superblock buffers: 64 Q8L columns + rt weight rows (Q6_K: 224-B granule span), +16 B
+// for the Q6_K realign reads past the last row
+size_t mmq_lds(int type, int rt) {
+    return 2 * (size_t)(64 * Q8L_STRIDE + rt * (type == Q6_K ? 224 : block_bytes(type))) + 16 + MMQ_PF_LDS;
 }
 
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
@@ -593,14 +617,11 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     a.m_cols = (int)M;
     a.y = y;
     a.y_col_stride = y_col_stride;
-    const void *fn = type == Q5_K ? (const void *)kq_mmq<Q5_K>
-                   : type == Q6_K ? (const void *)kq_mmq<Q6_K>
-                                  : (const void *)kq_mmq<Q4_K>;
-    // two superblock buffers: 64 Q8L columns + 64 weight rows (Q6_K: 224-B granule span), +16 B
-    // for the Q6_K realign reads past the last row
-    size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (type == Q6_K ? 224 : block_bytes(type))) + 16 + MMQ_PF_LDS;
-    dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + 63) / 64), 1);
-    dim3 block(256);
+    const int rt = mmq_rows();
+    const void *fn = mmq_fn(type, false, rt);
+    const size_t lds = mmq_lds(type, rt);
+    dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + rt - 1) / rt), 1);
+    dim3 block((unsigned)(4 * rt));
     std::string name = std::string("kq::kq_mmq<") + std::to_string(type) + ">";
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
@@ -639,6 +660,7 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     if (mixed)
         for (int d = 0; d < n_mat; ++d)
             if (types[d] != Q4_K && types[d] != Q6_K) return MI355X_E_INVAL;
+    const int rt = mmq_rows();
     MmqArgs a;
     memset(&a, 0, sizeof(a));
     a.n_mat = n_mat;
@@ -656,7 +678,7 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
         a.my[d] = y[d];
         a.my_col_stride[d] = y_col_stride[d];
         a.mtype[d] = types[d];
-        tiles += (int)((N[d] + 63) / 64);
+        tiles += (int)((N[d] + rt - 1) / rt);
         wbytes += (double)N[d] * a.nb * block_bytes(types[d]);
         ybytes += (double)M * N[d] * 4.0;
     }
@@ -675,23 +697,19 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     a.n_rows = a.mn_rows[0];
     a.y = a.my[0];
     a.y_col_stride = a.my_col_stride[0];
-    const void *fn = mixed          ? (const void *)kq_mmq_mixed
-                   : type == Q5_K ? (const void *)kq_mmq<Q5_K>
-                   : type == Q6_K ? (const void *)kq_mmq<Q6_K>
-                                  : (const void *)kq_mmq<Q4_K>;
-    const int ltype = mixed ? Q6_K : type;  // the larger LDS tile
-    const size_t lds = 2 * (size_t)(64 * Q8L_STRIDE + 64 * (ltype == Q6_K ? 224 : block_bytes(ltype))) + 16 + MMQ_PF_LDS;
+    const void *fn = mmq_fn(type, mixed, rt);
+    const size_t lds = mmq_lds(mixed ? Q6_K : type, rt);  // mixed: the larger (Q6_K) tile
     const dim3 grid((unsigned)((M + 63) / 64), (unsigned)tiles, 1);
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
     void *args[] = {&a};
     hipError_t e;
     if (timing_slot(stream, e0, e1)) {
-        e = hipExtLaunchKernel(fn, grid, dim3(256), args, lds, stream, e0, e1, 0);
+        e = hipExtLaunchKernel(fn, grid, dim3((unsigned)(4 * rt)), args, lds, stream, e0, e1, 0);
         timing_log(mixed ? std::string("kq::kq_mmq_mixed") : std::string("kq::kq_mmq<") + std::to_string(type) + ">", wbytes + (double)M * a.nb * Q8L_STRIDE + ybytes,
                    e0, e1);
     } else {
-        e = hipLaunchKernel(fn, grid, dim3(256), args, lds, stream);
+        e = hipLaunchKernel(fn, grid, dim3((unsigned)(4 * rt)), args, lds, stream);
     }
     if (e != hipSuccess) return (int)e;
     e = hipGetLastError();
@@ -1081,7 +1099,7 @@ int mi355x_gemv_impl(int impl) {
 }
 
 int mi355x_mmq_impl(int impl) {
-    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE64) return MI355X_E_INVAL;
+    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE128) return MI355X_E_INVAL;
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
     return prev;

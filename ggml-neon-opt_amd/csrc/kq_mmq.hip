@@ -60,6 +60,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #ifndef KQ_MMQ_Q4_VALU
 #define KQ_MMQ_Q4_VALU 0
 #endif
+#ifndef KQ_MMQ_Q5_VALU
+#define KQ_MMQ_Q5_VALU 0  // experiment build: Q5_K sub-block scales on VALU (the round-2 kernel)
+#endif
 
 namespace kq {
 
@@ -79,17 +82,21 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) {
     return r;
 }
 
-constexpr int MMQ_TILE = 64;                 // columns x rows per workgroup
+constexpr int MMQ_TILE = 64;                 // activation columns per workgroup
 constexpr int MMQ_A_BYTES = MMQ_TILE * Q8L_STRIDE;  // 19456 B per superblock
 constexpr int MMQ_A_INSTR = MMQ_A_BYTES / 1024;     // 19 DMA instructions (exact)
+// Weight rows per workgroup: RT = 64 (4 waves, 2 x 2 of 32 x 32) or 128 (8 waves, 2 x 4):
+// the activation tile is fetched once per RT rows, so RT = 128 halves its LDS-DMA traffic.
 
 // Weight bytes per row in the LDS tile: the superblock itself (Q4_K 144, Q5_K 176,
 // 16-B aligned rows), or for Q6_K (210 B, any alignment) the 14 granules from the
 // 16-B boundary below it.
 __host__ __device__ constexpr int mmq_row_bytes(int type) { return type == Q6_K ? 224 : block_bytes(type); }
-__host__ __device__ constexpr int mmq_b_instr(int type) { return MMQ_TILE * mmq_row_bytes(type) / 1024; }  // 9 / 11 / 14
-__host__ __device__ constexpr int mmq_nw(int type) { return (MMQ_A_INSTR + mmq_b_instr(type) + 3) / 4; }
-__host__ __device__ constexpr int mmq_buf(int type) { return MMQ_A_BYTES + MMQ_TILE * mmq_row_bytes(type); }
+__host__ __device__ constexpr int mmq_b_instr(int type, int rt) { return rt * mmq_row_bytes(type) / 1024; }  // 9 / 11 / 14 per 64 rows
+__host__ __device__ constexpr int mmq_nw(int type, int rt) {  // DMA instructions per wave (rt / 16 waves)
+    return (MMQ_A_INSTR + mmq_b_instr(type, rt) + rt / 16 - 1) / (rt / 16);
+}
+__host__ __device__ constexpr int mmq_buf(int type, int rt) { return MMQ_A_BYTES + rt * mmq_row_bytes(type); }
 
 // (KQ_MMQ_Q6_VALU experiment build) Q6_K superblock of one 32x32 tile: 8 chunks of 32 elements; a lane's 16 values
 // of a chunk are one 16-element scale group, so two MFMAs per chunk (the other
@@ -242,6 +249,17 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
     }
 }
 
+// Balanced int8 bytes of four unsigned quants x (bytes 0..31) times a 6-bit scale:
+// T = q*sc + 128 per 16-bit lane (q*sc <= 1953, no carry out of the lane), hi = T >> 8,
+// lo = (T & 255) - 128, so q*sc = 256*hi + lo with hi in [0, 8], lo in [-128, 127].
+__device__ __forceinline__ void balanced_bytes(uint32_t x, u16x2 scp, uint32_t &hi, uint32_t &lo) {
+    const u16x2 c128 = {128, 128};
+    const uint32_t t0 = as_u32(as_u16x2(__builtin_amdgcn_perm(0u, x, 0x0c010c00u)) * scp + c128);  // values 0, 1
+    const uint32_t t1 = as_u32(as_u16x2(__builtin_amdgcn_perm(0u, x, 0x0c030c02u)) * scp + c128);  // values 2, 3
+    lo = __builtin_amdgcn_perm(t1, t0, 0x06040200u) ^ 0x80808080u;
+    hi = __builtin_amdgcn_perm(t1, t0, 0x07050301u);
+}
+
 // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (speed only,
 // MI355X_MICROARCH.md), so the column tiles of one row tile go to blocks L, L + 8,
 // L + 16, ... (one XCD): the weight tile is fetched into that XCD's L2 once and
@@ -276,19 +294,21 @@ __device__ __forceinline__ int mmq_tile_of(const MmqArgs &a0, MmqArgs &a, int &t
     return d;
 }
 
-// One 64 x 64 output tile (4 waves of 32 x 32) over the whole K.
-template <int TYPE>
+// One 64-column x RT-row output tile (RT / 16 waves of 32 x 32) over the whole K.
+template <int TYPE, int RT>
 __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     constexpr int BSZ = block_bytes(TYPE);
-    constexpr int NB_I = mmq_b_instr(TYPE);
-    constexpr int NW = mmq_nw(TYPE);
-    constexpr int BUF = mmq_buf(TYPE);
+    constexpr int NWV = RT / 16;  // waves
+    constexpr int NB_I = mmq_b_instr(TYPE, RT);
+    constexpr int NW = mmq_nw(TYPE, RT);
+    constexpr int BUF = mmq_buf(TYPE, RT);
+    static_assert(RT == 64 || (RT == 128 && !KQ_MMQ_PF), "the L2 warm-up assumes 4 waves");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 1, wn = wave >> 1;
     const int r = lane & 31, h = lane >> 5;
-    const int col0 = tx * MMQ_TILE, row0 = ty * MMQ_TILE;
+    const int col0 = tx * MMQ_TILE, row0 = ty * RT;
     const int nb = a.nb;
 
     // ---- DMA plan: the superblock's 19 activation + NB_I weight instructions, NW per wave
@@ -296,7 +316,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         uint8_t *buf = smem + (b & 1) * BUF;
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
-            int t = wave + 4 * s;
+            int t = wave + NWV * s;
             if (t >= MMQ_A_INSTR + NB_I) t = MMQ_A_INSTR + NB_I - 1;  // pad: repeat the last one
             const int g = 64 * (t < MMQ_A_INSTR ? t : t - MMQ_A_INSTR) + lane;  // granule in its tile
             const uint8_t *src;
@@ -520,8 +540,30 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b1lo, s1, 0, 0, 0);
                 s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b8hi, s8, 0, 0, 0);
                 s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b1hi, s1, 0, 0, 0);
-            } else {  // Q5_K: 5-bit quants x 6-bit scale do not split into int8 halves
-                      // (and Q4_K in the KQ_MMQ_Q4_VALU experiment build)
+            } else if (TYPE == Q5_K && !KQ_MMQ_Q5_VALU) {
+                // Q5_K: q (5 bits) x sc (6 bits) <= 1953 does not split into int8 halves, so the
+                // scaled weight W = sc*q rides in two balanced int8 bytes as for Q6_K: one packed
+                // 16-bit multiply-add per two values gives T = W + 128, whose high byte is
+                // hi in [0, 8] and whose low byte xor 0x80 is lo in [-128, 127], W = 256*hi + lo.
+                // Both sums accumulate over the superblock in the matrix core (exact int32,
+                // |256*S_hi| < 2^27): sumi = 256*S_hi + S_lo, no per-sub-block VALU scaling and
+                // no MFMA result consumed right after its issue.
+                const u16x2 scl = {(uint16_t)sc_lo, (uint16_t)sc_lo}, sch = {(uint16_t)sc_hi, (uint16_t)sc_hi};
+                u32x4 bhl, bll, bhh, blh;  // hi / lo bytes of the lo-nibble and hi-nibble sub-blocks
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t th, tl;
+                    balanced_bytes(lo[k], scl, th, tl);
+                    bhl[k] = th, bll[k] = tl;
+                    balanced_bytes(hi[k], sch, th, tl);
+                    bhh[k] = th, blh[k] = tl;
+                }
+                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&bhl, s8, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&bll, s1, 0, 0, 0);
+                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&bhh, s8, 0, 0, 0);
+                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&blh, s1, 0, 0, 0);
+            } else {  // Q5_K in the KQ_MMQ_Q5_VALU experiment build (and Q4_K in KQ_MMQ_Q4_VALU):
+                      // per-sub-block dots scaled on VALU
                 const i32x16 zero = {};
                 i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, zero, 0, 0, 0);
 #pragma unroll
@@ -534,6 +576,10 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         if (TYPE == Q4_K && !KQ_MMQ_Q4_VALU) {
 #pragma unroll
             for (int i = 0; i < 16; ++i) sumi[i] = 8 * s8[i] + s1[i];
+        }
+        if (TYPE == Q5_K && !KQ_MMQ_Q5_VALU) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) sumi[i] = 256 * s8[i] + s1[i];
         }
         // summins = sum_j mn_j * bs_j exactly on one f16 MFMA 32x32x16 (bs_j = bsums[2j] +
         // bsums[2j+1] = 64*hi + lo, lo in 0..63): A = [lo_0..7 | hi_0..7] of the lane's
@@ -599,29 +645,35 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     }
 }
 
-template <int TYPE>
-__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) {
+template <int TYPE, int RT>
+__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     mmq_tile_of(a0, a, tx, ty);
-    mmq_tile<TYPE>(a, tx, ty);
+    mmq_tile<TYPE, RT>(a, tx, ty);
 }
 
 // Q4_K and Q6_K matrices on one activation in one launch (a prompt batch's q/k with a
 // Q6_K attn_v): each row tile runs its matrix's kernel body (a0.mtype), LDS sized for Q6_K.
-__global__ void __launch_bounds__(256) KQ_MMQ_WPE_ATTR kq_mmq_mixed(const MmqArgs a0) {
+template <int RT>
+__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq_mixed(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     const int d = mmq_tile_of(a0, a, tx, ty);
     if (a0.mtype[d] == Q6_K)
-        mmq_tile<Q6_K>(a, tx, ty);
+        mmq_tile<Q6_K, RT>(a, tx, ty);
     else
-        mmq_tile<Q4_K>(a, tx, ty);
+        mmq_tile<Q4_K, RT>(a, tx, ty);
 }
 
 
-template __global__ void kq_mmq<Q4_K>(const MmqArgs a);
-template __global__ void kq_mmq<Q5_K>(const MmqArgs a);
-template __global__ void kq_mmq<Q6_K>(const MmqArgs a);
+template __global__ void kq_mmq<Q4_K, 64>(const MmqArgs a);
+template __global__ void kq_mmq<Q5_K, 64>(const MmqArgs a);
+template __global__ void kq_mmq<Q6_K, 64>(const MmqArgs a);
+template __global__ void kq_mmq_mixed<64>(const MmqArgs a);
+template __global__ void kq_mmq<Q4_K, 128>(const MmqArgs a);
+template __global__ void kq_mmq<Q5_K, 128>(const MmqArgs a);
+template __global__ void kq_mmq<Q6_K, 128>(const MmqArgs a);
+template __global__ void kq_mmq_mixed<128>(const MmqArgs a);
 
 }  // namespace kq

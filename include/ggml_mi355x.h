@@ -237,11 +237,14 @@ int mi355x_diag_stamps(void *buf, size_t bytes);
 #define MI355X_GEMV_TASKS 1
 #define MI355X_GEMV_ROWS 2
 int mi355x_gemv_impl(int impl);
-/* Prefill (ne11 >= 16) GEMM selector: MI355X_MMQ_AUTO or MI355X_MMQ_TILE64, both the
- * 64 x 64-tile int8-MFMA kernel for every type (round 3 removed the streamed Q4_K kernel,
- * equal within the box spread at pp512). Returns the previous value, or MI355X_E_INVAL. */
+/* Prefill (ne11 >= 16) GEMM selector for the int8-MFMA tile kernel: MI355X_MMQ_TILE64
+ * (64 weight rows x 64 activation columns per workgroup), MI355X_MMQ_TILE128 (128 rows x
+ * 64 columns, 8 waves: the activation tile fetched once per 128 rows) or MI355X_MMQ_AUTO
+ * (the library's choice by shape). Same numerics in all. Returns the previous value, or
+ * MI355X_E_INVAL. */
 #define MI355X_MMQ_AUTO 0
 #define MI355X_MMQ_TILE64 1
+#define MI355X_MMQ_TILE128 2
 int mi355x_mmq_impl(int impl);
 /* Decode GEMV (kq_rows) waves per workgroup (A/B runs, parity of both launch shapes):
  * 0 = by launch size (6 waves under 10 MB of weights, else 12; env MI355X_GEMV_SMALL_MB

@@ -405,9 +405,9 @@ def prompt_impl(request):
     g.attn_prompt_impl(prev)
 
 
-@pytest.fixture(params=[0], ids=["mmq_auto"])
+@pytest.fixture(params=[0, 2], ids=["mmq_auto", "mmq_tile128"])
 def prompt_mmq(request):
-    """The prompt's GEMMs on the default choice (the 64 x 64-tile kernel; the streamed
+    """The prompt's GEMMs on the default choice and on the 128-row tiles (the streamed
     Q4_K kernel was removed in round 3)."""
     import ggml_mi355x as g
     prev = g.mmq_impl(request.param)

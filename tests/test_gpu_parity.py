@@ -291,9 +291,9 @@ def test_fused_ragged_partition(dev, oracle, npo, impl):
 
 
 # ---------------------------------------------------------------- batched (prefill) MFMA path
-@pytest.fixture(params=[0, 1], ids=["auto", "tile64"])
+@pytest.fixture(params=[0, 1, 2], ids=["auto", "tile64", "tile128"])
 def mmq(request):
-    """Runs a prefill test on every GEMM variant (Q5_K / Q6_K: the 64 x 64 kernel in all)."""
+    """Runs a prefill test on every GEMM variant (64 or 128 weight rows per workgroup)."""
     import ggml_mi355x as g
     prev = g.mmq_impl(request.param)
     yield request.param
