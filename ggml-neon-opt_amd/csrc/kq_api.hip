@@ -579,10 +579,15 @@ int mmq_impl() {
 }
 
 // Weight rows per prefill workgroup (kq_mmq's RT): 64 (4 waves) or 128 (8 waves, the
-// activation tile fetched once per 128 rows).
-int mmq_rows() {
+// activation tile fetched once per 128 rows). AUTO: 128 for Q4_K when the grid of 128-row
+// tiles still holds a workgroup per CU (Llama-3-8B q/o, gate/up, down 3-9 % faster than 64),
+// else 64 (Q5_K / Q6_K and small grids: the 64-row tiles are as fast or faster;
+// profiles/r03_mmq_onebar_tile128.txt).
+int mmq_rows(int type, int64_t rows, int64_t M) {
     const int impl = mmq_impl();
-    return impl == MI355X_MMQ_TILE128 ? 128 : 64;
+    if (impl == MI355X_MMQ_TILE128) return 128;
+    if (impl == MI355X_MMQ_TILE64) return 64;
+    return type == Q4_K && ((rows + 127) / 128) * ((M + 63) / 64) >= 256 ? 128 : 64;
 }
 const void *mmq_fn(int type, bool mixed, int rt) {
     if (rt == 128)
@@ -617,7 +622,7 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     a.m_cols = (int)M;
     a.y = y;
     a.y_col_stride = y_col_stride;
-    const int rt = mmq_rows();
+    const int rt = mmq_rows(type, N, M);
     const void *fn = mmq_fn(type, false, rt);
     const size_t lds = mmq_lds(type, rt);
     dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + rt - 1) / rt), 1);
@@ -660,7 +665,9 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     if (mixed)
         for (int d = 0; d < n_mat; ++d)
             if (types[d] != Q4_K && types[d] != Q6_K) return MI355X_E_INVAL;
-    const int rt = mmq_rows();
+    int64_t all_rows = 0;
+    for (int d = 0; d < n_mat; ++d) all_rows += N[d];
+    const int rt = mmq_rows(types[0], all_rows, M);  // (Q6_K beside Q4_K: on Q4_K's choice)
     MmqArgs a;
     memset(&a, 0, sizeof(a));
     a.n_mat = n_mat;

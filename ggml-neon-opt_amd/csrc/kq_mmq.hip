@@ -60,6 +60,13 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #ifndef KQ_MMQ_Q4_VALU
 #define KQ_MMQ_Q4_VALU 0
 #endif
+// One barrier per superblock (the next superblock's DMA issued right after it, into the
+// buffer every wave has finished reading) instead of a landing and a release barrier:
+// 2-12 % faster on every prefill shape (profiles/r03_mmq_onebar_tile128.txt). 0: the
+// round-2 loop (experiment build).
+#ifndef KQ_MMQ_ONEBAR
+#define KQ_MMQ_ONEBAR 1
+#endif
 #ifndef KQ_MMQ_Q5_VALU
 #define KQ_MMQ_Q5_VALU 0  // experiment build: Q5_K sub-block scales on VALU (the round-2 kernel)
 #endif
@@ -467,6 +474,13 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     } else {
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
+        if (KQ_MMQ_ONEBAR) {
+            // superblock b (the only DMA in flight) landed; after the barrier every wave's part
+            // of b is in LDS and every wave has finished reading b - 1's buffer (lgkmcnt(0)
+            // before it), so b + 1 goes into that buffer while b is computed
+            asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (b + 1 < nb) issue(b + 1);
+        } else {
         if (b + 1 < nb) {
             issue(b + 1);
             vm_wait<NWP>();  // superblock b's DMAs (older than b+1's NW) have landed
@@ -474,6 +488,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             vm_wait<0>();
         }
         asm volatile("s_barrier" ::: "memory");  // every wave's part of superblock b
+        }
         const uint8_t *buf = smem + (b & 1) * BUF;
         const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;          // this lane's activation column
         if (TYPE == Q6_K) {
@@ -481,7 +496,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 q6_superblock_valu(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
             else
                 q6_superblock(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (!KQ_MMQ_ONEBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             continue;
         }
         const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;   // this lane's weight row
@@ -609,7 +624,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 sumf[i] = fmaf((float)sumi[i], yd * xd, sumf[i]);
             }
         }
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer b&1 free for b+2
+        if (!KQ_MMQ_ONEBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer b&1 free for b+2
     }
 
     }
