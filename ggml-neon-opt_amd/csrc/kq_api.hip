@@ -24,9 +24,9 @@ template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void kq_rows(const RowsArgs a);
 template <bool AM>
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
-template <int TYPE, int RT>
+template <int TYPE, int RT, int CW>
 __global__ void kq_mmq(const MmqArgs a);
-template <int RT>
+template <int RT, int CW>
 __global__ void kq_mmq_mixed(const MmqArgs a);
 
 namespace {
@@ -570,7 +570,8 @@ int mmq_impl() {
     if (v < 0) {
         const char *e = getenv("MI355X_MMQ_IMPL");
         int x = MI355X_MMQ_AUTO;
-        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : strcmp(e, "tile128") == 0 ? MI355X_MMQ_TILE128 : x;
+        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : strcmp(e, "tile128") == 0 ? MI355X_MMQ_TILE128
+                : strcmp(e, "tile128w") == 0 ? MI355X_MMQ_TILE128W : x;
         int expect = -1;
         g_mmq_impl.compare_exchange_strong(expect, x);
         v = g_mmq_impl.load();
@@ -578,32 +579,44 @@ int mmq_impl() {
     return v;
 }
 
-// Weight rows per prefill workgroup (kq_mmq's RT): 64 (4 waves) or 128 (8 waves, the
-// activation tile fetched once per 128 rows). AUTO: 128 for Q4_K when the grid of 128-row
-// tiles still holds a workgroup per CU (Llama-3-8B q/o, gate/up, down 3-9 % faster than 64),
-// else 64 (Q5_K / Q6_K and small grids: the 64-row tiles are as fast or faster;
-// profiles/r03_mmq_onebar_tile128.txt).
-int mmq_rows(int type, int64_t rows, int64_t M) {
+// Prefill tile shape (kq_mmq's RT x CW): weight rows per workgroup RT = 64 (4 waves) or 128
+// (8 waves: the activation tile fetched once per 128 rows), activation columns 64 * CW (CW = 2:
+// each wave's weight operands feed two MFMA column tiles, half the operand-building vector
+// work per MFMA). AUTO, by the grid each shape would launch (profiles/r03_mmq_tiles.txt):
+//  * Q4_K / Q6_K whose 128 x 128 grid has >= 160 workgroups: 128 x 128 (TinyLlama Q6_K head
+//    256 -> 167 us, gate/up 28.3 -> 26.0, 8B ffn_up 98 -> 95); on 128-workgroup grids it
+//    loses 30-40 % (half the CUs idle);
+//  * else Q4_K whose 128 x 64 grid has >= 256 workgroups: 128 x 64 (8B q/o 33 -> 31, ffn_down
+//    108-116 -> 101-106);
+//  * else 64 x 64 (Q5_K, small grids).
+struct MmqShape {
+    int rt, cw;
+};
+MmqShape mmq_shape(int type, int64_t rows, int64_t M) {
     const int impl = mmq_impl();
-    if (impl == MI355X_MMQ_TILE128) return 128;
-    if (impl == MI355X_MMQ_TILE64) return 64;
-    return type == Q4_K && ((rows + 127) / 128) * ((M + 63) / 64) >= 256 ? 128 : 64;
+    if (impl == MI355X_MMQ_TILE128) return {128, 1};
+    if (impl == MI355X_MMQ_TILE128W) return {128, 2};
+    if (impl == MI355X_MMQ_TILE64) return {64, 1};
+    const int64_t rt128 = (rows + 127) / 128;
+    if ((type == Q4_K || type == Q6_K) && rt128 * ((M + 127) / 128) >= 160) return {128, 2};
+    if (type == Q4_K && rt128 * ((M + 63) / 64) >= 256) return {128, 1};
+    return {64, 1};
 }
-const void *mmq_fn(int type, bool mixed, int rt) {
-    if (rt == 128)
-        return mixed          ? (const void *)kq_mmq_mixed<128>
-             : type == Q5_K ? (const void *)kq_mmq<Q5_K, 128>
-             : type == Q6_K ? (const void *)kq_mmq<Q6_K, 128>
-                            : (const void *)kq_mmq<Q4_K, 128>;
-    return mixed          ? (const void *)kq_mmq_mixed<64>
-         : type == Q5_K ? (const void *)kq_mmq<Q5_K, 64>
-         : type == Q6_K ? (const void *)kq_mmq<Q6_K, 64>
-                        : (const void *)kq_mmq<Q4_K, 64>;
+const void *mmq_fn(int type, bool mixed, MmqShape sh) {
+#define KQ_MMQ_PICK(RT, CW)                                                      \
+    return mixed          ? (const void *)kq_mmq_mixed<RT, CW>                 \
+         : type == Q5_K ? (const void *)kq_mmq<Q5_K, RT, CW>                   \
+         : type == Q6_K ? (const void *)kq_mmq<Q6_K, RT, CW>                   \
+                        : (const void *)kq_mmq<Q4_K, RT, CW>;
+    if (sh.rt == 128 && sh.cw == 2) KQ_MMQ_PICK(128, 2)
+    if (sh.rt == 128) KQ_MMQ_PICK(128, 1)
+    KQ_MMQ_PICK(64, 1)
+#undef KQ_MMQ_PICK
 }
-// two superblock buffers: 64 Q8L columns + rt weight rows (Q6_K: 224-B granule span), +16 B
-// for the Q6_K realign reads past the last row
-size_t mmq_lds(int type, int rt) {
-    return 2 * (size_t)(64 * Q8L_STRIDE + rt * (type == Q6_K ? 224 : block_bytes(type))) + 16 + MMQ_PF_LDS;
+// two superblock buffers: 64 * cw Q8L columns + rt weight rows (Q6_K: 224-B granule span),
+// +16 B for the Q6_K realign reads past the last row
+size_t mmq_lds(int type, MmqShape sh) {
+    return 2 * (size_t)(64 * sh.cw * Q8L_STRIDE + sh.rt * (type == Q6_K ? 224 : block_bytes(type))) + 16 + MMQ_PF_LDS;
 }
 
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
@@ -622,11 +635,11 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     a.m_cols = (int)M;
     a.y = y;
     a.y_col_stride = y_col_stride;
-    const int rt = mmq_rows(type, N, M);
-    const void *fn = mmq_fn(type, false, rt);
-    const size_t lds = mmq_lds(type, rt);
-    dim3 grid((unsigned)((M + 63) / 64), (unsigned)((N + rt - 1) / rt), 1);
-    dim3 block((unsigned)(4 * rt));
+    const MmqShape sh = mmq_shape(type, N, M);
+    const void *fn = mmq_fn(type, false, sh);
+    const size_t lds = mmq_lds(type, sh);
+    dim3 grid((unsigned)((M + 64 * sh.cw - 1) / (64 * sh.cw)), (unsigned)((N + sh.rt - 1) / sh.rt), 1);
+    dim3 block((unsigned)(4 * sh.rt));
     std::string name = std::string("kq::kq_mmq<") + std::to_string(type) + ">";
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
@@ -667,7 +680,8 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
             if (types[d] != Q4_K && types[d] != Q6_K) return MI355X_E_INVAL;
     int64_t all_rows = 0;
     for (int d = 0; d < n_mat; ++d) all_rows += N[d];
-    const int rt = mmq_rows(types[0], all_rows, M);  // (Q6_K beside Q4_K: on Q4_K's choice)
+    const MmqShape sh = mmq_shape(types[0], all_rows, M);  // (Q6_K beside Q4_K: on Q4_K's choice)
+    const int rt = sh.rt;
     MmqArgs a;
     memset(&a, 0, sizeof(a));
     a.n_mat = n_mat;
@@ -704,9 +718,9 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     a.n_rows = a.mn_rows[0];
     a.y = a.my[0];
     a.y_col_stride = a.my_col_stride[0];
-    const void *fn = mmq_fn(type, mixed, rt);
-    const size_t lds = mmq_lds(mixed ? Q6_K : type, rt);  // mixed: the larger (Q6_K) tile
-    const dim3 grid((unsigned)((M + 63) / 64), (unsigned)tiles, 1);
+    const void *fn = mmq_fn(type, mixed, sh);
+    const size_t lds = mmq_lds(mixed ? Q6_K : type, sh);  // mixed: the larger (Q6_K) tile
+    const dim3 grid((unsigned)((M + 64 * sh.cw - 1) / (64 * sh.cw)), (unsigned)tiles, 1);
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
     void *args[] = {&a};
@@ -1106,7 +1120,7 @@ int mi355x_gemv_impl(int impl) {
 }
 
 int mi355x_mmq_impl(int impl) {
-    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE128) return MI355X_E_INVAL;
+    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE128W) return MI355X_E_INVAL;
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
     return prev;

@@ -51,12 +51,6 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #else
 #define KQ_MMQ_WPE_ATTR
 #endif
-#ifndef KQ_MMQ_PIPE
-#define KQ_MMQ_PIPE 0  // experiment build: Q4_K tile loop software-pipelined (measured neutral, +88 VGPRs)
-#endif
-#ifndef KQ_MMQ_Q6_VALU
-#define KQ_MMQ_Q6_VALU 0  // experiment build: Q6_K group scales on VALU (round-2 kernel)
-#endif
 #ifndef KQ_MMQ_Q4_VALU
 #define KQ_MMQ_Q4_VALU 0
 #endif
@@ -89,9 +83,7 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) {
     return r;
 }
 
-constexpr int MMQ_TILE = 64;                 // activation columns per workgroup
-constexpr int MMQ_A_BYTES = MMQ_TILE * Q8L_STRIDE;  // 19456 B per superblock
-constexpr int MMQ_A_INSTR = MMQ_A_BYTES / 1024;     // 19 DMA instructions (exact)
+
 // Weight rows per workgroup: RT = 64 (4 waves, 2 x 2 of 32 x 32) or 128 (8 waves, 2 x 4):
 // the activation tile is fetched once per RT rows, so RT = 128 halves its LDS-DMA traffic.
 
@@ -100,68 +92,7 @@ constexpr int MMQ_A_INSTR = MMQ_A_BYTES / 1024;     // 19 DMA instructions (exac
 // 16-B boundary below it.
 __host__ __device__ constexpr int mmq_row_bytes(int type) { return type == Q6_K ? 224 : block_bytes(type); }
 __host__ __device__ constexpr int mmq_b_instr(int type, int rt) { return rt * mmq_row_bytes(type) / 1024; }  // 9 / 11 / 14 per 64 rows
-__host__ __device__ constexpr int mmq_nw(int type, int rt) {  // DMA instructions per wave (rt / 16 waves)
-    return (MMQ_A_INSTR + mmq_b_instr(type, rt) + rt / 16 - 1) / (rt / 16);
-}
-__host__ __device__ constexpr int mmq_buf(int type, int rt) { return MMQ_A_BYTES + rt * mmq_row_bytes(type); }
 
-// (KQ_MMQ_Q6_VALU experiment build) Q6_K superblock of one 32x32 tile: 8 chunks of 32 elements; a lane's 16 values
-// of a chunk are one 16-element scale group, so two MFMAs per chunk (the other
-// half's operand zeroed) give each group's dot, scaled by its int8 scale on VALU.
-// The weight operand is q - 32 (sign-extended 6-bit), so the sum is directly the
-// reference's isum - 32*isum_mins (README.md:369-394 / lane_q6K): no mins term.
-__device__ __forceinline__ void q6_superblock_valu(const MmqArgs &a, const uint8_t *buf, const uint8_t *At, int n, int b,
-                                              int r, int h, int wm, int wn, f32x16 &sumf) {
-    const int nrow = n < a.n_rows ? n : a.n_rows - 1;  // the DMA clamped the same way
-    const uint32_t mis = (uint32_t)((uintptr_t)(a.w + (int64_t)nrow * a.row_stride + (int64_t)b * 210) & 15u);
-    const uint8_t *region = buf + MMQ_A_BYTES + (32 * wn + r) * 224 + mis;
-    const uint32_t s4 = (uint32_t)((uintptr_t)region & 3u);
-    const uint8_t *bb = region - s4;
-    const u32x4 SC = realign(*(const u32x4a *)(bb + 192), *(const uint32_t *)(bb + 208), s4);
-    const uint32_t dh = (*(const uint32_t *)(bb + 208) >> (8u * s4)) & 0xffffu;
-    i32x16 sumi;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) sumi[i] = 0;
-    const i32x16 zero = {};
-#pragma unroll
-    for (int nh = 0; nh < 2; ++nh) {
-        const u32x4 L0 = realign(*(const u32x4a *)(bb + 64 * nh + 16 * h), *(const uint32_t *)(bb + 64 * nh + 16 * h + 16), s4);
-        const u32x4 L1 = realign(*(const u32x4a *)(bb + 64 * nh + 32 + 16 * h),
-                                 *(const uint32_t *)(bb + 64 * nh + 48 + 16 * h), s4);
-        const u32x4 H = realign(*(const u32x4a *)(bb + 128 + 32 * nh + 16 * h),
-                                *(const uint32_t *)(bb + 144 + 32 * nh + 16 * h), s4);
-#pragma unroll KQ_MMQ_Q6_UNROLL
-        for (int cc = 0; cc < 4; ++cc) {
-            const int c = 4 * nh + cc;  // chunk: elements 32c .. 32c+31
-            const u32x4 L = (cc & 1) ? L1 : L0;
-            const uint32_t sh = (uint32_t)(cc >> 1) * 4u;
-            // x = q ^ 0x20 = (q - 32) in 6-bit two's complement; sign-extend bit 5 into bits 6-7
-            u32x4 q;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                const uint32_t x = ((L[k] >> sh) & 0x0f0f0f0fu) | ((((H[k] >> (2u * cc)) & 0x03030303u) ^ 0x02020202u) << 4);
-                const uint32_t sgn = x & 0x20202020u;
-                q[k] = x | (sgn << 1) | (sgn << 2);
-            }
-            const u32x4 act = *(const u32x4 *)(At + 16 + 32 * c + 16 * h);
-            const u32x4 q0 = h == 0 ? q : u32x4{0u, 0u, 0u, 0u};
-            const u32x4 q1 = h == 1 ? q : u32x4{0u, 0u, 0u, 0u};
-            const i32x16 d0 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&q0, zero, 0, 0, 0);
-            const i32x16 d1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&q1, zero, 0, 0, 0);
-            const int g0 = sbyte(SC, 2 * c), g1 = sbyte(SC, 2 * c + 1);  // int8 group scales of row n
-#pragma unroll
-            for (int i = 0; i < 16; ++i)  // 24-bit multiplies (full rate; |d| < 2^17, |g| < 2^7)
-                sumi[i] += __mul24(g0, d0[i]) + __mul24(g1, d1[i]);
-        }
-    }
-    const float xd = h2f(dh);
-#pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
-        const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
-        sumf[i] = fmaf(xd * yd, (float)sumi[i], sumf[i]);  // sum += d_all*y.d*(isum - 32*isum_mins)
-    }
-}
 
 // Scale-split multipliers of sub-blocks 2jp (lo nibbles) and 2jp+1 (hi nibbles) as 16-bit
 // pairs: sc = 8*sh + sl; sh / sl bytes of all four sub-blocks of a word split with two
@@ -208,16 +139,21 @@ __device__ __forceinline__ f16x8 mins_operand(uint32_t m03, uint32_t m47, int h)
 // the whole superblock in the matrix core, sumi = 256 * S_hi + S_lo exactly -- the
 // reference's isum - 32*isum_mins with its scales (README.md:369-394 / lane_q6K) --
 // instead of two half-empty MFMAs and 32 VALU multiplies per chunk.
-__device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *buf, const uint8_t *At, int n, int b,
-                                              int r, int h, int wm, int wn, f32x16 &sumf) {
+// With CW column tiles per wave the weight operands of a chunk are built once and feed
+// CW MFMA pairs (the activation operands differ per tile).
+template <int CW>
+__device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *Bbase, const uint8_t *const *At,
+                                              const float *yd, int n, int b, int h, f32x16 *sumf) {
     const int nrow = n < a.n_rows ? n : a.n_rows - 1;  // the DMA clamped the same way
     const uint32_t mis = (uint32_t)((uintptr_t)(a.w + (int64_t)nrow * a.row_stride + (int64_t)b * 210) & 15u);
-    const uint8_t *region = buf + MMQ_A_BYTES + (32 * wn + r) * 224 + mis;
+    const uint8_t *region = Bbase + mis;
     const uint32_t s4 = (uint32_t)((uintptr_t)region & 3u);
     const uint8_t *bb = region - s4;
     const u32x4 SC = realign(*(const u32x4a *)(bb + 192), *(const uint32_t *)(bb + 208), s4);
     const uint32_t dh = (*(const uint32_t *)(bb + 208) >> (8u * s4)) & 0xffffu;
-    i32x16 shi = {}, slo = {};
+    i32x16 shi[CW], slo[CW];
+#pragma unroll
+    for (int ct = 0; ct < CW; ++ct) shi[ct] = slo[ct] = i32x16{};
 #pragma unroll
     for (int nh = 0; nh < 2; ++nh) {
         const u32x4 L0 = realign(*(const u32x4a *)(bb + 64 * nh + 16 * h), *(const uint32_t *)(bb + 64 * nh + 16 * h + 16), s4);
@@ -242,18 +178,20 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *b
                 blo[k] = __builtin_amdgcn_perm(t1, t0, 0x06040200u) ^ 0x80808080u;
                 bhi[k] = __builtin_amdgcn_perm(t1, t0, 0x07050301u);
             }
-            const u32x4 act = *(const u32x4 *)(At + 16 + 32 * c + 16 * h);
-            shi = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&bhi, shi, 0, 0, 0);
-            slo = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&blo, slo, 0, 0, 0);
+#pragma unroll
+            for (int ct = 0; ct < CW; ++ct) {
+                const u32x4 act = *(const u32x4 *)(At[ct] + 16 + 32 * c + 16 * h);
+                shi[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&bhi, shi[ct], 0, 0, 0);
+                slo[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&act, *(const i32x4m *)&blo, slo[ct], 0, 0, 0);
+            }
         }
     }
     const float xd = h2f(dh);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) {
-        const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
-        const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
-        sumf[i] = fmaf(xd * yd, (float)(256 * shi[i] + slo[i]), sumf[i]);  // sum += d_all*y.d*(isum - 32*isum_mins)
-    }
+    for (int ct = 0; ct < CW; ++ct)
+#pragma unroll
+        for (int i = 0; i < 16; ++i)  // sum += d_all*y.d*(isum - 32*isum_mins)
+            sumf[ct][i] = fmaf(xd * yd[16 * ct + i], (float)(256 * shi[ct][i] + slo[ct][i]), sumf[ct][i]);
 }
 
 // Balanced int8 bytes of four unsigned quants x (bytes 0..31) times a 6-bit scale:
@@ -301,33 +239,37 @@ __device__ __forceinline__ int mmq_tile_of(const MmqArgs &a0, MmqArgs &a, int &t
     return d;
 }
 
-// One 64-column x RT-row output tile (RT / 16 waves of 32 x 32) over the whole K.
-template <int TYPE, int RT>
+// One (64 * CW)-column x RT-row output tile over the whole K: RT / 16 waves, each 32 weight
+// rows x 32 * CW columns (CW MFMA tiles sharing the wave's weight operands).
+template <int TYPE, int RT, int CW>
 __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     constexpr int BSZ = block_bytes(TYPE);
     constexpr int NWV = RT / 16;  // waves
+    constexpr int COLS = 64 * CW;
+    constexpr int A_BYTES = COLS * Q8L_STRIDE;
+    constexpr int A_INSTR = A_BYTES / 1024;  // 19 per 64 columns (exact)
     constexpr int NB_I = mmq_b_instr(TYPE, RT);
-    constexpr int NW = mmq_nw(TYPE, RT);
-    constexpr int BUF = mmq_buf(TYPE, RT);
-    static_assert(RT == 64 || (RT == 128 && !KQ_MMQ_PF), "the L2 warm-up assumes 4 waves");
+    constexpr int NW = (A_INSTR + NB_I + NWV - 1) / NWV;
+    constexpr int BUF = A_BYTES + RT * mmq_row_bytes(TYPE);
+    static_assert(!KQ_MMQ_PF || (RT == 64 && CW == 1), "the L2 warm-up assumes the 4-wave 64 x 64 tile");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int wm = wave & 1, wn = wave >> 1;
     const int r = lane & 31, h = lane >> 5;
-    const int col0 = tx * MMQ_TILE, row0 = ty * RT;
+    const int col0 = tx * COLS, row0 = ty * RT;
     const int nb = a.nb;
 
-    // ---- DMA plan: the superblock's 19 activation + NB_I weight instructions, NW per wave
+    // ---- DMA plan: the superblock's A_INSTR activation + NB_I weight instructions, NW per wave
     auto issue = [&](int b) {
         uint8_t *buf = smem + (b & 1) * BUF;
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
             int t = wave + NWV * s;
-            if (t >= MMQ_A_INSTR + NB_I) t = MMQ_A_INSTR + NB_I - 1;  // pad: repeat the last one
-            const int g = 64 * (t < MMQ_A_INSTR ? t : t - MMQ_A_INSTR) + lane;  // granule in its tile
+            if (t >= A_INSTR + NB_I) t = A_INSTR + NB_I - 1;  // pad: repeat the last one
+            const int g = 64 * (t < A_INSTR ? t : t - A_INSTR) + lane;  // granule in its tile
             const uint8_t *src;
-            if (t < MMQ_A_INSTR) {
+            if (t < A_INSTR) {
                 int c = g / (Q8L_STRIDE / 16);
                 const int piece = g - c * (Q8L_STRIDE / 16);
                 c = col0 + c < a.m_cols ? col0 + c : a.m_cols - 1;
@@ -340,7 +282,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 rw = row0 + rw < a.n_rows ? row0 + rw : a.n_rows - 1;
                 const uintptr_t blk = (uintptr_t)(a.w + (int64_t)rw * a.row_stride + (int64_t)b * BSZ);
                 src = (const uint8_t *)(blk & ~(uintptr_t)15) + 16 * piece;
-                dma16(src, (LDS void *)(buf + MMQ_A_BYTES + 1024 * (t - MMQ_A_INSTR)));
+                dma16(src, (LDS void *)(buf + A_BYTES + 1024 * (t - A_INSTR)));
             }
         }
         if (KQ_MMQ_PF) {  // L2 warm-up of superblock b + KQ_MMQ_PF's weight tile: one dword per
@@ -357,121 +299,13 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     };
     constexpr int NWP = NW + (KQ_MMQ_PF ? 1 : 0);  // vm instructions per issue()
 
-    f32x16 sumf;
+    f32x16 sumf[CW];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) sumf[i] = 0.f;
+    for (int ct = 0; ct < CW; ++ct)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) sumf[ct][i] = 0.f;
 
     issue(0);
-    if constexpr (TYPE == Q4_K && KQ_MMQ_PIPE && !KQ_MMQ_DIAG && !KQ_MMQ_Q4_VALU) {
-        // Software-pipelined Q4_K loop: superblock b's MFMAs are issued before superblock
-        // b-1's fp32 chain runs, so the wave's VALU epilogue overlaps its own matrix-core
-        // work instead of waiting for it. Superblock b-1 carries its MFMA sums (two
-        // alternating accumulator sets) and its scalars (mins, column scales, d, dmin) in
-        // registers; each element's chain still runs superblock by superblock in order.
-        i32x16 s8a = {}, s1a = {}, s8b = {}, s1b = {};
-        f32x16 mins = {};
-        float yd[16];
-        float xd = 0.f, xdm = 0.f, nxdm = 0.f;
-        auto mfmas = [&](const uint8_t *buf, i32x16 &s8, i32x16 &s1) {
-            const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;
-            const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;
-            const u32x4 hdr = *(const u32x4 *)Bt;
-            const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
-            const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
-            const SplitScales ss = split_scales(s03, s47);
-            const i32x16 zero = {};
-            s8 = zero;
-            s1 = zero;
-#pragma unroll
-            for (int jp = 0; jp < 4; ++jp) {
-                const u32x4 qv = *(const u32x4 *)(Bt + 16 + 32 * jp + 16 * h);
-                const u32x4 lo = qv & 0x0f0f0f0fu, hi = (qv >> 4) & 0x0f0f0f0fu;
-                const u32x4 alo = *(const u32x4 *)(At + 16 + 64 * jp + 16 * h);
-                const u32x4 ahi = *(const u32x4 *)(At + 48 + 64 * jp + 16 * h);
-                const int kb = 2 * (jp & 1);  // bytes of sub-blocks 2jp, 2jp+1 in their word
-                const u16x2 lh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb));
-                const u16x2 ll = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb));
-                const u16x2 hh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb + 1));
-                const u16x2 hl = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb + 1));
-                u32x4 b8lo, b1lo, b8hi, b1hi;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    b8lo[k] = as_u32(as_u16x2(lo[k]) * lh);
-                    b1lo[k] = as_u32(as_u16x2(lo[k]) * ll);
-                    b8hi[k] = as_u32(as_u16x2(hi[k]) * hh);
-                    b1hi[k] = as_u32(as_u16x2(hi[k]) * hl);
-                }
-                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b8lo, s8, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b1lo, s1, 0, 0, 0);
-                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b8hi, s8, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b1hi, s1, 0, 0, 0);
-            }
-        };
-        auto scalars = [&](const uint8_t *buf) {  // as the unpipelined loop below
-            const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;
-            const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;
-            const u32x4 hdr = *(const u32x4 *)Bt;
-            const uint32_t m03 = hdr.z & 0x3f3f3f3fu;
-            const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
-            const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
-            const f16x8 bm = mins_operand(m03, m47, h);
-            const f32x16 zero = {};
-            mins = __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
-            xd = h2f(hdr.x & 0xffffu);
-            xdm = h2f(hdr.x >> 16);
-            nxdm = -xdm;
-#pragma unroll
-            for (int i = 0; i < 16; ++i) yd[i] = *(const float *)(buf + (32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h) * Q8L_STRIDE);
-        };
-        auto epilogue = [&](const i32x16 &s8, const i32x16 &s1) {  // the reference's fp32 update
-#pragma unroll
-            for (int i = 0; i < 16; ++i) {
-                sumf[i] = fmaf(mins[i], yd[i] * nxdm, sumf[i]);  // = fmaf(-mins, yd*xdm, .) exactly
-                sumf[i] = fmaf((float)(8 * s8[i] + s1[i]), yd[i] * xd, sumf[i]);
-            }
-        };
-        auto land = [&](int b) {  // superblock b in LDS (and b+1 requested), every wave's part
-            if (b + 1 < nb) {
-                issue(b + 1);
-                vm_wait<NWP>();
-            } else {
-                vm_wait<0>();
-            }
-            asm volatile("s_barrier" ::: "memory");
-        };
-        auto release = [&]() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); };
-        land(0);
-        mfmas(smem, s8a, s1a);
-        scalars(smem);
-        release();
-        int b = 1;
-#pragma unroll 1
-        for (; b + 1 < nb; b += 2) {  // b into set B, b + 1 into set A
-            land(b);
-            const uint8_t *bufb = smem + (b & 1) * BUF;
-            mfmas(bufb, s8b, s1b);
-            epilogue(s8a, s1a);
-            scalars(bufb);
-            release();
-            land(b + 1);
-            const uint8_t *bufc = smem + ((b + 1) & 1) * BUF;
-            mfmas(bufc, s8a, s1a);
-            epilogue(s8b, s1b);
-            scalars(bufc);
-            release();
-        }
-        if (b < nb) {
-            land(b);
-            const uint8_t *bufb = smem + (b & 1) * BUF;
-            mfmas(bufb, s8b, s1b);
-            epilogue(s8a, s1a);
-            scalars(bufb);
-            release();
-            epilogue(s8b, s1b);
-        } else {
-            epilogue(s8a, s1a);
-        }
-    } else {
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
         if (KQ_MMQ_ONEBAR) {
@@ -481,25 +315,31 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
             if (b + 1 < nb) issue(b + 1);
         } else {
-        if (b + 1 < nb) {
-            issue(b + 1);
-            vm_wait<NWP>();  // superblock b's DMAs (older than b+1's NW) have landed
-        } else {
-            vm_wait<0>();
-        }
-        asm volatile("s_barrier" ::: "memory");  // every wave's part of superblock b
+            if (b + 1 < nb) {
+                issue(b + 1);
+                vm_wait<NWP>();  // superblock b's DMAs (older than b+1's NW) have landed
+            } else {
+                vm_wait<0>();
+            }
+            asm volatile("s_barrier" ::: "memory");  // every wave's part of superblock b
         }
         const uint8_t *buf = smem + (b & 1) * BUF;
-        const uint8_t *At = buf + (32 * wm + r) * Q8L_STRIDE;          // this lane's activation column
+        const uint8_t *At[CW];  // this lane's activation column of each tile
+        float yd[16 * CW];      // y.d of the columns each accumulator element belongs to
+#pragma unroll
+        for (int ct = 0; ct < CW; ++ct) {
+            const int cb = 32 * CW * wm + 32 * ct;
+            At[ct] = buf + (cb + r) * Q8L_STRIDE;
+#pragma unroll
+            for (int i = 0; i < 16; ++i)
+                yd[16 * ct + i] = *(const float *)(buf + (cb + (i & 3) + 8 * (i >> 2) + 4 * h) * Q8L_STRIDE);
+        }
+        const uint8_t *Bt = buf + A_BYTES + (32 * wn + r) * mmq_row_bytes(TYPE);  // this lane's weight row
         if (TYPE == Q6_K) {
-            if (KQ_MMQ_Q6_VALU)
-                q6_superblock_valu(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
-            else
-                q6_superblock(a, buf, At, row0 + 32 * wn + r, b, r, h, wm, wn, sumf);
+            q6_superblock<CW>(a, Bt, At, yd, row0 + 32 * wn + r, b, h, sumf);
             if (!KQ_MMQ_ONEBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             continue;
         }
-        const uint8_t *Bt = buf + MMQ_A_BYTES + (32 * wn + r) * BSZ;   // this lane's weight row
         const u32x4 hdr = *(const u32x4 *)Bt;
         // 6-bit scales / mins of the lane's row (get_scale_min_k4, README.md:732-739)
         const uint32_t s03 = hdr.y & 0x3f3f3f3fu;
@@ -507,9 +347,10 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
         const SplitScales ss = split_scales(s03, s47);
         const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
-        i32x16 sumi, s8 = {}, s1 = {};  // Q4_K: sumi = 8*s8 + s1 (scale split into 3-bit halves)
+        // Q4_K: sumi = 8*s8 + s1 (scale split into 3-bit halves); Q5_K: 256*s8 + s1 (balanced bytes)
+        i32x16 sumi[CW], s8[CW], s1[CW];
 #pragma unroll
-        for (int i = 0; i < 16; ++i) sumi[i] = 0;
+        for (int ct = 0; ct < CW; ++ct) sumi[ct] = s8[ct] = s1[ct] = i32x16{};
         u32x4 qh = {0u, 0u, 0u, 0u};
         if (TYPE == Q5_K) qh = *(const u32x4 *)(Bt + 16 + 16 * h);
 #pragma unroll
@@ -520,18 +361,25 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 lo = lo | (((qh >> (uint32_t)(2 * jp)) & 0x01010101u) << 4);
                 hi = hi | (((qh >> (uint32_t)(2 * jp + 1)) & 0x01010101u) << 4);
             }
-            const u32x4 alo = *(const u32x4 *)(At + 16 + 64 * jp + 16 * h);
-            const u32x4 ahi = *(const u32x4 *)(At + 48 + 64 * jp + 16 * h);
+            u32x4 alo[CW], ahi[CW];
+#pragma unroll
+            for (int ct = 0; ct < CW; ++ct) {
+                alo[ct] = *(const u32x4 *)(At[ct] + 16 + 64 * jp + 16 * h);
+                ahi[ct] = *(const u32x4 *)(At[ct] + 48 + 64 * jp + 16 * h);
+            }
             const uint32_t sw = jp < 2 ? s03 : s47;
             const int sc_lo = (int)((sw >> (16u * (uint32_t)(jp & 1))) & 0xffu);
             const int sc_hi = (int)((sw >> (16u * (uint32_t)(jp & 1) + 8u)) & 0xffu);
             if (TYPE == Q4_K && (KQ_MMQ_DIAG & 6)) {  // diagnostics (timing only)
-                if (!(KQ_MMQ_DIAG & 4)) {
-                    s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, s8, 0, 0, 0);
-                    s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&hi, s1, 0, 0, 0);
-                } else {
-                    s8[jp] += (int)(lo.x ^ alo.y ^ (uint32_t)sc_lo);
-                    s1[jp] += (int)(hi.y ^ ahi.x ^ (uint32_t)sc_hi);
+#pragma unroll
+                for (int ct = 0; ct < CW; ++ct) {
+                    if (!(KQ_MMQ_DIAG & 4)) {
+                        s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&lo, s8[ct], 0, 0, 0);
+                        s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&hi, s1[ct], 0, 0, 0);
+                    } else {
+                        s8[ct][jp] += (int)(lo.x ^ alo[ct].y ^ (uint32_t)sc_lo);
+                        s1[ct][jp] += (int)(hi.y ^ ahi[ct].x ^ (uint32_t)sc_hi);
+                    }
                 }
             } else if (TYPE == Q4_K && !KQ_MMQ_Q4_VALU) {
                 // sc = 8*sh + sl (3-bit halves): nibble*sh and nibble*sl <= 105 stay int8, and a
@@ -551,10 +399,13 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                     b8hi[k] = as_u32(as_u16x2(hi[k]) * hh);
                     b1hi[k] = as_u32(as_u16x2(hi[k]) * hl);
                 }
-                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b8lo, s8, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&b1lo, s1, 0, 0, 0);
-                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b8hi, s8, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&b1hi, s1, 0, 0, 0);
+#pragma unroll
+                for (int ct = 0; ct < CW; ++ct) {
+                    s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&b8lo, s8[ct], 0, 0, 0);
+                    s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&b1lo, s1[ct], 0, 0, 0);
+                    s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&b8hi, s8[ct], 0, 0, 0);
+                    s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&b1hi, s1[ct], 0, 0, 0);
+                }
             } else if (TYPE == Q5_K && !KQ_MMQ_Q5_VALU) {
                 // Q5_K: q (5 bits) x sc (6 bits) <= 1953 does not split into int8 halves, so the
                 // scaled weight W = sc*q rides in two balanced int8 bytes as for Q6_K: one packed
@@ -573,122 +424,132 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                     balanced_bytes(hi[k], sch, th, tl);
                     bhh[k] = th, blh[k] = tl;
                 }
-                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&bhl, s8, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&bll, s1, 0, 0, 0);
-                s8 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&bhh, s8, 0, 0, 0);
-                s1 = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&blh, s1, 0, 0, 0);
+#pragma unroll
+                for (int ct = 0; ct < CW; ++ct) {
+                    s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&bhl, s8[ct], 0, 0, 0);
+                    s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&bll, s1[ct], 0, 0, 0);
+                    s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&bhh, s8[ct], 0, 0, 0);
+                    s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&blh, s1[ct], 0, 0, 0);
+                }
             } else {  // Q5_K in the KQ_MMQ_Q5_VALU experiment build (and Q4_K in KQ_MMQ_Q4_VALU):
                       // per-sub-block dots scaled on VALU
                 const i32x16 zero = {};
-                i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo, *(const i32x4m *)&lo, zero, 0, 0, 0);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) sumi[i] += __mul24(sc_lo, c[i]);  // |c| < 2^17: full-rate i24
-                c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi, *(const i32x4m *)&hi, zero, 0, 0, 0);
+                for (int ct = 0; ct < CW; ++ct) {
+                    i32x16 c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&lo, zero, 0, 0, 0);
 #pragma unroll
-                for (int i = 0; i < 16; ++i) sumi[i] += __mul24(sc_hi, c[i]);
+                    for (int i = 0; i < 16; ++i) sumi[ct][i] += __mul24(sc_lo, c[i]);  // |c| < 2^17: full-rate i24
+                    c = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&hi, zero, 0, 0, 0);
+#pragma unroll
+                    for (int i = 0; i < 16; ++i) sumi[ct][i] += __mul24(sc_hi, c[i]);
+                }
             }
         }
-        if (TYPE == Q4_K && !KQ_MMQ_Q4_VALU) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) sumi[i] = 8 * s8[i] + s1[i];
-        }
-        if (TYPE == Q5_K && !KQ_MMQ_Q5_VALU) {
+        for (int ct = 0; ct < CW; ++ct) {
+            if (TYPE == Q4_K && !KQ_MMQ_Q4_VALU) {
 #pragma unroll
-            for (int i = 0; i < 16; ++i) sumi[i] = 256 * s8[i] + s1[i];
+                for (int i = 0; i < 16; ++i) sumi[ct][i] = 8 * s8[ct][i] + s1[ct][i];
+            }
+            if (TYPE == Q5_K && !KQ_MMQ_Q5_VALU) {
+#pragma unroll
+                for (int i = 0; i < 16; ++i) sumi[ct][i] = 256 * s8[ct][i] + s1[ct][i];
+            }
         }
-        // summins = sum_j mn_j * bs_j exactly on one f16 MFMA 32x32x16 (bs_j = bsums[2j] +
-        // bsums[2j+1] = 64*hi + lo, lo in 0..63): A = [lo_0..7 | hi_0..7] of the lane's
-        // activation column (stored so by the quantizer: the Q8L/mmq layout), B = [mn_0..7 |
-        // 64*mn_0..7] of its weight row; every product and partial sum is an integer below 2^24. (Four dependent f32 MFMAs 32x32x2 cost 256
-        // cycles per superblock against 32 for this one.)
-        f32x16 mins;
-        {
-            const f16x8 am = *(const f16x8 *)(At + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
-            const f16x8 bm = mins_operand(m03, m47, h);
-            const f32x16 zero = {};
-            mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
-        }
+        // summins = sum_j mn_j * bs_j exactly on one f16 MFMA 32x32x16 per tile (bs_j =
+        // bsums[2j] + bsums[2j+1] = 64*hi + lo, lo in 0..63): A = [lo_0..7 | hi_0..7] of the
+        // lane's activation column (stored so by the quantizer: the Q8L/mmq layout), B = [mn_0..7 |
+        // 64*mn_0..7] of its weight row; every product and partial sum is an integer below 2^24.
+        // (Four dependent f32 MFMAs 32x32x2 cost 256 cycles per superblock against 32 for this one.)
+        const f16x8 bm = mins_operand(m03, m47, h);
         // the reference's fp32 update per element, superblock order
         const float xd = h2f(hdr.x & 0xffffu), xdm = h2f(hdr.x >> 16), nxdm = -xdm;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int m = (i & 3) + 8 * (i >> 2) + 4 * h;
-            const float yd = *(const float *)(buf + (32 * wm + m) * Q8L_STRIDE);
-            if (KQ_MMQ_DIAG & 1) {  // diagnostics (timing only)
-                sumf[i] += (float)sumi[i] + mins[i] + yd;
-            } else if (TYPE == Q5_K) {
-                const float t = fmaf(yd * xd, (float)sumi[i], -((yd * xdm) * mins[i]));
-                sumf[i] = sumf[i] + t;
-            } else {
-                sumf[i] = fmaf(mins[i], yd * nxdm, sumf[i]);  // = fmaf(-mins, yd*xdm, .) exactly
-                sumf[i] = fmaf((float)sumi[i], yd * xd, sumf[i]);
+        for (int ct = 0; ct < CW; ++ct) {
+            const f16x8 am = *(const f16x8 *)(At[ct] + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
+            const f32x16 zero = {};
+            const f32x16 mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const float y = yd[16 * ct + i];
+                if (KQ_MMQ_DIAG & 1) {  // diagnostics (timing only)
+                    sumf[ct][i] += (float)sumi[ct][i] + mins[i] + y;
+                } else if (TYPE == Q5_K) {
+                    const float t = fmaf(y * xd, (float)sumi[ct][i], -((y * xdm) * mins[i]));
+                    sumf[ct][i] = sumf[ct][i] + t;
+                } else {
+                    sumf[ct][i] = fmaf(mins[i], y * nxdm, sumf[ct][i]);  // = fmaf(-mins, yd*xdm, .) exactly
+                    sumf[ct][i] = fmaf((float)sumi[ct][i], y * xd, sumf[ct][i]);
+                }
             }
         }
         if (!KQ_MMQ_ONEBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer b&1 free for b+2
     }
 
-    }
-
-    // ---- store: lane's weight row n, 16 activation columns
+    // ---- store: lane's weight row n, 16 activation columns per tile
     const int n = row0 + 32 * wn + r;
-    if (n < a.n_rows) {
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int m = col0 + 32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (m < a.m_cols)
-                a.y[(int64_t)m * a.y_col_stride + n] = a.res ? sumf[i] + a.res[(int64_t)m * a.res_col_stride + n] : sumf[i];
+    for (int ct = 0; ct < CW; ++ct) {
+        const int cb = col0 + 32 * CW * wm + 32 * ct;
+        if (n < a.n_rows) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int m = cb + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (m < a.m_cols)
+                    a.y[(int64_t)m * a.y_col_stride + n] =
+                        a.res ? sumf[ct][i] + a.res[(int64_t)m * a.res_col_stride + n] : sumf[ct][i];
+            }
         }
-    }
-    if (a.kv_cur) {  // the prompt's KV-cache cells, as kq_kv_store computes them (kq_ops.hip)
-        const int hd = a.kv_hd;
+        if (a.kv_cur) {  // the prompt's KV-cache cells, as kq_kv_store computes them (kq_ops.hip)
+            const int hd = a.kv_hd;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int m = col0 + 32 * wm + (i & 3) + 8 * (i >> 2) + 4 * h;
-            const float other = __shfl_xor(sumf[i], 1, 64);  // row n ^ 1: the rope partner
-            const int pos = m < a.m_cols ? a.kv_pos[m] : -1;
-            if (n >= a.n_rows || pos < 0 || pos >= a.kv_n_ctx) continue;  // no cell (its output is NaN)
-            if (a.kv_cur == 1) {
-                const int pr = (n % hd) >> 1;
-                const float *tc = a.kv_rope + (int64_t)pos * (hd / 2) * 2;
-                const bool odd = n & 1;
-                const float2 rk = rope_pair(odd ? other : sumf[i], odd ? sumf[i] : other, tc[2 * pr], tc[2 * pr + 1]);
-                a.kv_k_cache[(int64_t)pos * a.n_rows + n] = h2u(f2h_rne(odd ? rk.y : rk.x));
-            } else {
-                a.kv_v_cache[(int64_t)n * a.kv_n_ctx + pos] = h2u(f2h_rne(sumf[i]));
+            for (int i = 0; i < 16; ++i) {
+                const int m = cb + (i & 3) + 8 * (i >> 2) + 4 * h;
+                const float other = __shfl_xor(sumf[ct][i], 1, 64);  // row n ^ 1: the rope partner
+                const int pos = m < a.m_cols ? a.kv_pos[m] : -1;
+                if (n >= a.n_rows || pos < 0 || pos >= a.kv_n_ctx) continue;  // no cell (its output is NaN)
+                if (a.kv_cur == 1) {
+                    const int pr = (n % hd) >> 1;
+                    const float *tc = a.kv_rope + (int64_t)pos * (hd / 2) * 2;
+                    const bool odd = n & 1;
+                    const float2 rk = rope_pair(odd ? other : sumf[ct][i], odd ? sumf[ct][i] : other, tc[2 * pr], tc[2 * pr + 1]);
+                    a.kv_k_cache[(int64_t)pos * a.n_rows + n] = h2u(f2h_rne(odd ? rk.y : rk.x));
+                } else {
+                    a.kv_v_cache[(int64_t)n * a.kv_n_ctx + pos] = h2u(f2h_rne(sumf[ct][i]));
+                }
             }
         }
     }
 }
 
-template <int TYPE, int RT>
+template <int TYPE, int RT, int CW>
 __global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     mmq_tile_of(a0, a, tx, ty);
-    mmq_tile<TYPE, RT>(a, tx, ty);
+    mmq_tile<TYPE, RT, CW>(a, tx, ty);
 }
 
 // Q4_K and Q6_K matrices on one activation in one launch (a prompt batch's q/k with a
 // Q6_K attn_v): each row tile runs its matrix's kernel body (a0.mtype), LDS sized for Q6_K.
-template <int RT>
+template <int RT, int CW>
 __global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq_mixed(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     const int d = mmq_tile_of(a0, a, tx, ty);
     if (a0.mtype[d] == Q6_K)
-        mmq_tile<Q6_K, RT>(a, tx, ty);
+        mmq_tile<Q6_K, RT, CW>(a, tx, ty);
     else
-        mmq_tile<Q4_K, RT>(a, tx, ty);
+        mmq_tile<Q4_K, RT, CW>(a, tx, ty);
 }
 
-
-template __global__ void kq_mmq<Q4_K, 64>(const MmqArgs a);
-template __global__ void kq_mmq<Q5_K, 64>(const MmqArgs a);
-template __global__ void kq_mmq<Q6_K, 64>(const MmqArgs a);
-template __global__ void kq_mmq_mixed<64>(const MmqArgs a);
-template __global__ void kq_mmq<Q4_K, 128>(const MmqArgs a);
-template __global__ void kq_mmq<Q5_K, 128>(const MmqArgs a);
-template __global__ void kq_mmq<Q6_K, 128>(const MmqArgs a);
-template __global__ void kq_mmq_mixed<128>(const MmqArgs a);
+#define KQ_MMQ_INST(RT, CW)                                         \
+    template __global__ void kq_mmq<Q4_K, RT, CW>(const MmqArgs a); \
+    template __global__ void kq_mmq<Q5_K, RT, CW>(const MmqArgs a); \
+    template __global__ void kq_mmq<Q6_K, RT, CW>(const MmqArgs a); \
+    template __global__ void kq_mmq_mixed<RT, CW>(const MmqArgs a);
+KQ_MMQ_INST(64, 1)
+KQ_MMQ_INST(128, 1)
+KQ_MMQ_INST(128, 2)
 
 }  // namespace kq

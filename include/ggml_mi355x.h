@@ -239,12 +239,14 @@ int mi355x_diag_stamps(void *buf, size_t bytes);
 int mi355x_gemv_impl(int impl);
 /* Prefill (ne11 >= 16) GEMM selector for the int8-MFMA tile kernel: MI355X_MMQ_TILE64
  * (64 weight rows x 64 activation columns per workgroup), MI355X_MMQ_TILE128 (128 rows x
- * 64 columns, 8 waves: the activation tile fetched once per 128 rows) or MI355X_MMQ_AUTO
- * (the library's choice by shape). Same numerics in all. Returns the previous value, or
- * MI355X_E_INVAL. */
+ * 64 columns, 8 waves: the activation tile fetched once per 128 rows), MI355X_MMQ_TILE128W
+ * (128 rows x 128 columns: each wave's weight operands feed two MFMA column tiles) or
+ * MI355X_MMQ_AUTO (the library's choice by shape). Same numerics in all. Returns the
+ * previous value, or MI355X_E_INVAL. */
 #define MI355X_MMQ_AUTO 0
 #define MI355X_MMQ_TILE64 1
 #define MI355X_MMQ_TILE128 2
+#define MI355X_MMQ_TILE128W 3
 int mi355x_mmq_impl(int impl);
 /* Decode GEMV (kq_rows) waves per workgroup (A/B runs, parity of both launch shapes):
  * 0 = by launch size (6 waves under 10 MB of weights, else 12; env MI355X_GEMV_SMALL_MB
