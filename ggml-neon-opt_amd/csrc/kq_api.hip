@@ -571,7 +571,8 @@ int mmq_impl() {
         const char *e = getenv("MI355X_MMQ_IMPL");
         int x = MI355X_MMQ_AUTO;
         if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : strcmp(e, "tile128") == 0 ? MI355X_MMQ_TILE128
-                : strcmp(e, "tile128w") == 0 ? MI355X_MMQ_TILE128W : x;
+                : strcmp(e, "tile128w") == 0 ? MI355X_MMQ_TILE128W
+                : strcmp(e, "tile64w") == 0 ? MI355X_MMQ_TILE64W : x;
         int expect = -1;
         g_mmq_impl.compare_exchange_strong(expect, x);
         v = g_mmq_impl.load();
@@ -586,6 +587,8 @@ int mmq_impl() {
 //  * Q4_K / Q6_K whose 128 x 128 grid has >= 160 workgroups: 128 x 128 (TinyLlama Q6_K head
 //    256 -> 167 us, gate/up 28.3 -> 26.0, 8B ffn_up 98 -> 95); on 128-workgroup grids it
 //    loses 30-40 % (half the CUs idle);
+//  * else Q6_K whose 64 x 128 grid has >= 192 workgroups: 64 x 128 (one 4-wave workgroup per
+//    CU, every register: 8B Q6_K ffn_down 219-226 -> 192-194 us; Q4_K is slower on it);
 //  * else Q4_K whose 128 x 64 grid has >= 256 workgroups: 128 x 64 (8B q/o 33 -> 31, ffn_down
 //    108-116 -> 101-106);
 //  * else 64 x 64 (Q5_K, small grids).
@@ -596,9 +599,11 @@ MmqShape mmq_shape(int type, int64_t rows, int64_t M) {
     const int impl = mmq_impl();
     if (impl == MI355X_MMQ_TILE128) return {128, 1};
     if (impl == MI355X_MMQ_TILE128W) return {128, 2};
+    if (impl == MI355X_MMQ_TILE64W) return {64, 2};
     if (impl == MI355X_MMQ_TILE64) return {64, 1};
     const int64_t rt128 = (rows + 127) / 128;
     if ((type == Q4_K || type == Q6_K) && rt128 * ((M + 127) / 128) >= 160) return {128, 2};
+    if (type == Q6_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
     if (type == Q4_K && rt128 * ((M + 63) / 64) >= 256) return {128, 1};
     return {64, 1};
 }
@@ -609,6 +614,7 @@ const void *mmq_fn(int type, bool mixed, MmqShape sh) {
          : type == Q6_K ? (const void *)kq_mmq<Q6_K, RT, CW>                   \
                         : (const void *)kq_mmq<Q4_K, RT, CW>;
     if (sh.rt == 128 && sh.cw == 2) KQ_MMQ_PICK(128, 2)
+    if (sh.rt == 64 && sh.cw == 2) KQ_MMQ_PICK(64, 2)
     if (sh.rt == 128) KQ_MMQ_PICK(128, 1)
     KQ_MMQ_PICK(64, 1)
 #undef KQ_MMQ_PICK
@@ -1120,7 +1126,7 @@ int mi355x_gemv_impl(int impl) {
 }
 
 int mi355x_mmq_impl(int impl) {
-    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE128W) return MI355X_E_INVAL;
+    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE64W) return MI355X_E_INVAL;
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
     return prev;

@@ -522,8 +522,10 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     }
 }
 
+// (64 x 128: one 4-wave workgroup per CU by LDS, so one wave per SIMD and every register)
+#define KQ_MMQ_WPE_OF(RT, CW) __attribute__((amdgpu_waves_per_eu((RT) == 64 && (CW) == 2 ? 1 : KQ_MMQ_WPE)))
 template <int TYPE, int RT, int CW>
-__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a0) {
+__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_OF(RT, CW) kq_mmq(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     mmq_tile_of(a0, a, tx, ty);
@@ -533,7 +535,7 @@ __global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq(const MmqArgs a
 // Q4_K and Q6_K matrices on one activation in one launch (a prompt batch's q/k with a
 // Q6_K attn_v): each row tile runs its matrix's kernel body (a0.mtype), LDS sized for Q6_K.
 template <int RT, int CW>
-__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq_mixed(const MmqArgs a0) {
+__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_OF(RT, CW) kq_mmq_mixed(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     const int d = mmq_tile_of(a0, a, tx, ty);
@@ -551,5 +553,6 @@ __global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_ATTR kq_mmq_mixed(const Mmq
 KQ_MMQ_INST(64, 1)
 KQ_MMQ_INST(128, 1)
 KQ_MMQ_INST(128, 2)
+KQ_MMQ_INST(64, 2)
 
 }  // namespace kq

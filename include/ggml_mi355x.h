@@ -247,6 +247,7 @@ int mi355x_gemv_impl(int impl);
 #define MI355X_MMQ_TILE64 1
 #define MI355X_MMQ_TILE128 2
 #define MI355X_MMQ_TILE128W 3
+#define MI355X_MMQ_TILE64W 4 /* 64 rows x 128 columns, 4 waves (two column tiles per wave) */
 int mi355x_mmq_impl(int impl);
 /* Decode GEMV (kq_rows) waves per workgroup (A/B runs, parity of both launch shapes):
  * 0 = by launch size (6 waves under 10 MB of weights, else 12; env MI355X_GEMV_SMALL_MB

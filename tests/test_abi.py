@@ -174,9 +174,11 @@ VGPR_BUDGET = [
     (r"^_ZN2kq6kq_mmqILi12ELi(64|128)ELi1E", 160),
     (r"^_ZN2kq6kq_mmqILi13ELi(64|128)ELi1E", 256),
     (r"^_ZN2kq6kq_mmqILi14ELi(64|128)ELi1E", 168),
-    # the wide tiles (two MFMA column tiles per wave, one 8-wave workgroup per CU by LDS):
-    # two waves per SIMD is all they can be resident with, so the budget is 256
+    # the wide tiles (two MFMA column tiles per wave): 128 x 128 is one 8-wave workgroup per
+    # CU by LDS, two waves per SIMD, so the budget is 256; 64 x 128 one 4-wave workgroup,
+    # one wave per SIMD (512, no spill)
     (r"^_ZN2kq6kq_mmqILi1[2-4]ELi128ELi2E", 256),
+    (r"^_ZN2kq6kq_mmqILi1[2-4]ELi64ELi2E", 512),
     (r"^_ZN2kq14kq_attn_decode", 256),
 ]
 
