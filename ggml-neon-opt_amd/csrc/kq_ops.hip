@@ -27,7 +27,6 @@
 #include "kq_common.h"
 #include "kq_internal.h"
 #include "kq_attn_device.h"
-#include "kq_attn_wave.h"
 #include "kq_device.h"
 #include "kq_ops_device.h"
 #include "kq_rows_device.h"
@@ -445,19 +444,6 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     }
 }
 
-// One 64-thread workgroup per query head (kq_attn_wave.h): the same block on one wave, no
-// workgroup barrier; n_ctx <= ATTW_MAX_CTX (MI355X_ATTN_WAVE).
-template <int HD>
-__global__ void __launch_bounds__(64) kq_attn_wave(const AttnArgs a) {
-    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    int h = blockIdx.x;
-    if ((a.n_head & 7) == 0) h = (h & 7) * (a.n_head >> 3) + (h >> 3);  // XCD-aware head order (speed only)
-    const int gsz = a.n_head / a.n_head_kv;
-    const int pos_in = *a.pos;
-    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;  // no cache cell: NaN output, caches untouched
-    attn_head_wave<HD>(a, h, bad ? 0 : pos_in, bad, !bad && (h % gsz) == 0, smem, a.out, (int)threadIdx.x);
-}
-
 // One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read
 // once into LDS and serve its n_head/n_head_kv query heads, one wave each.
 template <int HD>
@@ -830,9 +816,7 @@ int attn_impl() {
     if (v < 0) {
         const char *e = getenv("MI355X_ATTN_IMPL");
         int expect = -1;
-        g_attn_impl.compare_exchange_strong(expect, e && strcmp(e, "group") == 0  ? MI355X_ATTN_GROUP
-                                                    : e && strcmp(e, "wave") == 0 ? MI355X_ATTN_WAVE
-                                                                                  : MI355X_ATTN_HEAD);
+        g_attn_impl.compare_exchange_strong(expect, e && strcmp(e, "group") == 0 ? MI355X_ATTN_GROUP : MI355X_ATTN_HEAD);
         v = g_attn_impl.load();
     }
     return v;
@@ -851,12 +835,6 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
         allow_lds((const void *)kq_attn_group<128>, glds);
         return timed_launch("kq::kq_attn_group<128>", bytes, kq_attn_group<128>, dim3(a.n_head_kv), dim3(64 * nw),
                             glds, s, a);
-    }
-    if (attn_impl() == MI355X_ATTN_WAVE && a.n_ctx <= ATTW_MAX_CTX) {
-        const size_t wl = attw_lds(a.head_dim);
-        if (a.head_dim == 64)
-            return timed_launch("kq::kq_attn_wave<64>", bytes, kq_attn_wave<64>, dim3(a.n_head), dim3(64), wl, s, a);
-        return timed_launch("kq::kq_attn_wave<128>", bytes, kq_attn_wave<128>, dim3(a.n_head), dim3(64), wl, s, a);
     }
     const size_t lds = attn_lds(a.head_dim, a.n_ctx);
     if (a.head_dim == 64)
@@ -1037,7 +1015,7 @@ int mi355x_attn_prompt_impl(int impl) {
 }
 
 int mi355x_attn_impl(int impl) {
-    if (impl != MI355X_ATTN_GROUP && impl != MI355X_ATTN_HEAD && impl != MI355X_ATTN_WAVE) return MI355X_E_INVAL;
+    if (impl != MI355X_ATTN_GROUP && impl != MI355X_ATTN_HEAD) return MI355X_E_INVAL;
     const int prev = attn_impl();
     g_attn_impl.store(impl);
     return prev;

@@ -29,7 +29,7 @@ FLAG_OUTPUT = 1
 E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM = 0, -1, -2, -3, -4, -6
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
-ATTN_GROUP, ATTN_HEAD, ATTN_WAVE = 0, 1, 2
+ATTN_GROUP, ATTN_HEAD = 0, 1
 MMQ_AUTO, MMQ_TILE64, MMQ_TILE128, MMQ_TILE128W, MMQ_TILE64W = 0, 1, 2, 3, 4
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).

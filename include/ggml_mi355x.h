@@ -326,7 +326,6 @@ int mi355x_attn_prompt(const mi355x_attn_desc *a, int n_tokens, void *stream);
  * MI355X_E_INVAL. */
 #define MI355X_ATTN_GROUP 0
 #define MI355X_ATTN_HEAD 1
-#define MI355X_ATTN_WAVE 2 /* decode only: one 64-thread workgroup per query head, n_ctx <= 256 */
 int mi355x_attn_impl(int impl);
 /* Prompt attention selector (A/B runs, parity of both): MI355X_ATTN_GROUP (default: one
  * workgroup per kv group and token, the group's query heads sharing every K/V load, where
