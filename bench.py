@@ -72,21 +72,24 @@ def use_more_bits(i, n):
     return i < n // 8 or i >= 7 * n // 8 or (i - n // 8) % 3 == 2
 
 
-def q4km_chain(model):
+def q4km_chain(model, mix="q4_k_m"):
     """Per-token GEMV chain: list of stages; a stage is a list of (name, type, K, N)
-    sharing one input vector (fused into one launch)."""
+    sharing one input vector (fused into one launch). mix: llama-quant.cpp's Q4_K_M
+    (default) or Q5_K_M [U] (every matrix Q5_K except attn_v / ffn_down of the
+    use_more_bits layers and the output, Q6_K: BASELINE config 5)."""
     m = MODELS[model]
     E, L, KV, FF, V = m["E"], m["L"], m["KV"], m["FF"], m["V"]
     big = model == "llama-3-70b"
+    base = g.TYPE_Q5_K if mix == "q5_k_m" else g.TYPE_Q4_K
     stages = []
     for i in range(L):
         mb = use_more_bits(i, L)
-        v_type = g.TYPE_Q6_K if mb else (g.TYPE_Q5_K if big else g.TYPE_Q4_K)
-        stages.append([(f"blk.{i}.attn_q", g.TYPE_Q4_K, E, E), (f"blk.{i}.attn_k", g.TYPE_Q4_K, E, KV),
+        v_type = g.TYPE_Q6_K if mb else (g.TYPE_Q5_K if big or mix == "q5_k_m" else g.TYPE_Q4_K)
+        stages.append([(f"blk.{i}.attn_q", base, E, E), (f"blk.{i}.attn_k", base, E, KV),
                        (f"blk.{i}.attn_v", v_type, E, KV)])
-        stages.append([(f"blk.{i}.attn_output", g.TYPE_Q4_K, E, E)])
-        stages.append([(f"blk.{i}.ffn_gate", g.TYPE_Q4_K, E, FF), (f"blk.{i}.ffn_up", g.TYPE_Q4_K, E, FF)])
-        stages.append([(f"blk.{i}.ffn_down", g.TYPE_Q6_K if mb else g.TYPE_Q4_K, FF, E)])
+        stages.append([(f"blk.{i}.attn_output", base, E, E)])
+        stages.append([(f"blk.{i}.ffn_gate", base, E, FF), (f"blk.{i}.ffn_up", base, E, FF)])
+        stages.append([(f"blk.{i}.ffn_down", g.TYPE_Q6_K if mb else base, FF, E)])
     stages.append([("output", g.TYPE_Q6_K, E, V)])
     return stages
 
@@ -206,7 +209,7 @@ class Token:
     gate/up, swiglu, down, add], rms_norm, output) on synthetic Q4_K_M weights of the
     real shapes (the chain's weights and type mix, plus token_embd Q4_K and f32 norms)."""
 
-    def __init__(self, model, dev, seed, be, n_ctx, split=None):
+    def __init__(self, model, dev, seed, be, n_ctx, split=None, mix="q4_k_m"):
         from ggml_mi355x.llama import LlamaDecoder, hparams
         from ggml_mi355x.rowsplit import TokenSplit
         m = MODELS[model]
@@ -216,7 +219,8 @@ class Token:
         self.split = TokenSplit(self.hp, *split) if split is not None else None  # (world, rank[, mode])
         gen = torch.Generator(device=dev)
         gen.manual_seed(seed)
-        self.stages = q4km_chain(model)
+        self.mix = mix
+        self.stages = q4km_chain(model, mix)
         w = {}
         self.bytes_per_token = 0  # this GPU's matmul weight bytes per token (its row slices)
         for stage in self.stages:
@@ -228,7 +232,8 @@ class Token:
                     K = 256 * (c1 - c0)
                 w[name] = (typ, random_kquant(typ, r1 - r0, K, gen, dev, rms_keep=True))
                 self.bytes_per_token += w[name][1].numel()
-        w["token_embd"] = (g.TYPE_Q4_K, random_kquant(g.TYPE_Q4_K, m["V"], m["E"], gen, dev))
+        et = g.TYPE_Q5_K if mix == "q5_k_m" else g.TYPE_Q4_K  # token_embd: the mix's base type [U]
+        w["token_embd"] = (et, random_kquant(et, m["V"], m["E"], gen, dev))
         w["output_norm"] = torch.rand(m["E"], device=dev, generator=gen) * 0.4 + 0.8
         for i in range(m["L"]):
             for nm in ("attn_norm", "ffn_norm"):
@@ -403,14 +408,15 @@ def chain_side(model, dev, be, steps=64, warmup=8):
     return out
 
 
-def model_side(model, dev, steps=64, warmup=8):
+def model_side(model, dev, steps=64, warmup=8, mix="q4_k_m"):
     """Another BASELINE config on the same executor: the full decode token of `model`
     (tg<steps> from an empty KV cache, hipGraph replay) and its pp512 (every matmul
-    of the token at ne11 = 512, kq_mmq). Llama-3-8B covers configs 3 (pp512 + tg)
-    and 5 (Q6_K output / attn_v / ffn_down beside Q4_K, one kernel template)."""
+    of the token at ne11 = 512, kq_mmq). Llama-3-8B covers configs 3 (pp512 + tg,
+    Q4_K_M) and 5 (mix "q5_k_m": Q5_K matrices beside the Q6_K output / attn_v /
+    ffn_down, one kernel template)."""
     be = g.Backend(torch.cuda.current_device())
     n_ctx = max(128, (steps + 31) // 32 * 32)
-    tk = Token(model, dev, 0x51A7, be, n_ctx)
+    tk = Token(model, dev, 0x51A7, be, n_ctx, mix=mix)
     for i in range(warmup):
         tk.dec.step(tk.tokens[i], i)
     be.synchronize()
@@ -427,7 +433,7 @@ def model_side(model, dev, steps=64, warmup=8):
     out = {"tg_tok_s": round(1e3 / ms, 1), "ms_per_token": round(ms, 4), "tg_steps": steps,
            "weights_MB_per_token": round(tk.bytes_per_token / 1e6, 1),
            "effective_GBps": round(tk.bytes_per_token / (ms * 1e-3) / 1e9, 1),
-           "launches_per_token": tk.launches(), "pp512_graph": prompt_side(tk, be),
+           "launches_per_token": tk.launches(), "mix": mix, "pp512_graph": prompt_side(tk, be),
            "pp512": prefill_chain(tk, dev)}
     del tk, be
     torch.cuda.empty_cache()
@@ -1024,9 +1030,10 @@ def main():
         if isinstance(chain, Token) and not args.no_chain and world == 1:
             side = chain_side(args.model, dev, be)
         large = None if args.no_large or world > 1 else large_gemv(dev)
-        l3 = None
+        l3 = l3q5 = None
         if isinstance(chain, Token) and not args.no_8b and world == 1 and args.model != "llama-3-8b":
             l3 = model_side("llama-3-8b", dev)
+            l3q5 = model_side("llama-3-8b", dev, mix="q5_k_m")  # BASELINE config 5
         prefill = None if args.no_prefill or world > 1 else prefill_chain(chain, dev)
         pp_graph = None
         if isinstance(chain, Token) and not args.no_prefill and world == 1:
@@ -1081,6 +1088,7 @@ def main():
             "pp512": pp_graph,
             "matmul_chain": side,
             "llama3_8b": l3,
+            "llama3_8b_q5_k_m": l3q5,
             "llama3_70b": l70,
             "replicas": reps,
             "rowsplit": splits,

@@ -584,14 +584,15 @@ int mmq_impl() {
 // (8 waves: the activation tile fetched once per 128 rows), activation columns 64 * CW (CW = 2:
 // each wave's weight operands feed two MFMA column tiles, half the operand-building vector
 // work per MFMA). AUTO, by the grid each shape would launch (profiles/r03_mmq_tiles.txt):
-//  * Q4_K / Q6_K whose 128 x 128 grid has >= 160 workgroups: 128 x 128 (TinyLlama Q6_K head
-//    256 -> 167 us, gate/up 28.3 -> 26.0, 8B ffn_up 98 -> 95); on 128-workgroup grids it
-//    loses 30-40 % (half the CUs idle);
-//  * else Q6_K whose 64 x 128 grid has >= 192 workgroups: 64 x 128 (one 4-wave workgroup per
-//    CU, every register: 8B Q6_K ffn_down 219-226 -> 192-194 us; Q4_K is slower on it);
+//  * a grid of >= 160 workgroups at 128 x 128: 128 x 128 (TinyLlama Q6_K head 256 -> 167 us,
+//    gate/up 28.3 -> 26.0, 8B ffn_up 98 -> 95, 8B Q5_K ffn_up 147 -> 125); on 128-workgroup
+//    grids it loses 30-40 % (half the CUs idle);
+//  * else Q5_K / Q6_K whose 64 x 128 grid has >= 192 workgroups: 64 x 128 (one 4-wave
+//    workgroup per CU, every register: 8B Q6_K ffn_down 219-226 -> 192-194 us, Q5_K ffn_down
+//    149 -> 140, q/o 46 -> 44; Q4_K is slower on it);
 //  * else Q4_K whose 128 x 64 grid has >= 256 workgroups: 128 x 64 (8B q/o 33 -> 31, ffn_down
 //    108-116 -> 101-106);
-//  * else 64 x 64 (Q5_K, small grids).
+//  * else 64 x 64 (small grids).
 struct MmqShape {
     int rt, cw;
 };
@@ -602,8 +603,8 @@ MmqShape mmq_shape(int type, int64_t rows, int64_t M) {
     if (impl == MI355X_MMQ_TILE64W) return {64, 2};
     if (impl == MI355X_MMQ_TILE64) return {64, 1};
     const int64_t rt128 = (rows + 127) / 128;
-    if ((type == Q4_K || type == Q6_K) && rt128 * ((M + 127) / 128) >= 160) return {128, 2};
-    if (type == Q6_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
+    if (rt128 * ((M + 127) / 128) >= 160) return {128, 2};
+    if (type != Q4_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
     if (type == Q4_K && rt128 * ((M + 63) / 64) >= 256) return {128, 1};
     return {64, 1};
 }

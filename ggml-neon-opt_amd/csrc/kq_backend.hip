@@ -853,7 +853,7 @@ int mi355x_backend_supports_op(const mi355x_tensor *op) {
             const mi355x_tensor *w = op->src[0], *ids = op->src[1];
             if (!w || !ids || ids->type != MI355X_TYPE_I32 || !ids->data || ids->nb[0] != 4 || !contig_f32(op))
                 return 0;
-            if (w->type != MI355X_TYPE_F32 && w->type != MI355X_TYPE_Q4_K && w->type != MI355X_TYPE_Q6_K) return 0;
+            if (w->type != MI355X_TYPE_F32 && !is_kquant(w->type)) return 0;
             if (op->ne[1] > 1 && op->nb[1] != (size_t)op->ne[0] * 4) return 0;  // dst rows packed (kernel: out + r*k)
             return op->ne[0] == w->ne[0] && op->ne[1] == ids->ne[0] && w->ne[0] % MI355X_QK_K == 0;
         }

@@ -35,8 +35,8 @@ namespace kq {
 
 // ------------------------------------------------------------ get_rows
 // One workgroup per (id, 2048-element chunk); thread t dequantizes 8 consecutive
-// elements. Q4_K: y = fmaf(d*sc, q, -(dmin*m)) (gcc contracts `d1*q - m1` [U]);
-// Q6_K: y = (d*sc)*q; F32: copy.
+// elements. Q4_K / Q5_K: y = fmaf(d*sc, q, -(dmin*m)) (gcc contracts `d1*q - m1` [U]; Q5_K's
+// q is the nibble + 16 * its qh bit); Q6_K: y = (d*sc)*q; F32: copy.
 __global__ void __launch_bounds__(256) kq_get_rows(int type, const uint8_t *__restrict__ table, int64_t k,
                                                    int64_t row_stride, int64_t n_rows,
                                                    const int32_t *__restrict__ ids, float *__restrict__ out) {
@@ -59,8 +59,9 @@ __global__ void __launch_bounds__(256) kq_get_rows(int type, const uint8_t *__re
     }
     const int64_t b = e0 / QK;
     const int e = (int)(e0 % QK);
-    if (type == MI355X_TYPE_Q4_K) {
-        const uint8_t *blk = row + b * 144;
+    if (type == MI355X_TYPE_Q4_K || type == MI355X_TYPE_Q5_K) {
+        const bool q5 = type == MI355X_TYPE_Q5_K;
+        const uint8_t *blk = row + b * (q5 ? 176 : 144);
         const float d = h2f(*(const uint16_t *)blk), dmin = h2f(*(const uint16_t *)(blk + 2));
         const uint8_t *sc = blk + 4;
         const int j = e / 64, h = (e / 32) & 1, l0 = e % 32;
@@ -74,9 +75,13 @@ __global__ void __launch_bounds__(256) kq_get_rows(int type, const uint8_t *__re
             m = (sc[is + 4] >> 4) | ((sc[is] >> 6) << 4);
         }
         const float d1 = d * (float)s, m1 = dmin * (float)m;
-        const uint8_t *q = blk + 16 + 32 * j + l0;
+        const uint8_t *q = blk + (q5 ? 48 : 16) + 32 * j + l0;
+        const uint8_t *qh = blk + 16 + l0;  // Q5_K: bit 2j + h of qh[l] is the fifth bit
 #pragma unroll
-        for (int i = 0; i < 8; ++i) y[i] = __builtin_fmaf(d1, (float)((q[i] >> (4 * h)) & 0xF), -m1);
+        for (int i = 0; i < 8; ++i) {
+            const int hb = q5 ? ((qh[i] >> (2 * j + h)) & 1) << 4 : 0;
+            y[i] = __builtin_fmaf(d1, (float)(((q[i] >> (4 * h)) & 0xF) + hb), -m1);
+        }
     } else {  // Q6_K
         const uint8_t *blk = row + b * 210;
         const float d = h2f((uint16_t)(blk[208] | (blk[209] << 8)));
@@ -912,7 +917,8 @@ extern "C" {
 int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, int64_t n_rows, const int32_t *ids,
                     int64_t n_ids, float *dst, void *stream) {
     if (!table || !ids || !dst || ne0 <= 0 || n_ids < 0 || n_rows < 0) return MI355X_E_INVAL;
-    if (type != MI355X_TYPE_F32 && type != MI355X_TYPE_Q4_K && type != MI355X_TYPE_Q6_K) return MI355X_E_UNSUPPORTED;
+    if (type != MI355X_TYPE_F32 && type != MI355X_TYPE_Q4_K && type != MI355X_TYPE_Q5_K && type != MI355X_TYPE_Q6_K)
+        return MI355X_E_UNSUPPORTED;
     if (ne0 % (type == MI355X_TYPE_F32 ? 8 : QK)) return MI355X_E_INVAL;
     if (row_stride < mi355x_row_size(type, ne0) && type != MI355X_TYPE_F32) return MI355X_E_INVAL;
     if (n_ids == 0) return MI355X_OK;

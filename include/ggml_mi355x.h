@@ -264,7 +264,7 @@ int mi355x_gemv_waves(int waves);
 
 /* GGML_OP_GET_ROWS (ggml_compute_forward_get_rows_q -> dequantize_row_q4_K,
  * out.folded:103-104): dst[r][0..ne0) = row ids[r] of `table` as f32. type F32 /
- * Q4_K / Q6_K; `n_rows` rows (ne01) of `row_stride` bytes; ids: device int32[n_ids].
+ * Q4_K / Q5_K / Q6_K; `n_rows` rows (ne01) of `row_stride` bytes; ids: device int32[n_ids].
  * An id outside [0, n_rows) (ggml: GGML_ASSERT(i01 >= 0 && i01 < ne01)) reads nothing
  * and writes a NaN row. */
 int mi355x_get_rows(int type, const void *table, int64_t ne0, size_t row_stride, int64_t n_rows,

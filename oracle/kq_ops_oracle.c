@@ -280,6 +280,26 @@ void kqo_get_rows(int type, const void *table, int64_t k, size_t row_stride, con
                     is += 2;
                 }
             }
+        } else if (type == 13) {  /* dequantize_row_q5_K [U], the same contraction as Q4_K */
+            const kqo_block_q5_K *x = (const kqo_block_q5_K *)row;
+            for (int64_t i = 0; i < k / 256; i++) {
+                const uint8_t *ql = x[i].qs, *qh = x[i].qh;
+                const float d = kqo_fp16_to_fp32(x[i].d), min = kqo_fp16_to_fp32(x[i].dmin);
+                int is = 0;
+                uint8_t sc, m, u1 = 1, u2 = 2;
+                for (int j = 0; j < 256; j += 64) {
+                    scale_min_k4(is + 0, x[i].scales, &sc, &m);
+                    const float d1 = d * sc, m1 = min * m;
+                    scale_min_k4(is + 1, x[i].scales, &sc, &m);
+                    const float d2 = d * sc, m2 = min * m;
+                    for (int l = 0; l < 32; ++l) *y++ = fmaf(d1, (float)((ql[l] & 0xF) + (qh[l] & u1 ? 16 : 0)), -m1);
+                    for (int l = 0; l < 32; ++l) *y++ = fmaf(d2, (float)((ql[l] >> 4) + (qh[l] & u2 ? 16 : 0)), -m2);
+                    ql += 32;
+                    is += 2;
+                    u1 <<= 2;
+                    u2 <<= 2;
+                }
+            }
         } else if (type == 14) {
             kqo_dequantize_row_q6_K((const kqo_block_q6_K *)row, y, k);
         }

@@ -36,14 +36,19 @@ def kquant(rng, type_, N, K, rms_keep=True):
     return raw.reshape(N, nb * B)
 
 
-def build(hp, seed=0, v_type=Q4_K):
+def build(hp, seed=0, v_type=Q4_K, mix="q4_k_m"):
     """Host weights: dict name -> (type, uint8 array) for matrices, f32 arrays for norms.
     v_type: attn_v outside the use_more_bits layers (Q4_K; Q5_K in Llama-3-70B's
-    Q4_K_M mix)."""
+    Q4_K_M mix). mix "q5_k_m": llama-quant.cpp's Q5_K_M [U] — every
+    matrix Q5_K (token_embd too) except attn_v / ffn_down of the use_more_bits layers and
+    the output, Q6_K (BASELINE config 5)."""
     rng = np.random.default_rng(seed)
     E, F, V, L = hp["n_embd"], hp["n_ff"], hp["n_vocab"], hp["n_layer"]
     kvw = hp["n_head_kv"] * hp["head_dim"]
-    w = {"token_embd": (Q4_K, kquant(rng, Q4_K, V, E, rms_keep=False)),
+    base = Q5_K if mix == "q5_k_m" else Q4_K
+    if mix == "q5_k_m":
+        v_type = Q5_K
+    w = {"token_embd": (base, kquant(rng, base, V, E, rms_keep=False)),
          "output": (Q6_K, kquant(rng, Q6_K, V, E)),
          "output_norm": rng.uniform(0.8, 1.2, E).astype(np.float32)}
     for i in range(L):
@@ -51,14 +56,15 @@ def build(hp, seed=0, v_type=Q4_K):
         mb = use_more_bits(i, L)
         w[p + "attn_norm"] = rng.uniform(0.8, 1.2, E).astype(np.float32)
         w[p + "ffn_norm"] = rng.uniform(0.8, 1.2, E).astype(np.float32)
-        w[p + "attn_q"] = (Q4_K, kquant(rng, Q4_K, E, E))
-        w[p + "attn_k"] = (Q4_K, kquant(rng, Q4_K, kvw, E))
+        w[p + "attn_q"] = (base, kquant(rng, base, E, E))
+        w[p + "attn_k"] = (base, kquant(rng, base, kvw, E))
         vt = Q6_K if mb else v_type
         w[p + "attn_v"] = (vt, kquant(rng, vt, kvw, E))
-        w[p + "attn_output"] = (Q4_K, kquant(rng, Q4_K, E, E))
-        w[p + "ffn_gate"] = (Q4_K, kquant(rng, Q4_K, F, E))
-        w[p + "ffn_up"] = (Q4_K, kquant(rng, Q4_K, F, E))
-        w[p + "ffn_down"] = (Q6_K if mb else Q4_K, kquant(rng, Q6_K if mb else Q4_K, E, F))
+        w[p + "attn_output"] = (base, kquant(rng, base, E, E))
+        w[p + "ffn_gate"] = (base, kquant(rng, base, F, E))
+        w[p + "ffn_up"] = (base, kquant(rng, base, F, E))
+        dt = Q6_K if mb else base
+        w[p + "ffn_down"] = (dt, kquant(rng, dt, E, F))
     return w
 
 

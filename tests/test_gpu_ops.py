@@ -24,7 +24,7 @@ def O():
 
 
 # ---------------------------------------------------------------- elementwise
-@pytest.mark.parametrize("type_", [0, 12, 14])
+@pytest.mark.parametrize("type_", [0, 12, 13, 14])
 def test_get_rows(dev, O, npo, type_):
     import torch
     import ggml_mi355x as g
@@ -240,27 +240,29 @@ def test_gemv_swiglu_epilogue(dev, O, oracle, npo, impl, n):
 
 
 # ---------------------------------------------------------------- the whole token
-def _decoder(dev, hp, seed, n_ctx, fuse=True):
+def _decoder(dev, hp, seed, n_ctx, fuse=True, mix="q4_k_m"):
     from tests import llama_model as LM
     import ggml_mi355x as g
     from ggml_mi355x.llama import LlamaDecoder
-    w = LM.build(hp, seed)
+    w = LM.build(hp, seed, mix=mix)
     b = g.Backend()
     dec = LlamaDecoder(b, hp, LM.to_device(w, dev), n_ctx, fuse=fuse)
     return w, b, dec
 
 
 @pytest.mark.parametrize("fuse", [True, False], ids=["fused", "unfused"])
-def test_llama_decode_tokens(dev, O, fuse):
-    """Two TinyLlama-width layers (Q4_K_M mix) + a 4096-token vocabulary: the logits and
-    every layer's residual stream of 5 consecutive tokens (hipGraph replay across
-    tokens) bit-exact with the oracle's llm_build_llama restatement."""
+@pytest.mark.parametrize("mix", ["q4_k_m", "q5_k_m"])
+def test_llama_decode_tokens(dev, O, fuse, mix):
+    """Two TinyLlama-width layers (Q4_K_M mix, and the Q5_K_M mix of BASELINE config 5:
+    Q5_K matrices and token_embd beside Q6_K attn_v / ffn_down / output) + a 4096-token
+    vocabulary: the logits and every layer's residual stream of 5 consecutive tokens
+    (hipGraph replay across tokens) bit-exact with the oracle's llm_build_llama restatement."""
     import torch
     from tests import llama_model as LM
     from ggml_mi355x.llama import hparams
     hp = hparams(2048, 2, 32, 4, 5632, 4096)
     n_ctx = 64
-    w, b, dec = _decoder(dev, hp, 3, n_ctx, fuse)
+    w, b, dec = _decoder(dev, hp, 3, n_ctx, fuse, mix=mix)
     model, cache = LM.oracle_model(hp, w, n_ctx)
     tokens = [1, 4095, 17, 17, 300]
     for p, tok in enumerate(tokens):
@@ -413,6 +415,36 @@ def prompt_mmq(request):
     prev = g.mmq_impl(request.param)
     yield request.param
     g.mmq_impl(prev)
+
+
+def test_llama_prompt_q5km(dev, O):
+    """BASELINE config 5's mix (Q5_K matrices, Q6_K attn_v / ffn_down / output) through the
+    prompt graph: the int8-MFMA GEMMs on Q5_K (balanced-byte operands) and Q6_K give the
+    oracle's logits for the last token of a 37-token prompt and the KV caches of decoding
+    the tokens one by one, bit for bit."""
+    from tests import llama_model as LM
+    from ggml_mi355x.llama import hparams
+    hp = hparams(2048, 2, 32, 4, 5632, 4096)
+    n_ctx = 64
+    w, b, dec = _decoder(dev, hp, 6, n_ctx, True, mix="q5_k_m")
+    model, cache = LM.oracle_model(hp, w, n_ctx)
+    tokens = np.random.default_rng(12).integers(0, hp["n_vocab"], size=37).tolist()
+    lg = dec.prompt(tokens, 0)
+    b.synchronize()
+    got = lg.cpu().numpy().copy()
+    kc = [c.clone() for c in dec.k_cache]
+    vc = [c.clone() for c in dec.v_cache]
+    for p, tok in enumerate(tokens):
+        ref, _ = O.decode_token(model, tok, p, cache)
+    assert bits_equal(got, ref), first_mismatch(got, ref)
+    dec.reset()
+    for p, tok in enumerate(tokens):
+        dec.step(tok, p)
+    b.synchronize()
+    for i in range(hp["n_layer"]):
+        assert (dec.k_cache[i].cpu().numpy() == kc[i].cpu().numpy()).all(), i
+        assert (dec.v_cache[i].cpu().numpy() == vc[i].cpu().numpy()).all(), i
+    b.close()
 
 
 @pytest.mark.parametrize("hd", [64, 128])

@@ -273,3 +273,41 @@ def test_softmax_group_sum_exactness_argument():
     d = np.array([1.0, 2.0 ** -53, 2.0 ** -53], np.float64)
     seq = (d[0] + d[1]) + d[2]
     assert seq != d[0] + (d[1] + d[2])
+
+
+def test_get_rows_q5K_matches_numpy_restatement(O):
+    """get_rows on a Q5_K table (dequantize_row_q5_K [U], the fifth bit from qh, gcc's
+    contraction of d1*q - m1 as in Q4_K) equals an independent numpy restatement with an
+    exact float32 fma, bit for bit."""
+    from oracle import kq_oracle_np as N
+    rng = np.random.default_rng(5)
+    K, R = 512, 6
+    nb = K // 256
+    raw = rng.integers(0, 256, size=(R, nb, 176), dtype=np.uint8)
+    d = rng.uniform(2.0 ** -14, 2.0 ** -6, size=(R, nb)).astype(np.float16).view(np.uint8).reshape(R, nb, 2)
+    dm = rng.uniform(2.0 ** -14, 2.0 ** -6, size=(R, nb)).astype(np.float16).view(np.uint8).reshape(R, nb, 2)
+    raw[..., 0:2], raw[..., 2:4] = d, dm
+    table = raw.reshape(R, nb * 176)
+    ids = np.array([3, 0, 5], np.int32)
+    got = O.get_rows(13, table, K, ids)
+    for r, i in enumerate(ids):
+        ref = []
+        for b in range(nb):
+            blk = table[i, 176 * b: 176 * (b + 1)]
+            dd = N.fp16_to_f32(blk[0:2].view(np.uint16))[0]
+            mn = N.fp16_to_f32(blk[2:4].view(np.uint16))[0]
+            sc, qh, qs = blk[4:16].astype(np.int32), blk[16:48].astype(np.int32), blk[48:176].astype(np.int32)
+
+            def scale_min(j):  # get_scale_min_k4 [U]
+                if j < 4:
+                    return sc[j] & 63, sc[j + 4] & 63
+                return (sc[j + 4] & 0xF) | ((sc[j - 4] >> 6) << 4), (sc[j + 4] >> 4) | ((sc[j] >> 6) << 4)
+            for j in range(4):
+                for h in range(2):
+                    s, m = scale_min(2 * j + h)
+                    q = ((qs[32 * j: 32 * j + 32] >> (4 * h)) & 0xF) + ((qh >> (2 * j + h)) & 1) * 16
+                    d1 = np.float32(dd * np.float32(s))
+                    m1 = np.float32(mn * np.float32(m))
+                    ref.append(N.fma_f32(np.full(32, d1, np.float32), q.astype(np.float32), np.full(32, -m1, np.float32)))
+        ref = np.concatenate(ref)
+        assert (got[r].view(np.uint32) == ref.view(np.uint32)).all(), r
