@@ -684,10 +684,13 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     for (int d = 1; d < n_mat; ++d) mixed |= types[d] != type;
     if (mixed)
         for (int d = 0; d < n_mat; ++d)
-            if (types[d] != Q4_K && types[d] != Q6_K) return MI355X_E_INVAL;
+            if (types[d] != Q4_K && types[d] != Q5_K && types[d] != Q6_K) return MI355X_E_INVAL;
     int64_t all_rows = 0;
     for (int d = 0; d < n_mat; ++d) all_rows += N[d];
-    const MmqShape sh = mmq_shape(types[0], all_rows, M);  // (Q6_K beside Q4_K: on Q4_K's choice)
+    MmqShape sh = mmq_shape(types[0], all_rows, M);  // (several types: on the first one's choice)
+    bool has_q5 = false;
+    for (int d = 0; d < n_mat; ++d) has_q5 |= types[d] == Q5_K;
+    if (mixed && has_q5 && sh.rt == 128 && sh.cw == 2) sh = {128, 1};  // kq_mmq_mixed<128, 2> has no Q5_K body
     const int rt = sh.rt;
     MmqArgs a;
     memset(&a, 0, sizeof(a));

@@ -265,11 +265,9 @@ bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
     return b->workspace_size >= mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], x->ne[1]);
 }
 
-// MUL_MATs that can share one tile-GEMM launch: one type, or Q4_K beside Q6_K (kq_mmq_mixed:
-// a prompt batch's q/k with the Q6_K attn_v of use_more_bits layers)
-bool multi_types_ok(int a, int b) {
-    return a == b || ((a == MI355X_TYPE_Q4_K || a == MI355X_TYPE_Q6_K) && (b == MI355X_TYPE_Q4_K || b == MI355X_TYPE_Q6_K));
-}
+// MUL_MATs that can share one tile-GEMM launch: one type, or K-quants of different types
+// (kq_mmq_mixed: a prompt batch's Q4_K / Q5_K q/k with the Q6_K attn_v of use_more_bits layers)
+bool multi_types_ok(int a, int b) { return a == b || (is_kquant(a) && is_kquant(b)); }
 
 std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const *nodes, int n, bool fuse) {
     std::vector<Launch> out;

@@ -532,17 +532,22 @@ __global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_OF(RT, CW) kq_mmq(const Mmq
     mmq_tile<TYPE, RT, CW>(a, tx, ty);
 }
 
-// Q4_K and Q6_K matrices on one activation in one launch (a prompt batch's q/k with a
+// Q4_K / Q5_K and Q6_K matrices on one activation in one launch (a prompt batch's q/k with a
 // Q6_K attn_v): each row tile runs its matrix's kernel body (a0.mtype), LDS sized for Q6_K.
 template <int RT, int CW>
 __global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_OF(RT, CW) kq_mmq_mixed(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     const int d = mmq_tile_of(a0, a, tx, ty);
-    if (a0.mtype[d] == Q6_K)
+    if (a0.mtype[d] == Q6_K) {
         mmq_tile<Q6_K, RT, CW>(a, tx, ty);
-    else
+    } else if (a0.mtype[d] == Q5_K) {
+        // (the host never launches a Q5_K matrix on the mixed 128 x 128 tiles: beside the
+        // Q6_K body its registers would spill; launch_mmq_multi takes 128 x 64 there)
+        if constexpr (!(RT == 128 && CW == 2)) mmq_tile<Q5_K, RT, CW>(a, tx, ty);
+    } else {
         mmq_tile<Q4_K, RT, CW>(a, tx, ty);
+    }
 }
 
 #define KQ_MMQ_INST(RT, CW)                                         \
