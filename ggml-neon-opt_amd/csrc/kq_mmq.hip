@@ -194,17 +194,6 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *B
             sumf[ct][i] = fmaf(xd * yd[16 * ct + i], (float)(256 * shi[ct][i] + slo[ct][i]), sumf[ct][i]);
 }
 
-// Balanced int8 bytes of four unsigned quants x (bytes 0..31) times a 6-bit scale:
-// T = q*sc + 128 per 16-bit lane (q*sc <= 1953, no carry out of the lane), hi = T >> 8,
-// lo = (T & 255) - 128, so q*sc = 256*hi + lo with hi in [0, 8], lo in [-128, 127].
-__device__ __forceinline__ void balanced_bytes(uint32_t x, u16x2 scp, uint32_t &hi, uint32_t &lo) {
-    const u16x2 c128 = {128, 128};
-    const uint32_t t0 = as_u32(as_u16x2(__builtin_amdgcn_perm(0u, x, 0x0c010c00u)) * scp + c128);  // values 0, 1
-    const uint32_t t1 = as_u32(as_u16x2(__builtin_amdgcn_perm(0u, x, 0x0c030c02u)) * scp + c128);  // values 2, 3
-    lo = __builtin_amdgcn_perm(t1, t0, 0x06040200u) ^ 0x80808080u;
-    hi = __builtin_amdgcn_perm(t1, t0, 0x07050301u);
-}
-
 // XCD-aware tile order: workgroups are dealt round-robin over the 8 XCDs (speed only,
 // MI355X_MICROARCH.md), so the column tiles of one row tile go to blocks L, L + 8,
 // L + 16, ... (one XCD): the weight tile is fetched into that XCD's L2 once and
@@ -325,17 +314,19 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         }
         const uint8_t *buf = smem + (b & 1) * BUF;
         const uint8_t *At[CW];  // this lane's activation column of each tile
-        float yd[16 * CW];      // y.d of the columns each accumulator element belongs to
 #pragma unroll
-        for (int ct = 0; ct < CW; ++ct) {
-            const int cb = 32 * CW * wm + 32 * ct;
-            At[ct] = buf + (cb + r) * Q8L_STRIDE;
-#pragma unroll
-            for (int i = 0; i < 16; ++i)
-                yd[16 * ct + i] = *(const float *)(buf + (cb + (i & 3) + 8 * (i >> 2) + 4 * h) * Q8L_STRIDE);
-        }
+        for (int ct = 0; ct < CW; ++ct) At[ct] = buf + (32 * CW * wm + 32 * ct + r) * Q8L_STRIDE;
+        // y.d of the column accumulator element i of tile ct belongs to (read where it is used)
+        auto yd_of = [&](int ct, int i) {
+            return *(const float *)(buf + (32 * CW * wm + 32 * ct + (i & 3) + 8 * (i >> 2) + 4 * h) * Q8L_STRIDE);
+        };
         const uint8_t *Bt = buf + A_BYTES + (32 * wn + r) * mmq_row_bytes(TYPE);  // this lane's weight row
         if (TYPE == Q6_K) {
+            float yd[16 * CW];
+#pragma unroll
+            for (int ct = 0; ct < CW; ++ct)
+#pragma unroll
+                for (int i = 0; i < 16; ++i) yd[16 * ct + i] = yd_of(ct, i);
             q6_superblock<CW>(a, Bt, At, yd, row0 + 32 * wn + r, b, h, sumf);
             if (!KQ_MMQ_ONEBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             continue;
@@ -347,7 +338,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         const uint32_t s47 = (hdr.w & 0x0f0f0f0fu) | ((hdr.y >> 2) & 0x30303030u);
         const SplitScales ss = split_scales(s03, s47);
         const uint32_t m47 = ((hdr.w >> 4) & 0x0f0f0f0fu) | ((hdr.z >> 2) & 0x30303030u);
-        // Q4_K: sumi = 8*s8 + s1 (scale split into 3-bit halves); Q5_K: 256*s8 + s1 (balanced bytes)
+        // Q4_K / Q5_K: sumi = 8*s8 + s1 (scale split into 3-bit halves; Q5_K's fifth bit in s8)
         i32x16 sumi[CW], s8[CW], s1[CW];
 #pragma unroll
         for (int ct = 0; ct < CW; ++ct) sumi[ct] = s8[ct] = s1[ct] = i32x16{};
@@ -357,7 +348,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         for (int jp = 0; jp < 4; ++jp) {
             const u32x4 qv = *(const u32x4 *)(Bt + (TYPE == Q5_K ? 48 : 16) + 32 * jp + 16 * h);
             u32x4 lo = qv & 0x0f0f0f0fu, hi = (qv >> 4) & 0x0f0f0f0fu;
-            if (TYPE == Q5_K) {
+            if (TYPE == Q5_K && KQ_MMQ_Q5_VALU) {  // the whole 5-bit quant (the VALU-scaled experiment)
                 lo = lo | (((qh >> (uint32_t)(2 * jp)) & 0x01010101u) << 4);
                 hi = hi | (((qh >> (uint32_t)(2 * jp + 1)) & 0x01010101u) << 4);
             }
@@ -407,29 +398,37 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                     s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&b1hi, s1[ct], 0, 0, 0);
                 }
             } else if (TYPE == Q5_K && !KQ_MMQ_Q5_VALU) {
-                // Q5_K: q (5 bits) x sc (6 bits) <= 1953 does not split into int8 halves, so the
-                // scaled weight W = sc*q rides in two balanced int8 bytes as for Q6_K: one packed
-                // 16-bit multiply-add per two values gives T = W + 128, whose high byte is
-                // hi in [0, 8] and whose low byte xor 0x80 is lo in [-128, 127], W = 256*hi + lo.
-                // Both sums accumulate over the superblock in the matrix core (exact int32,
-                // |256*S_hi| < 2^27): sumi = 256*S_hi + S_lo, no per-sub-block VALU scaling and
-                // no MFMA result consumed right after its issue.
-                const u16x2 scl = {(uint16_t)sc_lo, (uint16_t)sc_lo}, sch = {(uint16_t)sc_hi, (uint16_t)sc_hi};
-                u32x4 bhl, bll, bhh, blh;  // hi / lo bytes of the lo-nibble and hi-nibble sub-blocks
+                // Q5_K: q = ql + 16 qh (ql the nibble, qh the fifth bit) and, as for Q4_K,
+                // sc = 8 sh + sl (3-bit halves): W = sc q = 8 (sh ql + 2 sc qh) + sl ql with
+                // sh ql, sl ql <= 105 and 2 sc qh <= 126 all int8, so three MFMAs per sub-block,
+                // two of them into the x8 sum, accumulate over the superblock in the matrix core:
+                // sumi = 8 S8 + S1 (exact int32). The packed 16-bit multiplies scale two bytes
+                // per lane half without carries, as in the Q4_K split.
+                const int kb = 2 * (jp & 1);  // bytes of sub-blocks 2jp, 2jp+1 in their word
+                const u16x2 lh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb));
+                const u16x2 ll = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb));
+                const u16x2 hh = as_u16x2(bcast16(jp < 2 ? ss.sh03 : ss.sh47, kb + 1));
+                const u16x2 hl = as_u16x2(bcast16(jp < 2 ? ss.sl03 : ss.sl47, kb + 1));
+                const u16x2 scl = {(uint16_t)(2 * sc_lo), (uint16_t)(2 * sc_lo)};
+                const u16x2 sch = {(uint16_t)(2 * sc_hi), (uint16_t)(2 * sc_hi)};
 #pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    uint32_t th, tl;
-                    balanced_bytes(lo[k], scl, th, tl);
-                    bhl[k] = th, bll[k] = tl;
-                    balanced_bytes(hi[k], sch, th, tl);
-                    bhh[k] = th, blh[k] = tl;
-                }
+                for (int half = 0; half < 2; ++half) {  // sub-block 2jp (lo nibbles), then 2jp+1
+                    const u32x4 &qn = half ? hi : lo;
+                    const u16x2 m8 = half ? hh : lh, m1 = half ? hl : ll, mq = half ? sch : scl;
+                    u32x4 b8, b1, bq;
 #pragma unroll
-                for (int ct = 0; ct < CW; ++ct) {
-                    s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&bhl, s8[ct], 0, 0, 0);
-                    s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&alo[ct], *(const i32x4m *)&bll, s1[ct], 0, 0, 0);
-                    s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&bhh, s8[ct], 0, 0, 0);
-                    s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&ahi[ct], *(const i32x4m *)&blh, s1[ct], 0, 0, 0);
+                    for (int k = 0; k < 4; ++k) {
+                        b8[k] = as_u32(as_u16x2(qn[k]) * m8);
+                        b1[k] = as_u32(as_u16x2(qn[k]) * m1);
+                        bq[k] = as_u32(as_u16x2((qh[k] >> (uint32_t)(2 * jp + half)) & 0x01010101u) * mq);
+                    }
+#pragma unroll
+                    for (int ct = 0; ct < CW; ++ct) {
+                        const u32x4 &av = half ? ahi[ct] : alo[ct];
+                        s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&av, *(const i32x4m *)&b8, s8[ct], 0, 0, 0);
+                        s1[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&av, *(const i32x4m *)&b1, s1[ct], 0, 0, 0);
+                        s8[ct] = __builtin_amdgcn_mfma_i32_32x32x32_i8(*(const i32x4m *)&av, *(const i32x4m *)&bq, s8[ct], 0, 0, 0);
+                    }
                 }
             } else {  // Q5_K in the KQ_MMQ_Q5_VALU experiment build (and Q4_K in KQ_MMQ_Q4_VALU):
                       // per-sub-block dots scaled on VALU
@@ -453,7 +452,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             }
             if (TYPE == Q5_K && !KQ_MMQ_Q5_VALU) {
 #pragma unroll
-                for (int i = 0; i < 16; ++i) sumi[ct][i] = 256 * s8[ct][i] + s1[ct][i];
+                for (int i = 0; i < 16; ++i) sumi[ct][i] = 8 * s8[ct][i] + s1[ct][i];
             }
         }
         // summins = sum_j mn_j * bs_j exactly on one f16 MFMA 32x32x16 per tile (bs_j =
@@ -471,7 +470,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             const f32x16 mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
-                const float y = yd[16 * ct + i];
+                const float y = yd_of(ct, i);
                 if (KQ_MMQ_DIAG & 1) {  // diagnostics (timing only)
                     sumf[ct][i] += (float)sumi[ct][i] + mins[i] + y;
                 } else if (TYPE == Q5_K) {
