@@ -587,11 +587,12 @@ int mmq_impl() {
 //  * a grid of >= 160 workgroups at 128 x 128: 128 x 128 (TinyLlama Q6_K head 256 -> 167 us,
 //    gate/up 28.3 -> 26.0, 8B ffn_up 98 -> 95, 8B Q5_K ffn_up 147 -> 125); on 128-workgroup
 //    grids it loses 30-40 % (half the CUs idle);
-//  * else Q5_K / Q6_K whose 64 x 128 grid has >= 192 workgroups: 64 x 128 (one 4-wave
-//    workgroup per CU, every register: 8B Q6_K ffn_down 219-226 -> 192-194 us, Q5_K ffn_down
-//    149 -> 140, q/o 46 -> 44; Q4_K is slower on it);
-//  * else Q4_K whose 128 x 64 grid has >= 256 workgroups: 128 x 64 (8B q/o 33 -> 31, ffn_down
-//    108-116 -> 101-106);
+//  * else Q6_K whose 64 x 128 grid has >= 192 workgroups: 64 x 128 (one 4-wave workgroup
+//    per CU, every register: 8B Q6_K ffn_down 219-226 -> 192-194 us; Q4_K / Q5_K are slower
+//    on it);
+//  * else Q4_K / Q5_K whose 128 x 64 grid has >= 256 workgroups: 128 x 64 (8B q/o 33 -> 31,
+//    ffn_down 108-116 -> 101-106; Q5_K q/o 42.4 -> 40.5, ffn_down 132 -> 128 with the
+//    three-MFMA Q5_K split, profiles/r03_mmq_q5_tiles.txt);
 //  * else 64 x 64 (small grids).
 struct MmqShape {
     int rt, cw;
@@ -604,8 +605,8 @@ MmqShape mmq_shape(int type, int64_t rows, int64_t M) {
     if (impl == MI355X_MMQ_TILE64) return {64, 1};
     const int64_t rt128 = (rows + 127) / 128;
     if (rt128 * ((M + 127) / 128) >= 160) return {128, 2};
-    if (type != Q4_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
-    if (type == Q4_K && rt128 * ((M + 63) / 64) >= 256) return {128, 1};
+    if (type == Q6_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
+    if (type != Q6_K && rt128 * ((M + 63) / 64) >= 256) return {128, 1};
     return {64, 1};
 }
 const void *mmq_fn(int type, bool mixed, MmqShape sh) {
