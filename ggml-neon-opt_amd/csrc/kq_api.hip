@@ -28,6 +28,10 @@ template <int TYPE, int RT, int CW>
 __global__ void kq_mmq(const MmqArgs a);
 template <int RT, int CW>
 __global__ void kq_mmq_mixed(const MmqArgs a);
+__global__ void kq_quantize_f16img(const float *x, int64_t x_stride, uint8_t *img, uint8_t *bs, int nb, int64_t nblocks);
+template <int TYPE>
+__global__ void kq_mmf(const MmfArgs a);
+__global__ void kq_mmf_reduce(const float *slab, int n_split, int m_cols, int n_rows, float *y, int64_t y_col_stride);
 
 namespace {
 
@@ -666,6 +670,123 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     return e == hipSuccess ? MI355X_OK : (int)e;
 }
 
+// ------------------------------------------- prefill on the f16 matrix core (stated tolerance)
+// mi355x_prefill_precision: MI355X_PREFILL_EXACT (kq_mmq, bit-exact, the default) or
+// MI355X_PREFILL_F16 (kq_mmf: the reference's Q8_K activation and integer unpacking, the
+// accumulated dot on v_mfma_f32_32x32x16_f16 within the tolerance of kq_mmf.hip's header).
+// -1 until first read from MI355X_PREFILL ("f16" / "exact").
+std::atomic<int> g_prefill{-1};
+int prefill_precision() {
+    int v = g_prefill.load();
+    if (v < 0) {
+        const char *e = getenv("MI355X_PREFILL");
+        const int x = e && strcmp(e, "f16") == 0 ? MI355X_PREFILL_F16 : MI355X_PREFILL_EXACT;
+        int expect = -1;
+        g_prefill.compare_exchange_strong(expect, x);
+        v = g_prefill.load();
+    }
+    return v;
+}
+
+// K split of kq_mmf: double it while the grid has fewer workgroups than CUs and every
+// split keeps >= 4 superblocks (8 half-superblock steps); splits combine in order.
+struct MmfPlan {
+    int n_ct, n_rt, n_split, nbs;
+};
+MmfPlan mmf_plan(int64_t N, int64_t M, int64_t nb) {
+    MmfPlan p;
+    p.n_ct = (int)((M + MMF_COLS - 1) / MMF_COLS);
+    p.n_rt = (int)((N + MMF_RT - 1) / MMF_RT);
+    int s = 1;
+    while ((int64_t)p.n_ct * p.n_rt * s < 256 && nb >= 8 * s) s *= 2;
+    p.nbs = (int)((nb + s - 1) / s);
+    p.n_split = (int)((nb + p.nbs - 1) / p.nbs);
+    return p;
+}
+size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
+// workspace: activation image + d*bsum16 (+ the split-K slabs)
+size_t mmf_workspace(int64_t N, int64_t M, int64_t nb) {
+    const MmfPlan p = mmf_plan(N, M, nb);
+    size_t w = al256((size_t)M * nb * MMF_IMG) + al256((size_t)M * nb * MMF_BSB);
+    if (p.n_split > 1) w += al256((size_t)p.n_split * M * N * 4);
+    return w;
+}
+bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M) {
+    if (prefill_precision() != MI355X_PREFILL_F16) return false;
+    if (!rows_enabled() || M < kMmqMinCols || N <= 0) return false;
+    if (type != Q4_K && type != Q5_K && type != Q6_K) return false;
+    if (N >= (1ll << 31) || M >= (1ll << 31)) return false;
+    if (type == Q6_K) return true;  // 210-B blocks: unaligned vector loads
+    return ((uintptr_t)w & 15u) == 0 && (row_stride & 15u) == 0;
+}
+
+int launch_mmf(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const float *x, int64_t x_stride,
+               int64_t M, float *y, int64_t y_col_stride, uint8_t *ws, hipStream_t stream) {
+    const int64_t nb = K / QK;
+    const MmfPlan p = mmf_plan(N, M, nb);
+    uint8_t *img = ws, *bs = ws + al256((size_t)M * nb * MMF_IMG);
+    float *slab = (float *)(bs + al256((size_t)M * nb * MMF_BSB));
+    const int64_t nblocks = nb * M;
+    const int64_t qwgs = (nblocks + WAVES_PER_WG - 1) / WAVES_PER_WG;
+    hipEvent_t e0, e1;
+    if (timing_slot(stream, e0, e1)) {
+        hipExtLaunchKernelGGL(kq_quantize_f16img, dim3((unsigned)qwgs), dim3(WG_THREADS), 0, stream, e0, e1, 0, x,
+                              x_stride, img, bs, (int)nb, nblocks);
+        timing_log("kq::kq_quantize_f16img", (double)nblocks * (QK * 4.0 + MMF_IMG + MMF_BSB), e0, e1);
+    } else {
+        hipLaunchKernelGGL(kq_quantize_f16img, dim3((unsigned)qwgs), dim3(WG_THREADS), 0, stream, x, x_stride, img, bs,
+                           (int)nb, nblocks);
+    }
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    MmfArgs a;
+    memset(&a, 0, sizeof(a));
+    a.w = (const uint8_t *)w;
+    a.row_stride = (int64_t)row_stride;
+    a.n_rows = (int)N;
+    a.img = img;
+    a.bs = bs;
+    a.m_cols = (int)M;
+    a.y = y;
+    a.y_col_stride = y_col_stride;
+    a.slab = slab;
+    a.nb = (int)nb;
+    a.nbs = p.nbs;
+    a.n_split = p.n_split;
+    a.n_ct = p.n_ct;
+    const void *fn = type == Q5_K ? (const void *)kq_mmf<Q5_K> : type == Q6_K ? (const void *)kq_mmf<Q6_K>
+                                                                              : (const void *)kq_mmf<Q4_K>;
+    const size_t lds = 2 * (size_t)MMF_BUF;
+    allow_lds(fn, lds);
+    const dim3 grid((unsigned)((int64_t)p.n_ct * p.n_rt * p.n_split)), block(256);
+    void *args[] = {&a};
+    if (timing_slot(stream, e0, e1)) {
+        e = hipExtLaunchKernel(fn, grid, block, args, lds, stream, e0, e1, 0);
+        timing_log(std::string("kq::kq_mmf<") + std::to_string(type) + ">",
+                   (double)N * nb * block_bytes(type) + (double)M * nb * (MMF_IMG + MMF_BSB) + (double)M * N * 4.0, e0,
+                   e1);
+    } else {
+        e = hipLaunchKernel(fn, grid, block, args, lds, stream);
+    }
+    if (e != hipSuccess) return (int)e;
+    e = hipGetLastError();
+    if (e != hipSuccess) return (int)e;
+    if (p.n_split > 1) {
+        const int64_t total = M * N;
+        const dim3 rg((unsigned)((total + 255) / 256));
+        if (timing_slot(stream, e0, e1)) {
+            hipExtLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, e0, e1, 0, (const float *)slab, p.n_split,
+                                  (int)M, (int)N, y, y_col_stride);
+            timing_log("kq::kq_mmf_reduce", (double)total * 4.0 * (p.n_split + 1), e0, e1);
+        } else {
+            hipLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, (const float *)slab, p.n_split, (int)M, (int)N, y,
+                               y_col_stride);
+        }
+        e = hipGetLastError();
+    }
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
 // Whether launch_mmq would run this GEMM on the 64 x 64 tile kernel: every GEMM since the
 // streamed kernel was removed (kept as the backend's batching test).
 bool mmq_tile64(int type, int64_t N, int64_t M) {
@@ -902,7 +1023,7 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
 uint64_t api_selector_key() {
     rows_enabled();  // resolve the environment defaults first
     return (uint64_t)(uint32_t)(g_impl.load() + 1) | ((uint64_t)(uint32_t)g_rows_waves.load() << 8) |
-           ((uint64_t)(uint32_t)(mmq_impl() + 1) << 16);
+           ((uint64_t)(uint32_t)(mmq_impl() + 1) << 16) | ((uint64_t)(uint32_t)(prefill_precision() + 1) << 24);
 }
 
 }  // namespace kq
@@ -1016,10 +1137,14 @@ void mi355x_quantize_row_q8_K(const float *x, void *y, int64_t k) {
 }
 
 size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, int64_t ne11) {
-    (void)ne01;
     if (!block_bytes(src0_type) || ne00 <= 0 || ne00 % QK || ne11 < 0) return 0;
     if (ne11 == 0 || (ne11 == 1 && ne00 / QK <= kFusedQMaxNb)) return 0;
-    const size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * Q8L_STRIDE;  // >= raw 292-B blocks
+    size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * Q8L_STRIDE;  // >= raw 292-B blocks
+    // the f16 prefill path (mi355x_prefill_precision) may run instead at ne11 >= 16
+    if (ne11 >= kMmqMinCols && ne01 > 0) {
+        const size_t f = mmf_workspace(ne01, ne11, ne00 / QK);
+        bytes = f > bytes ? f : bytes;
+    }
     return (bytes + 255) & ~(size_t)255;
 }
 
@@ -1064,6 +1189,11 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     }
     size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
+    if (mmf_applies(src0_type, src0, ne01, nb01, ne11) && ((uintptr_t)workspace & 15u) == 0) {
+        if (!device_ok()) return MI355X_E_NODEVICE;
+        return launch_mmf(src0_type, src0, ne00, ne01, nb01, src1, (int64_t)(nb11 / 4), ne11, dst, (int64_t)(nb1 / 4),
+                          (uint8_t *)workspace, (hipStream_t)stream);
+    }
     if (mmq_applies(src0_type, src0, ne01, nb01, ne11) && ((uintptr_t)workspace & 15u) == 0) {
         if (!device_ok()) return MI355X_E_NODEVICE;
         int rc = launch_quantize_q8L(src1, (int64_t)(nb11 / 4), workspace, ne00, ne11, (hipStream_t)stream, true);
@@ -1134,6 +1264,14 @@ int mi355x_mmq_impl(int impl) {
     if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE64W) return MI355X_E_INVAL;
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
+    return prev;
+}
+
+int mi355x_prefill_precision(int precision) {
+    if (precision < 0) return prefill_precision();  // query
+    if (precision > MI355X_PREFILL_F16) return MI355X_E_INVAL;
+    const int prev = prefill_precision();
+    g_prefill.store(precision);
     return prev;
 }
 

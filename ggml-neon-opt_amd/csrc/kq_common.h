@@ -242,4 +242,30 @@ struct MmqArgs {
     int64_t my_col_stride[4];
 };
 
+// ------------------------------------------- batched (prefill) f16 MFMA GEMM, stated tolerance
+// kq_mmf (MI355X_PREFILL_F16): 128 weight rows x 128 activation columns per 4-wave
+// workgroup, K in half-superblock steps. The activation goes through kq_quantize_f16img
+// (the reference's Q8_K quantization, then f16(d*q) in the kernel's k order, 512 B per
+// superblock, plus f16(d*bsum16) x 16 = 32 B), the weights are dequantized in registers.
+constexpr int MMF_RT = 128;                      // weight rows per workgroup (4 waves x 32)
+constexpr int MMF_COLS = 128;                    // activation columns per workgroup (4 MFMA tiles)
+constexpr int MMF_IMG = 512;                     // f16 image bytes per superblock and column
+constexpr int MMF_BSB = 32;                      // f16 d*bsum16 bytes per superblock and column
+constexpr int MMF_BUF = MMF_COLS * (MMF_IMG / 2 + MMF_BSB);  // one half-superblock LDS buffer (36 KB)
+struct MmfArgs {
+    const uint8_t *w;          // weight rows
+    int64_t row_stride;        // bytes
+    int n_rows;
+    const uint8_t *img;        // activation image, column j at img + j * nb * 512
+    const uint8_t *bs;         // d*bsum16, column j at bs + j * nb * 32
+    int m_cols;
+    float *y;                  // dst column j at y + j * y_col_stride (n_split == 1)
+    int64_t y_col_stride;      // floats
+    float *slab;               // n_split > 1: partial sums [n_split][m_cols][n_rows]
+    int nb;                    // superblocks of K
+    int nbs;                   // superblocks per K split
+    int n_split;
+    int n_ct;                  // column tiles
+};
+
 }  // namespace kq

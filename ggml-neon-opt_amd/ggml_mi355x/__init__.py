@@ -31,6 +31,7 @@ PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 ATTN_GROUP, ATTN_HEAD = 0, 1
 MMQ_AUTO, MMQ_TILE64, MMQ_TILE128, MMQ_TILE128W, MMQ_TILE64W = 0, 1, 2, 3, 4
+PREFILL_EXACT, PREFILL_F16 = 0, 1
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -54,6 +55,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_comm_id_size", "mi355x_comm_get_unique_id", "mi355x_backend_set_comm", "mi355x_backend_comm_world",
     "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph", "mi355x_attn_impl",
     "mi355x_mmq_impl",
+    "mi355x_prefill_precision",
     "mi355x_gemv_waves",
     "mi355x_attn_prompt",
     "mi355x_attn_prompt_impl",
@@ -200,6 +202,8 @@ def lib():
     L.mi355x_attn_impl.restype = i32
     L.mi355x_mmq_impl.argtypes = [i32]
     L.mi355x_mmq_impl.restype = i32
+    L.mi355x_prefill_precision.argtypes = [i32]
+    L.mi355x_prefill_precision.restype = i32
     L.mi355x_gemv_waves.argtypes = [i32]
     L.mi355x_gemv_waves.restype = i32
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
@@ -371,6 +375,12 @@ def gemv_fused(mats, x, stream=None, workspace=None):
 def mmq_impl(impl):
     """Prefill GEMM variant (MMQ_*); returns the previous."""
     return int(lib().mi355x_mmq_impl(impl))
+
+
+def prefill_precision(p=-1):
+    """Prefill (M >= 16) precision: PREFILL_EXACT (bit-exact kq_mmq) or PREFILL_F16 (kq_mmf,
+    stated tolerance); -1 queries. Returns the previous value."""
+    return int(lib().mi355x_prefill_precision(p))
 
 
 def gemv_waves(waves):

@@ -263,3 +263,56 @@ def random_blocks(rng, type_, N, K, d_lo=2.0 ** -14, d_hi=2.0 ** -6):
     elif type_ == Q6_K:
         raw[..., 208:210] = f16(0)[..., None].view(np.uint8).reshape(N, nb, 2)
     return raw.reshape(N, nb * B)
+
+
+# ------------------------------------------- f16 prefill path (kq_mmf), stated tolerance
+def mmf_operands(w, type_, K, x):
+    """The operands kq_mmf feeds the f16 matrix core, as float64 of their f16 values, and
+    the per-element magnitude A used by the tolerance bound.
+
+    Returns (W16 (N, K), X16 (M, K), G16w (N, nb*16), G16x (M, nb*16), A (N, K), Xhat (M, K)):
+    y ~= W16 @ X16.T + G16w @ G16x.T (main + per-group terms, csrc/kq_mmf.hip header)."""
+    nb = K // QK_K
+    q, sc, mn, f = weights_int(w, type_, K)
+    N = q.shape[0]
+    f16 = np.float16
+    q8 = quantize_q8_K(x)
+    d = q8["d"].astype(F32)                                # (M, nb)
+    qs = q8["qs"].astype(F32)                              # (M, nb, 256)
+    X16 = (d[..., None] * qs).astype(F32).astype(f16).astype(F64).reshape(-1, K)
+    Xhat = (d[..., None].astype(F64) * qs.astype(F64)).reshape(-1, K)
+    bs16 = q8["bsums"].astype(F32)                         # (M, nb, 16)
+    G16x = (d[..., None] * bs16).astype(F32).astype(f16).astype(F64).reshape(-1, nb * 16)
+    if type_ in (Q4_K, Q5_K):
+        dd = fp16_to_f32(f["d"])[..., None]                # (N, nb, 1)
+        dm = fp16_to_f32(f["dmin"])[..., None]
+        dsc = (dd * sc.astype(F32)).astype(f16)            # (N, nb, 8) one rounding
+        W16 = (np.repeat(dsc.astype(F64), 32, -1) * q).astype(f16).astype(F64).reshape(N, K)
+        mneg = -(dm * mn.astype(F32)).astype(f16).astype(F64)  # (N, nb, 8)
+        G16w = np.repeat(mneg, 2, -1).reshape(N, nb * 16)
+        A = (np.repeat(np.abs(dsc.astype(F64)), 32, -1) * q + np.repeat(np.abs(mneg), 32, -1)).reshape(N, K)
+    else:
+        dd = fp16_to_f32(f["d"])[..., None]
+        dsc = (dd * sc.astype(F32)).astype(f16)            # (N, nb, 16)
+        W16 = (np.repeat(dsc.astype(F64), 16, -1) * q).astype(f16).astype(F64).reshape(N, K)
+        G16w = (-32.0 * dsc.astype(F64)).reshape(N, nb * 16)
+        A = (np.repeat(np.abs(dsc.astype(F64)), 16, -1) * (q + 32)).reshape(N, K)
+    return W16, X16, G16w, G16x, A, Xhat
+
+
+def mmf_emulate(w, type_, K, x):
+    """kq_mmf's value up to the f32 accumulation order: (M, N) float64."""
+    W16, X16, G16w, G16x, _, _ = mmf_operands(w, type_, K, x)
+    return X16 @ W16.T + G16x @ G16w.T
+
+
+MMF_REL_TOL = 2.0 ** -8
+
+
+def mmf_bound(w, type_, K, x):
+    """Stated tolerance of the f16 prefill path against the bit-exact reference (M, N):
+    2^-8 * sum_k A_k |x^_k| + 2^-24 * K * max A * max |x^|, with A_k = |f16(d sc)| q_k +
+    |f16(dmin m)| (Q4_K/Q5_K) or |f16(d sc)| (q_k + 32) (Q6_K) and x^ = y.d * q8."""
+    _, _, _, _, A, Xhat = mmf_operands(w, type_, K, x)
+    S = np.abs(Xhat) @ A.T
+    return MMF_REL_TOL * S + 2.0 ** -24 * K * float(A.max(initial=0.0)) * float(np.abs(Xhat).max(initial=0.0))

@@ -20,6 +20,10 @@ SHAPES = [("l3 q/o", 12, 4096, 4096), ("l3 up", 12, 4096, 14336), ("l3 down", 12
 
 def main(M=512, reps=10, only=None):
     dev = torch.device("cuda:0")
+    f16 = os.environ.get("MI355X_PREFILL") == "f16"
+    if f16:
+        g.prefill_precision(g.PREFILL_F16)
+    peak = 2.5e15 if f16 else 5e15
     gen = torch.Generator(device=dev)
     gen.manual_seed(2)
     for label, typ, K, N in SHAPES:
@@ -37,10 +41,10 @@ def main(M=512, reps=10, only=None):
         per = len(rows) // reps
         names = [r[0] for r in rows[:per]]
         tot = np.median([sum(r[2] for r in rows[i * per:(i + 1) * per]) for i in range(reps)])
-        mm = np.median([r[2] for r in rows if "mmq" in r[0]]) if any("mmq" in n for n in names) else float("nan")
+        mm = np.median([sum(r[2] for r in rows[i * per:(i + 1) * per] if "quantize" not in r[0]) for i in range(reps)])
         ops = 2.0 * N * K * M
         print(f"{label:8s} K={K:6d} N={N:6d} M={M}: total {tot * 1e3:8.1f} us ({ops / (tot * 1e-3) / 1e12:7.1f} TOPS), "
-              f"gemm {mm * 1e3:8.1f} us ({ops / (mm * 1e-3) / 1e12:7.1f} TOPS, {ops / (mm * 1e-3) / 5e15 * 100:5.1f} % of 5 POPS) "
+              f"gemm {mm * 1e3:8.1f} us ({ops / (mm * 1e-3) / 1e12:7.1f} TOPS, {ops / (mm * 1e-3) / peak * 100:5.1f} % of {peak / 1e15:.1f} P) "
               f"{'+'.join(names)}", flush=True)
 
 
