@@ -321,6 +321,27 @@ def large_gemv(dev, reps=20):
     return out
 
 
+F16_PEAK_TFLOPS = 2500.0  # dense f16 MFMA peak (MI355X_MICROARCH.md)
+
+
+def on_f16(fn, *a, **kw):
+    """fn on the stated-tolerance f16 prefill path (mi355x_prefill_precision F16, kq_mmf),
+    the bit-exact kq_mmq restored after."""
+    prev = g.prefill_precision(g.PREFILL_F16)
+    try:
+        out = fn(*a, **kw)
+    finally:
+        g.prefill_precision(prev)
+    if out is not None:
+        out["precision"] = "f16 MFMA (kq_mmf), stated tolerance: csrc/kq_mmf.hip, tests/test_gpu_mmf.py"
+        out["note"] = out["note"].replace("kq_mmq", "kq_mmf").replace("int8-MFMA", "f16-MFMA")
+        if "int_TOPS" in out:
+            out["f16_TFLOPS"] = out.pop("int_TOPS")
+            out["roofline"] = {"bound": "mfma", "achieved": out["f16_TFLOPS"], "peak": F16_PEAK_TFLOPS,
+                               "unit": "TFLOP/s (f16 dense)", "frac": round(out["f16_TFLOPS"] / F16_PEAK_TFLOPS, 4)}
+    return out
+
+
 def prefill_chain(chain, dev, M=512, reps=3):
     """pp512-style prefill of the same weights: every matrix of the chain times an
     M-column activation block (ne11 = M: Q8_K quantization + the int8-MFMA kq_mmq
@@ -434,7 +455,8 @@ def model_side(model, dev, steps=64, warmup=8, mix="q4_k_m"):
            "weights_MB_per_token": round(tk.bytes_per_token / 1e6, 1),
            "effective_GBps": round(tk.bytes_per_token / (ms * 1e-3) / 1e9, 1),
            "launches_per_token": tk.launches(), "mix": mix, "pp512_graph": prompt_side(tk, be),
-           "pp512": prefill_chain(tk, dev)}
+           "pp512": prefill_chain(tk, dev),
+           "pp512_graph_f16": on_f16(prompt_side, tk, be), "pp512_f16": on_f16(prefill_chain, tk, dev)}
     del tk, be
     torch.cuda.empty_cache()
     return out
@@ -1035,9 +1057,12 @@ def main():
             l3 = model_side("llama-3-8b", dev)
             l3q5 = model_side("llama-3-8b", dev, mix="q5_k_m")  # BASELINE config 5
         prefill = None if args.no_prefill or world > 1 else prefill_chain(chain, dev)
-        pp_graph = None
+        pp_graph = prefill_f16 = pp_graph_f16 = None
+        if not args.no_prefill and world == 1:
+            prefill_f16 = on_f16(prefill_chain, chain, dev)
         if isinstance(chain, Token) and not args.no_prefill and world == 1:
             pp_graph = prompt_side(chain, be)
+            pp_graph_f16 = on_f16(prompt_side, chain, be)
         if prefill is not None:
             prefill["roofline"] = {"bound": "mfma", "achieved": prefill["int_TOPS"], "peak": I8_PEAK_TOPS,
                                    "unit": "TOPS (int8 dense)", "frac": round(prefill["int_TOPS"] / I8_PEAK_TOPS, 4),
@@ -1086,6 +1111,8 @@ def main():
             "gemv_large": large,
             "prefill_pp512": prefill,
             "pp512": pp_graph,
+            "prefill_pp512_f16": prefill_f16,
+            "pp512_f16": pp_graph_f16,
             "matmul_chain": side,
             "llama3_8b": l3,
             "llama3_8b_q5_k_m": l3q5,

@@ -29,9 +29,10 @@ __global__ void kq_mmq(const MmqArgs a);
 template <int RT, int CW>
 __global__ void kq_mmq_mixed(const MmqArgs a);
 __global__ void kq_quantize_f16img(const float *x, int64_t x_stride, uint8_t *img, uint8_t *bs, int nb, int64_t nblocks);
-template <int TYPE>
+template <int TYPE, int RR>
 __global__ void kq_mmf(const MmfArgs a);
-__global__ void kq_mmf_reduce(const float *slab, int n_split, int m_cols, int n_rows, float *y, int64_t y_col_stride);
+__global__ void kq_mmf_reduce(const float *slab, int n_split, int m_cols, int n_rows, float *y, int64_t y_col_stride,
+                              const float *res, int64_t res_col_stride);
 
 namespace {
 
@@ -688,28 +689,48 @@ int prefill_precision() {
     return v;
 }
 
-// K split of kq_mmf: double it while the grid has fewer workgroups than CUs and every
-// split keeps >= 4 superblocks (8 half-superblock steps); splits combine in order.
+// Row tiles per wave of kq_mmf (MI355X_MMF_RR, A/B only): 1 (128-row workgroups, two per
+// CU), 2 (256-row workgroups, one per CU), 0 by shape.
+int mmf_rr_env() {
+    static const int v = getenv("MI355X_MMF_RR") ? atoi(getenv("MI355X_MMF_RR")) : 0;
+    return v;
+}
+// K split of kq_mmf: double it while the grid has fewer workgroups than CUs (RR = 1:
+// filling both resident slots per CU with a 4-way split measured slower on 8B q/o, 34 ->
+// 37 us) or, at RR = 2, fits one round of one workgroup per CU; every split keeps >= 4
+// superblocks (8 half-superblock steps); splits combine in order.
 struct MmfPlan {
-    int n_ct, n_rt, n_split, nbs;
+    int rr, n_ct, n_rt, n_split, nbs;
 };
-MmfPlan mmf_plan(int64_t N, int64_t M, int64_t nb) {
+MmfPlan mmf_plan_rr(int64_t N, int64_t M, int64_t nb, int rr) {
     MmfPlan p;
+    p.rr = rr;
     p.n_ct = (int)((M + MMF_COLS - 1) / MMF_COLS);
-    p.n_rt = (int)((N + MMF_RT - 1) / MMF_RT);
+    p.n_rt = (int)((N + 128 * rr - 1) / (128 * rr));
     int s = 1;
-    while ((int64_t)p.n_ct * p.n_rt * s < 256 && nb >= 8 * s) s *= 2;
+    if (rr == 1)
+        while ((int64_t)p.n_ct * p.n_rt * s < 256 && nb >= 8 * s) s *= 2;
+    else
+        while ((int64_t)p.n_ct * p.n_rt * s * 2 <= 256 && nb >= 8 * s) s *= 2;
     p.nbs = (int)((nb + s - 1) / s);
     p.n_split = (int)((nb + p.nbs - 1) / p.nbs);
     return p;
 }
+// AUTO takes RR = 1 everywhere: RR = 2 (one wave per SIMD) measured equal on the 8B
+// ffn_down and 3-18 % slower on every other prefill shape (profiles/r03_mmf_rr_ab.txt).
+MmfPlan mmf_plan(int64_t N, int64_t M, int64_t nb) {
+    return mmf_plan_rr(N, M, nb, mmf_rr_env() == 2 ? 2 : 1);
+}
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
-// workspace: activation image + d*bsum16 (+ the split-K slabs)
+// workspace: activation image + d*bsum16 (+ the split-K slabs of either tile shape)
 size_t mmf_workspace(int64_t N, int64_t M, int64_t nb) {
-    const MmfPlan p = mmf_plan(N, M, nb);
-    size_t w = al256((size_t)M * nb * MMF_IMG) + al256((size_t)M * nb * MMF_BSB);
-    if (p.n_split > 1) w += al256((size_t)p.n_split * M * N * 4);
-    return w;
+    size_t w = al256((size_t)M * nb * MMF_IMG) + al256((size_t)M * nb * MMF_BSB), slab = 0;
+    for (int rr = 1; rr <= 2; ++rr) {
+        const MmfPlan p = mmf_plan_rr(N, M, nb, rr);
+        const size_t sb = p.n_split > 1 ? al256((size_t)p.n_split * M * N * 4) : 0;
+        slab = sb > slab ? sb : slab;
+    }
+    return w + slab;
 }
 bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M) {
     if (prefill_precision() != MI355X_PREFILL_F16) return false;
@@ -720,13 +741,13 @@ bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t 
     return ((uintptr_t)w & 15u) == 0 && (row_stride & 15u) == 0;
 }
 
-int launch_mmf(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const float *x, int64_t x_stride,
-               int64_t M, float *y, int64_t y_col_stride, uint8_t *ws, hipStream_t stream) {
+bool mmf_on() { return prefill_precision() == MI355X_PREFILL_F16; }
+
+int launch_f16img(const float *x, int64_t x_stride, uint8_t *ws, int64_t K, int64_t M, hipStream_t stream) {
     const int64_t nb = K / QK;
-    const MmfPlan p = mmf_plan(N, M, nb);
     uint8_t *img = ws, *bs = ws + al256((size_t)M * nb * MMF_IMG);
-    float *slab = (float *)(bs + al256((size_t)M * nb * MMF_BSB));
     const int64_t nblocks = nb * M;
+    if (nblocks == 0) return MI355X_OK;
     const int64_t qwgs = (nblocks + WAVES_PER_WG - 1) / WAVES_PER_WG;
     hipEvent_t e0, e1;
     if (timing_slot(stream, e0, e1)) {
@@ -737,8 +758,16 @@ int launch_mmf(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
         hipLaunchKernelGGL(kq_quantize_f16img, dim3((unsigned)qwgs), dim3(WG_THREADS), 0, stream, x, x_stride, img, bs,
                            (int)nb, nblocks);
     }
-    hipError_t e = hipGetLastError();
-    if (e != hipSuccess) return (int)e;
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
+}
+
+int launch_mmf_gemm(int type, const void *w, int64_t K, int64_t N, size_t row_stride, uint8_t *ws, int64_t M,
+                    float *y, int64_t y_col_stride, hipStream_t stream, const float *res, int64_t res_col_stride) {
+    const int64_t nb = K / QK;
+    const MmfPlan p = mmf_plan(N, M, nb);
+    uint8_t *img = ws, *bs = ws + al256((size_t)M * nb * MMF_IMG);
+    float *slab = (float *)(bs + al256((size_t)M * nb * MMF_BSB));
     MmfArgs a;
     memset(&a, 0, sizeof(a));
     a.w = (const uint8_t *)w;
@@ -754,15 +783,24 @@ int launch_mmf(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     a.nbs = p.nbs;
     a.n_split = p.n_split;
     a.n_ct = p.n_ct;
-    const void *fn = type == Q5_K ? (const void *)kq_mmf<Q5_K> : type == Q6_K ? (const void *)kq_mmf<Q6_K>
-                                                                              : (const void *)kq_mmf<Q4_K>;
+    a.n_rt = p.n_rt;
+    a.res = res;
+    a.res_col_stride = res_col_stride;
+    static const int order = getenv("MI355X_MMF_ORDER") ? atoi(getenv("MI355X_MMF_ORDER")) : 0;  // A/B only
+    a.order = order;
+    const void *fn = p.rr == 2 ? (type == Q5_K ? (const void *)kq_mmf<Q5_K, 2> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 2>
+                                                                                          : (const void *)kq_mmf<Q4_K, 2>)
+                               : (type == Q5_K ? (const void *)kq_mmf<Q5_K, 1> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 1>
+                                                                                          : (const void *)kq_mmf<Q4_K, 1>);
     const size_t lds = 2 * (size_t)MMF_BUF;
     allow_lds(fn, lds);
     const dim3 grid((unsigned)((int64_t)p.n_ct * p.n_rt * p.n_split)), block(256);
     void *args[] = {&a};
+    hipEvent_t e0, e1;
+    hipError_t e;
     if (timing_slot(stream, e0, e1)) {
         e = hipExtLaunchKernel(fn, grid, block, args, lds, stream, e0, e1, 0);
-        timing_log(std::string("kq::kq_mmf<") + std::to_string(type) + ">",
+        timing_log(std::string("kq::kq_mmf<") + std::to_string(type) + ", " + std::to_string(p.rr) + ">",
                    (double)N * nb * block_bytes(type) + (double)M * nb * (MMF_IMG + MMF_BSB) + (double)M * N * 4.0, e0,
                    e1);
     } else {
@@ -776,11 +814,11 @@ int launch_mmf(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
         const dim3 rg((unsigned)((total + 255) / 256));
         if (timing_slot(stream, e0, e1)) {
             hipExtLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, e0, e1, 0, (const float *)slab, p.n_split,
-                                  (int)M, (int)N, y, y_col_stride);
+                                  (int)M, (int)N, y, y_col_stride, res, res_col_stride);
             timing_log("kq::kq_mmf_reduce", (double)total * 4.0 * (p.n_split + 1), e0, e1);
         } else {
             hipLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, (const float *)slab, p.n_split, (int)M, (int)N, y,
-                               y_col_stride);
+                               y_col_stride, res, res_col_stride);
         }
         e = hipGetLastError();
     }
@@ -1191,8 +1229,10 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
     if (mmf_applies(src0_type, src0, ne01, nb01, ne11) && ((uintptr_t)workspace & 15u) == 0) {
         if (!device_ok()) return MI355X_E_NODEVICE;
-        return launch_mmf(src0_type, src0, ne00, ne01, nb01, src1, (int64_t)(nb11 / 4), ne11, dst, (int64_t)(nb1 / 4),
-                          (uint8_t *)workspace, (hipStream_t)stream);
+        int rc = launch_f16img(src1, (int64_t)(nb11 / 4), (uint8_t *)workspace, ne00, ne11, (hipStream_t)stream);
+        if (rc) return rc;
+        return launch_mmf_gemm(src0_type, src0, ne00, ne01, nb01, (uint8_t *)workspace, ne11, dst, (int64_t)(nb1 / 4),
+                               (hipStream_t)stream);
     }
     if (mmq_applies(src0_type, src0, ne01, nb01, ne11) && ((uintptr_t)workspace & 15u) == 0) {
         if (!device_ok()) return MI355X_E_NODEVICE;

@@ -209,6 +209,7 @@ struct Q8State {
     const void *src = nullptr;
     int64_t k = 0, m = 0;
     size_t nb = 0;
+    bool f16 = false;  // the workspace holds kq_mmf's f16 activation image, not Q8L blocks
 };
 
 int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8, float *y = nullptr,
@@ -219,7 +220,24 @@ int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8, f
         y_stride = (int64_t)(t->nb[1] / 4);
     }
     const int64_t K = w->ne[0], M = x->ne[1];
-    const bool same = q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1];
+    const bool f16 = kq::mmf_on();
+    const bool same = q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1] && q8.f16 == f16;
+    if (f16) {  // the stated-tolerance f16 path: image once per activation, then the GEMM
+        int rc = 0;
+        if (!same) {
+            rc = kq::launch_f16img((const float *)x->data, (int64_t)(x->nb[1] / 4), (uint8_t *)b->workspace, K, M,
+                                   b->stream);
+            q8 = Q8State();
+            if (rc) return rc;
+            q8.src = x->data, q8.k = K, q8.m = M, q8.nb = x->nb[1], q8.f16 = true;
+        }
+        rc = kq::launch_mmf_gemm(w->type, w->data, K, w->ne[1], w->nb[1], (uint8_t *)b->workspace, M, y, y_stride,
+                                 b->stream, res, res_stride);
+        const uintptr_t o0 = (uintptr_t)y, o1 = o0 + (size_t)y_stride * 4 * (size_t)t->ne[1];
+        const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;
+        if (rc || (o0 < s1 && s0 < o1)) q8 = Q8State();
+        return rc;
+    }
     if (!same) {
         const int rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
                                                b->stream, true);
@@ -261,7 +279,9 @@ bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
     if (t->op != MI355X_OP_MUL_MAT) return false;
     const mi355x_tensor *w = t->src[0], *x = t->src[1];
     if (x->ne[1] < 16 || (x->nb[1] & 3u) || (t->nb[1] & 3u) || ((uintptr_t)b->workspace & 15u)) return false;
-    if (!kq::mmq_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1])) return false;
+    if (kq::mmf_on() ? !kq::mmf_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1])
+                     : !kq::mmq_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1]))
+        return false;
     return b->workspace_size >= mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], x->ne[1]);
 }
 
@@ -356,7 +376,9 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
         }
         // prefill (batched, ne11 >= 16) fusions: the normed / swiglu'd activation goes straight
         // into the GEMMs' Q8L blocks (never written as f32), and MUL_MAT -> ADD as the GEMM's
-        // epilogue; only where every consumer takes the shared-activation GEMM
+        // epilogue; only where every consumer takes the shared-activation GEMM. On the f16
+        // path (kq_mmf) only the ADD epilogue: its GEMMs read an f16 image of the f32 activation.
+        const bool q8l = !kq::mmf_on();
         if (fuse) {
             auto shares_run = [&](int first, const mi355x_tensor *src, int &cnt) {
                 cnt = 0;
@@ -366,7 +388,7 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 return cnt > 0;
             };
             int cnt = 0;
-            if (t->op == MI355X_OP_RMS_NORM && t->ne[1] >= 16 && i + 2 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
+            if (q8l && t->op == MI355X_OP_RMS_NORM && t->ne[1] >= 16 && i + 2 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
                 nodes[i + 1]->src[0] == t && elidable(t, readers[i]) && nodes[i + 1]->ne[0] == t->ne[0] &&
                 nodes[i + 1]->ne[1] == t->ne[1] && nodes[i + 1]->src[1]->ne[0] == t->ne[0] &&
                 nelem(nodes[i + 1]->src[1]) == t->ne[0] && t->nb[1] == (size_t)t->ne[0] * 4 &&
@@ -384,7 +406,7 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 i += 2;
                 continue;
             }
-            if (t->op == MI355X_OP_SWIGLU && t->ne[1] >= 16 && t->ne[0] % MI355X_QK_K == 0 &&
+            if (q8l && t->op == MI355X_OP_SWIGLU && t->ne[1] >= 16 && t->ne[0] % MI355X_QK_K == 0 &&
                 t->nb[1] == (size_t)t->ne[0] * 4 && t->src[0]->nb[1] == t->nb[1] && t->src[1]->nb[1] == t->nb[1] &&
                 nelem(t->src[0]) == nelem(t) && nelem(t->src[1]) == nelem(t) && !(t->flags & MI355X_TENSOR_FLAG_OUTPUT) &&
                 shares_run(i + 1, t, cnt) && readers[i] == cnt) {
@@ -397,7 +419,7 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 i += 1;
                 continue;
             }
-            if (t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] >= 16 && batched_mm_shares(b, t) &&
+            if (q8l && t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] >= 16 && batched_mm_shares(b, t) &&
                 kq::mmq_tile64(t->src[0]->type, t->src[0]->ne[1], t->src[1]->ne[1])) {
                 int run = 1;
                 while (i + run < n && run < 4) {
@@ -532,6 +554,7 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
 bool attn_feeds_batched_mm(const mi355x_backend *b, const mi355x_tensor *t, const Launch &next,
                            mi355x_tensor *const *nodes) {
     if (t->src[0]->ne[1] < 16 || t->nb[1] != (size_t)t->ne[0] * 4) return false;
+    if (kq::mmf_on()) return false;  // the f16 GEMMs read an f16 image, not Q8L blocks
     if (next.kind != 0 && next.kind != 3 && next.kind != 4) return false;
     const mi355x_tensor *m = nodes[next.first];
     if (m->op != MI355X_OP_MUL_MAT || m->src[1] != t || m->src[0]->ne[0] != t->ne[0]) return false;

@@ -266,6 +266,10 @@ struct MmfArgs {
     int nbs;                   // superblocks per K split
     int n_split;
     int n_ct;                  // column tiles
+    int n_rt;                  // row tiles
+    int order;                 // tile order (speed only): 0 row tiles, 1 column tiles consecutive per XCD
+    const float *res;          // ADD epilogue (null: none): y = mul_mat + res, column j at
+    int64_t res_col_stride;    //   res + j * res_col_stride
 };
 
 }  // namespace kq

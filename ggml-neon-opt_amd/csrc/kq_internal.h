@@ -61,6 +61,15 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
                float *y, int64_t y_col_stride, hipStream_t stream, const float *res = nullptr,
                int64_t res_col_stride = 0);  // res: ADD epilogue
 bool mmq_tile64(int type, int64_t N, int64_t M);  // launch_mmq would use the 64 x 64 tile kernel
+// f16 prefill path (mi355x_prefill_precision F16, csrc/kq_mmf.hip): the activation image
+// (kq_quantize_f16img) at the workspace start, then the GEMM (its split-K slabs after the
+// image); res: ADD epilogue
+bool mmf_on();
+bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M);
+int launch_f16img(const float *x, int64_t x_stride_floats, uint8_t *ws, int64_t K, int64_t M, hipStream_t stream);
+int launch_mmf_gemm(int type, const void *w, int64_t K, int64_t N, size_t row_stride, uint8_t *ws, int64_t M,
+                    float *y, int64_t y_col_stride, hipStream_t stream, const float *res = nullptr,
+                    int64_t res_col_stride = 0);
 // KV-cache store epilogue of launch_mmq_multi (a prompt's k / v projections): kind[d] 1 k,
 // 2 v, 0 none; the cells of kq_kv_store (rope(k) -> f16 rows, v -> f16 transposed)
 struct MmqKv {

@@ -26,6 +26,18 @@
 // (each weight byte is read by one wave only), so only the activation goes through LDS.
 #include "kq_device.h"
 
+// Pin the one-step-ahead activation reads with a scheduling barrier (hipcc otherwise
+// moves each read next to its MFMA).
+// Timing-only ablations (experiment builds, make variant-mmf NAME=d1 VFLAGS=-DKQ_MMF_DIAG=1):
+// 1 no activation refill after the first step, 8 no workgroup barrier (round 3, RR = 1:
+// the 8B ffn_up 79 -> 69 us without the refill, 66 us without both).
+#ifndef KQ_MMF_DIAG
+#define KQ_MMF_DIAG 0
+#endif
+#ifndef KQ_MMF_PIN
+#define KQ_MMF_PIN 1
+#endif
+
 namespace kq {
 
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
@@ -199,23 +211,39 @@ __global__ void __launch_bounds__(WG_THREADS) kq_quantize_f16img(const float *__
 }
 
 // ------------------------------------------------------------------ GEMM
-template <int TYPE>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) kq_mmf(const MmfArgs a) {
+// RR row tiles of 32 per wave: RR = 1 (128 weight rows per workgroup, two workgroups per
+// CU) or RR = 2 (256 rows, one workgroup per CU, every register: each activation fragment
+// read from LDS feeds two MFMAs, the LDS-DMA and LDS reads per MFMA halve).
+template <int TYPE, int RR>
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 1 ? 2 : 1))) kq_mmf(const MmfArgs a) {
     constexpr int HALF = MMF_COLS * MMF_IMG / 2;  // 32 KB of image per step
+    constexpr int RT = 128 * RR;                  // weight rows per workgroup
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
     const int r = lane & 31, h = lane >> 5;
 
-    // XCD-aware order (speed only): blocks L, L+8, ... share an XCD; consecutive tiles T
-    // -- the column tiles of one row tile and K split -- go to one XCD, so the weight
-    // bytes are fetched into that XCD's L2 once (bijective for any grid size).
+    // XCD-aware order (speed only): blocks L, L+8, ... share an XCD and get consecutive
+    // tiles T (bijective for any grid size). order 0: the row tiles of one column tile
+    // and K split are consecutive, so an XCD's L2 holds ~one column tile's activation
+    // image (K x 128 x 2 B) and the weights stream past it; order 1: the column tiles of
+    // one row tile (the weight bytes shared in L2). Measured equal (round 3).
     const int G = gridDim.x, L = blockIdx.x;
     const int q8 = G >> 3, r8 = G & 7, xcd = L & 7;
     const int T = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-    const int tx = T % a.n_ct, rest = T / a.n_ct;
-    const int kz = rest % a.n_split, ty = rest / a.n_split;
-    const int col0 = tx * MMF_COLS, row0 = ty * MMF_RT;
+    int tx, ty, kz;
+    if (a.order == 0) {
+        ty = T % a.n_rt;
+        const int rest = T / a.n_rt;
+        kz = rest % a.n_split;
+        tx = rest / a.n_split;
+    } else {
+        tx = T % a.n_ct;
+        const int rest = T / a.n_ct;
+        kz = rest % a.n_split;
+        ty = rest / a.n_split;
+    }
+    const int col0 = tx * MMF_COLS, row0 = ty * RT;
     const int b0 = kz * a.nbs;
     const int b1 = b0 + a.nbs < a.nb ? b0 + a.nbs : a.nb;
     const int nst = 2 * (b1 - b0);
@@ -242,23 +270,32 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
         }
     };
 
-    int wrow = row0 + 32 * wave + r;
-    wrow = wrow < a.n_rows ? wrow : a.n_rows - 1;
-    const uint8_t *wp = a.w + (int64_t)wrow * a.row_stride;
+    const uint8_t *wp[RR];
+#pragma unroll
+    for (int rr = 0; rr < RR; ++rr) {
+        int wrow = row0 + 32 * (RR * wave + rr) + r;
+        wrow = wrow < a.n_rows ? wrow : a.n_rows - 1;
+        wp[rr] = a.w + (int64_t)wrow * a.row_stride;
+    }
     constexpr int BSZ = block_bytes(TYPE);
 
-    f32x16 acc[4];
+    f32x16 acc[RR][4];
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int rr = 0; rr < RR; ++rr)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) acc[ct][i] = 0.f;
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[rr][ct][i] = 0.f;
 
-    MmfW wc, wn;
-    mmf_load<TYPE>(wc, wp + (int64_t)b0 * BSZ, h);
+    MmfW wc[RR], wn[RR];
+#pragma unroll
+    for (int rr = 0; rr < RR; ++rr) mmf_load<TYPE>(wc[rr], wp[rr] + (int64_t)b0 * BSZ, h);
     issue(0);
 #pragma unroll 1
     for (int b = b0; b < b1; ++b) {
-        const MmfS s = mmf_setup<TYPE>(wc, h);
+        MmfS s[RR];
+#pragma unroll
+        for (int rr = 0; rr < RR; ++rr) s[rr] = mmf_setup<TYPE>(wc[rr], h);
 #pragma unroll
         for (int hf = 0; hf < 2; ++hf) {
             const int st = 2 * (b - b0) + hf;
@@ -268,63 +305,85 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(2))) k
             // loads of the previous superblock have landed and inserts no counted wait of
             // its own -- one that, blind to the LDS-DMA, would stall on the refill below)
             __builtin_amdgcn_s_waitcnt(0);
-            asm volatile("s_barrier" ::: "memory");
-            if (st + 1 < nst) issue(st + 1);
-            if (hf == 0 && b + 1 < b1) mmf_load<TYPE>(wn, wp + (int64_t)(b + 1) * BSZ, h);
+            if (!(KQ_MMF_DIAG & 8)) asm volatile("s_barrier" ::: "memory");
+            if (st + 1 < nst && !((KQ_MMF_DIAG & 1) && st > 0)) issue(st + 1);
+            if (hf == 0 && b + 1 < b1)
+#pragma unroll
+                for (int rr = 0; rr < RR; ++rr) mmf_load<TYPE>(wn[rr], wp[rr] + (int64_t)(b + 1) * BSZ, h);
             const uint8_t *buf = smem + (st & 1) * MMF_BUF;
             if (hf == 0) {  // per-group term: mins (Q4_K/Q5_K) or the -32 offset (Q6_K)
 #pragma unroll
                 for (int ct = 0; ct < 4; ++ct) {
                     const f16x8 ab = *(const f16x8 *)(buf + HALF + (32 * ct + r) * MMF_BSB + 16 * h);
-                    acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab, s.wg, acc[ct], 0, 0, 0);
+#pragma unroll
+                    for (int rr = 0; rr < RR; ++rr)
+                        acc[rr][ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ab, s[rr].wg, acc[rr][ct], 0, 0, 0);
                 }
             }
+            // activation fragments one step ahead of their MFMAs (the LDS latency of step
+            // sl+1's four reads runs under step sl's MFMAs)
+            auto act = [&](f16x8 *av, int sl) {
+                const int slot = (2 * sl + h) ^ (r & 15);
 #pragma unroll
-            for (int pl = 0; pl < 2; ++pl) {
+                for (int ct = 0; ct < 4; ++ct) av[ct] = *(const f16x8 *)(buf + (32 * ct + r) * (MMF_IMG / 2) + 16 * slot);
+            };
+            f16x8 av[2][4];
+            act(av[0], 0);
 #pragma unroll
-                for (int t = 0; t < 4; ++t) {
-                    const int p = 2 * hf + pl;
-                    const f16x8 wf = mmf_frag<TYPE>(wc, s, p, t);
-                    const int slot = (8 * pl + 2 * t + h) ^ (r & 15);
+            for (int sl = 0; sl < 8; ++sl) {
+                if (sl < 7) act(av[(sl + 1) & 1], sl + 1);
+                if (KQ_MMF_PIN) __builtin_amdgcn_sched_barrier(0);  // keep the reads ahead
 #pragma unroll
-                    for (int ct = 0; ct < 4; ++ct) {
-                        const f16x8 av = *(const f16x8 *)(buf + (32 * ct + r) * (MMF_IMG / 2) + 16 * slot);
-                        acc[ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av, wf, acc[ct], 0, 0, 0);
-                    }
+                for (int rr = 0; rr < RR; ++rr) {
+                    const f16x8 wf = mmf_frag<TYPE>(wc[rr], s[rr], 2 * hf + (sl >> 2), sl & 3);
+#pragma unroll
+                    for (int ct = 0; ct < 4; ++ct)
+                        acc[rr][ct] = __builtin_amdgcn_mfma_f32_32x32x16_f16(av[sl & 1][ct], wf, acc[rr][ct], 0, 0, 0);
                 }
             }
         }
-        wc = wn;
+#pragma unroll
+        for (int rr = 0; rr < RR; ++rr) wc[rr] = wn[rr];
     }
 
     // ---- store: lane's weight row, accumulator element i = column (i&3) + 8(i>>2) + 4h
-    const int n = row0 + 32 * wave + r;
-    if (n >= a.n_rows) return;
     float *dst = a.n_split > 1 ? a.slab + (int64_t)kz * a.m_cols * a.n_rows : a.y;
     const int64_t cs = a.n_split > 1 ? (int64_t)a.n_rows : a.y_col_stride;
 #pragma unroll
-    for (int ct = 0; ct < 4; ++ct)
+    for (int rr = 0; rr < RR; ++rr) {
+        const int n = row0 + 32 * (RR * wave + rr) + r;
+        if (n >= a.n_rows) continue;
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-            const int c = col0 + 32 * ct + (i & 3) + 8 * (i >> 2) + 4 * h;
-            if (c < a.m_cols) dst[(int64_t)c * cs + n] = acc[ct][i];
-        }
+        for (int ct = 0; ct < 4; ++ct)
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int c = col0 + 32 * ct + (i & 3) + 8 * (i >> 2) + 4 * h;
+                if (c < a.m_cols)
+                    dst[(int64_t)c * cs + n] = a.res && a.n_split == 1
+                                                   ? acc[rr][ct][i] + a.res[(int64_t)c * a.res_col_stride + n]
+                                                   : acc[rr][ct][i];
+            }
+    }
 }
 
-// Split-K combine: y = sum of the n_split partial slabs, in split order.
+// Split-K combine: y = sum of the n_split partial slabs, in split order (+ res).
 __global__ void __launch_bounds__(256) kq_mmf_reduce(const float *__restrict__ slab, int n_split, int m_cols,
-                                                     int n_rows, float *__restrict__ y, int64_t y_col_stride) {
+                                                     int n_rows, float *__restrict__ y, int64_t y_col_stride,
+                                                     const float *__restrict__ res, int64_t res_col_stride) {
     const int64_t total = (int64_t)m_cols * n_rows;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= total) return;
     float s = slab[i];
     for (int k = 1; k < n_split; ++k) s += slab[(int64_t)k * total + i];
     const int64_t c = i / n_rows, n = i - c * n_rows;
-    y[c * y_col_stride + n] = s;
+    y[c * y_col_stride + n] = res ? s + res[c * res_col_stride + n] : s;
 }
 
-template __global__ void kq_mmf<Q4_K>(const MmfArgs a);
-template __global__ void kq_mmf<Q5_K>(const MmfArgs a);
-template __global__ void kq_mmf<Q6_K>(const MmfArgs a);
+template __global__ void kq_mmf<Q4_K, 1>(const MmfArgs a);
+template __global__ void kq_mmf<Q5_K, 1>(const MmfArgs a);
+template __global__ void kq_mmf<Q6_K, 1>(const MmfArgs a);
+template __global__ void kq_mmf<Q4_K, 2>(const MmfArgs a);
+template __global__ void kq_mmf<Q5_K, 2>(const MmfArgs a);
+template __global__ void kq_mmf<Q6_K, 2>(const MmfArgs a);
 
 }  // namespace kq

@@ -78,3 +78,55 @@ def test_prefill_precision_selector(dev):
     assert g.prefill_precision(-1) == g.PREFILL_F16
     assert g.prefill_precision(prev) == g.PREFILL_F16
     assert g.lib().mi355x_prefill_precision(7) == g.E_INVAL
+
+
+@pytest.mark.parametrize("mix", ["q4_k_m", "q5_k_m"])
+def test_llama_prompt_f16(dev, f16path, mix):
+    """The prompt graph on the f16 GEMMs (every MUL_MAT at ne11 = 37 through kq_mmf, the
+    norm / swiglu as their own nodes, the residual ADD as the GEMM's epilogue):
+    * fused (ADD epilogue, one activation image shared by q/k/v and gate/up) and unfused
+      graphs give bit-identical logits and caches, and a replay repeats them exactly;
+    * layer 0's K cache (one GEMM deep) is within a relative L2 error of 2^-9 of the
+      bit-exact prompt's;
+    * the logits are within 2^-5 (relative L2) of the oracle's sequential llm_build_llama.
+      The synthetic model's random attention is sharp (|q.k| scores in the tens), so a
+      GEMM-level difference of ~2^-11 grows ~10x per layer (layer 1's K cache: ~2^-7);
+      the GEMM-level tolerance itself is test_mmf_within_stated_tolerance's."""
+    import torch
+    from oracle import kq_ops_oracle as O
+    from tests import llama_model as LM
+    from tests.test_gpu_ops import _decoder
+    import ggml_mi355x as g
+    from ggml_mi355x.llama import hparams
+    O.lib()
+    hp = hparams(2048, 2, 32, 4, 5632, 4096)
+    n_ctx, n = 64, 37
+    tokens = np.random.default_rng(13).integers(0, hp["n_vocab"], size=n).tolist()
+    out = {}
+    for name, prec, fuse in (("exact", g.PREFILL_EXACT, True), ("f16", g.PREFILL_F16, True),
+                             ("f16_unfused", g.PREFILL_F16, False)):
+        g.prefill_precision(prec)
+        w, b, dec = _decoder(dev, hp, 7, n_ctx, fuse, mix=mix)
+        lg = dec.prompt(tokens, 0)
+        b.synchronize()
+        first = lg.cpu().numpy().copy()
+        lg = dec.prompt(tokens, 0)  # replay of the captured graph
+        b.synchronize()
+        assert np.array_equal(first.view(np.uint32), lg.cpu().numpy().view(np.uint32)), name
+        out[name] = (first.astype(np.float64).ravel(),
+                     [c[:n].view(torch.float16).float().cpu().numpy() for c in dec.k_cache])
+        b.close()
+    g.prefill_precision(g.PREFILL_F16)
+    assert np.array_equal(out["f16"][0], out["f16_unfused"][0])
+    assert all(np.array_equal(a, c) for a, c in zip(out["f16"][1], out["f16_unfused"][1]))
+    k0, k0e = out["f16"][1][0], out["exact"][1][0]
+    assert np.isfinite(k0).all() and np.linalg.norm(k0 - k0e) <= 2.0 ** -9 * np.linalg.norm(k0e)
+    model, cache = LM.oracle_model(hp, w, n_ctx)
+    for p, tok in enumerate(tokens):
+        ref, _ = O.decode_token(model, tok, p, cache)
+    ref = np.asarray(ref, np.float64).ravel()
+    assert np.array_equal(out["exact"][0], ref)  # the default path stays bit-exact
+    got = out["f16"][0]
+    assert np.isfinite(got).all()
+    assert np.linalg.norm(got - ref) <= 2.0 ** -5 * np.linalg.norm(ref)
+    torch.cuda.synchronize()
