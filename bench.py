@@ -27,8 +27,12 @@ q/k/v and gate/up fuse into one launch each, 89 launches per token from one hipG
 
 "roofline": the dominant kernel's algorithmic bytes per launch over its event-timed
 launch duration; "traffic": its HBM read per launch from the committed rocprofv3
-PMC pass (profiles/). "gemv_large": single decode GEMVs of the Llama-3 configs.
-"prefill_pp512": every matmul of the token at ne11 = 512 (int8 MFMA). "cpu_baseline":
+PMC pass (profiles/). "gemv_large": single decode GEMVs of the Llama-3 configs, each
+beside the single-launch streaming ceiling of its byte count ("stream_us": LDS-DMA of
+a once-read buffer, no arithmetic; "of_stream_ceiling" = stream_us / us_median).
+"prefill_pp512": every matmul of the token at ne11 = 512 (int8 MFMA, bit-exact);
+"prefill_pp512_f16" / "pp512_f16" the same on the stated-tolerance f16 path (kq_mmf,
+mi355x_prefill_precision), with an f16-peak roofline. "cpu_baseline":
 the oracle's restated ggml-cpu token on this host's cores, a bounded sample.
 
 Multi-GPU (--gpus N under torch.distributed.run): every rank decodes its own
@@ -312,11 +316,29 @@ def large_gemv(dev, reps=20):
         per_call = len(rows) // reps  # K > 8192: Q8_K quantize launch + GEMV launch
         ms = [sum(r[2] for r in rows[i * per_call:(i + 1) * per_call]) for i in range(reps)]
         b = nbytes + K * 4 + sum(Ns) * 4
+        del ws
+        # the single-launch streaming ceiling of the same byte count (mi355x_debug_stream:
+        # LDS-DMA of a once-read buffer, no arithmetic), buffers rotated the same way
+        pool = torch.empty(nbuf * ((nbytes + 4095) // 4096 * 4096), dtype=torch.uint8, device=dev)
+        sink = torch.zeros(16, dtype=torch.int32, device=dev)
+        step = pool.numel() // nbuf
+        st = torch.cuda.current_stream().cuda_stream
+        for i in range(nbuf):
+            g.lib().mi355x_debug_stream(pool.data_ptr() + i * step, nbytes, sink.data_ptr(), st)
+        g.timing_enable(True)
+        for r in range(reps):
+            assert g.lib().mi355x_debug_stream(pool.data_ptr() + (r % nbuf) * step, nbytes, sink.data_ptr(), st) == 0
+        srows = g.timing_read()
+        g.timing_enable(False)
+        sus = float(np.median([r[2] for r in srows])) * 1e3
         out[label] = {"bytes": b, "launches_per_call": per_call, "kernel": rows[per_call - 1][0],
                       "us_median": round(float(np.median(ms) * 1e3), 2),
                       "GBps_median": round(b / (np.median(ms) * 1e-3) / 1e9, 1),
-                      "frac_median": round(b / (np.median(ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4)}
-        del ws
+                      "frac_median": round(b / (np.median(ms) * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                      "stream_us": round(sus, 2),
+                      "stream_frac": round(nbytes / (sus * 1e-6) / 1e9 / HBM_PEAK_GBS, 4),
+                      "of_stream_ceiling": round(sus / float(np.median(ms) * 1e3), 3)}
+        del pool
         torch.cuda.empty_cache()
     return out
 

@@ -28,6 +28,7 @@ template <int TYPE, int RT, int CW>
 __global__ void kq_mmq(const MmqArgs a);
 template <int RT, int CW>
 __global__ void kq_mmq_mixed(const MmqArgs a);
+__global__ void kq_stream_ceiling(const uint8_t *buf, int64_t per_wave, int waves_total, uint32_t *sink);
 __global__ void kq_quantize_f16img(const float *x, int64_t x_stride, uint8_t *img, uint8_t *bs, int nb, int64_t nblocks);
 template <int TYPE, int RR>
 __global__ void kq_mmf(const MmfArgs a);
@@ -1022,7 +1023,10 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
     const size_t need = (size_t)(k / QK) * 292;
     if (rows_enabled()) {
         RowsPlan rp;
-        const bool rows_fq = k / QK <= kRowsFusedMaxNb && ((uintptr_t)x & 15u) == 0;
+        // MI355X_GEMV_FQMAX (A/B only): the most superblocks quantized inside kq_rows; above
+        // it one kq_quantize_q8L launch first and the GEMV DMAs the Q8L row
+        static const int64_t fq_max = getenv("MI355X_GEMV_FQMAX") ? atoll(getenv("MI355X_GEMV_FQMAX")) : kRowsFusedMaxNb;
+        const bool rows_fq = k / QK <= fq_max && k / QK <= kRowsFusedMaxNb && ((uintptr_t)x & 15u) == 0;
         int rc = plan_rows(d, n, k, rows_fq, rp);
         if (rc == MI355X_OK) {
             if (rows_fq) {
@@ -1274,6 +1278,30 @@ int mi355x_gemv_fused_ext(const mi355x_gemv_desc *descs, int n_desc, const float
         if (ext && ext->residual[i] && ((uintptr_t)ext->residual[i] & 3u)) return MI355X_E_INVAL;
     }
     return gemv_m1(descs, n_desc, x, k, workspace, workspace_size, (hipStream_t)stream, ext);
+}
+
+int mi355x_debug_stream(const void *buf, size_t bytes, void *sink, void *stream) {
+    if (!buf || !sink || ((uintptr_t)buf & 15u)) return MI355X_E_INVAL;
+    int dev = current_device();
+    if (dev < 0 || !device_ok()) return MI355X_E_NODEVICE;
+    const int cus = g_dev_cus[dev] > 0 ? g_dev_cus[dev] : 256;
+    const int waves = cus * 12;
+    const int64_t per_wave = (int64_t)(bytes / waves) / 2048 * 2048;
+    if (per_wave <= 0) return MI355X_E_INVAL;
+    const size_t lds = 4 * 4 * 2048;
+    allow_lds((const void *)kq_stream_ceiling, lds);
+    hipStream_t st = (hipStream_t)stream;
+    hipEvent_t e0, e1;
+    if (timing_slot(st, e0, e1)) {
+        hipExtLaunchKernelGGL(kq_stream_ceiling, dim3((unsigned)(cus * 3)), dim3(256), (uint32_t)lds, st, e0, e1, 0,
+                              (const uint8_t *)buf, per_wave, waves, (uint32_t *)sink);
+        timing_log("kq::kq_stream_ceiling", (double)per_wave * waves, e0, e1);
+    } else {
+        hipLaunchKernelGGL(kq_stream_ceiling, dim3((unsigned)(cus * 3)), dim3(256), lds, st, (const uint8_t *)buf,
+                           per_wave, waves, (uint32_t *)sink);
+    }
+    const hipError_t e = hipGetLastError();
+    return e == hipSuccess ? MI355X_OK : (int)e;
 }
 
 int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, int64_t ne01, size_t nb01,

@@ -354,4 +354,41 @@ KQ_GEMV_INST_TM(4, false, false)
 KQ_GEMV_INST_TM(8, false, false)
 KQ_GEMV_INST_TM(1, false, true)
 
+
+// ------------------------------------------------------------------ streaming ceiling (diagnostic)
+// mi355x_debug_stream: the bytes of a buffer pulled into per-wave LDS rings by LDS-DMA
+// (nt), 2-KB steps, 4 in flight, 12 waves per CU, one contiguous range per wave, no
+// arithmetic -- the time a decode GEMV launch of that many weight bytes could approach
+// (tools/stream_size.hip; bench.py gemv_large "stream_us"). Not on any product path.
+__global__ void __launch_bounds__(256) kq_stream_ceiling(const uint8_t *buf, int64_t per_wave, int waves_total,
+                                                         uint32_t *sink) {
+    constexpr int IPS = 2, D = 4;
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int gw = blockIdx.x * 4 + wave;
+    if (gw >= waves_total) return;
+    uint8_t *ring = smem + wave * D * IPS * 1024;
+    const uint8_t *src = buf + (int64_t)gw * per_wave;
+    const int T = (int)(per_wave / (IPS * 1024));
+    for (int t = 0; t < D && t < T; ++t)
+#pragma unroll
+        for (int i = 0; i < IPS; ++i)
+            dma16_nt(src + (int64_t)t * IPS * 1024 + i * 1024 + 16 * lane, (LDS void *)(ring + (t % D) * IPS * 1024 + 1024 * i));
+    uint32_t acc = 0;
+    for (int t = 0; t < T; ++t) {
+        if (T - t >= D)
+            vm_wait<IPS * (D - 1)>();
+        else
+            vm_wait<0>();
+        acc += *(volatile uint32_t *)(ring + (t % D) * IPS * 1024 + 4 * lane);
+        if (t + D < T)
+#pragma unroll
+            for (int i = 0; i < IPS; ++i)
+                dma16_nt(src + (int64_t)(t + D) * IPS * 1024 + i * 1024 + 16 * lane,
+                         (LDS void *)(ring + (t % D) * IPS * 1024 + 1024 * i));
+    }
+    if (acc == 0x12345678u) sink[0] = acc;
+}
+
 }  // namespace kq

@@ -38,7 +38,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_row_size", "mi355x_version", "mi355x_device_available",
     "mi355x_quantize_row_q8_K", "mi355x_vec_dot_q4_K_q8_K", "mi355x_vec_dot_q5_K_q8_K",
     "mi355x_vec_dot_q6_K_q8_K", "mi355x_quantize_q8_K", "mi355x_mul_mat_workspace_size",
-    "mi355x_mul_mat", "mi355x_mul_mat_q8", "mi355x_gemv_fused", "mi355x_debug_block_partials",
+    "mi355x_mul_mat", "mi355x_mul_mat_q8", "mi355x_gemv_fused", "mi355x_debug_block_partials", "mi355x_debug_stream",
     "mi355x_backend_init", "mi355x_backend_free", "mi355x_backend_name", "mi355x_backend_stream",
     "mi355x_backend_alloc", "mi355x_backend_free_buffer", "mi355x_backend_set_tensor",
     "mi355x_backend_get_tensor", "mi355x_backend_synchronize", "mi355x_backend_supports_op",
@@ -150,6 +150,8 @@ def lib():
     L.mi355x_gemv_fused.restype = i32
     L.mi355x_debug_block_partials.argtypes = [i32, vp, i64, i64, sz, vp, vp, vp]
     L.mi355x_debug_block_partials.restype = i32
+    L.mi355x_debug_stream.argtypes = [vp, sz, vp, vp]
+    L.mi355x_debug_stream.restype = i32
     L.mi355x_backend_init.argtypes = [i32]
     L.mi355x_backend_init.restype = vp
     L.mi355x_backend_free.argtypes = [vp]

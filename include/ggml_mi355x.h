@@ -204,6 +204,12 @@ int mi355x_gemv_fused_ext(const mi355x_gemv_desc *descs, int n_desc, const float
  * dot, as the GEMV kernel computes them. For each row r and superblock b:
  * out[2*(r*nb+b)+0] = sumi (sum_j sc_j * dot_j), out[...+1] = summins
  * (sum_g bsums_g * m_{g/2}; for Q6_K: sum_g bsums_g * sc_g). Device pointers. */
+/* Diagnostic (no reference counterpart): the streaming ceiling of one launch -- the
+ * buffer's first `bytes` (rounded down to whole 2-KB steps of 12 waves per CU) pulled into
+ * LDS by non-temporal LDS-DMA, no arithmetic, on `stream`. The time a decode GEMV of that
+ * many weight bytes could approach; bench.py's gemv_large "stream_us". buf 16-B aligned,
+ * sink >= 4 device bytes. */
+int mi355x_debug_stream(const void *buf, size_t bytes, void *sink, void *stream);
 int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, int64_t ne01,
                                 size_t nb01, const void *src1_q8, int32_t *out, void *stream);
 
