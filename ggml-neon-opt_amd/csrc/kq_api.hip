@@ -32,8 +32,8 @@ __global__ void kq_stream_ceiling(const uint8_t *buf, int64_t per_wave, int wave
 __global__ void kq_quantize_f16img(const float *x, int64_t x_stride, uint8_t *img, uint8_t *bs, int nb, int64_t nblocks);
 template <int TYPE, int RR>
 __global__ void kq_mmf(const MmfArgs a);
-__global__ void kq_mmf_reduce(const float *slab, int n_split, int m_cols, int n_rows, float *y, int64_t y_col_stride,
-                              const float *res, int64_t res_col_stride);
+__global__ void kq_mmf_reduce(const float *slab, int n_split, int m_cols, int n_rows, int slab_rows, float *y,
+                              int64_t y_col_stride, const float *res, int64_t res_col_stride);
 
 namespace {
 
@@ -719,9 +719,6 @@ MmfPlan mmf_plan_rr(int64_t N, int64_t M, int64_t nb, int rr) {
 }
 // AUTO takes RR = 1 everywhere: RR = 2 (one wave per SIMD) measured equal on the 8B
 // ffn_down and 3-18 % slower on every other prefill shape (profiles/r03_mmf_rr_ab.txt).
-MmfPlan mmf_plan(int64_t N, int64_t M, int64_t nb) {
-    return mmf_plan_rr(N, M, nb, mmf_rr_env() == 2 ? 2 : 1);
-}
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 // workspace: activation image + d*bsum16 (+ the split-K slabs of either tile shape)
 size_t mmf_workspace(int64_t N, int64_t M, int64_t nb) {
@@ -763,47 +760,75 @@ int launch_f16img(const float *x, int64_t x_stride, uint8_t *ws, int64_t K, int6
     return e == hipSuccess ? MI355X_OK : (int)e;
 }
 
-int launch_mmf_gemm(int type, const void *w, int64_t K, int64_t N, size_t row_stride, uint8_t *ws, int64_t M,
-                    float *y, int64_t y_col_stride, hipStream_t stream, const float *res, int64_t res_col_stride) {
+int launch_mmf_multi(int type, int n_mat, const void *const *w, const int64_t *N, const size_t *row_stride,
+                     float *const *y, const int64_t *y_col_stride, int64_t K, uint8_t *ws, size_t ws_size, int64_t M,
+                     hipStream_t stream, const float *res, int64_t res_col_stride) {
+    if (n_mat < 1 || n_mat > 4 || (res && n_mat > 1)) return MI355X_E_INVAL;
     const int64_t nb = K / QK;
-    const MmfPlan p = mmf_plan(N, M, nb);
+    const int rr = mmf_rr_env() == 2 ? 2 : 1;
+    int64_t n_total = 0, tiles = 0;
+    for (int d = 0; d < n_mat; ++d) {
+        n_total += N[d];
+        tiles += (N[d] + 128 * rr - 1) / (128 * rr);
+    }
+    MmfPlan p = mmf_plan_rr(tiles * 128 * rr, M, nb, rr);  // the split by the grid's row tiles
     uint8_t *img = ws, *bs = ws + al256((size_t)M * nb * MMF_IMG);
-    float *slab = (float *)(bs + al256((size_t)M * nb * MMF_BSB));
+    uint8_t *slab_at = bs + al256((size_t)M * nb * MMF_BSB);
+    if (p.n_split > 1 && (size_t)(slab_at - ws) + (size_t)p.n_split * M * n_total * 4 > ws_size) {
+        p.n_split = 1;  // the slabs do not fit this workspace: no K split
+        p.nbs = (int)nb;
+    }
     MmfArgs a;
     memset(&a, 0, sizeof(a));
-    a.w = (const uint8_t *)w;
-    a.row_stride = (int64_t)row_stride;
-    a.n_rows = (int)N;
+    a.w = (const uint8_t *)w[0];
+    a.row_stride = (int64_t)row_stride[0];
+    a.n_rows = (int)n_total;
     a.img = img;
     a.bs = bs;
     a.m_cols = (int)M;
-    a.y = y;
-    a.y_col_stride = y_col_stride;
-    a.slab = slab;
+    a.y = y[0];
+    a.y_col_stride = y_col_stride[0];
+    a.slab = (float *)slab_at;
     a.nb = (int)nb;
     a.nbs = p.nbs;
     a.n_split = p.n_split;
     a.n_ct = p.n_ct;
-    a.n_rt = p.n_rt;
+    a.n_rt = (int)tiles;
     a.res = res;
     a.res_col_stride = res_col_stride;
+    a.n_mat = n_mat;
+    int64_t t0 = 0, r0 = 0;
+    for (int d = 0; d < n_mat; ++d) {
+        a.tile0[d] = (int)t0;
+        a.roff[d] = (int)r0;
+        a.mw[d] = (const uint8_t *)w[d];
+        a.mrow_stride[d] = (int64_t)row_stride[d];
+        a.mn_rows[d] = (int)N[d];
+        a.my[d] = y[d];
+        a.my_col_stride[d] = y_col_stride[d];
+        t0 += (N[d] + 128 * rr - 1) / (128 * rr);
+        r0 += N[d];
+    }
+    a.tile0[n_mat] = (int)t0;
+    if (n_mat == 1) a.n_rows = (int)N[0];
     static const int order = getenv("MI355X_MMF_ORDER") ? atoi(getenv("MI355X_MMF_ORDER")) : 0;  // A/B only
     a.order = order;
-    const void *fn = p.rr == 2 ? (type == Q5_K ? (const void *)kq_mmf<Q5_K, 2> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 2>
-                                                                                          : (const void *)kq_mmf<Q4_K, 2>)
-                               : (type == Q5_K ? (const void *)kq_mmf<Q5_K, 1> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 1>
-                                                                                          : (const void *)kq_mmf<Q4_K, 1>);
+    const void *fn = rr == 2 ? (type == Q5_K ? (const void *)kq_mmf<Q5_K, 2> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 2>
+                                                                                        : (const void *)kq_mmf<Q4_K, 2>)
+                             : (type == Q5_K ? (const void *)kq_mmf<Q5_K, 1> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 1>
+                                                                                        : (const void *)kq_mmf<Q4_K, 1>);
     const size_t lds = 2 * (size_t)MMF_BUF;
     allow_lds(fn, lds);
-    const dim3 grid((unsigned)((int64_t)p.n_ct * p.n_rt * p.n_split)), block(256);
+    const dim3 grid((unsigned)((int64_t)p.n_ct * tiles * p.n_split)), block(256);
     void *args[] = {&a};
     hipEvent_t e0, e1;
     hipError_t e;
     if (timing_slot(stream, e0, e1)) {
         e = hipExtLaunchKernel(fn, grid, block, args, lds, stream, e0, e1, 0);
-        timing_log(std::string("kq::kq_mmf<") + std::to_string(type) + ", " + std::to_string(p.rr) + ">",
-                   (double)N * nb * block_bytes(type) + (double)M * nb * (MMF_IMG + MMF_BSB) + (double)M * N * 4.0, e0,
-                   e1);
+        timing_log(std::string("kq::kq_mmf<") + std::to_string(type) + ", " + std::to_string(rr) + ">",
+                   (double)n_total * nb * block_bytes(type) + (double)M * nb * (MMF_IMG + MMF_BSB) +
+                       (double)M * n_total * 4.0,
+                   e0, e1);
     } else {
         e = hipLaunchKernel(fn, grid, block, args, lds, stream);
     }
@@ -811,19 +836,30 @@ int launch_mmf_gemm(int type, const void *w, int64_t K, int64_t N, size_t row_st
     e = hipGetLastError();
     if (e != hipSuccess) return (int)e;
     if (p.n_split > 1) {
-        const int64_t total = M * N;
-        const dim3 rg((unsigned)((total + 255) / 256));
-        if (timing_slot(stream, e0, e1)) {
-            hipExtLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, e0, e1, 0, (const float *)slab, p.n_split,
-                                  (int)M, (int)N, y, y_col_stride, res, res_col_stride);
-            timing_log("kq::kq_mmf_reduce", (double)total * 4.0 * (p.n_split + 1), e0, e1);
-        } else {
-            hipLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, (const float *)slab, p.n_split, (int)M, (int)N, y,
-                               y_col_stride, res, res_col_stride);
+        for (int d = 0; d < n_mat; ++d) {
+            const int64_t total = M * N[d];
+            const dim3 rg((unsigned)((total + 255) / 256));
+            const float *sl = (const float *)slab_at + a.roff[d];
+            const float *rs = n_mat == 1 ? res : nullptr;
+            if (timing_slot(stream, e0, e1)) {
+                hipExtLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, e0, e1, 0, sl, p.n_split, (int)M, (int)N[d],
+                                      (int)n_total, y[d], y_col_stride[d], rs, res_col_stride);
+                timing_log("kq::kq_mmf_reduce", (double)total * 4.0 * (p.n_split + 1), e0, e1);
+            } else {
+                hipLaunchKernelGGL(kq_mmf_reduce, rg, dim3(256), 0, stream, sl, p.n_split, (int)M, (int)N[d], (int)n_total,
+                                   y[d], y_col_stride[d], rs, res_col_stride);
+            }
+            e = hipGetLastError();
+            if (e != hipSuccess) return (int)e;
         }
-        e = hipGetLastError();
     }
-    return e == hipSuccess ? MI355X_OK : (int)e;
+    return MI355X_OK;
+}
+
+int launch_mmf_gemm(int type, const void *w, int64_t K, int64_t N, size_t row_stride, uint8_t *ws, int64_t M,
+                    float *y, int64_t y_col_stride, hipStream_t stream, const float *res, int64_t res_col_stride) {
+    return launch_mmf_multi(type, 1, &w, &N, &row_stride, &y, &y_col_stride, K, ws, mmf_workspace(N, M, K / QK), M,
+                            stream, res, res_col_stride);
 }
 
 // Whether launch_mmq would run this GEMM on the 64 x 64 tile kernel: every GEMM since the

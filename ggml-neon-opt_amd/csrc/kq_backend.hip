@@ -419,13 +419,14 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 i += 1;
                 continue;
             }
-            if (q8l && t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] >= 16 && batched_mm_shares(b, t) &&
+            if (t->op == MI355X_OP_MUL_MAT && t->src[1]->ne[1] >= 16 && batched_mm_shares(b, t) &&
                 kq::mmq_tile64(t->src[0]->type, t->src[0]->ne[1], t->src[1]->ne[1])) {
+                // (the f16 GEMM: one weight type per launch)
                 int run = 1;
                 while (i + run < n && run < 4) {
                     const mi355x_tensor *u = nodes[i + run];
                     if (u->op != MI355X_OP_MUL_MAT || u->src[1] != t->src[1] ||
-                        !multi_types_ok(t->src[0]->type, u->src[0]->type) ||
+                        !(q8l ? multi_types_ok(t->src[0]->type, u->src[0]->type) : t->src[0]->type == u->src[0]->type) ||
                         u->src[0]->ne[0] != t->src[0]->ne[0] || !batched_mm_shares(b, u) ||
                         !kq::mmq_tile64(u->src[0]->type, u->src[0]->ne[1], u->src[1]->ne[1]))
                         break;
@@ -641,6 +642,38 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
             q8.k = K;
             q8.m = M;
             q8.nb = m->nb[1];
+            continue;
+        }
+        if (l.kind == 4 && kq::mmf_on()) {  // the same on the f16 GEMM: the image once, one launch
+            const mi355x_tensor *x = t->src[1];
+            const int64_t K = t->src[0]->ne[0], M = x->ne[1];
+            if (!(q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1] && q8.f16)) {
+                q8 = Q8State();
+                rc = kq::launch_f16img((const float *)x->data, (int64_t)(x->nb[1] / 4), (uint8_t *)b->workspace, K, M,
+                                       b->stream);
+                if (rc) return rc;
+                q8.src = x->data, q8.k = K, q8.m = M, q8.nb = x->nb[1], q8.f16 = true;
+            }
+            const void *w[4];
+            int64_t N[4], ycs[4];
+            size_t rs[4];
+            float *y[4];
+            for (int k = 0; k < l.count; ++k) {
+                const mi355x_tensor *u = nodes[l.first + k];
+                w[k] = u->src[0]->data;
+                N[k] = u->src[0]->ne[1];
+                rs[k] = u->src[0]->nb[1];
+                y[k] = (float *)u->data;
+                ycs[k] = (int64_t)(u->nb[1] / 4);
+            }
+            rc = kq::launch_mmf_multi(t->src[0]->type, l.count, w, N, rs, y, ycs, K, (uint8_t *)b->workspace,
+                                      b->workspace_size, M, b->stream);
+            if (rc) return rc;
+            const uintptr_t s0 = (uintptr_t)q8.src, s1 = s0 + q8.nb * (size_t)q8.m;
+            for (int k = 0; k < l.count; ++k) {  // an output over the imaged activation invalidates it
+                const uintptr_t o0 = (uintptr_t)y[k], o1 = o0 + (size_t)ycs[k] * 4 * (size_t)M;
+                if (o0 < s1 && s0 < o1) q8 = Q8State();
+            }
             continue;
         }
         if (l.kind == 4) {  // several batched MUL_MATs on one activation: one tile-GEMM launch

@@ -270,6 +270,17 @@ struct MmfArgs {
     int order;                 // tile order (speed only): 0 row tiles, 1 column tiles consecutive per XCD
     const float *res;          // ADD epilogue (null: none): y = mul_mat + res, column j at
     int64_t res_col_stride;    //   res + j * res_col_stride
+    // up to 4 matrices of one type on one activation image in one launch (a prompt batch's
+    // q/k/v or gate/up): row tiles [tile0[d], tile0[d+1]) are matrix d's, its rows are slab
+    // columns [roff[d], roff[d] + mn_rows[d]) of n_rows (the sum); n_mat 1: the fields above
+    int n_mat;
+    int tile0[5];
+    int roff[4];
+    const uint8_t *mw[4];
+    int64_t mrow_stride[4];
+    int mn_rows[4];
+    float *my[4];
+    int64_t my_col_stride[4];
 };
 
 }  // namespace kq

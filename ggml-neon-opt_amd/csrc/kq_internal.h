@@ -70,6 +70,11 @@ int launch_f16img(const float *x, int64_t x_stride_floats, uint8_t *ws, int64_t 
 int launch_mmf_gemm(int type, const void *w, int64_t K, int64_t N, size_t row_stride, uint8_t *ws, int64_t M,
                     float *y, int64_t y_col_stride, hipStream_t stream, const float *res = nullptr,
                     int64_t res_col_stride = 0);
+// up to 4 matrices of one type on the image in one launch (split-K slabs only where they
+// fit ws_size)
+int launch_mmf_multi(int type, int n_mat, const void *const *w, const int64_t *N, const size_t *row_stride,
+                     float *const *y, const int64_t *y_col_stride, int64_t K, uint8_t *ws, size_t ws_size, int64_t M,
+                     hipStream_t stream, const float *res = nullptr, int64_t res_col_stride = 0);
 // KV-cache store epilogue of launch_mmq_multi (a prompt's k / v projections): kind[d] 1 k,
 // 2 v, 0 none; the cells of kq_kv_store (rope(k) -> f16 rows, v -> f16 transposed)
 struct MmqKv {

@@ -243,6 +243,27 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 
         kz = rest % a.n_split;
         ty = rest / a.n_split;
     }
+    // several matrices on one activation: this row tile's matrix (slab columns from roff)
+    const uint8_t *wmat = a.w;
+    int64_t wstride = a.row_stride;
+    int n_rows = a.n_rows, roff = 0;
+    float *y = a.y;
+    int64_t ycs = a.y_col_stride;
+    if (a.n_mat > 1) {
+        int t0 = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)  // selects, no dynamic index into the kernel arguments (scratch)
+            if (k < a.n_mat && ty >= a.tile0[k]) {
+                wmat = a.mw[k];
+                wstride = a.mrow_stride[k];
+                n_rows = a.mn_rows[k];
+                roff = a.roff[k];
+                y = a.my[k];
+                ycs = a.my_col_stride[k];
+                t0 = a.tile0[k];
+            }
+        ty -= t0;
+    }
     const int col0 = tx * MMF_COLS, row0 = ty * RT;
     const int b0 = kz * a.nbs;
     const int b1 = b0 + a.nbs < a.nb ? b0 + a.nbs : a.nb;
@@ -274,8 +295,8 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 
 #pragma unroll
     for (int rr = 0; rr < RR; ++rr) {
         int wrow = row0 + 32 * (RR * wave + rr) + r;
-        wrow = wrow < a.n_rows ? wrow : a.n_rows - 1;
-        wp[rr] = a.w + (int64_t)wrow * a.row_stride;
+        wrow = wrow < n_rows ? wrow : n_rows - 1;
+        wp[rr] = wmat + (int64_t)wrow * wstride;
     }
     constexpr int BSZ = block_bytes(TYPE);
 
@@ -347,12 +368,12 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 
     }
 
     // ---- store: lane's weight row, accumulator element i = column (i&3) + 8(i>>2) + 4h
-    float *dst = a.n_split > 1 ? a.slab + (int64_t)kz * a.m_cols * a.n_rows : a.y;
-    const int64_t cs = a.n_split > 1 ? (int64_t)a.n_rows : a.y_col_stride;
+    float *dst = a.n_split > 1 ? a.slab + (int64_t)kz * a.m_cols * a.n_rows + roff : y;
+    const int64_t cs = a.n_split > 1 ? (int64_t)a.n_rows : ycs;
 #pragma unroll
     for (int rr = 0; rr < RR; ++rr) {
         const int n = row0 + 32 * (RR * wave + rr) + r;
-        if (n >= a.n_rows) continue;
+        if (n >= n_rows) continue;
 #pragma unroll
         for (int ct = 0; ct < 4; ++ct)
 #pragma unroll
@@ -366,16 +387,20 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 
     }
 }
 
-// Split-K combine: y = sum of the n_split partial slabs, in split order (+ res).
+// Split-K combine: y = sum of the n_split partial slabs, in split order (+ res). The slab
+// holds n_split planes of m_cols x slab_rows; this matrix is its columns [0, n_rows) from
+// `slab` on.
 __global__ void __launch_bounds__(256) kq_mmf_reduce(const float *__restrict__ slab, int n_split, int m_cols,
-                                                     int n_rows, float *__restrict__ y, int64_t y_col_stride,
-                                                     const float *__restrict__ res, int64_t res_col_stride) {
-    const int64_t total = (int64_t)m_cols * n_rows;
+                                                     int n_rows, int slab_rows, float *__restrict__ y,
+                                                     int64_t y_col_stride, const float *__restrict__ res,
+                                                     int64_t res_col_stride) {
+    const int64_t total = (int64_t)m_cols * n_rows, plane = (int64_t)m_cols * slab_rows;
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x;
     if (i >= total) return;
-    float s = slab[i];
-    for (int k = 1; k < n_split; ++k) s += slab[(int64_t)k * total + i];
     const int64_t c = i / n_rows, n = i - c * n_rows;
+    const float *p = slab + c * slab_rows + n;
+    float s = p[0];
+    for (int k = 1; k < n_split; ++k) s += p[(int64_t)k * plane];
     y[c * y_col_stride + n] = res ? s + res[c * res_col_stride + n] : s;
 }
 

@@ -84,8 +84,9 @@ def test_prefill_precision_selector(dev):
 def test_llama_prompt_f16(dev, f16path, mix):
     """The prompt graph on the f16 GEMMs (every MUL_MAT at ne11 = 37 through kq_mmf, the
     norm / swiglu as their own nodes, the residual ADD as the GEMM's epilogue):
-    * fused (ADD epilogue, one activation image shared by q/k/v and gate/up) and unfused
-      graphs give bit-identical logits and caches, and a replay repeats them exactly;
+    * a replay of the captured graph repeats its logits exactly, and the fused graph
+      (multi-matrix launches, ADD epilogue, one activation image per activation) gives
+      layer 0's K cache of the unfused one bit for bit;
     * layer 0's K cache (one GEMM deep) is within a relative L2 error of 2^-9 of the
       bit-exact prompt's;
     * the logits are within 2^-5 (relative L2) of the oracle's sequential llm_build_llama.
@@ -117,8 +118,11 @@ def test_llama_prompt_f16(dev, f16path, mix):
                      [c[:n].view(torch.float16).float().cpu().numpy() for c in dec.k_cache])
         b.close()
     g.prefill_precision(g.PREFILL_F16)
-    assert np.array_equal(out["f16"][0], out["f16_unfused"][0])
-    assert all(np.array_equal(a, c) for a, c in zip(out["f16"][1], out["f16_unfused"][1]))
+    # fused (q/k/v and gate/up as multi-matrix launches) vs unfused: layer 0's K cache (one
+    # GEMM deep, the same K split either way) bit for bit; later values differ by the f32
+    # summation order of other splits, grown by the model (test_mmf_multi_matrix_launch
+    # checks the multi-matrix GEMM itself)
+    assert np.array_equal(out["f16"][1][0], out["f16_unfused"][1][0])
     k0, k0e = out["f16"][1][0], out["exact"][1][0]
     assert np.isfinite(k0).all() and np.linalg.norm(k0 - k0e) <= 2.0 ** -9 * np.linalg.norm(k0e)
     model, cache = LM.oracle_model(hp, w, n_ctx)
@@ -130,3 +134,40 @@ def test_llama_prompt_f16(dev, f16path, mix):
     assert np.isfinite(got).all()
     assert np.linalg.norm(got - ref) <= 2.0 ** -5 * np.linalg.norm(ref)
     torch.cuda.synchronize()
+
+
+@pytest.mark.parametrize("K,Ns,M", [(2048, (2048, 256, 256), 37), (4096, (4096, 1024, 1024), 128),
+                                    (1024, (300, 130), 200)], ids=["tl_qkv", "l3_qkv", "ragged"])
+def test_mmf_multi_matrix_launch(dev, oracle, npo, f16path, K, Ns, M):
+    """Several MUL_MATs on one activation in one backend graph run as ONE f16 launch (row
+    tiles per matrix, slab columns per matrix for split-K): every output within the stated
+    bound of the oracle, and equal to the single-matrix launches up to f32 summation order."""
+    import ggml_mi355x as g
+    rng = np.random.default_rng(K + sum(Ns) + M)
+    be = g.Backend()
+    x = rng.standard_normal((M, K)).astype(np.float32)
+    xp = be.alloc(x.nbytes)
+    be.set_tensor(xp, x)
+    xt = g.make_tensor(g.TYPE_F32, K, M, xp)
+    ws, nodes, outs, keep = [], [], [], [xt]
+    for N in Ns:
+        w = npo.random_blocks(rng, 12, N, K)
+        p = be.alloc(w.nbytes)
+        be.set_tensor(p, w)
+        wt = g.make_tensor(12, K, N, p)
+        y = be.alloc(M * N * 4)
+        nodes.append(g.make_tensor(g.TYPE_F32, N, M, y, op=g.OP_MUL_MAT, src0=wt, src1=xt))
+        ws.append(w)
+        outs.append(y)
+        keep.append(wt)
+    assert be.graph_compute(nodes, use_graph=True) == 0
+    be.synchronize()
+    for w, y, N in zip(ws, outs, Ns):
+        got = np.zeros((M, N), np.float32)
+        be.get_tensor(got, y)
+        be.synchronize()
+        check(got, w, 12, K, x, oracle, npo)
+        single = g.mul_mat(12, t(w, dev), K, t(x, dev)).cpu().numpy().astype(np.float64)
+        bound = npo.mmf_bound(w, 12, K, x)
+        assert (np.abs(got.astype(np.float64) - single) <= bound * 2.0 ** -6).all()
+    be.close()
