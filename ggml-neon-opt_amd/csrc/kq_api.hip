@@ -682,7 +682,9 @@ int prefill_precision() {
     int v = g_prefill.load();
     if (v < 0) {
         const char *e = getenv("MI355X_PREFILL");
-        const int x = e && strcmp(e, "f16") == 0 ? MI355X_PREFILL_F16 : MI355X_PREFILL_EXACT;
+        const int x = e && strcmp(e, "f16") == 0       ? MI355X_PREFILL_F16
+                      : e && strcmp(e, "f16_all") == 0 ? MI355X_PREFILL_F16_ALL
+                                                       : MI355X_PREFILL_EXACT;
         int expect = -1;
         g_prefill.compare_exchange_strong(expect, x);
         v = g_prefill.load();
@@ -730,16 +732,25 @@ size_t mmf_workspace(int64_t N, int64_t M, int64_t nb) {
     }
     return w + slab;
 }
-bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M) {
-    if (prefill_precision() != MI355X_PREFILL_F16) return false;
+// Where the f16 path is the faster one (M = 512, profiles/r03_mmf_*): Q5_K and Q6_K
+// everywhere; Q4_K from N*K >= 32 M elements (8B ffn_up / ffn_down), while the int8 tiles
+// stay ahead on the smaller Q4_K GEMMs (8B q/o 36 vs 38 us, TinyLlama gate 31 vs 36 us).
+// The precision switch promises the stated tolerance, which the bit-exact kernel meets
+// trivially; MI355X_PREFILL_F16_ALL forces the f16 kernel on every shape (A/B, tests).
+bool mmf_prefers(int type, int64_t N, int64_t K) {
+    return prefill_precision() == MI355X_PREFILL_F16_ALL || type != Q4_K || N * K >= ((int64_t)32 << 20);
+}
+bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M, int64_t K) {
+    if (prefill_precision() < MI355X_PREFILL_F16) return false;
     if (!rows_enabled() || M < kMmqMinCols || N <= 0) return false;
     if (type != Q4_K && type != Q5_K && type != Q6_K) return false;
     if (N >= (1ll << 31) || M >= (1ll << 31)) return false;
+    if (!mmf_prefers(type, N, K)) return false;
     if (type == Q6_K) return true;  // 210-B blocks: unaligned vector loads
     return ((uintptr_t)w & 15u) == 0 && (row_stride & 15u) == 0;
 }
 
-bool mmf_on() { return prefill_precision() == MI355X_PREFILL_F16; }
+bool mmf_on() { return prefill_precision() >= MI355X_PREFILL_F16; }
 
 int launch_f16img(const float *x, int64_t x_stride, uint8_t *ws, int64_t K, int64_t M, hipStream_t stream) {
     const int64_t nb = K / QK;
@@ -1267,7 +1278,7 @@ int mi355x_mul_mat(int src0_type, const void *src0, int64_t ne00, int64_t ne01, 
     }
     size_t need = mi355x_mul_mat_workspace_size(src0_type, ne00, ne01, ne11);
     if (!workspace || workspace_size < need) return MI355X_E_WORKSPACE;
-    if (mmf_applies(src0_type, src0, ne01, nb01, ne11) && ((uintptr_t)workspace & 15u) == 0) {
+    if (mmf_applies(src0_type, src0, ne01, nb01, ne11, ne00) && ((uintptr_t)workspace & 15u) == 0) {
         if (!device_ok()) return MI355X_E_NODEVICE;
         int rc = launch_f16img(src1, (int64_t)(nb11 / 4), (uint8_t *)workspace, ne00, ne11, (hipStream_t)stream);
         if (rc) return rc;
@@ -1373,7 +1384,7 @@ int mi355x_mmq_impl(int impl) {
 
 int mi355x_prefill_precision(int precision) {
     if (precision < 0) return prefill_precision();  // query
-    if (precision > MI355X_PREFILL_F16) return MI355X_E_INVAL;
+    if (precision > MI355X_PREFILL_F16_ALL) return MI355X_E_INVAL;
     const int prev = prefill_precision();
     g_prefill.store(precision);
     return prev;

@@ -220,7 +220,7 @@ int enqueue_batched_mm(mi355x_backend *b, const mi355x_tensor *t, Q8State &q8, f
         y_stride = (int64_t)(t->nb[1] / 4);
     }
     const int64_t K = w->ne[0], M = x->ne[1];
-    const bool f16 = kq::mmf_on();
+    const bool f16 = kq::mmf_applies(w->type, w->data, w->ne[1], w->nb[1], M, K);
     const bool same = q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1] && q8.f16 == f16;
     if (f16) {  // the stated-tolerance f16 path: image once per activation, then the GEMM
         int rc = 0;
@@ -275,12 +275,19 @@ void attn_desc_of(const mi355x_tensor *t, mi355x_attn_desc &a) {
     a.n_ctx = (int)t->src[4]->ne[1];
 }
 
+// A batched MUL_MAT that runs on the int8 GEMM (kq_mmq, Q8L activation blocks): always in
+// the exact precision, and in the f16 one where kq_mmf is not the faster kernel
+bool mm_exact(const mi355x_tensor *t) {
+    const mi355x_tensor *w = t->src[0], *x = t->src[1];
+    return !kq::mmf_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1], w->ne[0]);
+}
+
 bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
     if (t->op != MI355X_OP_MUL_MAT) return false;
     const mi355x_tensor *w = t->src[0], *x = t->src[1];
     if (x->ne[1] < 16 || (x->nb[1] & 3u) || (t->nb[1] & 3u) || ((uintptr_t)b->workspace & 15u)) return false;
-    if (kq::mmf_on() ? !kq::mmf_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1])
-                     : !kq::mmq_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1]))
+    if (!kq::mmf_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1], w->ne[0]) &&
+        !kq::mmq_applies(w->type, w->data, w->ne[1], w->nb[1], x->ne[1]))
         return false;
     return b->workspace_size >= mi355x_mul_mat_workspace_size(w->type, w->ne[0], w->ne[1], x->ne[1]);
 }
@@ -377,18 +384,19 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
         // prefill (batched, ne11 >= 16) fusions: the normed / swiglu'd activation goes straight
         // into the GEMMs' Q8L blocks (never written as f32), and MUL_MAT -> ADD as the GEMM's
         // epilogue; only where every consumer takes the shared-activation GEMM. On the f16
-        // path (kq_mmf) only the ADD epilogue: its GEMMs read an f16 image of the f32 activation.
-        const bool q8l = !kq::mmf_on();
+        // path (kq_mmf) only where every consumer stays on the int8 GEMM: kq_mmf reads an f16
+        // image of the f32 activation.
         if (fuse) {
             auto shares_run = [&](int first, const mi355x_tensor *src, int &cnt) {
                 cnt = 0;
                 while (first + cnt < n && nodes[first + cnt]->op == MI355X_OP_MUL_MAT &&
-                       nodes[first + cnt]->src[1] == src && batched_mm_shares(b, nodes[first + cnt]))
+                       nodes[first + cnt]->src[1] == src && batched_mm_shares(b, nodes[first + cnt]) &&
+                       mm_exact(nodes[first + cnt]))
                     ++cnt;
                 return cnt > 0;
             };
             int cnt = 0;
-            if (q8l && t->op == MI355X_OP_RMS_NORM && t->ne[1] >= 16 && i + 2 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
+            if (t->op == MI355X_OP_RMS_NORM && t->ne[1] >= 16 && i + 2 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
                 nodes[i + 1]->src[0] == t && elidable(t, readers[i]) && nodes[i + 1]->ne[0] == t->ne[0] &&
                 nodes[i + 1]->ne[1] == t->ne[1] && nodes[i + 1]->src[1]->ne[0] == t->ne[0] &&
                 nelem(nodes[i + 1]->src[1]) == t->ne[0] && t->nb[1] == (size_t)t->ne[0] * 4 &&
@@ -406,7 +414,7 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 i += 2;
                 continue;
             }
-            if (q8l && t->op == MI355X_OP_SWIGLU && t->ne[1] >= 16 && t->ne[0] % MI355X_QK_K == 0 &&
+            if (t->op == MI355X_OP_SWIGLU && t->ne[1] >= 16 && t->ne[0] % MI355X_QK_K == 0 &&
                 t->nb[1] == (size_t)t->ne[0] * 4 && t->src[0]->nb[1] == t->nb[1] && t->src[1]->nb[1] == t->nb[1] &&
                 nelem(t->src[0]) == nelem(t) && nelem(t->src[1]) == nelem(t) && !(t->flags & MI355X_TENSOR_FLAG_OUTPUT) &&
                 shares_run(i + 1, t, cnt) && readers[i] == cnt) {
@@ -426,7 +434,8 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
                 while (i + run < n && run < 4) {
                     const mi355x_tensor *u = nodes[i + run];
                     if (u->op != MI355X_OP_MUL_MAT || u->src[1] != t->src[1] ||
-                        !(q8l ? multi_types_ok(t->src[0]->type, u->src[0]->type) : t->src[0]->type == u->src[0]->type) ||
+                        !(mm_exact(t) ? multi_types_ok(t->src[0]->type, u->src[0]->type)
+                                      : t->src[0]->type == u->src[0]->type) ||
                         u->src[0]->ne[0] != t->src[0]->ne[0] || !batched_mm_shares(b, u) ||
                         !kq::mmq_tile64(u->src[0]->type, u->src[0]->ne[1], u->src[1]->ne[1]))
                         break;
@@ -555,9 +564,9 @@ int enqueue_node(mi355x_backend *b, const Launch &l, const mi355x_tensor *t) {
 bool attn_feeds_batched_mm(const mi355x_backend *b, const mi355x_tensor *t, const Launch &next,
                            mi355x_tensor *const *nodes) {
     if (t->src[0]->ne[1] < 16 || t->nb[1] != (size_t)t->ne[0] * 4) return false;
-    if (kq::mmf_on()) return false;  // the f16 GEMMs read an f16 image, not Q8L blocks
     if (next.kind != 0 && next.kind != 3 && next.kind != 4) return false;
     const mi355x_tensor *m = nodes[next.first];
+    if (m->op == MI355X_OP_MUL_MAT && !mm_exact(m)) return false;  // kq_mmf reads an f16 image, not Q8L
     if (m->op != MI355X_OP_MUL_MAT || m->src[1] != t || m->src[0]->ne[0] != t->ne[0]) return false;
     if (next.kind == 0 && next.count != 1) return false;
     if (!batched_mm_shares(b, m)) return false;
@@ -644,7 +653,12 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
             q8.nb = m->nb[1];
             continue;
         }
-        if (l.kind == 4 && kq::mmf_on()) {  // the same on the f16 GEMM: the image once, one launch
+        bool f16_run = l.kind == 4 && kq::mmf_on();
+        for (int k = 0; f16_run && k < l.count; ++k) {  // every matrix where the f16 kernel is the faster one
+            const mi355x_tensor *u = nodes[l.first + k]->src[0];
+            f16_run = kq::mmf_applies(u->type, u->data, u->ne[1], u->nb[1], nodes[l.first + k]->src[1]->ne[1], u->ne[0]);
+        }
+        if (f16_run) {  // the same on the f16 GEMM: the image once, one launch
             const mi355x_tensor *x = t->src[1];
             const int64_t K = t->src[0]->ne[0], M = x->ne[1];
             if (!(q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1] && q8.f16)) {
@@ -679,7 +693,8 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
         if (l.kind == 4) {  // several batched MUL_MATs on one activation: one tile-GEMM launch
             const mi355x_tensor *x = t->src[1];
             const int64_t K = t->src[0]->ne[0], M = x->ne[1];
-            if (!(q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1])) {
+            if (!(q8.src == x->data && q8.k == K && q8.m == M && q8.nb == x->nb[1] && !q8.f16)) {
+                q8 = Q8State();
                 rc = kq::launch_quantize_q8L((const float *)x->data, (int64_t)(x->nb[1] / 4), b->workspace, K, M,
                                              b->stream, true);
                 if (rc) return rc;

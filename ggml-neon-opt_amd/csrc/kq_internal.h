@@ -65,7 +65,8 @@ bool mmq_tile64(int type, int64_t N, int64_t M);  // launch_mmq would use the 64
 // (kq_quantize_f16img) at the workspace start, then the GEMM (its split-K slabs after the
 // image); res: ADD epilogue
 bool mmf_on();
-bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M);
+bool mmf_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M, int64_t K);  // + mmf_prefers
+bool mmf_prefers(int type, int64_t N, int64_t K);  // the f16 kernel is the faster one at this shape
 int launch_f16img(const float *x, int64_t x_stride_floats, uint8_t *ws, int64_t K, int64_t M, hipStream_t stream);
 int launch_mmf_gemm(int type, const void *w, int64_t K, int64_t N, size_t row_stride, uint8_t *ws, int64_t M,
                     float *y, int64_t y_col_stride, hipStream_t stream, const float *res = nullptr,

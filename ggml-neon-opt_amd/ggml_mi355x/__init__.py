@@ -31,7 +31,7 @@ PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 ATTN_GROUP, ATTN_HEAD = 0, 1
 MMQ_AUTO, MMQ_TILE64, MMQ_TILE128, MMQ_TILE128W, MMQ_TILE64W = 0, 1, 2, 3, 4
-PREFILL_EXACT, PREFILL_F16 = 0, 1
+PREFILL_EXACT, PREFILL_F16, PREFILL_F16_ALL = 0, 1, 2
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).
 EXPORTED_SYMBOLS = (
@@ -380,8 +380,9 @@ def mmq_impl(impl):
 
 
 def prefill_precision(p=-1):
-    """Prefill (M >= 16) precision: PREFILL_EXACT (bit-exact kq_mmq) or PREFILL_F16 (kq_mmf,
-    stated tolerance); -1 queries. Returns the previous value."""
+    """Prefill (M >= 16) precision: PREFILL_EXACT (bit-exact kq_mmq), PREFILL_F16 (stated
+    tolerance: kq_mmf where it is faster) or PREFILL_F16_ALL (kq_mmf on every shape); -1
+    queries. Returns the previous value."""
     return int(lib().mi355x_prefill_precision(p))
 
 

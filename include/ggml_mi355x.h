@@ -256,15 +256,18 @@ int mi355x_gemv_impl(int impl);
 #define MI355X_MMQ_TILE64W 4 /* 64 rows x 128 columns, 4 waves (two column tiles per wave) */
 int mi355x_mmq_impl(int impl);
 /* Prefill (ne11 >= 16) precision: MI355X_PREFILL_EXACT (kq_mmq, int8 MFMA, bit-exact
- * against ggml's per-(row, column) vec_dot loop; the default) or MI355X_PREFILL_F16
- * (kq_mmf: the same Q8_K activation quantization and integer unpacking, the accumulated
- * dot on the f16 matrix core within a stated tolerance, csrc/kq_mmf.hip). The
- * north_star's "within a stated fp32 tolerance on the accumulated dot". Replaces no
- * reference interface (ggml-cpu has one precision); a backend option like llama.cpp's
- * GGML_CUDA_FORCE_MMQ / cuBLAS choice. A negative value queries. Environment default:
- * MI355X_PREFILL=f16. Returns the previous value, or MI355X_E_INVAL. */
+ * against ggml's per-(row, column) vec_dot loop; the default), MI355X_PREFILL_F16 (within
+ * a stated tolerance: kq_mmf -- the same Q8_K activation quantization and integer
+ * unpacking, the accumulated dot on the f16 matrix core, csrc/kq_mmf.hip -- on the shapes
+ * where it is the faster kernel, kq_mmq elsewhere) or MI355X_PREFILL_F16_ALL (kq_mmf on
+ * every shape; A/B and tests). The north_star's "within a stated fp32 tolerance on the
+ * accumulated dot". Replaces no reference interface (ggml-cpu has one precision); a
+ * backend option like llama.cpp's GGML_CUDA_FORCE_MMQ / cuBLAS choice. A negative value
+ * queries. Environment default: MI355X_PREFILL=f16 / f16_all. Returns the previous value,
+ * or MI355X_E_INVAL. */
 #define MI355X_PREFILL_EXACT 0
 #define MI355X_PREFILL_F16 1
+#define MI355X_PREFILL_F16_ALL 2
 int mi355x_prefill_precision(int precision);
 /* Decode GEMV (kq_rows) waves per workgroup (A/B runs, parity of both launch shapes):
  * 0 = by launch size (6 waves under 10 MB of weights, else 12; env MI355X_GEMV_SMALL_MB

@@ -16,8 +16,9 @@ def t(a, dev):
 
 @pytest.fixture
 def f16path():
+    """The f16 kernel on every shape (PREFILL_F16_ALL), so that each test exercises kq_mmf."""
     import ggml_mi355x as g
-    prev = g.prefill_precision(g.PREFILL_F16)
+    prev = g.prefill_precision(g.PREFILL_F16_ALL)
     yield
     g.prefill_precision(prev)
 
@@ -76,8 +77,36 @@ def test_prefill_precision_selector(dev):
     assert prev == g.PREFILL_EXACT  # the default: bit-exact kq_mmq
     assert g.prefill_precision(g.PREFILL_F16) == prev
     assert g.prefill_precision(-1) == g.PREFILL_F16
-    assert g.prefill_precision(prev) == g.PREFILL_F16
+    assert g.prefill_precision(g.PREFILL_F16_ALL) == g.PREFILL_F16
+    assert g.prefill_precision(prev) == g.PREFILL_F16_ALL
     assert g.lib().mi355x_prefill_precision(7) == g.E_INVAL
+
+
+def test_prefill_f16_per_shape_choice(dev, oracle, npo):
+    """PREFILL_F16 runs kq_mmf where it is the faster kernel (Q5_K / Q6_K, large Q4_K) and
+    the bit-exact kq_mmq elsewhere: the launch names say which, every result within the
+    stated bound (and the exact ones bit-exact)."""
+    import ggml_mi355x as g
+    prev = g.prefill_precision(g.PREFILL_F16)
+    try:
+        rng = np.random.default_rng(21)
+        for type_, K, N, want in ((12, 2048, 256, "kq_mmq"), (14, 2048, 256, "kq_mmf"), (13, 512, 64, "kq_mmf"),
+                                  (12, 8192, 4096, "kq_mmf")):
+            M = 32
+            w = npo.random_blocks(rng, type_, N, K)
+            x = rng.standard_normal((M, K)).astype(np.float32)
+            g.timing_enable(True)
+            got = g.mul_mat(type_, t(w, dev), K, t(x, dev)).cpu().numpy()
+            names = [r[0] for r in g.timing_read()]
+            g.timing_enable(False)
+            assert any(want in n for n in names), (type_, K, N, names)
+            if want == "kq_mmq":
+                assert np.array_equal(got.view(np.uint32), oracle.mul_mat(type_, w, x).view(np.uint32))
+            else:
+                ref = oracle.mul_mat(type_, w, x).astype(np.float64)
+                assert (np.abs(got - ref) <= npo.mmf_bound(w, type_, K, x)).all()
+    finally:
+        g.prefill_precision(prev)
 
 
 @pytest.mark.parametrize("mix", ["q4_k_m", "q5_k_m"])
@@ -104,8 +133,8 @@ def test_llama_prompt_f16(dev, f16path, mix):
     n_ctx, n = 64, 37
     tokens = np.random.default_rng(13).integers(0, hp["n_vocab"], size=n).tolist()
     out = {}
-    for name, prec, fuse in (("exact", g.PREFILL_EXACT, True), ("f16", g.PREFILL_F16, True),
-                             ("f16_unfused", g.PREFILL_F16, False)):
+    for name, prec, fuse in (("exact", g.PREFILL_EXACT, True), ("f16", g.PREFILL_F16_ALL, True),
+                             ("f16_unfused", g.PREFILL_F16_ALL, False), ("f16_auto", g.PREFILL_F16, True)):
         g.prefill_precision(prec)
         w, b, dec = _decoder(dev, hp, 7, n_ctx, fuse, mix=mix)
         lg = dec.prompt(tokens, 0)
@@ -117,7 +146,9 @@ def test_llama_prompt_f16(dev, f16path, mix):
         out[name] = (first.astype(np.float64).ravel(),
                      [c[:n].view(torch.float16).float().cpu().numpy() for c in dec.k_cache])
         b.close()
-    g.prefill_precision(g.PREFILL_F16)
+    g.prefill_precision(g.PREFILL_F16_ALL)
+    got = out["f16_auto"][0]  # the per-shape choice (kq_mmq on TinyLlama's small Q4_K GEMMs)
+    assert np.isfinite(got).all()
     # fused (q/k/v and gate/up as multi-matrix launches) vs unfused: layer 0's K cache (one
     # GEMM deep, the same K split either way) bit for bit; later values differ by the f32
     # summation order of other splits, grown by the model (test_mmf_multi_matrix_launch
