@@ -30,7 +30,7 @@ template <int RT, int CW>
 __global__ void kq_mmq_mixed(const MmqArgs a);
 __global__ void kq_stream_ceiling(const uint8_t *buf, int64_t per_wave, int waves_total, uint32_t *sink);
 __global__ void kq_quantize_f16img(const float *x, int64_t x_stride, uint8_t *img, uint8_t *bs, int nb, int64_t nblocks);
-template <int TYPE, int RR>
+template <int TYPE, int NW>
 __global__ void kq_mmf(const MmfArgs a);
 __global__ void kq_mmf_reduce(const float *slab, int n_split, int m_cols, int n_rows, int slab_rows, float *y,
                               int64_t y_col_stride, const float *res, int64_t res_col_stride);
@@ -692,41 +692,39 @@ int prefill_precision() {
     return v;
 }
 
-// Row tiles per wave of kq_mmf (MI355X_MMF_RR, A/B only): 1 (128-row workgroups, two per
-// CU), 2 (256-row workgroups, one per CU), 0 by shape.
-int mmf_rr_env() {
-    static const int v = getenv("MI355X_MMF_RR") ? atoi(getenv("MI355X_MMF_RR")) : 0;
-    return v;
+// Waves per kq_mmf workgroup (MI355X_MMF_WAVES, A/B only): 4 (128-row workgroups, two per
+// CU) or 8 (256-row workgroups, one per CU); 0 by shape: 8 from K >= 8192, where the
+// activation tile's refill is the longer wait (8B ffn_down Q4_K 99-106 -> 88-96 us, Q6_K
+// 134 -> 117-122, Q5_K 104 -> 93), 4 below it (8B ffn_up 82.5 vs 99.7 us on 8 waves:
+// its 224-workgroup grid leaves CUs idle) -- profiles/r03_mmf_waves_ab.txt.
+int mmf_nw(int64_t K) {
+    static const int v = getenv("MI355X_MMF_WAVES") ? atoi(getenv("MI355X_MMF_WAVES")) : 0;
+    return v == 4 || v == 8 ? v : K >= 8192 ? 8 : 4;
 }
-// K split of kq_mmf: double it while the grid has fewer workgroups than CUs (RR = 1:
+// K split of kq_mmf: double it while the grid has fewer workgroups than CUs and every
+// split keeps >= 4 superblocks (8 half-superblock steps); splits combine in order (NW = 4:
 // filling both resident slots per CU with a 4-way split measured slower on 8B q/o, 34 ->
-// 37 us) or, at RR = 2, fits one round of one workgroup per CU; every split keeps >= 4
-// superblocks (8 half-superblock steps); splits combine in order.
+// 37 us).
 struct MmfPlan {
-    int rr, n_ct, n_rt, n_split, nbs;
+    int nw, n_ct, n_rt, n_split, nbs;
 };
-MmfPlan mmf_plan_rr(int64_t N, int64_t M, int64_t nb, int rr) {
+MmfPlan mmf_plan_nw(int64_t N, int64_t M, int64_t nb, int nw) {
     MmfPlan p;
-    p.rr = rr;
+    p.nw = nw;
     p.n_ct = (int)((M + MMF_COLS - 1) / MMF_COLS);
-    p.n_rt = (int)((N + 128 * rr - 1) / (128 * rr));
+    p.n_rt = (int)((N + 32 * nw - 1) / (32 * nw));
     int s = 1;
-    if (rr == 1)
-        while ((int64_t)p.n_ct * p.n_rt * s < 256 && nb >= 8 * s) s *= 2;
-    else
-        while ((int64_t)p.n_ct * p.n_rt * s * 2 <= 256 && nb >= 8 * s) s *= 2;
+    while ((int64_t)p.n_ct * p.n_rt * s < 256 && nb >= 8 * s) s *= 2;
     p.nbs = (int)((nb + s - 1) / s);
     p.n_split = (int)((nb + p.nbs - 1) / p.nbs);
     return p;
 }
-// AUTO takes RR = 1 everywhere: RR = 2 (one wave per SIMD) measured equal on the 8B
-// ffn_down and 3-18 % slower on every other prefill shape (profiles/r03_mmf_rr_ab.txt).
 size_t al256(size_t v) { return (v + 255) & ~(size_t)255; }
 // workspace: activation image + d*bsum16 (+ the split-K slabs of either tile shape)
 size_t mmf_workspace(int64_t N, int64_t M, int64_t nb) {
     size_t w = al256((size_t)M * nb * MMF_IMG) + al256((size_t)M * nb * MMF_BSB), slab = 0;
-    for (int rr = 1; rr <= 2; ++rr) {
-        const MmfPlan p = mmf_plan_rr(N, M, nb, rr);
+    for (int nw = 4; nw <= 8; nw += 4) {
+        const MmfPlan p = mmf_plan_nw(N, M, nb, nw);
         const size_t sb = p.n_split > 1 ? al256((size_t)p.n_split * M * N * 4) : 0;
         slab = sb > slab ? sb : slab;
     }
@@ -776,13 +774,13 @@ int launch_mmf_multi(int type, int n_mat, const void *const *w, const int64_t *N
                      hipStream_t stream, const float *res, int64_t res_col_stride) {
     if (n_mat < 1 || n_mat > 4 || (res && n_mat > 1)) return MI355X_E_INVAL;
     const int64_t nb = K / QK;
-    const int rr = mmf_rr_env() == 2 ? 2 : 1;
+    const int nw = mmf_nw(K);
     int64_t n_total = 0, tiles = 0;
     for (int d = 0; d < n_mat; ++d) {
         n_total += N[d];
-        tiles += (N[d] + 128 * rr - 1) / (128 * rr);
+        tiles += (N[d] + 32 * nw - 1) / (32 * nw);
     }
-    MmfPlan p = mmf_plan_rr(tiles * 128 * rr, M, nb, rr);  // the split by the grid's row tiles
+    MmfPlan p = mmf_plan_nw(tiles * 32 * nw, M, nb, nw);  // the split by the grid's row tiles
     uint8_t *img = ws, *bs = ws + al256((size_t)M * nb * MMF_IMG);
     uint8_t *slab_at = bs + al256((size_t)M * nb * MMF_BSB);
     if (p.n_split > 1 && (size_t)(slab_at - ws) + (size_t)p.n_split * M * n_total * 4 > ws_size) {
@@ -817,26 +815,26 @@ int launch_mmf_multi(int type, int n_mat, const void *const *w, const int64_t *N
         a.mn_rows[d] = (int)N[d];
         a.my[d] = y[d];
         a.my_col_stride[d] = y_col_stride[d];
-        t0 += (N[d] + 128 * rr - 1) / (128 * rr);
+        t0 += (N[d] + 32 * nw - 1) / (32 * nw);
         r0 += N[d];
     }
     a.tile0[n_mat] = (int)t0;
     if (n_mat == 1) a.n_rows = (int)N[0];
     static const int order = getenv("MI355X_MMF_ORDER") ? atoi(getenv("MI355X_MMF_ORDER")) : 0;  // A/B only
     a.order = order;
-    const void *fn = rr == 2 ? (type == Q5_K ? (const void *)kq_mmf<Q5_K, 2> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 2>
-                                                                                        : (const void *)kq_mmf<Q4_K, 2>)
-                             : (type == Q5_K ? (const void *)kq_mmf<Q5_K, 1> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 1>
-                                                                                        : (const void *)kq_mmf<Q4_K, 1>);
+    const void *fn = nw == 8 ? (type == Q5_K ? (const void *)kq_mmf<Q5_K, 8> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 8>
+                                                                                        : (const void *)kq_mmf<Q4_K, 8>)
+                             : (type == Q5_K ? (const void *)kq_mmf<Q5_K, 4> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 4>
+                                                                                        : (const void *)kq_mmf<Q4_K, 4>);
     const size_t lds = 2 * (size_t)MMF_BUF;
     allow_lds(fn, lds);
-    const dim3 grid((unsigned)((int64_t)p.n_ct * tiles * p.n_split)), block(256);
+    const dim3 grid((unsigned)((int64_t)p.n_ct * tiles * p.n_split)), block(64 * nw);
     void *args[] = {&a};
     hipEvent_t e0, e1;
     hipError_t e;
     if (timing_slot(stream, e0, e1)) {
         e = hipExtLaunchKernel(fn, grid, block, args, lds, stream, e0, e1, 0);
-        timing_log(std::string("kq::kq_mmf<") + std::to_string(type) + ", " + std::to_string(rr) + ">",
+        timing_log(std::string("kq::kq_mmf<") + std::to_string(type) + ", " + std::to_string(nw) + ">",
                    (double)n_total * nb * block_bytes(type) + (double)M * nb * (MMF_IMG + MMF_BSB) +
                        (double)M * n_total * 4.0,
                    e0, e1);

@@ -211,13 +211,16 @@ __global__ void __launch_bounds__(WG_THREADS) kq_quantize_f16img(const float *__
 }
 
 // ------------------------------------------------------------------ GEMM
-// RR row tiles of 32 per wave: RR = 1 (128 weight rows per workgroup, two workgroups per
-// CU) or RR = 2 (256 rows, one workgroup per CU, every register: each activation fragment
-// read from LDS feeds two MFMAs, the LDS-DMA and LDS reads per MFMA halve).
-template <int TYPE, int RR>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 1 ? 2 : 1))) kq_mmf(const MmfArgs a) {
+// NW waves of 32 weight rows each: NW = 4 (128 rows per workgroup, two workgroups per CU)
+// or NW = 8 (256 rows, one workgroup per CU: the activation tile's LDS-DMA shared by twice
+// the rows). Round 3 also measured two row tiles per wave (256 rows on 4 waves, one wave
+// per SIMD, accumulators in AGPRs): equal on 8B ffn_down, 3-18 % slower elsewhere
+// (profiles/r03_mmf_rr_ab.txt); removed.
+template <int TYPE, int NW>
+__global__ void __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(2))) kq_mmf(const MmfArgs a) {
+    constexpr int RR = 1;
     constexpr int HALF = MMF_COLS * MMF_IMG / 2;  // 32 KB of image per step
-    constexpr int RT = 128 * RR;                  // weight rows per workgroup
+    constexpr int RT = 32 * NW;                   // weight rows per workgroup
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -272,19 +275,19 @@ __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(RR == 
 
     // DMA of step st (superblock b0 + st/2, half st&1): 32 image instructions (4 columns
     // x 16 chunks each, chunk q of column c at slot q ^ (c & 15): conflict-free
-    // ds_read_b128) and, on the first half, 4 of d*bsum16 -- 8 (+1) per wave.
+    // ds_read_b128) and, on the first half, 4 of d*bsum16 (waves 0-3) -- 32/NW (+1) per wave.
     auto issue = [&](int st) {
         uint8_t *buf = smem + (st & 1) * MMF_BUF;
         const int b = b0 + (st >> 1), hf = st & 1;
 #pragma unroll
-        for (int i = 0; i < 8; ++i) {
-            const int inst = 8 * wave + i;
+        for (int i = 0; i < 32 / NW; ++i) {
+            const int inst = (32 / NW) * wave + i;
             const int c = 4 * inst + (lane >> 4), slot = lane & 15;
             const int cc = col0 + c < a.m_cols ? col0 + c : a.m_cols - 1;
             const uint8_t *src = a.img + cc * icol + (int64_t)b * MMF_IMG + hf * (MMF_IMG / 2) + 16 * (slot ^ (c & 15));
             dma16(src, (LDS void *)(buf + 1024 * inst));
         }
-        if (!hf) {
+        if (!hf && wave < 4) {
             const int c = 32 * wave + (lane >> 1);
             const int cc = col0 + c < a.m_cols ? col0 + c : a.m_cols - 1;
             dma16(a.bs + cc * bcol + (int64_t)b * MMF_BSB + 16 * (lane & 1), (LDS void *)(buf + HALF + 1024 * wave));
@@ -404,11 +407,11 @@ __global__ void __launch_bounds__(256) kq_mmf_reduce(const float *__restrict__ s
     y[c * y_col_stride + n] = res ? s + res[c * res_col_stride + n] : s;
 }
 
-template __global__ void kq_mmf<Q4_K, 1>(const MmfArgs a);
-template __global__ void kq_mmf<Q5_K, 1>(const MmfArgs a);
-template __global__ void kq_mmf<Q6_K, 1>(const MmfArgs a);
-template __global__ void kq_mmf<Q4_K, 2>(const MmfArgs a);
-template __global__ void kq_mmf<Q5_K, 2>(const MmfArgs a);
-template __global__ void kq_mmf<Q6_K, 2>(const MmfArgs a);
+template __global__ void kq_mmf<Q4_K, 4>(const MmfArgs a);
+template __global__ void kq_mmf<Q5_K, 4>(const MmfArgs a);
+template __global__ void kq_mmf<Q6_K, 4>(const MmfArgs a);
+template __global__ void kq_mmf<Q4_K, 8>(const MmfArgs a);
+template __global__ void kq_mmf<Q5_K, 8>(const MmfArgs a);
+template __global__ void kq_mmf<Q6_K, 8>(const MmfArgs a);
 
 }  // namespace kq

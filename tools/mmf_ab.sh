@@ -6,6 +6,6 @@ mkdir -p gpurun_out
 for pass in 1 2; do
   for cfg in "$@"; do
     echo "== pass $pass: $cfg"
-    env MI355X_PREFILL=f16 $cfg timeout -k 10 120 python -u tools/prefill_bench.py 2>&1 | grep -v amdgpu.ids || exit $?
+    env MI355X_PREFILL=${PREC:-f16_all} $cfg timeout -k 10 120 python -u tools/prefill_bench.py 2>&1 | grep -v amdgpu.ids || exit $?
   done
 done
