@@ -283,6 +283,26 @@ __device__ __forceinline__ void dma16_nt(const void *src, LDS void *dst) {
     asm volatile("s_mov_b32 m0, %0\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off nt" ::"s"(m0), "v"(src)
                  : "memory", "m0");
 }
+// dma16_nt for lanes [0, n) only, the lane mask applied inside the asm: the instruction
+// is issued on every path (no compiler branch around a partial mask), so a counted wait
+// that covers it holds on every path the ISA lint walks (tools/vmem_lint.py). A
+// vector-memory instruction counts in vmcnt whatever its mask (kq_rows' prologue step,
+// KQ_ROWS_MASKED).
+__device__ __forceinline__ void dma16_nt_lanes(const void *src, LDS void *dst, int lane, int n) {
+    const uint32_t m0 = (uint32_t)(uintptr_t)dst;
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "v_cmp_gt_i32_e32 vcc, %2, %3\n\t"
+        "s_and_b64 exec, exec, vcc\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %4, off nt\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(save)
+        : "s"(m0), "s"(n), "v"(lane), "v"(src)
+        : "memory", "m0", "vcc");
+}
 #pragma clang diagnostic pop
 
 template <int N>

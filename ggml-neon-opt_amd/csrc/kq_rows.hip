@@ -55,6 +55,14 @@
 #ifndef KQ_ROWS_L2PF
 #define KQ_ROWS_L2PF 0
 #endif
+// Prologue DMA and activation wait (profiles/r03_masked_ab.txt): 2 (product) issues the
+// step's partial last DMA instruction with its lane mask inside the asm, so it is issued on
+// every path, and the activation wait then leaves the residual load (younger than x, a
+// gather from memory the previous launches did not touch) in flight: TinyLlama token +4.8 %,
+// Llama-3-8B +3.1 %. 1: the masked DMA with the old wait; 0: both as before (experiments).
+#ifndef KQ_ROWS_MASKED
+#define KQ_ROWS_MASKED 2
+#endif
 #ifndef KQ_ROWS_LINT_BREAK
 #define KQ_ROWS_LINT_BREAK 0  // 1: drop the activation wait (a lint self-test build, never run)
 #endif
@@ -303,9 +311,23 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             const uint8_t *xb = (const uint8_t *)a.x + 16 * lane;
 #pragma unroll
             for (int i = 0; i < NI; ++i)
-                if (i + 1 < NI || lane < GRAN - 64 * (NI - 1)) dma16_nt(xb, (LDS void *)(islot + 1024 * i));
+                if (KQ_ROWS_MASKED && i + 1 == NI) dma16_nt_lanes(xb, (LDS void *)(islot + 1024 * i), lane, GRAN - 64 * (NI - 1));
+                else if (i + 1 < NI || lane < GRAN - 64 * (NI - 1)) dma16_nt(xb, (LDS void *)(islot + 1024 * i));
         }
-        for (int j = 0; j < pre0; ++j) issue();
+        if (KQ_ROWS_MASKED && kConstPre && T > 0) {  // the one step, its partial DMA masked in asm
+            const uint8_t *base = s16 + 16 * lane;
+            const uint8_t *lim = T > 1 ? base + 1024 * (NI - 1) : base + 1024 * (NI - 1) < last16 ? base + 1024 * (NI - 1) : last16;
+#pragma unroll
+            for (int i = 0; i + 1 < NI; ++i) {
+                const uint8_t *p = base + 1024 * i;
+                dma16_nt(T > 1 || p < last16 ? p : last16, (LDS void *)(islot + 1024 * i));
+            }
+            dma16_nt_lanes(lim, (LDS void *)(islot + 1024 * (NI - 1)), lane, GRAN - 64 * (NI - 1));
+            islot = islot + SLOT == ring_end ? ring : islot + SLOT;
+            ++it_;
+        } else {
+            for (int j = 0; j < pre0; ++j) issue();
+        }
         if (pf_on) {  // L2 prefetch of the stream just past the ring (younger than the pre0 steps)
             const uint8_t *p = s16 + (int64_t)D * (ROWS_SB * BSZ) + 64 * lane;
 #pragma unroll
@@ -346,6 +368,10 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             // compile-time pre0 / prefetch a constant per path
             if (KQ_ROWS_LINT_BREAK) {
                 // deliberately broken build (tests/test_abi.py: the ISA lint must flag it): no wait
+            } else if (kConstPre && KQ_ROWS_MASKED == 2) {
+                // x landed: the residual load (rv, younger than x) and the step's NI DMA
+                // instructions (all issued on every path) may still be in flight
+                vm_wait<NI + 1>();
             } else if (kConstPre) {
                 vm_wait<NI>();  // all but the one step's DMA instructions (fewer if predicated off: a stronger wait)
             } else {
