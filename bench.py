@@ -35,15 +35,17 @@ a once-read buffer, no arithmetic; "of_stream_ceiling" = stream_us / us_median).
 mi355x_prefill_precision), with an f16-peak roofline. "cpu_baseline":
 the oracle's restated ggml-cpu token on this host's cores, a bounded sample.
 
-Multi-GPU (--gpus N under torch.distributed.run): every rank decodes its own
-token stream with its own copy of the weights ("replicas", weak scaling); value
-is the aggregate tokens/s = N*K / max-over-ranks time. Beside it the line carries the
-north_star's row-split path for TinyLlama and Llama-3-70B in both exchange schedules
-("rowsplit": gather = every matrix by rows + one RCCL all-gather per stage; reduce =
-attn_output / ffn_down split along K + one RCCL all-reduce per K-split stage, 2 per
-layer), and "collectives_us", the per-collective cost of those exchanges on the job's
-ranks. `--mode rowsplit` / `rowsplit-reduce` make one of the splits the headline
-(strong scaling). DESIGN.md §6 has the budget of when a split pays.
+Multi-GPU (--gpus N under torch.distributed.run): the headline is the north_star's
+row-split path, ONE TinyLlama token stream split over the N GPUs in the reduce schedule
+(q/k/v by heads and gate/up by ffn rows, attn_output / ffn_down split along K at
+superblock boundaries, one RCCL all-reduce per K-split stage: 2 per layer; "scaling":
+"strong", value = tokens/s of that one stream, max-over-ranks time). Beside it the line
+carries "replicas" (every rank decodes its own stream with its own weights: the
+data-parallel serving figure, weak scaling), the gather schedule ("rowsplit.gather":
+every matrix by rows + one RCCL all-gather per stage), Llama-3-70B (config 4) in both
+schedules with its per-GPU token_hbm_frac, and "collectives_us", the per-collective
+cost on the job's ranks. `--mode replicas|rowsplit|rowsplit-reduce` picks the headline
+explicitly. DESIGN.md §6 has the budget of when a split pays.
 """
 from __future__ import annotations
 
@@ -862,18 +864,39 @@ def collective_side(dev, world, rank, local, barrier, n_chain=64, reps=20):
     return out
 
 
+def resolve_mode(mode, world):
+    """--mode auto: one GPU decodes one token stream; at N > 1 the headline is the row split
+    in the reduce schedule -- the multi-GPU path north_star names ("weight rows shard
+    across the GPUs ... a single RCCL all-reduce ... >= 3.5x at 4 GPUs on the row-split
+    path", SURVEY.md section 8e), not data-parallel replicas."""
+    if mode == "auto":
+        return "rowsplit-reduce" if world > 1 else "replicas"
+    return mode
+
+
+def headline_fields(mode, world):
+    """The line's scaling / parallelism for a resolved --mode (rowsplit* at N = 1 runs the
+    same graph over a 1-rank RCCL communicator)."""
+    if mode == "replicas":
+        return {"scaling": "weak", "parallelism": f"replicas x{world}", "tokens_per_step": world}
+    split_mode = "reduce" if mode == "rowsplit-reduce" else "gather"
+    return {"scaling": "strong", "parallelism": f"rowsplit-{split_mode}{world}", "tokens_per_step": 1}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=128)
     ap.add_argument("--warmup", type=int, default=16)
     ap.add_argument("--model", default="tinyllama-1.1b", choices=sorted(MODELS))
-    ap.add_argument("--mode", default="replicas", choices=["replicas", "rowsplit", "rowsplit-reduce"],
-                    help="the headline at N GPUs: replicas (default: an independent token stream per GPU, "
-                         "weak scaling), rowsplit (one token stream, the weight rows split over the GPUs, one "
-                         "RCCL all-gather per stage: strong scaling) or rowsplit-reduce (one stream, "
-                         "attn_output / ffn_down split along K, one RCCL all-reduce per K-split stage). At N > 1 "
-                         "the line carries both row splits of TinyLlama and Llama-3-70B beside the headline")
+    ap.add_argument("--mode", default="auto", choices=["auto", "replicas", "rowsplit", "rowsplit-reduce"],
+                    help="the headline at N GPUs: auto (default: N = 1 one token stream on one GPU; N > 1 "
+                         "rowsplit-reduce, the north_star's row-split path), replicas (an independent token "
+                         "stream per GPU, weak scaling), rowsplit (one token stream, the weight rows split over "
+                         "the GPUs, one RCCL all-gather per stage: strong scaling) or rowsplit-reduce (one "
+                         "stream, attn_output / ffn_down split along K, one RCCL all-reduce per K-split stage, "
+                         "strong scaling). At N > 1 the line carries the replicas figure and both row splits of "
+                         "TinyLlama and Llama-3-70B beside the headline")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-large", action="store_true")
@@ -894,6 +917,8 @@ def main():
                     help="skip the ~0.3 s untimed device warm-up before the warmup steps")
     ap.add_argument("--no-70b", action="store_true",
                     help="skip the Llama-3-70B side figure (config 4: row split over the job's GPUs, 1 GPU at N = 1)")
+    ap.add_argument("--knob", action="append", default=[], metavar="NAME=VALUE",
+                    help="A/B runs only: set a library experiment knob (mi355x_debug_knob; the line records it)")
     args = ap.parse_args()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         spawn_ranks(args.gpus)  # exits
@@ -903,7 +928,7 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    mode = args.mode
+    mode = resolve_mode(args.mode, world)
     if mode != "replicas" and args.workload != "token":
         raise SystemExit("bench: the row split runs the decode token workload")
     if world > 1:
@@ -918,6 +943,11 @@ def main():
     if not g.device_available():
         raise SystemExit("bench: no gfx950 device or libggml_mi355x.so not loadable")
     g.gemv_impl({"auto": g.GEMV_AUTO, "rows": g.GEMV_ROWS, "tasks": g.GEMV_TASKS}[args.impl])
+    knobs = {}
+    for kv in args.knob:
+        name, val = kv.split("=", 1)
+        g.debug_knob(name, float(val))
+        knobs[name] = float(val)
 
     def barrier():
         if world > 1:
@@ -1001,7 +1031,8 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         t_max = float(t.item())
-    tokens_total = args.steps * (1 if rowsplit else world)
+    head = headline_fields(mode if rowsplit else "replicas", world)  # (a failed communicator: replicas)
+    tokens_total = args.steps * head["tokens_per_step"]
     value = tokens_total / t_max
 
     # per-launch kernel timing (every rank: the row split's eager steps are collective)
@@ -1018,7 +1049,9 @@ def main():
     splits = None  # N > 1: both row-split schedules of the headline model, one token stream each
     if isinstance(chain, Token) and world > 1:
         splits = {m: split_model_side(args.model, dev, world, rank, local, barrier, steps=32, warmup=4, mode=m)
-                  for m in ("gather", "reduce")}
+                  for m in ("gather", "reduce") if not (rowsplit and m == split_mode)}
+        if rowsplit:
+            splits[split_mode] = "the headline"
     l70 = None
     if isinstance(chain, Token) and not args.no_70b and args.model != "llama-3-70b":
         if world > 1:
@@ -1108,7 +1141,7 @@ def main():
             "metric": "tg128 tok/s + Q4_K GEMV achieved-HBM-GB/s, TinyLlama-1.1B Q4_K_M @1 GPU",
             "value": round(value, 2), "unit": "tok/s", "n_gpus": world, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": round(t_max / args.steps * 1e3, 4),
-            "higher_is_better": True, "scaling": "strong" if rowsplit else "weak",
+            "higher_is_better": True, "scaling": head["scaling"],
             "vs_baseline": None, "dtype": "q4_K/q6_K x q8_K (u4/u6*i8 dot4 -> i32, f32 combine)",
             "data": (f"GGUF weights {os.path.basename(args.gguf)}; random f32 first activation" if args.gguf else
                      "synthetic (random valid K-quant blocks of the real shapes, f32 norms, random token ids)"
@@ -1121,7 +1154,7 @@ def main():
                        "weights_MB_per_token_per_gpu": round(local_bytes / 1e6, 1),
                        "stages_per_token": chain.launches(),
                        "executor": executor,
-                       "parallelism": (f"rowsplit-{split_mode}{world}" if rowsplit else f"replicas x{world}"),
+                       "parallelism": head["parallelism"],
                        "hipgraph": not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
             "effective_GBps": round(per_gpu_rate * local_bytes / 1e9, 1),
@@ -1143,6 +1176,7 @@ def main():
             "rowsplit": splits,
             "collectives_us": colls,
             "rowsplit_error": comm_error,
+            "debug_knobs": knobs or None,
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

@@ -101,6 +101,23 @@ constexpr int64_t kRowsFusedMaxNb = ROWS_QPASS * 4 * ROWS_WAVES;  // kq_rows: up
 constexpr double kRowsSmallBytes = 10e6;  // launches below this many weight bytes: ROWS_WAVES_SMALL waves
 std::atomic<int> g_rows_waves{0};         // mi355x_gemv_waves: 0 = by size, else fixed
 
+// ------------------------------------------------------------------ debug knobs
+// Product defaults; mi355x_debug_knob() (tools / A/B runs) overrides them per process.
+struct KnobDef {
+    const char *name;
+    double def;
+};
+const KnobDef kKnobs[KNOB_COUNT] = {
+    {"GEMV_DIAG", 0},  {"GEMV_RING", 0},     {"GEMV_PRE0", 1},       {"GEMV_PF", 0},
+    {"GEMV_XMODE", 0}, {"GEMV_SMALL_MB", kRowsSmallBytes / 1e6},      {"GEMV_WPC", 0},
+    {"GEMV_SMALL_WG", 0}, {"GEMV_FQMAX", (double)kRowsFusedMaxNb},   {"MMF_WAVES", 0},
+    {"MMF_ORDER", 0},  {"ATTN_DIAG", 0},     {"LOOPBACK_NOCOPY", 0},
+};
+std::atomic<double> g_knob[KNOB_COUNT];
+std::atomic<bool> g_knob_set[KNOB_COUNT];
+std::atomic<uint32_t> g_knob_gen{0};
+
+
 uint64_t *g_stamps = nullptr;  // diagnostics (mi355x_diag_stamps)
 int64_t g_stamps_cap = 0;
 
@@ -127,6 +144,9 @@ int resident_wgs(const void *fn, size_t lds) {
 }
 
 }  // namespace
+
+double knob(Knob k) { return g_knob_set[k].load(std::memory_order_relaxed) ? g_knob[k].load() : kKnobs[k].def; }
+uint32_t knob_generation() { return g_knob_gen.load(); }
 
 // ------------------------------------------------------------ launch timing
 struct TimedLaunch {
@@ -262,20 +282,8 @@ int plan_gemv(const mi355x_gemv_desc *d, int n_desc, int64_t K, int64_t M, int n
     pl.debug = debug;
     pl.tmask = tmask;
     pl.fn = pick_gemv(ncol, fusedq, debug, tmask);
-    {
-        static int diag = -1;
-        if (diag < 0) {
-            const char *e = getenv("MI355X_GEMV_DIAG");
-            diag = e ? atoi(e) : 0;
-        }
-        a.diag = diag;
-        static int ring_env = -1;
-        if (ring_env < 0) {
-            const char *e = getenv("MI355X_GEMV_RING");
-            ring_env = e ? atoi(e) : 0;
-        }
-        a.ring_override = ring_env;
-    }
+    a.diag = (int)knob(KNOB_GEMV_DIAG);
+    a.ring_override = (int)knob(KNOB_GEMV_RING);
     a.stamps = g_stamps;
     a.stamps_cap = g_stamps_cap;
     // One workgroup per 8-row task, at most one round of resident workgroups; each
@@ -336,19 +344,9 @@ int launch_gemv(const GemvPlan &pl, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------ row-stream decode GEMV
-std::atomic<int> g_impl{-1};
+std::atomic<int> g_impl{MI355X_GEMV_AUTO};
 bool rows_enabled() {
-    int v = g_impl.load();
-    if (v < 0) {
-        const char *e = getenv("MI355X_GEMV_IMPL");  // "tasks" / "rows": A/B runs
-        v = (e && strcmp(e, "tasks") == 0)  ? MI355X_GEMV_TASKS
-            : (e && strcmp(e, "rows") == 0)  ? MI355X_GEMV_ROWS
-                                             : MI355X_GEMV_AUTO;
-        int expect = -1;
-        g_impl.compare_exchange_strong(expect, v);
-        v = g_impl.load();
-    }
-    return v != MI355X_GEMV_TASKS;
+    return g_impl.load() != MI355X_GEMV_TASKS;  // mi355x_gemv_impl()
 }
 
 
@@ -409,25 +407,15 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
         a.y[i] = d[i].y;
     }
     {
-        static int diag = -1, pre_env = -1, pf_env = -1, xm_env = -1;
-        if (diag < 0) {
-            const char *e = getenv("MI355X_GEMV_DIAG");
-            diag = e ? atoi(e) : 0;
-            e = getenv("MI355X_GEMV_PRE0");
-            pre_env = e ? atoi(e) : 1;
-            e = getenv("MI355X_GEMV_PF");
-            pf_env = e ? atoi(e) : 0;
-            e = getenv("MI355X_GEMV_XMODE");
-            xm_env = e ? atoi(e) & 7 : 0;
-        }
-        a.pf = pf_env;
-        a.xmode = xm_env;
-        a.diag = diag;
+        a.pf = (int)knob(KNOB_GEMV_PF);
+        a.xmode = (int)knob(KNOB_GEMV_XMODE) & 7;
+        a.diag = (int)knob(KNOB_GEMV_DIAG);
         // weight steps issued before the activation is quantized. One: a deeper early burst
         // delays the activation loads queued behind it. Alone, K = 2048 GEMVs ran 5-9 %
         // faster with the whole ring (tools/gemv_sweep.py pre0=3), but with the fused norm
         // prologue (two vectors to fetch) the decode token was 1.6 % slower.
-        a.pre0 = pre_env < 0 ? 0 : pre_env > 3 ? 3 : pre_env;
+        const int pre = (int)knob(KNOB_GEMV_PRE0);
+        a.pre0 = pre < 0 ? 0 : pre > 3 ? 3 : pre;
     }
     a.stamps = g_stamps;
     a.stamps_cap = g_stamps_cap;
@@ -436,10 +424,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     // to dispatch, the short stream does not need them; profiles/r02_rows_waves.md). Each
     // matrix gets waves in proportion to its bytes (never more waves than rows), rows
     // split evenly.
-    static const double small_bytes = [] {  // A/B knob: MI355X_GEMV_SMALL_MB (0: never)
-        const char *e = getenv("MI355X_GEMV_SMALL_MB");
-        return e ? atof(e) * 1e6 : kRowsSmallBytes;
-    }();
+    const double small_bytes = knob(KNOB_GEMV_SMALL_MB) * 1e6;  // (0: never)
     if (waves_per_cu <= 0) {
         const int fixed = g_rows_waves.load();
         const int want = fixed > 0 ? fixed : bytes_total * nb < small_bytes ? ROWS_WAVES_SMALL : ROWS_WAVES;
@@ -448,16 +433,10 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     }
     if (waves_per_cu > ROWS_WAVES) return MI355X_E_INVAL;
     pl.nwv = waves_per_cu;
-    static const int wpc_env = [] {  // experiment knob: cap on active waves per CU
-        const char *e = getenv("MI355X_GEMV_WPC");
-        return e ? atoi(e) : 0;
-    }();
+    const int wpc_env = (int)knob(KNOB_GEMV_WPC);  // experiment knob: cap on active waves per CU
     if (wpc_env > 0 && wpc_env < waves_per_cu) waves_per_cu = wpc_env;
-    // workgroups: one per CU; an A/B knob caps it for small launches (MI355X_GEMV_SMALL_WG)
-    static const int small_wg_env = [] {
-        const char *e = getenv("MI355X_GEMV_SMALL_WG");
-        return e ? atoi(e) : 0;
-    }();
+    // workgroups: one per CU; an A/B knob caps it for small launches (GEMV_SMALL_WG)
+    const int small_wg_env = (int)knob(KNOB_GEMV_SMALL_WG);
     int64_t n_wg = num_cus();
     if (small_wg_env > 0 && bytes_total * nb < small_bytes && small_wg_env < n_wg) n_wg = small_wg_env;
     const int64_t cap = n_wg * waves_per_cu;
@@ -570,21 +549,8 @@ constexpr int64_t kMmqMinCols = 16;  // below this the NCOL GEMV streams the wei
 // Round 3 removed the streamed Q4_K kernel (kq_mmq_k4): equal to the 64 x 64 tiles
 // within the box spread at pp512, 17-40 % slower on every shape forced onto it
 // (profiles/r02_mmq_impl_ab.txt); AUTO and TILE64 now both select the 64 x 64 tiles.
-std::atomic<int> g_mmq_impl{-1};
-int mmq_impl() {
-    int v = g_mmq_impl.load();
-    if (v < 0) {
-        const char *e = getenv("MI355X_MMQ_IMPL");
-        int x = MI355X_MMQ_AUTO;
-        if (e) x = strcmp(e, "tile64") == 0 ? MI355X_MMQ_TILE64 : strcmp(e, "tile128") == 0 ? MI355X_MMQ_TILE128
-                : strcmp(e, "tile128w") == 0 ? MI355X_MMQ_TILE128W
-                : strcmp(e, "tile64w") == 0 ? MI355X_MMQ_TILE64W : x;
-        int expect = -1;
-        g_mmq_impl.compare_exchange_strong(expect, x);
-        v = g_mmq_impl.load();
-    }
-    return v;
-}
+std::atomic<int> g_mmq_impl{MI355X_MMQ_AUTO};  // mi355x_mmq_impl()
+int mmq_impl() { return g_mmq_impl.load(); }
 
 // Prefill tile shape (kq_mmq's RT x CW): weight rows per workgroup RT = 64 (4 waves) or 128
 // (8 waves: the activation tile fetched once per 128 rows), activation columns 64 * CW (CW = 2:
@@ -676,21 +642,9 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
 // mi355x_prefill_precision: MI355X_PREFILL_EXACT (kq_mmq, bit-exact, the default) or
 // MI355X_PREFILL_F16 (kq_mmf: the reference's Q8_K activation and integer unpacking, the
 // accumulated dot on v_mfma_f32_32x32x16_f16 within the tolerance of kq_mmf.hip's header).
-// -1 until first read from MI355X_PREFILL ("f16" / "exact").
-std::atomic<int> g_prefill{-1};
-int prefill_precision() {
-    int v = g_prefill.load();
-    if (v < 0) {
-        const char *e = getenv("MI355X_PREFILL");
-        const int x = e && strcmp(e, "f16") == 0       ? MI355X_PREFILL_F16
-                      : e && strcmp(e, "f16_all") == 0 ? MI355X_PREFILL_F16_ALL
-                                                       : MI355X_PREFILL_EXACT;
-        int expect = -1;
-        g_prefill.compare_exchange_strong(expect, x);
-        v = g_prefill.load();
-    }
-    return v;
-}
+// Set only through mi355x_prefill_precision(): the numerics never change from the environment.
+std::atomic<int> g_prefill{MI355X_PREFILL_EXACT};
+int prefill_precision() { return g_prefill.load(); }
 
 // Waves per kq_mmf workgroup (MI355X_MMF_WAVES, A/B only): 4 (128-row workgroups, two per
 // CU) or 8 (256-row workgroups, one per CU); 0 by shape: 8 from K >= 8192, where the
@@ -698,7 +652,7 @@ int prefill_precision() {
 // 134 -> 117-122, Q5_K 104 -> 93), 4 below it (8B ffn_up 82.5 vs 99.7 us on 8 waves:
 // its 224-workgroup grid leaves CUs idle) -- profiles/r03_mmf_waves_ab.txt.
 int mmf_nw(int64_t K) {
-    static const int v = getenv("MI355X_MMF_WAVES") ? atoi(getenv("MI355X_MMF_WAVES")) : 0;
+    const int v = (int)knob(KNOB_MMF_WAVES);
     return v == 4 || v == 8 ? v : K >= 8192 ? 8 : 4;
 }
 // K split of kq_mmf: double it while the grid has fewer workgroups than CUs and every
@@ -820,8 +774,7 @@ int launch_mmf_multi(int type, int n_mat, const void *const *w, const int64_t *N
     }
     a.tile0[n_mat] = (int)t0;
     if (n_mat == 1) a.n_rows = (int)N[0];
-    static const int order = getenv("MI355X_MMF_ORDER") ? atoi(getenv("MI355X_MMF_ORDER")) : 0;  // A/B only
-    a.order = order;
+    a.order = (int)knob(KNOB_MMF_ORDER);  // A/B only
     const void *fn = nw == 8 ? (type == Q5_K ? (const void *)kq_mmf<Q5_K, 8> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 8>
                                                                                         : (const void *)kq_mmf<Q4_K, 8>)
                              : (type == Q5_K ? (const void *)kq_mmf<Q5_K, 4> : type == Q6_K ? (const void *)kq_mmf<Q6_K, 4>
@@ -1068,9 +1021,9 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
     const size_t need = (size_t)(k / QK) * 292;
     if (rows_enabled()) {
         RowsPlan rp;
-        // MI355X_GEMV_FQMAX (A/B only): the most superblocks quantized inside kq_rows; above
-        // it one kq_quantize_q8L launch first and the GEMV DMAs the Q8L row
-        static const int64_t fq_max = getenv("MI355X_GEMV_FQMAX") ? atoll(getenv("MI355X_GEMV_FQMAX")) : kRowsFusedMaxNb;
+        // GEMV_FQMAX (A/B only): the most superblocks quantized inside kq_rows; above it one
+        // kq_quantize_q8L launch first and the GEMV DMAs the Q8L row
+        const int64_t fq_max = (int64_t)knob(KNOB_GEMV_FQMAX);
         const bool rows_fq = k / QK <= fq_max && k / QK <= kRowsFusedMaxNb && ((uintptr_t)x & 15u) == 0;
         int rc = plan_rows(d, n, k, rows_fq, rp);
         if (rc == MI355X_OK) {
@@ -1108,9 +1061,9 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
 }
 
 uint64_t api_selector_key() {
-    rows_enabled();  // resolve the environment defaults first
     return (uint64_t)(uint32_t)(g_impl.load() + 1) | ((uint64_t)(uint32_t)g_rows_waves.load() << 8) |
-           ((uint64_t)(uint32_t)(mmq_impl() + 1) << 16) | ((uint64_t)(uint32_t)(prefill_precision() + 1) << 24);
+           ((uint64_t)(uint32_t)(mmq_impl() + 1) << 16) | ((uint64_t)(uint32_t)(prefill_precision() + 1) << 24) |
+           ((uint64_t)knob_generation() << 32);
 }
 
 }  // namespace kq
@@ -1369,8 +1322,24 @@ int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, i
 
 int mi355x_gemv_impl(int impl) {
     if (impl < MI355X_GEMV_AUTO || impl > MI355X_GEMV_ROWS) return MI355X_E_INVAL;
-    rows_enabled();  // resolve the environment default first
     return g_impl.exchange(impl);
+}
+
+int mi355x_debug_knob(const char *name, double value, double *previous) {
+    if (!name) return MI355X_E_INVAL;
+    for (int k = 0; k < KNOB_COUNT; ++k) {
+        if (strcmp(name, kKnobs[k].name) != 0) continue;
+        if (previous) *previous = knob((Knob)k);
+        if (value != value) {  // NaN: back to the product default
+            g_knob_set[k].store(false);
+        } else {
+            g_knob[k].store(value);
+            g_knob_set[k].store(true);
+        }
+        g_knob_gen.fetch_add(1);
+        return MI355X_OK;
+    }
+    return MI355X_E_INVAL;
 }
 
 int mi355x_mmq_impl(int impl) {

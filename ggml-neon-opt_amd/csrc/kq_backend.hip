@@ -647,6 +647,7 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
                      ? kq::launch_rms_norm_q8L(l.x, l.x2, b->workspace, K, M, l.eps, b->stream)
                      : kq::launch_swiglu_q8L(l.x, l.x2, b->workspace, K, M, b->stream);
             if (rc) return rc;
+            q8 = Q8State();  // int8 Q8L blocks now (a preceding f16 GEMM may have left f16 = true)
             q8.src = m->data;
             q8.k = K;
             q8.m = M;
@@ -1040,8 +1041,7 @@ int mi355x_backend_set_comm_loopback(mi355x_backend_t b, int rank, int world) {
     b->loop_world = world;
     // timing only: emulated ALL_GATHERs skip their own-slice copy, so a token's time is the
     // rank's compute alone (the gathered vectors are then stale: never for parity runs)
-    const char *e = getenv("MI355X_LOOPBACK_NOCOPY");
-    b->loop_nocopy = e && atoi(e) != 0;
+    b->loop_nocopy = kq::knob(kq::KNOB_LOOPBACK_NOCOPY) != 0;  // mi355x_debug_knob("LOOPBACK_NOCOPY")
     return MI355X_OK;
 }
 

@@ -98,6 +98,27 @@ bool attn_group_ok(const AttnArgs &a, int nwaves);      // the one-workgroup-per
 size_t attn_group_bytes(const AttnArgs &a, int nwaves);  // its LDS
 // kq_api.hip
 void allow_lds(const void *fn, size_t lds);
+// Experiment / diagnostic knobs of A/B runs. The product reads no environment: a knob
+// holds its product default until mi355x_debug_knob() sets it (tools only), and every
+// knob that changes a launch plan bumps knob_generation() (part of the graph key).
+enum Knob {
+    KNOB_GEMV_DIAG,        // timing stops of the KQ_ROWS_DIAG / KQ_GEMV_DIAG builds
+    KNOB_GEMV_RING,        // kq_gemv ring depth override (0: by LDS)
+    KNOB_GEMV_PRE0,        // kq_rows weight steps issued before the activation (1)
+    KNOB_GEMV_PF,          // kq_rows L2 prefetch of the stream (experiment builds)
+    KNOB_GEMV_XMODE,       // kq_rows prologue variants (experiment builds)
+    KNOB_GEMV_SMALL_MB,    // launches below this many MB of weights: ROWS_WAVES_SMALL waves
+    KNOB_GEMV_WPC,         // cap on active waves per CU (0: none)
+    KNOB_GEMV_SMALL_WG,    // cap on workgroups of small launches (0: one per CU)
+    KNOB_GEMV_FQMAX,       // most superblocks quantized inside kq_rows
+    KNOB_MMF_WAVES,        // kq_mmf waves per workgroup (0: by K)
+    KNOB_MMF_ORDER,        // kq_mmf tile order
+    KNOB_ATTN_DIAG,        // timing stops of the KQ_ATTN_DIAG build
+    KNOB_LOOPBACK_NOCOPY,  // emulated ALL_GATHERs skip their own-slice copy (timing only)
+    KNOB_COUNT
+};
+double knob(Knob k);
+uint32_t knob_generation();
 // Process-wide kernel selectors a captured launch plan depends on (gemv impl / waves,
 // mmq impl; attention decode / prompt impl), packed for the backend's graph key.
 uint64_t api_selector_key();

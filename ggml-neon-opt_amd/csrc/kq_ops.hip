@@ -814,18 +814,9 @@ bool attn_group_ok(const AttnArgs &a, int nwaves) {
 // MI355X_ATTN_HEAD (one workgroup per query head: the default, the fastest launch) or
 // MI355X_ATTN_GROUP (one workgroup per kv group: each group's cells read once, 1/gsz of the
 // cache traffic, +2.3 us per launch on the TinyLlama token: profiles/r02_attention_ab.md);
-// -1 until the first launch reads MI355X_ATTN_IMPL ("group" / "head").
-std::atomic<int> g_attn_impl{-1};
-int attn_impl() {
-    int v = g_attn_impl.load();
-    if (v < 0) {
-        const char *e = getenv("MI355X_ATTN_IMPL");
-        int expect = -1;
-        g_attn_impl.compare_exchange_strong(expect, e && strcmp(e, "group") == 0 ? MI355X_ATTN_GROUP : MI355X_ATTN_HEAD);
-        v = g_attn_impl.load();
-    }
-    return v;
-}
+// Set only through mi355x_attn_impl().
+std::atomic<int> g_attn_impl{MI355X_ATTN_HEAD};
+int attn_impl() { return g_attn_impl.load(); }
 
 int launch_attn(const AttnArgs &a, hipStream_t s) {
     const double bytes = 0;  // context-dependent; not a roofline kernel
@@ -1049,11 +1040,7 @@ int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a) {
     a.rope_row = d->rope_row ? 1 : 0;
     a.q8_out = nullptr;
     a.no_store = 0;
-    static const int diag = [] {
-        const char *e = getenv("MI355X_ATTN_DIAG");
-        return e ? atoi(e) : 0;
-    }();
-    a.diag = diag;
+    a.diag = (int)knob(KNOB_ATTN_DIAG);  // KQ_ATTN_DIAG builds only
     return check_attn(a);
 }
 

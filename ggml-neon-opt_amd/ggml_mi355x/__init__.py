@@ -57,6 +57,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_mmq_impl",
     "mi355x_prefill_precision",
     "mi355x_gemv_waves",
+    "mi355x_debug_knob",
     "mi355x_attn_prompt",
     "mi355x_attn_prompt_impl",
 )
@@ -208,6 +209,8 @@ def lib():
     L.mi355x_prefill_precision.restype = i32
     L.mi355x_gemv_waves.argtypes = [i32]
     L.mi355x_gemv_waves.restype = i32
+    L.mi355x_debug_knob.argtypes = [ctypes.c_char_p, ctypes.c_double, ctypes.POINTER(ctypes.c_double)]
+    L.mi355x_debug_knob.restype = i32
     for n in ("mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
               "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode", "mi355x_attn_prompt"):
         getattr(L, n).restype = i32
@@ -389,6 +392,20 @@ def prefill_precision(p=-1):
 def gemv_waves(waves):
     """kq_rows waves per workgroup: 0 = by launch size, else fixed (1..12); returns the previous."""
     return int(lib().mi355x_gemv_waves(waves))
+
+
+DEBUG_KNOBS = ("GEMV_DIAG", "GEMV_RING", "GEMV_PRE0", "GEMV_PF", "GEMV_XMODE", "GEMV_SMALL_MB", "GEMV_WPC",
+               "GEMV_SMALL_WG", "GEMV_FQMAX", "MMF_WAVES", "MMF_ORDER", "ATTN_DIAG", "LOOPBACK_NOCOPY")
+
+
+def debug_knob(name, value=float("nan")):
+    """Experiment knob of A/B runs (mi355x_debug_knob; the library reads no environment):
+    set `name` to `value` (NaN: back to the product default). Returns the previous value."""
+    prev = ctypes.c_double(0.0)
+    rc = lib().mi355x_debug_knob(name.encode(), float(value), ctypes.byref(prev))
+    if rc != 0:
+        raise Mi355xError(f"debug_knob: unknown knob {name!r}")
+    return prev.value
 
 
 def attn_prompt_impl(impl):

@@ -263,18 +263,30 @@ int mi355x_mmq_impl(int impl);
  * every shape; A/B and tests). The north_star's "within a stated fp32 tolerance on the
  * accumulated dot". Replaces no reference interface (ggml-cpu has one precision); a
  * backend option like llama.cpp's GGML_CUDA_FORCE_MMQ / cuBLAS choice. A negative value
- * queries. Environment default: MI355X_PREFILL=f16 / f16_all. Returns the previous value,
- * or MI355X_E_INVAL. */
+ * queries. The library reads no environment: the precision changes only through this
+ * call (process-wide; a graph captured before it is re-planned, and a caller sizing its
+ * workspace with mi355x_mul_mat_workspace_size must query it again after switching to
+ * F16). Returns the previous value, or MI355X_E_INVAL. */
 #define MI355X_PREFILL_EXACT 0
 #define MI355X_PREFILL_F16 1
 #define MI355X_PREFILL_F16_ALL 2
 int mi355x_prefill_precision(int precision);
 /* Decode GEMV (kq_rows) waves per workgroup (A/B runs, parity of both launch shapes):
- * 0 = by launch size (6 waves under 10 MB of weights, else 12; env MI355X_GEMV_SMALL_MB
- * moves the threshold), or a fixed count 1..12 where the launch allows it (the in-kernel
+ * 0 = by launch size (6 waves under 10 MB of weights, else 12; the debug knob
+ * "GEMV_SMALL_MB" moves the threshold), or a fixed count 1..12 where the launch allows it (the in-kernel
  * quantization covers 12 superblocks per wave). Returns the previous value, or
  * MI355X_E_INVAL. */
 int mi355x_gemv_waves(int waves);
+/* Experiment / diagnostic knobs of A/B runs and timing tools (replaces no reference
+ * interface). The library reads no environment variable; every knob holds its product
+ * default until set here, process-wide: "GEMV_DIAG", "GEMV_RING", "GEMV_PRE0",
+ * "GEMV_PF", "GEMV_XMODE", "GEMV_SMALL_MB", "GEMV_WPC", "GEMV_SMALL_WG", "GEMV_FQMAX",
+ * "MMF_WAVES", "MMF_ORDER", "ATTN_DIAG", "LOOPBACK_NOCOPY" (csrc/kq_internal.h). None
+ * changes numerics: the DIAG knobs act only in the diagnostic builds (make variant),
+ * the others move launch shapes of bit-exact kernels, and LOOPBACK_NOCOPY (timing only)
+ * leaves emulated all-gathers stale. value NaN restores the default; *previous (may be
+ * NULL) receives the value in force before. 0, or MI355X_E_INVAL for an unknown name. */
+int mi355x_debug_knob(const char *name, double value, double *previous);
 
 /* --------------------------------------- decode ops of the llama graph (§8f) */
 /* The non-matmul nodes of one llama decode token (llm_build_llama, out.folded:249),

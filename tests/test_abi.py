@@ -117,6 +117,34 @@ def test_product_has_no_oracle_dependency():
     assert "oracle" not in out.stdout
 
 
+def test_product_reads_no_environment():
+    """no run-time environment switch in the product. The library's sources
+    have no getenv and the shared library imports none; A/B knobs go through the explicit
+    mi355x_debug_knob() entry point and hold the product defaults until set; precision
+    changes only through mi355x_prefill_precision()."""
+    import ggml_mi355x as g
+    src = os.path.join(ROOT, "ggml-neon-opt_amd", "csrc")
+    for fn in sorted(os.listdir(src)):
+        txt = open(os.path.join(src, fn), errors="ignore").read()
+        assert "getenv" not in txt and "secure_getenv" not in txt, fn
+    out = subprocess.run(["nm", "-D", "--undefined-only", g.LIB_PATH], capture_output=True, text=True).stdout
+    assert not [l for l in out.splitlines() if "getenv" in l], out
+    L = g.lib()
+    os.environ["MI355X_PREFILL"] = "f16"  # the old switch: no effect any more
+    try:
+        assert g.prefill_precision(-1) == g.PREFILL_EXACT
+    finally:
+        del os.environ["MI355X_PREFILL"]
+    for k in g.DEBUG_KNOBS:
+        d = g.debug_knob(k, 5)  # the default in force before
+        assert g.debug_knob(k) == 5  # NaN: restore the default ...
+        assert g.debug_knob(k) == d  # ... which is what it then reads
+    assert g.debug_knob("GEMV_PRE0") == 1 and g.debug_knob("GEMV_FQMAX") == 144
+    prev = __import__("ctypes").c_double(0)
+    assert L.mi355x_debug_knob(b"NO_SUCH_KNOB", 1.0, None) == -1
+    assert L.mi355x_debug_knob(None, 1.0, prev) == -1
+
+
 def _gfx950_code_objects(path):
     """gfx950 ELF code objects of every clang offload bundle in the shared library."""
     import struct

@@ -48,3 +48,20 @@ def test_tinyllama_model_size_matches_published():
     total += (2 * L + 1) * E * 4                          # attn_norm, ffn_norm, output_norm (f32)
     mib = total / 2 ** 20
     assert abs(mib - 636.18) <= 0.01, mib
+
+
+@pytest.mark.parametrize("world", [1, 2, 4, 8])
+def test_multi_gpu_headline_is_the_row_split(world):
+    """at N > 1 the driver's scaling line measures the north_star's row-split
+    path (one TinyLlama token stream, reduce schedule, strong scaling), not replicas; at
+    N = 1 the line stays one stream on one GPU. Explicit --mode values are kept."""
+    m = bench.resolve_mode("auto", world)
+    h = bench.headline_fields(m, world)
+    if world == 1:
+        assert m == "replicas" and h == {"scaling": "weak", "parallelism": "replicas x1", "tokens_per_step": 1}
+    else:
+        assert m == "rowsplit-reduce"
+        assert h == {"scaling": "strong", "parallelism": f"rowsplit-reduce{world}", "tokens_per_step": 1}
+    assert bench.resolve_mode("replicas", world) == "replicas"
+    assert bench.headline_fields("replicas", world)["tokens_per_step"] == world
+    assert bench.headline_fields("rowsplit", world)["parallelism"] == f"rowsplit-gather{world}"

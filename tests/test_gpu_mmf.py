@@ -167,6 +167,56 @@ def test_llama_prompt_f16(dev, f16path, mix):
     torch.cuda.synchronize()
 
 
+def test_llama_prompt_f16_auto_then_exact_prologue(dev, f16path):
+    """PREFILL_F16 with the per-shape choice on 5 TinyLlama-width layers: layer 2 is a
+    use_more_bits layer, so its Q6_K ffn_down runs on kq_mmf (f16); layer 3's q/k/v are
+    Q4_K and stay on kq_mmq behind the fused rms_norm -> Q8L prologue. That prologue must
+    publish int8 Q8L blocks even though the launch before it was an f16 GEMM (ADVICE r3:
+    a stale `f16` flag made the q/k/v GEMMs re-quantize a never-written f32 buffer).
+    Checked: every layer's K cache within a relative L2 error of 2^-4 of the bit-exact
+    prompt's (garbage or zeros there would be ~1), layers 0-2 (no f16 GEMM before them)
+    bit-exact, and the logits within 2^-3 of the oracle's sequential llm_build_llama."""
+    import torch
+    from oracle import kq_ops_oracle as O
+    from tests import llama_model as LM
+    from tests.test_gpu_ops import _decoder
+    import ggml_mi355x as g
+    from ggml_mi355x.llama import hparams
+    O.lib()
+    hp = hparams(2048, 5, 32, 4, 5632, 4096)
+    assert [LM.use_more_bits(i, 5) for i in range(5)] == [False, False, True, False, True]
+    n_ctx, n = 64, 29
+    tokens = np.random.default_rng(17).integers(0, hp["n_vocab"], size=n).tolist()
+    out = {}
+    for name, prec in (("exact", g.PREFILL_EXACT), ("f16_auto", g.PREFILL_F16)):
+        g.prefill_precision(prec)
+        w, b, dec = _decoder(dev, hp, 11, n_ctx, True)
+        lg = dec.prompt(tokens, 0)
+        b.synchronize()
+        out[name] = (lg.cpu().numpy().astype(np.float64).ravel(),
+                     [c[:n].view(torch.float16).float().cpu().numpy() for c in dec.k_cache])
+        b.close()
+    g.prefill_precision(g.PREFILL_F16_ALL)
+    errs = []
+    for li in range(5):
+        k, ke = out["f16_auto"][1][li], out["exact"][1][li]
+        assert np.isfinite(k).all(), li
+        errs.append(float(np.linalg.norm(k - ke) / np.linalg.norm(ke)))
+    print("K-cache relative L2 per layer:", errs)
+    assert errs[0] == errs[1] == errs[2] == 0.0, errs
+    assert max(errs) <= 2.0 ** -4, errs
+    model, cache = LM.oracle_model(hp, w, n_ctx)
+    for p, tok in enumerate(tokens):
+        ref, _ = O.decode_token(model, tok, p, cache)
+    ref = np.asarray(ref, np.float64).ravel()
+    assert np.array_equal(out["exact"][0], ref)
+    got = out["f16_auto"][0]
+    rel = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
+    print("logits relative L2:", rel)
+    assert np.isfinite(got).all() and rel <= 2.0 ** -3, rel
+    torch.cuda.synchronize()
+
+
 @pytest.mark.parametrize("K,Ns,M", [(2048, (2048, 256, 256), 37), (4096, (4096, 1024, 1024), 128),
                                     (1024, (300, 130), 200)], ids=["tl_qkv", "l3_qkv", "ragged"])
 def test_mmf_multi_matrix_launch(dev, oracle, npo, f16path, K, Ns, M):

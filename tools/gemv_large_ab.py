@@ -8,6 +8,10 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "ggml-neon-opt_amd")]
 import torch  # noqa: E402
 
 import bench  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()  # the MI355X_* A/B environment -> explicit library calls
+
 
 out = bench.large_gemv(torch.device("cuda:0"))
 for k, v in out.items():

@@ -9,6 +9,10 @@ sys.path[:0] = [ROOT, os.path.join(ROOT, "ggml-neon-opt_amd")]
 import torch  # noqa: E402
 
 import ggml_mi355x as g  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()  # the MI355X_* A/B environment -> explicit library calls
+
 from bench import random_kquant  # noqa: E402
 
 

@@ -10,6 +10,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ggml_mi355x as g  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()  # the MI355X_* A/B environment -> explicit library calls
+
 from bench import random_kquant  # noqa: E402
 
 SHAPES = [("l3 q/o", 12, 4096, 4096), ("l3 up", 12, 4096, 14336), ("l3 down", 12, 14336, 4096),

@@ -25,6 +25,10 @@ import torch  # noqa: E402
 
 import bench  # noqa: E402
 import ggml_mi355x as g  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()  # the MI355X_* A/B environment -> explicit library calls
+
 
 
 def time_token(model, dev, world, mode, steps, warmup=4):

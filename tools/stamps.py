@@ -12,6 +12,10 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 import ggml_mi355x as g  # noqa: E402
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+import knobs  # noqa: E402
+knobs.apply_env()  # the MI355X_* A/B environment -> explicit library calls
+
 from bench import random_kquant  # noqa: E402
 
 SHAPES = [("tl q", 12, 2048, 2048), ("tl 8rows", 12, 2048, 8), ("tl gate+up", 12, 2048, 11264),
