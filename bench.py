@@ -710,6 +710,13 @@ def connect(be, world, rank):
     the error every rank agrees on (a failure on any rank fails all, so no rank waits in a
     collective the others never enter)."""
     err = None
+    if os.environ.get("BENCH_ONE_DEVICE") and world > 1:
+        # rehearsal of the N-rank job on ONE GPU (RCCL refuses two ranks on one device):
+        # every rank runs its own split graph with the collectives emulated (loopback: no
+        # data exchanged, so the values are not the model's) -- the control plane, the
+        # line's fields and each rank's compute, never a scaling figure
+        be.set_comm_loopback(rank, world)
+        return None
     try:
         uid = torch.zeros(g.lib().mi355x_comm_id_size(), dtype=torch.uint8)
         if rank == 0:
@@ -1177,6 +1184,9 @@ def main():
             "collectives_us": colls,
             "rowsplit_error": comm_error,
             "debug_knobs": knobs or None,
+            "rehearsal": ("BENCH_ONE_DEVICE: all ranks on one GPU, collectives emulated (loopback, no data "
+                          "exchanged): fields and control plane only, not a measurement"
+                          if os.environ.get("BENCH_ONE_DEVICE") and world > 1 else None),
             "cpu_baseline": cpu,
         }
         print(json.dumps(result), flush=True)

@@ -16,6 +16,7 @@
 // include/ggml_mi355x.h and runs through the lowering (host only, no device).
 #pragma once
 
+#include <cstdint>
 #include <cstring>
 #include <deque>
 #include <string>
@@ -88,14 +89,61 @@ struct Context {
     std::vector<mi355x_tensor *> nodes;
 };
 
-// The cells == positions promise of mi355x_lower_opts: the caller passes the host copies
-// of every SET_ROWS K index vector and inp_pos (T entries each, read back from the device
-// by the real adapter) and whether the batch is one sequence; true only if they agree.
-inline bool cells_eq_pos(const int64_t *k_idxs, const int32_t *pos, int64_t n_tokens, bool one_sequence) {
-    if (!one_sequence || n_tokens <= 0 || !k_idxs || !pos) return false;
+// The cells == positions promise of mi355x_lower_opts, established from the graph's own
+// inputs (host copies, T tokens): every token's K cell index (SET_ROWS k_idxs) equals its
+// position (inp_pos), and its KQ mask row (SOFT_MAX src[1], n_kv entries per row, row
+// stride `mask_row_bytes`, f32 or f16) is the causal mask over cells [0, pos]: 0 there and
+// -INFINITY after. ATTN_DECODE stores cell pos and attends over [0, pos], so that is
+// exactly what the graph asks for -- whatever the number of sequences in the cache: cells
+// of another sequence, a removed or shifted cell inside [0, pos] shows up as a -INF entry
+// there (or a k_idx that is not the position) and the promise is refused (the ADVICE r3
+// gap: a one_sequence flag nobody could check).
+inline bool cells_eq_pos(const int64_t *k_idxs, const int32_t *pos, int64_t n_tokens) {
+    if (n_tokens <= 0 || !k_idxs || !pos) return false;
     for (int64_t i = 0; i < n_tokens; ++i)
-        if (k_idxs[i] != (int64_t)pos[i]) return false;
+        if (k_idxs[i] != (int64_t)pos[i] || pos[i] < 0) return false;
     return true;
+}
+
+// mask_type: 0 = f32, 1 = f16 (ggml type numbers)
+inline bool kq_mask_causal(const void *mask, int mask_type, int64_t n_kv, size_t mask_row_bytes,
+                           const int32_t *pos, int64_t n_tokens) {
+    if (!mask || !pos || n_kv <= 0 || n_tokens <= 0 || (mask_type != 0 && mask_type != 1)) return false;
+    for (int64_t t = 0; t < n_tokens; ++t) {
+        if (pos[t] < 0 || pos[t] >= n_kv) return false;
+        const unsigned char *row = (const unsigned char *)mask + (size_t)t * mask_row_bytes;
+        for (int64_t j = 0; j < n_kv; ++j) {
+            bool zero, ninf;
+            if (mask_type == 0) {
+                uint32_t u;
+                std::memcpy(&u, row + 4 * j, 4);
+                zero = (u & 0x7fffffffu) == 0;
+                ninf = u == 0xff800000u;
+            } else {
+                uint16_t h;
+                std::memcpy(&h, row + 2 * j, 2);
+                zero = (h & 0x7fffu) == 0;
+                ninf = h == 0xfc00u;
+            }
+            if (j <= pos[t] ? !zero : !ninf) return false;
+        }
+    }
+    return true;
+}
+
+// Rope table parameters the lowering checks a ROPE node against (ggml rope op_params:
+// [1] n_dims, [2] mode, [5] freq_base, [6] freq_scale as float bits).
+struct RopeParams {
+    int n_dims = 0;
+    float freq_base = 0.f, freq_scale = 0.f;
+};
+template <typename Tensor>
+inline bool rope_params_of(const Tensor *rope, RopeParams &p) {
+    if (!rope) return false;
+    p.n_dims = rope->op_params[1];
+    std::memcpy(&p.freq_base, &rope->op_params[5], 4);
+    std::memcpy(&p.freq_scale, &rope->op_params[6], 4);
+    return p.n_dims > 0 && (p.n_dims % 2) == 0;
 }
 
 // Lower `n` graph nodes; 0 and the backend node list, or the lowering's status.

@@ -827,6 +827,28 @@ std::vector<uint64_t> graph_key_of(mi355x_tensor *const *nodes, int n_nodes) {
 
 extern "C" {
 
+int mi355x_device_count(void) {
+    int ndev = 0, n = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess) return 0;
+    for (int d = 0; d < ndev; ++d) {
+        DeviceGuard dg(d);
+        n += kq::device_ok() ? 1 : 0;  // gfx950 with the library's code object
+    }
+    return n;
+}
+
+int mi355x_device_memory(int device, size_t *free_bytes, size_t *total_bytes) {
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return MI355X_E_NODEVICE;
+    DeviceGuard dg(device);
+    size_t f = 0, t = 0;
+    const hipError_t e = hipMemGetInfo(&f, &t);
+    if (e != hipSuccess) return (int)e;
+    if (free_bytes) *free_bytes = f;
+    if (total_bytes) *total_bytes = t;
+    return MI355X_OK;
+}
+
 mi355x_backend_t mi355x_backend_init(int device) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return nullptr;
@@ -873,6 +895,14 @@ void mi355x_backend_free_buffer(mi355x_backend_t b, void *ptr) {
     hipStreamSynchronize(b->stream);
     drop_graph(b);  // a captured graph may reference the buffer
     hipFree(ptr);
+}
+
+int mi355x_backend_memset(mi355x_backend_t b, void *dst, int value, size_t size) {
+    if (!b || (!dst && size)) return MI355X_E_INVAL;
+    if (!size) return MI355X_OK;
+    DeviceGuard dg(b->device);
+    const hipError_t e = hipMemsetAsync(dst, value & 0xff, size, b->stream);
+    return e == hipSuccess ? MI355X_OK : (int)e;
 }
 
 int mi355x_backend_set_tensor(mi355x_backend_t b, void *dst, const void *host_src, size_t size) {

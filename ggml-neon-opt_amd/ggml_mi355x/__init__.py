@@ -58,6 +58,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_prefill_precision",
     "mi355x_gemv_waves",
     "mi355x_debug_knob",
+    "mi355x_device_count", "mi355x_device_memory", "mi355x_backend_memset",
     "mi355x_attn_prompt",
     "mi355x_attn_prompt_impl",
 )
@@ -134,6 +135,11 @@ def lib():
     L.mi355x_row_size.restype = sz
     L.mi355x_version.restype = ctypes.c_char_p
     L.mi355x_device_available.restype = i32
+    L.mi355x_device_count.restype = i32
+    L.mi355x_device_memory.argtypes = [i32, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
+    L.mi355x_device_memory.restype = i32
+    L.mi355x_backend_memset.argtypes = [ctypes.c_void_p, ctypes.c_void_p, i32, ctypes.c_size_t]
+    L.mi355x_backend_memset.restype = i32
     L.mi355x_quantize_row_q8_K.argtypes = [vp, vp, i64]
     for n in ("q4_K", "q5_K", "q6_K"):
         getattr(L, f"mi355x_vec_dot_{n}_q8_K").argtypes = [i32, vp, sz, vp, sz, vp, sz, i32]

@@ -418,6 +418,12 @@ typedef struct mi355x_tensor {
 
 typedef struct mi355x_backend *mi355x_backend_t;
 
+/* Devices this library runs on (gfx950 with its code object), for the ggml-backend
+ * registration's get_device_count (ggml_backend_reg_i [U], ggml-backend-impl.h; the
+ * CPU sibling registers one device, ggml-cpu.cpp). 0 without a GPU. */
+int mi355x_device_count(void);
+/* Free / total device memory (ggml_backend_device_i.get_memory [U]): 0 or an error. */
+int mi355x_device_memory(int device, size_t *free_bytes, size_t *total_bytes);
 mi355x_backend_t mi355x_backend_init(int device);        /* NULL on failure */
 void mi355x_backend_free(mi355x_backend_t backend);
 const char *mi355x_backend_name(mi355x_backend_t backend);
@@ -428,6 +434,9 @@ int mi355x_backend_set_tensor(mi355x_backend_t backend, void *dst, const void *h
                               size_t size);              /* async H2D, bytes unchanged */
 int mi355x_backend_get_tensor(mi355x_backend_t backend, void *host_dst, const void *src,
                               size_t size);              /* async D2H */
+/* async device memset of `size` bytes to (uint8_t)value (ggml_backend_buffer_i.memset_tensor
+ * / clear [U]) */
+int mi355x_backend_memset(mi355x_backend_t backend, void *dst, int value, size_t size);
 int mi355x_backend_synchronize(mi355x_backend_t backend);
 int mi355x_backend_supports_op(const mi355x_tensor *op); /* 1 / 0 */
 /* Node fusion in graph_compute (default on): RMS_NORM -> MUL(norm weight) ->

@@ -57,10 +57,32 @@ static int self_checks() {
     bad += mi355x_adapter::gop_of_name("CPY") != MI355X_GOP_CPY;
     const int64_t k[3] = {5, 6, 7};
     const int32_t p[3] = {5, 6, 7}, q[3] = {5, 6, 8};
-    bad += !mi355x_adapter::cells_eq_pos(k, p, 3, true);
-    bad += mi355x_adapter::cells_eq_pos(k, q, 3, true);   // a moved cell
-    bad += mi355x_adapter::cells_eq_pos(k, p, 3, false);  // several sequences
-    bad += mi355x_adapter::cells_eq_pos(k, p, 0, true);   // empty batch
+    bad += !mi355x_adapter::cells_eq_pos(k, p, 3);
+    bad += mi355x_adapter::cells_eq_pos(k, q, 3);  // a moved cell
+    bad += mi355x_adapter::cells_eq_pos(k, p, 0);  // empty batch
+    // KQ mask rows (n_kv 8): causal over [0, pos] passes; another sequence's cell inside
+    // [0, pos] (-INF there), a visible cell after pos, or a wrong type is refused
+    const float NI = -__builtin_inff();
+    float m32[2][8];
+    uint16_t m16[2][8];
+    const int32_t pp[2] = {2, 5};
+    for (int t = 0; t < 2; ++t)
+        for (int j = 0; j < 8; ++j) {
+            m32[t][j] = j <= pp[t] ? 0.f : NI;
+            m16[t][j] = j <= pp[t] ? 0 : 0xfc00;
+        }
+    bad += !mi355x_adapter::kq_mask_causal(m32, 0, 8, 32, pp, 2);
+    bad += !mi355x_adapter::kq_mask_causal(m16, 1, 8, 16, pp, 2);
+    bad += mi355x_adapter::kq_mask_causal(m16, 0, 8, 16, pp, 2);
+    m32[1][3] = NI;  // cell 3 belongs to another sequence
+    bad += mi355x_adapter::kq_mask_causal(m32, 0, 8, 32, pp, 2);
+    m32[1][3] = 0.f;
+    m32[0][4] = 0.f;  // a visible cell after the position
+    bad += mi355x_adapter::kq_mask_causal(m32, 0, 8, 32, pp, 2);
+    m32[0][4] = NI;
+    bad += !mi355x_adapter::kq_mask_causal(m32, 0, 8, 32, pp, 2);
+    const int32_t far[1] = {8};  // position past the mask
+    bad += mi355x_adapter::kq_mask_causal(m32, 0, 8, 32, far, 1);
     return bad;
 }
 

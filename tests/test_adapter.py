@@ -142,3 +142,89 @@ def test_adapter_leaves_what_it_cannot_run(adapter_bin, tmp_path):
     assert run_adapter(adapter_bin, tmp_path, G.nodes, tab, 32, 500000.0)[0] == g.E_UNSUPPORTED
     next(t for t in G.nodes if t.op == g.GOP_SOFT_MAX).op = 99  # -> "FLASH_ATTN_EXT"
     assert run_adapter(adapter_bin, tmp_path, G.nodes, tab, 32, hp["freq_base"])[0] == g.E_UNSUPPORTED
+
+
+# ---------------------------------------------------------------- the registration glue
+BASE = 1 << 44  # glue_test.cpp: tensor data at BASE + offset lives in the backend's buffer
+
+
+@pytest.fixture(scope="module")
+def glue_bin(tmp_path_factory):
+    """adapter/ggml-mi355x.cpp (the whole ggml-backend registration: reg, device, buffer
+    type, buffer, backend iface, GGML_BACKEND_DL_IMPL) + tests/adapter/glue_test.cpp,
+    compiled with -Werror against the restated ggml-backend-impl.h subset."""
+    out = tmp_path_factory.mktemp("glue")
+    r = subprocess.run(["make", "-B", "-C", os.path.join(ROOT, "tests", "adapter"), f"BIN={out}"],
+                       capture_output=True, text=True)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return str(out / "glue_test")
+
+
+def test_glue_compiles_and_registers(glue_bin):
+    """reg -> device count (= the library's gfx950 devices: 0 on this host) -> the DL
+    entry points (ggml_backend_init returns the same registry, ggml_backend_score 0 without a
+    device) -> init on a missing device is NULL, not a crash."""
+    r = subprocess.run([glue_bin, "reg"], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0 and r.stdout.strip().endswith("ok"), r.stdout + r.stderr
+    n = int(r.stdout.split()[1])
+    assert n == g.lib().mi355x_device_count()
+
+
+def glue_inputs(tmp_path, hp, n_ctx, seed, tokens):
+    """The files glue_test decode reads: llm_build_llama's decode graph with every tensor in
+    ONE backend buffer (weights, norms, KV caches, inputs, node outputs at BASE + offset),
+    the weight / norm bytes to upload, the tokens. Returns (argv tail, host weights)."""
+    import numpy as np
+    from tests import llama_model as LM
+    w = LM.build(hp, seed)
+    off, blob = [0], []
+
+    def place(nbytes, data=None):
+        o = (off[0] + 255) // 256 * 256
+        off[0] = o + max(int(nbytes), 1)
+        if data is not None:
+            blob.append((o, np.ascontiguousarray(data).tobytes()))
+        return BASE + o
+
+    L = {}
+    for k, v in w.items():
+        if isinstance(v, tuple):
+            t, a = v
+            L[k] = (t, a.shape[1] // g.BLOCK_BYTES[t] * 256, a.shape[0], place(a.nbytes, a), a.shape[1])
+        else:
+            L[k] = place(v.nbytes, v)
+    kvw = hp["n_head_kv"] * hp["head_dim"]
+    for i in range(hp["n_layer"]):
+        L[f"k_cache.{i}"] = place(n_ctx * kvw * 2)
+        L[f"v_cache.{i}"] = place(n_ctx * kvw * 2)
+    L["inp_tokens"], L["inp_pos"] = place(4), place(4)
+    L["kq_mask"], L["k_idxs"], L["v_idxs"] = place(n_ctx * 2), place(8), place(kvw * 8)
+    G = GG.llama_decode_graph(hp, L, n_ctx, alloc=lambda nb: place(nb))
+    (tmp_path / "graph.txt").write_text(serialize(G.nodes))
+    with open(tmp_path / "blob.bin", "wb") as f:
+        for o, b in blob:
+            f.write(np.array([o, len(b)], np.uint64).tobytes())
+            f.write(b)
+    (tmp_path / "tokens.txt").write_text(" ".join(str(t) for t in tokens))
+    total = (off[0] + 4095) // 4096 * 4096
+    argv = [str(tmp_path / "graph.txt"), str(tmp_path / "blob.bin"), str(tmp_path / "tokens.txt"),
+            str(tmp_path / "logits.bin"), str(total), str(hp["n_vocab"])]
+    return argv, w
+
+
+def test_glue_inputs_address_one_buffer(tmp_path):
+    """The decode files describe one buffer: every tensor's data is BASE + offset inside it
+    (so the harness's single alloc_buffer holds the whole graph), and the graph carries
+    the inputs the glue's cells == positions check reads (k_idxs, inp_pos, the f16 mask)."""
+    hp = hparams(512, 1, 8, 2, 768, 1024)
+    argv, _ = glue_inputs(tmp_path, hp, 32, 0, [1, 2])
+    total = int(argv[4])
+    names = set()
+    for ln in open(argv[0]):
+        f = ln.split()
+        if f[0] != "T":
+            continue
+        data = int(f[-2])
+        assert BASE <= data < BASE + total, ln[:80]
+        names.add(f[-1])
+    assert {"inp_tokens", "inp_pos", "kq_mask", "k_idxs", "v_idxs", "result_output"} <= names
