@@ -1,0 +1,275 @@
+// kq_attn_head.h — decode attention of one query head on 256 threads (rope + f16 KV-cache
+// write + KQ + soft_max + KQV), the body of kq_attn_decode (kq_ops.hip) and of the fused
+// attention + o-proj kernel (kq_attn_oproj.hip).
+#pragma once
+
+#include "kq_attn_device.h"
+#include "kq_device.h"
+#include "kq_ops_device.h"
+
+namespace kq {
+
+// ------------------------------------------------------------ decode attention
+// One workgroup per query head h (kv head g = h / (n_head/n_head_kv)), 256 threads.
+//  0. Every load that does not depend on the position is issued together with the
+//     position itself: this token's q/k/v, K-cache row t (the cell thread t scores in
+//     the first pass) and the first VPF 8-cell groups of this thread's V-cache row(s).
+//     Only the rope-table row waits for the position, so a launch pays two memory
+//     latencies instead of four. Prefetched cells at or after pos are never used (the
+//     new cell comes from LDS, later cells are masked).
+//  1. rope(q_h), rope(k_g) at `pos` -> f16; v_g -> f16. The first query head of each
+//     kv group writes the new cell to the caches (K [cell][kvw], V transposed
+//     [ch][n_ctx]); every workgroup uses its own LDS copy of that cell, so no
+//     workgroup reads a cache cell written in this launch.
+//  2. kq[c] = vec_dot_f16(k_cache[c], q16) for c <= pos (NEON FP16 structure), * scale;
+//     cells pos < c < n_kv are masked (-INF) and contribute exact zeros below
+//     (the cache is zero-initialised, so their dot products are finite).
+//  3. soft_max: max; v_expf(w - max) per cell, group sums of 4 in the vaddvq order,
+//     the double sum over groups in order (one lane), p = e * (float)(1.0/sum) -> f16.
+//  4. kqv[d] = vec_dot_f16(v_cache[g*hd+d][0..n_kv), p16): thread (d, j) runs
+//     accumulator j (8 lanes) over cells 32it+8j+l, then the f16 reduce tree.
+// A position outside the cache fails loudly: NaN output, caches untouched.
+// Timing diagnostics (MI355X_ATTN_DIAG stops) only in experiment builds
+// (make variant-ops NAME=adiag VFLAGS=-DKQ_ATTN_DIAG=1); the product kernel has none.
+#ifndef KQ_ATTN_DIAG
+#define KQ_ATTN_DIAG 0
+#endif
+#if KQ_ATTN_DIAG
+#define ADIAG(a) ((a).diag)
+#else
+#define ADIAG(a) 0
+#endif
+// The per-head body, shared by kq_attn_decode (one 256-thread workgroup per head) and the
+// fused attention + o-proj kernel (kq_attn_oproj.hip: several heads per workgroup, 256
+// threads each; every __syncthreads() is reached by all of them in the same order since the
+// control flow depends only on the position). t: the thread's index within the head's 256;
+// smem: this head's LDS (attn_lds bytes); out: where output d of the head goes
+// (out[d], global or LDS); may_write: this workgroup may store the new KV cell.
+// TPH: threads per head (256; 128 for head_dim 64 in the fused kernel, where 4 heads share a
+// workgroup and 256 threads each would cap it at 128 VGPRs): the register path holds one
+// cell per thread (n_kv <= TPH), KQV runs HD * 4 / TPH (d, j) items per thread.
+// VPF0: V-cache iterations (32 cells each) prefetched with the position (0: 8 / ITEMS).
+template <int HD, int TPH = 256, int VPF0 = 0>
+__device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8_t *smem, float *out,
+                                          bool may_write) {
+    static_assert(HD == 64 || HD == 128, "head_dim");
+    constexpr int KV4 = HD / 8;          // 16-B pieces of one K-cache row
+    static_assert(TPH == 256 || (TPH == 128 && HD == 64), "threads per head");
+    constexpr int ITEMS = HD * 4 / TPH;  // KQV (d, j) items per thread
+    constexpr int VPF = VPF0 > 0 ? VPF0 : 8 / ITEMS;  // prefetched 32-cell iterations per item
+    const int gsz = a.n_head / a.n_head_kv;
+    const int g = h / gsz;
+    const int kvw = a.n_head_kv * HD;
+    if (ADIAG(a) == 4) return;  // diagnostics (MI355X_ATTN_DIAG): empty launch
+
+    // ---- 0. position-independent loads, issued with the position
+    const int pos_in = *a.pos;
+    float x0 = 0.f, x1 = 0.f, y0 = 0.f, y1 = 0.f;
+    float rc = 0.f, rs = 0.f;  // rope_row: cos/sin of the thread's pair, staged with the position
+    if (t < HD / 2) {
+        if (a.rope_row) {
+            rc = a.rope_table[2 * t];
+            rs = a.rope_table[2 * t + 1];
+        }
+        const float *qp = a.q + (int64_t)h * HD + 2 * t;
+        const float *kp = a.k + (int64_t)g * HD + 2 * t;
+        x0 = qp[0];
+        x1 = qp[1];
+        y0 = kp[0];
+        y1 = kp[1];
+    } else if (t < HD / 2 + HD) {
+        x0 = a.v[(int64_t)g * HD + (t - HD / 2)];
+    }
+    uint4 kpre[KV4] = {};
+    if (t < a.n_ctx && ADIAG(a) != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
+        const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)t * kvw + (int64_t)g * HD);
+#pragma unroll
+        for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
+    }
+    uint4 vpre[ITEMS][VPF] = {};
+#pragma unroll
+    for (int ii = 0; ii < ITEMS; ++ii) {
+        const int item = t + TPH * ii, d = item >> 2, j = item & 3;
+        const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx + 8 * j;
+#pragma unroll
+        for (int it = 0; it < VPF; ++it)
+            if (32 * it < a.n_ctx && ADIAG(a) != 5) vpre[ii][it] = *(const uint4 *)(vr + 32 * it);
+    }
+
+    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;  // no cache cell for this position
+    const int pos = bad ? 0 : pos_in;
+    int n_kv = (pos + 1 + 31) / 32 * 32;
+    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
+    // LDS (attn_lds): q16 | k16 | v16 (HD f16 each) | w (n_ctx f32) | p16 (n_ctx f16) |
+    // red (HD*32 f16 accumulators) | scal (max, 1/sum, 2 pad) [| gsum]; every piece 16-B aligned
+    uint16_t *q16 = (uint16_t *)smem;
+    uint16_t *k16 = q16 + HD;
+    uint16_t *v16 = k16 + HD;
+    float *w = (float *)(smem + 6 * HD);
+    uint16_t *p16 = (uint16_t *)(w + a.n_ctx);
+    h16 *red = (h16 *)(p16 + a.n_ctx);
+    float *scal = (float *)(red + HD * 32);
+    // per group of 4 cells: (double)((e0 + e1) + (e2 + e3)); lives in `red` (free until
+    // KQV) when it fits, past scal otherwise
+    double *gsum = (a.n_ctx / 4) * 8 <= HD * 64 ? (double *)red : (double *)(scal + 4);
+
+    const float *tc = a.rope_table + (a.rope_row ? 0 : (int64_t)pos * (HD / 2) * 2);
+    const bool writer = may_write && !bad && (h % gsz) == 0;
+    if (t < HD / 2) {
+        const float c = a.rope_row ? rc : tc[2 * t], s = a.rope_row ? rs : tc[2 * t + 1];
+        const float2 rq = rope_pair(x0, x1, c, s);
+        q16[2 * t] = h2u(f2h_rne(rq.x));
+        q16[2 * t + 1] = h2u(f2h_rne(rq.y));
+        const float2 rk = rope_pair(y0, y1, c, s);
+        const uint16_t k0 = h2u(f2h_rne(rk.x)), k1 = h2u(f2h_rne(rk.y));
+        k16[2 * t] = k0;
+        k16[2 * t + 1] = k1;
+        if (writer) *(uint32_t *)(a.k_cache + (int64_t)pos * kvw + (int64_t)g * HD + 2 * t) = k0 | ((uint32_t)k1 << 16);
+    } else if (t < HD / 2 + HD) {
+        const int d = t - HD / 2;
+        const uint16_t vv = h2u(f2h_rne(x0));
+        v16[d] = vv;
+        if (writer) a.v_cache[(int64_t)(g * HD + d) * a.n_ctx + pos] = vv;
+    }
+    __syncthreads();
+    if (ADIAG(a) == 1 || ADIAG(a) == 5) {  // diagnostics: stop after the loads and rope
+        if (t < HD) out[t] = x0 + __uint_as_float(kpre[0].x ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
+        return;
+    }
+
+    if (n_kv <= TPH) {  // one cell per thread: score, max, exp and group sum stay in registers
+        const int c = t;
+        float sc = -INFINITY;
+        if (c < n_kv && c <= pos) {
+            uint4 kv[KV4];
+            if (c == pos) {
+#pragma unroll
+                for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+            } else {
+#pragma unroll
+                for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
+            }
+            sc = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+        }
+        const float wmx = wave_fmax(sc);  // max (order-free): per wave, then over the 4 waves
+        if ((t & 63) == 0) scal[t >> 6] = wmx;
+        __syncthreads();
+        if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
+            if (t < HD) out[t] = sc + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
+        }
+        const float mx = TPH == 256 ? fmaxf(fmaxf(scal[0], scal[1]), fmaxf(scal[2], scal[3])) : fmaxf(scal[0], scal[1]);
+        const float ec = c < n_kv && sc != -INFINITY ? v_expf(sc - mx) : 0.0f;
+        // group sum of cells 4g..4g+3 (lanes 4g..4g+3) in the vaddvq order (e0 + e1) + (e2 + e3)
+        const float s01 = ec + dpp_mov_f32<0xB1>(ec);   // lane 4g: e0 + e1, lane 4g+2: e2 + e3
+        const float g4 = s01 + dpp_mov_f32<0x4E>(s01);  // lane 4g: (e0 + e1) + (e2 + e3)
+        if ((t & 3) == 0 && c < n_kv) gsum[t >> 2] = (double)g4;
+        __syncthreads();
+        // every wave computes the same sum (no barrier to publish it): ggml's in-order double
+        // sum, as a tree where that is exact (softmax_group_sum)
+        const double sum = softmax_group_sum(gsum, n_kv / 4, t & 63);
+        const float inv = (float)(1.0 / sum);
+        if (c < n_kv) p16[c] = h2u(f2h_rne(ec * inv));
+        __syncthreads();
+        if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
+            if (t < HD) out[t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
+        }
+    } else {
+        // KQ + scale + mask; the first pass (c == t) scores the prefetched row
+        for (int c = t; c < n_kv; c += TPH) {
+            float s = -INFINITY;
+            if (c <= pos) {
+                uint4 kv[KV4];
+                if (c == pos) {
+#pragma unroll
+                    for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+                } else if (c == t) {
+#pragma unroll
+                    for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
+                } else {
+                    const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+#pragma unroll
+                    for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
+                }
+                s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+            }
+            w[c] = s;
+        }
+        __syncthreads();
+        if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
+            if (t < HD) out[t] = w[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
+        }
+        // max (order-free), then exp + group sums
+        if (t < 64) {
+            float m = -INFINITY;
+            for (int c = t; c < n_kv; c += 64) m = fmaxf(m, w[c]);
+#pragma unroll
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            if (t == 0) scal[0] = m;
+        }
+        __syncthreads();
+        const float mx = scal[0];
+        for (int gi = t; gi < n_kv / 4; gi += TPH) {
+            float e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float wv = w[4 * gi + k];
+                e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[4 * gi + k] = e[k];
+            gsum[gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));  // the vaddvq group sum, in parallel
+        }
+        __syncthreads();
+        if (t < 64) {  // ggml's in-order double sum over the groups (a tree where exact)
+            double sum = softmax_group_sum(gsum, n_kv / 4, t);
+            sum = 1.0 / sum;
+            if (t == 0) scal[1] = (float)sum;
+        }
+        __syncthreads();
+        const float inv = scal[1];
+        for (int c = t; c < n_kv; c += TPH) p16[c] = h2u(f2h_rne(w[c] * inv));
+        __syncthreads();
+        if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
+            if (t < HD) out[t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            return;
+        }
+
+    }
+
+    // KQV: thread (d, j) -> accumulator j of output d
+    const int n_it = (pos + 32) / 32;  // iterations holding a cell <= pos; later ones add exact zeros
+#pragma unroll
+    for (int ii = 0; ii < ITEMS; ++ii) {
+        const int item = t + TPH * ii;
+        const int d = item >> 2, j = item & 3;
+        const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
+        uint32_t acc[4] = {};  // lanes 2k, 2k+1 of accumulator j in word k
+        for (int it = 0; it < n_it; ++it) {  // VPF prefetched iterations, then global loads
+            const int c0 = 32 * it + 8 * j;
+            uint4 vv;
+            if (it < VPF) {
+#pragma unroll
+                for (int k = 0; k < VPF; ++k)
+                    if (k == it) vv = vpre[ii][k];
+            } else {
+                vv = *(const uint4 *)(vr + c0);
+            }
+            const uint4 pp = *(const uint4 *)(p16 + c0);
+            uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
+            const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+            if (pos >= c0 && pos < c0 + 8) {  // the new cell: LDS copy
+                const int l = pos - c0;
+                vw[l >> 1] = (vw[l >> 1] & (0xffff0000u >> (16 * (l & 1)))) | ((uint32_t)v16[d] << (16 * (l & 1)));
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc[k] = pk_fma_w(vw[k], pw[k], acc[k]);
+        }
+        const float o = f16x8_reduce_quad(acc);  // accumulators j = 0..3 of output d: one quad of lanes
+        if (j == 0) out[d] = bad ? __builtin_nanf("") : o;
+    }
+}
+
+}  // namespace kq

@@ -36,6 +36,10 @@ struct mi355x_backend {
     };
     std::vector<Captured> graphs;
     bool fuse = true;
+    bool attn_oproj = true;  // decode attention + o-proj GEMV in one launch (kq_attn_oproj.hip)
+    void *fx = nullptr;      // its arrival counters (zeroed at allocation) and records
+    size_t fx_size = 0;
+    int fx_nsb = 0;          // the superblock count the counters' rounds are aligned to
     ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
     bool loop_nocopy = false;   // emulated rank, timing only (MI355X_LOOPBACK_NOCOPY)
     int rank = 0, world = 0;
@@ -128,7 +132,8 @@ mi355x_backend::Captured *find_graph(mi355x_backend *b, const std::vector<uint64
 struct Launch {
     int first, count;  // nodes[first .. first+count): the MUL_MAT run, or the single node
     int kind = 0;      // 0 single node, 1 MUL_MAT run (GEMV), 2 prefill prologue -> Q8L, 3 batched MUL_MAT + ADD,
-                       // 4 batched MUL_MATs of one type on one activation in one tile-GEMM launch
+                       // 4 batched MUL_MATs of one type on one activation in one tile-GEMM launch,
+                       // 5 decode ATTN_DECODE -> MUL_MAT (-> ADD) in one launch (kq_attn_oproj)
     const mi355x_tensor *q8_of = nullptr;  // kind 2: the node whose (never written) output the Q8L blocks stand for
     int pro = MI355X_PRO_NONE;
     const float *x = nullptr, *x2 = nullptr;  // GEMV input (prologue source) and its second operand
@@ -296,6 +301,18 @@ bool batched_mm_shares(const mi355x_backend *b, const mi355x_tensor *t) {
 // (kq_mmq_mixed: a prompt batch's Q4_K / Q5_K q/k with the Q6_K attn_v of use_more_bits layers)
 bool multi_types_ok(int a, int b) { return a == b || (is_kquant(a) && is_kquant(b)); }
 
+// A decode attention whose output only the next node, a GEMV (the o-proj), reads: both
+// run as one kq_attn_oproj launch when its shape allows (bit-identical: kq_attn_oproj.hip).
+bool attn_oproj_fusable(const mi355x_backend *b, const mi355x_tensor *t, const mi355x_tensor *mm, int readers) {
+    if (!b->attn_oproj || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] != 1) return false;
+    if (kq::attn_impl() != MI355X_ATTN_HEAD || !elidable(t, readers)) return false;
+    if (!is_gemv_node(mm) || mm->src[1] != t || !is_kquant(mm->src[0]->type)) return false;
+    const mi355x_tensor *w = mm->src[0];
+    if (w->ne[0] != t->ne[0] || w->ne[2] != 1 || w->ne[3] != 1 || mm->nb[0] != 4) return false;
+    const int nh = t->op_params[0], nkv = t->op_params[1], hd = t->op_params[2];
+    return kq::attn_oproj_buffer(hd, nh, nkv, (int)t->src[4]->ne[1], w->type, w->ne[0], w->ne[1], nullptr) > 0;
+}
+
 std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const *nodes, int n, bool fuse) {
     std::vector<Launch> out;
     const std::vector<int> readers = fuse ? count_readers(nodes, n) : std::vector<int>(n, 0);
@@ -311,6 +328,29 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
         l.first = i;
         l.count = 1;
         int head = i;  // first MUL_MAT of a run
+        if (fuse && i + 1 < n && attn_oproj_fusable(b, t, nodes[i + 1], readers[i])) {
+            const mi355x_tensor *mm = nodes[i + 1];
+            l.kind = 5;
+            l.count = 2;
+            l.y[0] = (float *)mm->data;
+            int end = i + 2;
+            if (end < n && nodes[end]->op == MI355X_OP_ADD && elidable(mm, readers[i + 1])) {
+                const mi355x_tensor *ad = nodes[end];
+                const int s_mm = ad->src[0] == mm ? 0 : ad->src[1] == mm ? 1 : -1;
+                const mi355x_tensor *other = s_mm >= 0 ? ad->src[1 - s_mm] : nullptr;
+                if (other && index_of(other, i, end) < 0 && ad->ne[0] == mm->ne[0] && ad->ne[1] == 1 &&
+                    ad->type == MI355X_TYPE_F32 && other->type == MI355X_TYPE_F32 && nelem(other) == ad->ne[0] &&
+                    other->nb[0] == 4 && ad->nb[0] == 4) {
+                    l.res[0] = (const float *)other->data;
+                    l.y[0] = (float *)ad->data;
+                    l.count = 3;
+                    ++end;
+                }
+            }
+            out.push_back(l);
+            i = end;
+            continue;
+        }
         // prologue fusion: RMS_NORM -> MUL -> MUL_MAT run, SWIGLU -> MUL_MAT run
         if (fuse && t->op == MI355X_OP_RMS_NORM && i + 2 < n && nodes[i + 1]->op == MI355X_OP_MUL &&
             nodes[i + 1]->src[0] == t && elidable(t, readers[i]) && is_gemv_node(nodes[i + 2]) &&
@@ -654,6 +694,21 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
             q8.nb = m->nb[1];
             continue;
         }
+        if (l.kind == 5) {  // decode attention + o-proj (+ residual): one launch
+            const mi355x_tensor *mm = nodes[l.first + 1];
+            mi355x_attn_desc d;
+            attn_desc_of(t, d);
+            d.rope_row = t->src[6]->ne[1] == 1 ? 1 : 0;  // the position's row, staged with pos
+            kq::AttnArgs a;
+            rc = kq::attn_args_from(&d, a);
+            if (rc) return rc;
+            const mi355x_tensor *w = mm->src[0];
+            rc = kq::launch_attn_oproj(a, w->type, w->data, w->ne[1], w->nb[1], l.res[0], l.y[0], (uint8_t *)b->fx,
+                                       b->fx_size, b->stream);
+            if (rc) return rc;
+            q8 = Q8State();
+            continue;
+        }
         bool f16_run = l.kind == 4 && kq::mmf_on();
         for (int k = 0; f16_run && k < l.count; ++k) {  // every matrix where the f16 kernel is the faster one
             const mi355x_tensor *u = nodes[l.first + k]->src[0];
@@ -871,6 +926,7 @@ void mi355x_backend_free(mi355x_backend_t b) {
     hipStreamSynchronize(b->stream);
     drop_graph(b);
     if (b->workspace) hipFree(b->workspace);
+    if (b->fx) hipFree(b->fx);
     if (b->comm) rccl().comm_destroy(b->comm);
     hipStreamDestroy(b->stream);
     }
@@ -1075,6 +1131,18 @@ int mi355x_backend_set_comm_loopback(mi355x_backend_t b, int rank, int world) {
     return MI355X_OK;
 }
 
+int mi355x_backend_set_attn_oproj(mi355x_backend_t b, int enable) {
+    if (!b) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
+    const int prev = b->attn_oproj ? 1 : 0;
+    if ((enable != 0) != b->attn_oproj) {
+        hipStreamSynchronize(b->stream);
+        drop_graph(b);
+        b->attn_oproj = enable != 0;
+    }
+    return prev;
+}
+
 int mi355x_backend_set_fusion(mi355x_backend_t b, int enable) {
     if (!b) return MI355X_E_INVAL;
     DeviceGuard dg(b->device);
@@ -1122,6 +1190,35 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
         b->workspace_size = ws;
     }
     const std::vector<Launch> launches = plan_launches(b, nodes, n_nodes, b->fuse);
+    {  // the fused attention + o-proj launches' buffer: sized and zeroed outside any capture
+        size_t need = 0;
+        int nsb = 0;
+        bool mixed = false;
+        for (const Launch &l : launches) {
+            if (l.kind != 5) continue;
+            const mi355x_tensor *t = nodes[l.first], *w = nodes[l.first + 1]->src[0];
+            int k = 0;
+            const size_t sz = kq::attn_oproj_buffer(t->op_params[2], t->op_params[0], t->op_params[1],
+                                                    (int)t->src[4]->ne[1], w->type, w->ne[0], w->ne[1], &k);
+            need = sz > need ? sz : need;
+            mixed |= nsb && k != nsb;
+            nsb = k;
+        }
+        if (mixed) return MI355X_E_UNSUPPORTED;  // (never built by plan_launches' callers: one o-proj shape per graph)
+        if (need && (need > b->fx_size || nsb != b->fx_nsb)) {
+            hipStreamSynchronize(b->stream);
+            drop_graph(b);
+            if (need > b->fx_size) {
+                if (b->fx) hipFree(b->fx);
+                b->fx = nullptr;
+                b->fx_size = 0;
+                if (hipMalloc(&b->fx, need) != hipSuccess) return MI355X_E_WORKSPACE;
+                b->fx_size = need;
+            }
+            if (hipMemset(b->fx, 0, kq::kAttnOprojCounterBytes) != hipSuccess) return MI355X_E_WORKSPACE;
+            b->fx_nsb = nsb;
+        }
+    }
     if (!use_graph) return enqueue(b, nodes, launches);
     std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);
     mi355x_backend::Captured *c = find_graph(b, key);

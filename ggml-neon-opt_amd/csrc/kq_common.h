@@ -208,6 +208,22 @@ struct AttnArgs {
                       // for the next GEMM (row i's superblock b at (i*nb + b)*304), or null
 };
 
+// Decode attention fused with the o-proj GEMV (kq_attn_oproj.hip): workgroup (s, rb) runs the
+// attention of the heads of superblock s of the o-proj's K, quantizes them (one Q8_K
+// superblock) and writes the exact per-superblock records of rows [rb*R, rb*R + R); the
+// last of the nsb workgroups of row block rb replays each row's chain in superblock order.
+struct AttnOprojArgs {
+    AttnArgs at;              // the attention (this node's heads; at.out unused)
+    const uint8_t *w;         // o-proj weights: n_rows rows of nsb superblocks, row_stride bytes
+    int64_t row_stride;
+    int n_rows, nsb, R, n_rb;
+    int head_lds;             // LDS bytes per head (attn_lds, 16-B multiple)
+    const float *res;         // residual (ggml_add after the mul_mat), or null
+    float *y;                 // n_rows outputs
+    uint8_t *recs;            // [n_rb][R][nsb] 16-B records (written sc1, read sc1)
+    uint32_t *cnt;            // [n_rb] arrival counters (monotonic: last = old % nsb == nsb - 1)
+};
+
 // ---------------------------------------------------------------- batched (prefill) MFMA GEMM
 // kq_mmq (M > 1): 64 x 64 output tiles, Q8L activations in a workspace.
 struct MmqArgs {

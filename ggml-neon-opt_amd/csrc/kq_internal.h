@@ -96,6 +96,14 @@ int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a);  // + check_attn
 int launch_attn(const AttnArgs &a, hipStream_t s);
 bool attn_group_ok(const AttnArgs &a, int nwaves);      // the one-workgroup-per-kv-group path applies
 size_t attn_group_bytes(const AttnArgs &a, int nwaves);  // its LDS
+// kq_attn_oproj.hip: decode attention + the o-proj GEMV (+ residual ADD) in one launch.
+// attn_oproj_buffer: bytes of the device buffer it needs (arrival counters, zeroed once,
+// then the records), 0 when the shape is not supported; *nsb: the superblocks of K.
+constexpr size_t kAttnOprojCounterBytes = 1024;
+size_t attn_oproj_buffer(int hd, int n_head, int n_head_kv, int n_ctx, int type, int64_t K, int64_t n_rows, int *nsb);
+int launch_attn_oproj(const AttnArgs &a, int type, const void *w, int64_t n_rows, size_t row_stride, const float *res,
+                      float *y, uint8_t *buf, size_t buf_size, hipStream_t stream);
+int attn_impl();  // mi355x_attn_impl (kq_ops.hip)
 // kq_api.hip
 void allow_lds(const void *fn, size_t lds);
 // Experiment / diagnostic knobs of A/B runs. The product reads no environment: a knob

@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_prefill_precision",
     "mi355x_gemv_waves",
     "mi355x_debug_knob",
-    "mi355x_device_count", "mi355x_device_memory", "mi355x_backend_memset",
+    "mi355x_device_count", "mi355x_device_memory", "mi355x_backend_memset", "mi355x_backend_set_attn_oproj",
     "mi355x_attn_prompt",
     "mi355x_attn_prompt_impl",
 )
@@ -140,6 +140,8 @@ def lib():
     L.mi355x_device_memory.restype = i32
     L.mi355x_backend_memset.argtypes = [ctypes.c_void_p, ctypes.c_void_p, i32, ctypes.c_size_t]
     L.mi355x_backend_memset.restype = i32
+    L.mi355x_backend_set_attn_oproj.argtypes = [ctypes.c_void_p, i32]
+    L.mi355x_backend_set_attn_oproj.restype = i32
     L.mi355x_quantize_row_q8_K.argtypes = [vp, vp, i64]
     for n in ("q4_K", "q5_K", "q6_K"):
         getattr(L, f"mi355x_vec_dot_{n}_q8_K").argtypes = [i32, vp, sz, vp, sz, vp, sz, i32]
@@ -605,6 +607,10 @@ class Backend:
 
     def set_fusion(self, enable):
         return int(lib().mi355x_backend_set_fusion(self.h, 1 if enable else 0))
+
+    def set_attn_oproj(self, enable):
+        """Decode attention + o-proj GEMV in one launch (default on); returns the previous."""
+        return int(lib().mi355x_backend_set_attn_oproj(self.h, 1 if enable else 0))
 
     def set_comm(self, rank, world, unique_id: bytes):
         """Join the RCCL communicator of a row split (every rank, same id bytes)."""

@@ -446,6 +446,15 @@ int mi355x_backend_supports_op(const mi355x_tensor *op); /* 1 / 0 */
  * kernel. Fused intermediates (not flagged OUTPUT, read by no other node) are not
  * written. Results are bit-identical with fusion off. Returns the previous value. */
 int mi355x_backend_set_fusion(mi355x_backend_t backend, int enable);
+/* Decode attention fused with the o-proj GEMV (default on, with fusion on): an ATTN_DECODE
+ * of one token whose output only the next node reads, a K-quant MUL_MAT (+ its residual
+ * ADD), runs as ONE launch -- workgroup (s, rb) computes the heads of the o-proj's K
+ * superblock s, quantizes them to that Q8_K superblock and writes the exact integer records
+ * of rows block rb; the last workgroup of each row block replays every row's fp32 chain in
+ * superblock order (csrc/kq_attn_oproj.hip). Bit-identical to the two launches. Applies with
+ * the per-head attention kernel (mi355x_attn_impl ATTN_HEAD), head_dim 64 / 128, the heads
+ * of one K superblock in one KV group and K <= 4096. Returns the previous value. */
+int mi355x_backend_set_attn_oproj(mi355x_backend_t backend, int enable);
 /* Runs nodes in order on the backend stream. Consecutive MUL_MAT nodes with
  * ne11 == 1 that share src[1] are fused into one launch. When `use_graph` is
  * non-zero the launch sequence is captured once into a hipGraph and replayed
