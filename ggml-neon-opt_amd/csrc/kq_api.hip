@@ -1180,8 +1180,9 @@ size_t mi355x_mul_mat_workspace_size(int src0_type, int64_t ne00, int64_t ne01, 
     if (!block_bytes(src0_type) || ne00 <= 0 || ne00 % QK || ne11 < 0) return 0;
     if (ne11 == 0 || (ne11 == 1 && ne00 / QK <= kFusedQMaxNb)) return 0;
     size_t bytes = (size_t)ne11 * (size_t)(ne00 / QK) * Q8L_STRIDE;  // >= raw 292-B blocks
-    // the f16 prefill path (mi355x_prefill_precision) may run instead at ne11 >= 16
-    if (ne11 >= kMmqMinCols && ne01 > 0) {
+    // the f16 prefill path runs instead at ne11 >= 16 once mi355x_prefill_precision selects it
+    // (its image and split-K slabs; callers re-query after switching)
+    if (ne11 >= kMmqMinCols && ne01 > 0 && prefill_precision() >= MI355X_PREFILL_F16) {
         const size_t f = mmf_workspace(ne01, ne11, ne00 / QK);
         bytes = f > bytes ? f : bytes;
     }

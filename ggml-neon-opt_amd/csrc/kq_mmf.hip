@@ -14,7 +14,7 @@
 // rounding of an exact product (v_pk_fma_f16 of the magic-exponent quant 1024 + q with
 // dsc and the exact -1024 * dsc), every activation operand one rounding of the reference's
 // own d * q. Tolerance (tests/test_gpu_mmf.py): |y - y_ref| <= 2^-8 * sum_k |w_k| |x^_k|
-// + 2^-20 * K * max|w| max|x^| (w, x^ the dequantized operands), y_ref the oracle's
+// + 2^-24 * K * max|w| max|x^| (w, x^ the dequantized operands; mmf_bound of the tests' numpy checker), y_ref the oracle's
 // bit-exact mul_mat.
 //
 // Tiles: a workgroup of 4 waves owns 128 weight rows (32 per wave: the MFMA's columns)

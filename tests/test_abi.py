@@ -62,6 +62,15 @@ def test_argument_validation_without_device():
     assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 5) == ((5 * 8 * 304 + 255) // 256) * 256
     assert L.mi355x_mul_mat_workspace_size(12, 2048, 64, 1) == 0
     assert L.mi355x_mul_mat_workspace_size(12, 28672, 64, 1) == ((112 * 304 + 255) // 256) * 256
+    # the f16 prefill image is sized only once mi355x_prefill_precision selects it
+    exact = L.mi355x_mul_mat_workspace_size(12, 4096, 14336, 512)
+    assert exact == ((512 * 16 * 304 + 255) // 256) * 256
+    prev = L.mi355x_prefill_precision(g.PREFILL_F16)
+    try:
+        assert L.mi355x_mul_mat_workspace_size(12, 4096, 14336, 512) > exact
+    finally:
+        L.mi355x_prefill_precision(prev)
+    assert L.mi355x_mul_mat_workspace_size(12, 4096, 14336, 512) == exact
     # misaligned weights
     descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1002, 4, 144, 0x3000))
     assert L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None, 0, None) == -1
