@@ -248,12 +248,22 @@ class Token:
         self.wl = [[w[name] for name, _, _, _ in stage] for stage in self.stages]  # per stage, as Chain.w
         self.n_ctx = n_ctx
         self.dec = LlamaDecoder(be, self.hp, w, n_ctx, split=self.split)
+        self.n_launch = None
         rng = np.random.default_rng(0x51A7)  # the same token stream on every rank
         self.tokens = rng.integers(0, m["V"], size=n_ctx).tolist()
 
     def launches(self):
-        n = 5 * self.hp["n_layer"] + 2
-        return n + (self.split.collectives_per_token() if self.split is not None else 0)
+        """Kernel launches (+ collectives) per token, counted on one eager token at position 0
+        (the backend's fusions decide: 4 per layer with attention + o-proj in one launch, 5
+        without). Collective under a row split: every rank calls it."""
+        if self.n_launch is None:
+            g.timing_enable(True)
+            self.dec.step(self.tokens[0], 0, use_graph=False)
+            rows = g.timing_read()
+            g.timing_enable(False)
+            self.dec.reset()
+            self.n_launch = len(rows) + (self.split.collectives_per_token() if self.split is not None else 0)
+        return self.n_launch
 
 
 def timed_kernel_stats(be, chain, tokens):
@@ -267,6 +277,8 @@ def timed_kernel_stats(be, chain, tokens):
         assert rc == 0, rc
     rows = g.timing_read()
     g.timing_enable(False)
+    if isinstance(chain, Token) and tokens > 0:  # launches per token, measured (every rank runs this)
+        chain.n_launch = len(rows) // tokens + (chain.split.collectives_per_token() if chain.split is not None else 0)
     if os.environ.get("BENCH_KINDS_OUT") and tokens > 0:  # launch kinds of one token, in order (profiles)
         n = len(rows) // tokens
         with open(os.environ["BENCH_KINDS_OUT"], "w") as f:
@@ -1136,7 +1148,8 @@ def main():
         local_bytes = chain.bytes_per_token  # weight bytes one GPU streams per token
         if isinstance(chain, Token):
             executor = ("LlamaDecoder -> mi355x_backend_graph_compute: node fusion (norm/swiglu GEMV prologues, "
-                        "residual/swiglu epilogues), kq_rows + kq_attn_decode" +
+                        "residual/swiglu epilogues), kq_rows + kq_attn_oproj (attention, o-proj and residual in one "
+                        "launch where the shape allows; kq_attn_decode otherwise)" +
                         ((", RCCL ncclAllReduce per K-split stage (row split, reduce)" if split_mode == "reduce" else
                           ", RCCL ncclAllGather per stage (row split)") if rowsplit else "") + ", " +
                         ("hipGraph replay" if not args.no_graph else "eager"))

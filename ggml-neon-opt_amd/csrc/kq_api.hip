@@ -111,7 +111,8 @@ const KnobDef kKnobs[KNOB_COUNT] = {
     {"GEMV_DIAG", 0},  {"GEMV_RING", 0},     {"GEMV_PRE0", 1},       {"GEMV_PF", 0},
     {"GEMV_XMODE", 0}, {"GEMV_SMALL_MB", kRowsSmallBytes / 1e6},      {"GEMV_WPC", 0},
     {"GEMV_SMALL_WG", 0}, {"GEMV_FQMAX", (double)kRowsFusedMaxNb},   {"MMF_WAVES", 0},
-    {"MMF_ORDER", 0},  {"ATTN_DIAG", 0},     {"LOOPBACK_NOCOPY", 0},
+    {"MMF_ORDER", 0},  {"ATTN_DIAG", 0},     {"LOOPBACK_NOCOPY", 0}, {"ATTN_OPROJ", 1},
+    {"AO_NRB", 0},
 };
 std::atomic<double> g_knob[KNOB_COUNT];
 std::atomic<bool> g_knob_set[KNOB_COUNT];

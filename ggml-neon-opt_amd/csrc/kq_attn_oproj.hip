@@ -33,6 +33,13 @@
 #include "kq_internal.h"
 #include "kq_rows_device.h"
 
+// Timing-only ablations, compile time (experiment builds: make variant-ao NAME=ao1
+// VFLAGS=-DKQ_AO_DIAG=1): 1 no attention (zeros), 2 stop after the attention, 4 stop after
+// the record stores (no hand-off), 8 no weight DMA.
+#ifndef KQ_AO_DIAG
+#define KQ_AO_DIAG 0
+#endif
+
 namespace kq {
 
 namespace {
@@ -75,7 +82,7 @@ __global__ void __launch_bounds__(512) kq_attn_oproj(const AttnOprojArgs p) {
     // ---- o-proj weights of this workgroup (superblock s of rows row0 ..), by LDS-DMA at
     // entry: granule gi = 64 j + lane of instruction j is piece gi % P of row gi / P; lanes
     // past the last row re-read the last granule into the padding behind it
-    {
+    if (!(KQ_AO_DIAG & 8)) {
         const int G = nrows * P;
         const uint8_t *const wb = p.w + (int64_t)s * BSZ;
         for (int j = wave; 64 * j < G; j += nwaves) {
@@ -89,11 +96,20 @@ __global__ void __launch_bounds__(512) kq_attn_oproj(const AttnOprojArgs p) {
     }
 
     // ---- attention of head s*HPS + hi (threads [TPH hi, TPH hi + TPH)), output into act
-    attn_head<HD, TPH>(p.at, s * HPS + hi, t, smem + hi * p.head_lds, act + hi * HD, rb == 0);
+    if (KQ_AO_DIAG & 1) {
+        if (t < HD) act[hi * HD + t] = 0.f;
+    } else {
+        attn_head<HD, TPH>(p.at, s * HPS + hi, t, smem + hi * p.head_lds, act + hi * HD, rb == 0);
+    }
 
     // ---- the superblock's Q8_K block (quantize_row_q8_K_ref, as kq_rows' fused quantization)
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's weight DMAs landed
     __syncthreads();                                    // every head's output and every DMA in LDS
+    if (KQ_AO_DIAG & 6) {  // ablations: the residual passes through (finite values downstream)
+        if (s == 0 && (KQ_AO_DIAG & 2) && (int)threadIdx.x < nrows)
+            p.y[row0 + (int)threadIdx.x] = p.res ? p.res[row0 + (int)threadIdx.x] : 0.f;
+        if (KQ_AO_DIAG & 2) return;
+    }
     if (threadIdx.x < 16) {
         u32x4 v[4];
 #pragma unroll
@@ -131,6 +147,10 @@ __global__ void __launch_bounds__(512) kq_attn_oproj(const AttnOprojArgs p) {
 
     // ---- hand-off: every wave drains its write-through stores, then one lane counts the
     // workgroup in; the last of the round replays the row block
+    if (KQ_AO_DIAG & 4) {
+        if (s == 0 && (int)threadIdx.x < nrows) p.y[row0 + (int)threadIdx.x] = p.res ? p.res[row0 + (int)threadIdx.x] : 0.f;
+        return;
+    }
     const float resv = p.res && (int)threadIdx.x < nrows ? p.res[row0 + (int)threadIdx.x] : 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
@@ -205,6 +225,8 @@ bool ao_shape(int hd, int n_head, int n_head_kv, int n_ctx, int type, int64_t K,
     sh.nsb = (int)(K / QK);
     if (sh.nsb > 16 || n_rows <= 0 || n_rows > (1 << 24)) return false;
     int n_rb = 256 / sh.nsb;
+    const int nrb_knob = (int)knob(KNOB_AO_NRB);  // A/B only
+    if (nrb_knob > 0) n_rb = nrb_knob;
     if (n_rb < 1) n_rb = 1;
     const int64_t max_rb = (n_rows + 15) / 16;
     if (n_rb > max_rb) n_rb = (int)max_rb;

@@ -304,7 +304,7 @@ bool multi_types_ok(int a, int b) { return a == b || (is_kquant(a) && is_kquant(
 // A decode attention whose output only the next node, a GEMV (the o-proj), reads: both
 // run as one kq_attn_oproj launch when its shape allows (bit-identical: kq_attn_oproj.hip).
 bool attn_oproj_fusable(const mi355x_backend *b, const mi355x_tensor *t, const mi355x_tensor *mm, int readers) {
-    if (!b->attn_oproj || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] != 1) return false;
+    if (!b->attn_oproj || kq::knob(kq::KNOB_ATTN_OPROJ) == 0 || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] != 1) return false;
     if (kq::attn_impl() != MI355X_ATTN_HEAD || !elidable(t, readers)) return false;
     if (!is_gemv_node(mm) || mm->src[1] != t || !is_kquant(mm->src[0]->type)) return false;
     const mi355x_tensor *w = mm->src[0];

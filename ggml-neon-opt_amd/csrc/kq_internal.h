@@ -123,6 +123,8 @@ enum Knob {
     KNOB_MMF_ORDER,        // kq_mmf tile order
     KNOB_ATTN_DIAG,        // timing stops of the KQ_ATTN_DIAG build
     KNOB_LOOPBACK_NOCOPY,  // emulated ALL_GATHERs skip their own-slice copy (timing only)
+    KNOB_ATTN_OPROJ,       // 0: no attention + o-proj fusion in any backend (A/B of kq_attn_oproj)
+    KNOB_AO_NRB,           // kq_attn_oproj row blocks (0: by shape)
     KNOB_COUNT
 };
 double knob(Knob k);
