@@ -597,7 +597,7 @@ const void *mmq_fn(int type, bool mixed, MmqShape sh) {
 // two superblock buffers: 64 * cw Q8L columns + rt weight rows (Q6_K: 224-B granule span),
 // +16 B for the Q6_K realign reads past the last row
 size_t mmq_lds(int type, MmqShape sh) {
-    return 2 * (size_t)(64 * sh.cw * Q8L_STRIDE + sh.rt * (type == Q6_K ? 224 : block_bytes(type))) + 16 + MMQ_PF_LDS;
+    return (size_t)mmq_nbuf(type, sh.rt, sh.cw) * (size_t)mmq_buf_bytes(type, sh.rt, sh.cw) + 16 + MMQ_PF_LDS;
 }
 
 int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride, const uint8_t *xq, int64_t M,
@@ -889,7 +889,8 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     a.y = a.my[0];
     a.y_col_stride = a.my_col_stride[0];
     const void *fn = mmq_fn(type, mixed, sh);
-    const size_t lds = mmq_lds(mixed ? Q6_K : type, sh);  // mixed: the larger (Q6_K) tile
+    size_t lds = mmq_lds(mixed ? Q6_K : type, sh);  // mixed: the largest tile of its bodies
+    if (mixed) lds = std::max(lds, std::max(mmq_lds(Q4_K, sh), mmq_lds(Q5_K, sh)));
     const dim3 grid((unsigned)((M + 64 * sh.cw - 1) / (64 * sh.cw)), (unsigned)tiles, 1);
     allow_lds(fn, lds);
     hipEvent_t e0, e1;

@@ -34,6 +34,11 @@ namespace kq {
 #ifndef KQ_ATTN_DIAG
 #define KQ_ATTN_DIAG 0
 #endif
+// Cells whose K row / V chunk is loaded with the position, before it is known (the rest,
+// up to the position, after it): 0 = every cell of the register path (TPH) / 8 V iterations.
+#ifndef KQ_ATTN_PFC
+#define KQ_ATTN_PFC 0
+#endif
 #if KQ_ATTN_DIAG
 #define ADIAG(a) ((a).diag)
 #else
@@ -56,7 +61,9 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     constexpr int KV4 = HD / 8;          // 16-B pieces of one K-cache row
     static_assert(TPH == 256 || (TPH == 128 && HD == 64), "threads per head");
     constexpr int ITEMS = HD * 4 / TPH;  // KQV (d, j) items per thread
-    constexpr int VPF = VPF0 > 0 ? VPF0 : 8 / ITEMS;  // prefetched 32-cell iterations per item
+    constexpr int VPF = VPF0 > 0 ? VPF0 : KQ_ATTN_PFC > 0 ? (KQ_ATTN_PFC / 32 < 8 / ITEMS ? KQ_ATTN_PFC / 32 : 8 / ITEMS)
+                                                         : 8 / ITEMS;  // prefetched 32-cell iterations per item
+    constexpr int KPF = KQ_ATTN_PFC > 0 && KQ_ATTN_PFC < TPH ? KQ_ATTN_PFC : TPH;  // K rows prefetched (thread t < KPF)
     const int gsz = a.n_head / a.n_head_kv;
     const int g = h / gsz;
     const int kvw = a.n_head_kv * HD;
@@ -81,7 +88,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         x0 = a.v[(int64_t)g * HD + (t - HD / 2)];
     }
     uint4 kpre[KV4] = {};
-    if (t < a.n_ctx && ADIAG(a) != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
+    if (t < a.n_ctx && t < KPF && ADIAG(a) != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
         const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)t * kvw + (int64_t)g * HD);
 #pragma unroll
         for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
@@ -145,6 +152,10 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             if (c == pos) {
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+            } else if (KPF < TPH && c >= KPF) {  // a cell past the prefetched ones (below the position)
+                const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+#pragma unroll
+                for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
             } else {
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
@@ -184,7 +195,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 if (c == pos) {
 #pragma unroll
                     for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
-                } else if (c == t) {
+                } else if (c == t && t < KPF) {
 #pragma unroll
                     for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
                 } else {

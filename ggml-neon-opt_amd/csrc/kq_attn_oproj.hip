@@ -11,10 +11,10 @@
 // from its records (chain_step, kq_device.h): the same operations in the same order.
 //
 // Decomposition (TinyLlama: 8 superblocks x 32 row blocks = 256 workgroups):
-//  * workgroup (s, rb), s = blockIdx % nsb: the attention of heads [s*HPS, s*HPS + HPS) on
-//    512 / HPS threads each (kq_attn_head.h; 512 threads per workgroup; workgroups b and b + 8 share an XCD, so the nsb/8
-//    superblocks of a KV group read its cells from one L2); only row block 0 stores the new
-//    KV cell. The head outputs stay in LDS, one wave quantizes them (quant16_store).
+//  * workgroup (s, rb): the attention of heads [s*HPS, s*HPS + HPS) on 512 / HPS threads each
+//    (kq_attn_head.h; 512 threads per workgroup); the nsb workgroups of row block rb run on one
+//    XCD (placement below); only row block 0 stores the new KV cell. The head outputs stay in
+//    LDS, one wave quantizes them (quant16_store).
 //  * its o-proj bytes (rows [rb*R, rb*R + R), superblock s) arrive by LDS-DMA issued at
 //    entry, under the attention; lane quad q computes one row's superblock (quad_q4K/5K/6K)
 //    and stores the 16-B record write-through (sc1) at recs[rb][row][s].
@@ -67,7 +67,18 @@ __global__ void __launch_bounds__(512) kq_attn_oproj(const AttnOprojArgs p) {
     constexpr int BSZ = block_bytes(TYPE);
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int nsb = p.nsb;
-    const int s = (int)blockIdx.x % nsb, rb = (int)blockIdx.x / nsb;
+    // XCD-aware placement (workgroup b runs on XCD b % 8): the nsb workgroups of a row block
+    // share one XCD, so its rows' weight lines (a superblock of 144-210 B straddles two 128-B
+    // lines, shared with the neighbouring superblocks) are fetched into ONE L2, not nsb of them
+    int s, rb;
+    if ((p.n_rb & 7) == 0) {
+        const int x = (int)blockIdx.x & 7, j = (int)blockIdx.x >> 3;
+        rb = x * (p.n_rb >> 3) + j / nsb;
+        s = j % nsb;
+    } else {
+        s = (int)blockIdx.x % nsb;
+        rb = (int)blockIdx.x / nsb;
+    }
     const int hi = (int)threadIdx.x / TPH, t = (int)threadIdx.x % TPH;
     const int lane = (int)threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
@@ -94,6 +105,9 @@ __global__ void __launch_bounds__(512) kq_attn_oproj(const AttnOprojArgs p) {
             dma16_nt(src + 16 * pc, (LDS void *)(wl + 1024 * j));
         }
     }
+
+    // the residual of the row this thread may replay, loaded long before the hand-off's drain
+    const float resv = p.res && (int)threadIdx.x < nrows ? p.res[row0 + (int)threadIdx.x] : 0.f;
 
     // ---- attention of head s*HPS + hi (threads [TPH hi, TPH hi + TPH)), output into act
     if (KQ_AO_DIAG & 1) {
@@ -151,7 +165,6 @@ __global__ void __launch_bounds__(512) kq_attn_oproj(const AttnOprojArgs p) {
         if (s == 0 && (int)threadIdx.x < nrows) p.y[row0 + (int)threadIdx.x] = p.res ? p.res[row0 + (int)threadIdx.x] : 0.f;
         return;
     }
-    const float resv = p.res && (int)threadIdx.x < nrows ? p.res[row0 + (int)threadIdx.x] : 0.f;
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {

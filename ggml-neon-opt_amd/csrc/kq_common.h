@@ -149,6 +149,21 @@ constexpr int ROWS_SB = 16;     // superblocks per step (4 lanes each)
 #endif
 constexpr int MMQ_PF_LDS = KQ_MMQ_PF ? 1024 : 0;  // its scratch: 256 B per wave
 constexpr int Q8L_STRIDE = 304; // LDS/workspace Q8_K block: d @0, qs @16, bsums @272 (16-B aligned)
+#ifndef KQ_MMQ_NBUF
+#define KQ_MMQ_NBUF 2  // kq_mmq superblock buffers in LDS (experiment: 3 on the one-workgroup-per-CU tiles)
+#endif
+// Superblock buffers of a kq_mmq tile (RT weight rows x 64*CW columns): KQ_MMQ_NBUF where the
+// tile already runs one workgroup per CU (128 x 64 at two waves per SIMD, 64 x 128) and the
+// buffers fit the CU's LDS; else 2.
+__host__ __device__ constexpr int mmq_buf_bytes(int type, int rt, int cw) {
+    return 64 * cw * Q8L_STRIDE + rt * (type == Q6_K ? 224 : block_bytes(type));
+}
+__host__ __device__ constexpr int mmq_nbuf(int type, int rt, int cw) {
+    return KQ_MMQ_NBUF >= 3 && ((rt == 128 && cw == 1) || (rt == 64 && cw == 2)) &&
+                   3 * mmq_buf_bytes(type, rt, cw) + 16 + MMQ_PF_LDS <= 160 * 1024
+               ? 3
+               : 2;
+}
 constexpr int ROWS_RECS = 64;   // chain records per wave per batch (soft cap)
 __host__ __device__ constexpr int rows_gran(int type) { return block_bytes(type) + 1; }
 __host__ __device__ constexpr int rows_slot(int type) { return 16 * rows_gran(type); }

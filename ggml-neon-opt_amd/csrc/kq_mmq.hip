@@ -240,6 +240,8 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     constexpr int NB_I = mmq_b_instr(TYPE, RT);
     constexpr int NW = (A_INSTR + NB_I + NWV - 1) / NWV;
     constexpr int BUF = A_BYTES + RT * mmq_row_bytes(TYPE);
+    constexpr int NBUF = mmq_nbuf(TYPE, RT, CW);
+    static_assert(BUF == mmq_buf_bytes(TYPE, RT, CW), "host and kernel agree on the buffer size");
     static_assert(!KQ_MMQ_PF || (RT == 64 && CW == 1), "the L2 warm-up assumes the 4-wave 64 x 64 tile");
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
@@ -251,7 +253,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
 
     // ---- DMA plan: the superblock's A_INSTR activation + NB_I weight instructions, NW per wave
     auto issue = [&](int b) {
-        uint8_t *buf = smem + (b & 1) * BUF;
+        uint8_t *buf = smem + (NBUF == 2 ? (b & 1) : b % NBUF) * BUF;
 #pragma unroll
         for (int s = 0; s < NW; ++s) {
             int t = wave + NWV * s;
@@ -283,7 +285,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             rw = rw < a.n_rows ? rw : a.n_rows - 1;
             const int off = part < 3 ? 64 * part : BSZ - 4;
             dma4((const void *)((uintptr_t)(a.w + (int64_t)rw * a.row_stride + (int64_t)bp * BSZ + off) & ~(uintptr_t)3),
-                 (LDS void *)(smem + 2 * BUF + 16 + 256 * wave));
+                 (LDS void *)(smem + NBUF * BUF + 16 + 256 * wave));
         }
     };
     constexpr int NWP = NW + (KQ_MMQ_PF ? 1 : 0);  // vm instructions per issue()
@@ -295,9 +297,17 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
         for (int i = 0; i < 16; ++i) sumf[ct][i] = 0.f;
 
     issue(0);
+    if (NBUF == 3 && nb > 1) issue(1);
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
-        if (KQ_MMQ_ONEBAR) {
+        if (NBUF == 3) {
+            // superblock b landed (b + 1's DMAs, younger, may be in flight); after the barrier
+            // every wave has finished reading b - 1's buffer, where b + 2 goes
+            if (b + 1 < nb) vm_wait<NWP>();
+            else vm_wait<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (b + 2 < nb) issue(b + 2);
+        } else if (KQ_MMQ_ONEBAR) {
             // superblock b (the only DMA in flight) landed; after the barrier every wave's part
             // of b is in LDS and every wave has finished reading b - 1's buffer (lgkmcnt(0)
             // before it), so b + 1 goes into that buffer while b is computed
@@ -312,7 +322,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             }
             asm volatile("s_barrier" ::: "memory");  // every wave's part of superblock b
         }
-        const uint8_t *buf = smem + (b & 1) * BUF;
+        const uint8_t *buf = smem + (NBUF == 2 ? (b & 1) : b % NBUF) * BUF;
         const uint8_t *At[CW];  // this lane's activation column of each tile
 #pragma unroll
         for (int ct = 0; ct < CW; ++ct) At[ct] = buf + (32 * CW * wm + 32 * ct + r) * Q8L_STRIDE;

@@ -281,9 +281,10 @@ int mi355x_gemv_waves(int waves);
  * interface). The library reads no environment variable; every knob holds its product
  * default until set here, process-wide: "GEMV_DIAG", "GEMV_RING", "GEMV_PRE0",
  * "GEMV_PF", "GEMV_XMODE", "GEMV_SMALL_MB", "GEMV_WPC", "GEMV_SMALL_WG", "GEMV_FQMAX",
- * "MMF_WAVES", "MMF_ORDER", "ATTN_DIAG", "LOOPBACK_NOCOPY" (csrc/kq_internal.h). None
- * changes numerics: the DIAG knobs act only in the diagnostic builds (make variant),
- * the others move launch shapes of bit-exact kernels, and LOOPBACK_NOCOPY (timing only)
+ * "MMF_WAVES", "MMF_ORDER", "ATTN_DIAG", "LOOPBACK_NOCOPY", "ATTN_OPROJ", "AO_NRB"
+ * (csrc/kq_internal.h). None changes numerics: the DIAG knobs act only in the diagnostic
+ * builds (make variant), the others move launch shapes of bit-exact kernels (ATTN_OPROJ 0:
+ * no attention + o-proj fusion in any backend), and LOOPBACK_NOCOPY (timing only)
  * leaves emulated all-gathers stale. value NaN restores the default; *previous (may be
  * NULL) receives the value in force before. 0, or MI355X_E_INVAL for an unknown name. */
 int mi355x_debug_knob(const char *name, double value, double *previous);

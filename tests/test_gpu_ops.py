@@ -129,7 +129,8 @@ def test_attn_decode_sequence(dev, O, attn_impl, hd, nh, nkv, n_ctx, rope_row):
     kc_ref = np.zeros((n_ctx, kvw), np.uint16)
     vc_ref = np.zeros((kvw, n_ctx), np.uint16)
     scale = float(np.float32(1.0) / np.sqrt(np.float32(hd)))
-    positions = list(range(0, 40)) + ([127, 128, 255, 256, 300] if n_ctx > 256 else []) + [n_ctx - 1]
+    positions = list(range(0, 40)) + ([63, 64, 65, 100] if n_ctx > 100 else []) + \
+        ([127, 128, 255, 256, 300] if n_ctx > 256 else []) + [n_ctx - 1]
     for p in positions:
         q = (rng.standard_normal(nh * hd) * 2).astype(np.float32)
         k = (rng.standard_normal(kvw) * 2).astype(np.float32)
