@@ -232,6 +232,9 @@ struct AoShape {
 bool ao_shape(int hd, int n_head, int n_head_kv, int n_ctx, int type, int64_t K, int64_t n_rows, AoShape &sh) {
     if (hd != 64 && hd != 128) return false;
     if (type != Q4_K && type != Q5_K && type != Q6_K) return false;
+    // every row block re-runs its superblock's heads: at long contexts that replicated
+    // KV-cache traffic outgrows the launch it saves (n_rb x the group's cells per head)
+    if (n_ctx > kAttnOprojMaxCtx) return false;
     sh.hps = 256 / hd;
     if (n_head_kv <= 0 || n_head % n_head_kv || (n_head / n_head_kv) % sh.hps) return false;  // a superblock's heads share one KV group
     if (K != (int64_t)n_head * hd || K % QK) return false;

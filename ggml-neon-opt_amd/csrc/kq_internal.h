@@ -100,6 +100,7 @@ size_t attn_group_bytes(const AttnArgs &a, int nwaves);  // its LDS
 // attn_oproj_buffer: bytes of the device buffer it needs (arrival counters, zeroed once,
 // then the records), 0 when the shape is not supported; *nsb: the superblocks of K.
 constexpr size_t kAttnOprojCounterBytes = 1024;
+constexpr int kAttnOprojMaxCtx = 256;  // kq_attn_oproj fuses caches of at most this many cells
 size_t attn_oproj_buffer(int hd, int n_head, int n_head_kv, int n_ctx, int type, int64_t K, int64_t n_rows, int *nsb);
 int launch_attn_oproj(const AttnArgs &a, int type, const void *w, int64_t n_rows, size_t row_stride, const float *res,
                       float *y, uint8_t *buf, size_t buf_size, hipStream_t stream);
