@@ -1148,8 +1148,7 @@ def main():
         local_bytes = chain.bytes_per_token  # weight bytes one GPU streams per token
         if isinstance(chain, Token):
             executor = ("LlamaDecoder -> mi355x_backend_graph_compute: node fusion (norm/swiglu GEMV prologues, "
-                        "residual/swiglu epilogues), kq_rows + kq_attn_oproj (attention, o-proj and residual in one "
-                        "launch where the shape allows; kq_attn_decode otherwise)" +
+                        "residual/swiglu epilogues), kq_rows + kq_attn_decode" +
                         ((", RCCL ncclAllReduce per K-split stage (row split, reduce)" if split_mode == "reduce" else
                           ", RCCL ncclAllGather per stage (row split)") if rowsplit else "") + ", " +
                         ("hipGraph replay" if not args.no_graph else "eager"))

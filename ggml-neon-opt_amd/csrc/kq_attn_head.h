@@ -37,7 +37,7 @@ namespace kq {
 // Cells whose K row / V chunk is loaded with the position, before it is known (the rest,
 // up to the position, after it): 0 = every cell of the register path (TPH) / 8 V iterations.
 #ifndef KQ_ATTN_PFC
-#define KQ_ATTN_PFC 0
+#define KQ_ATTN_PFC 64  // 0 (all of them) -> 64: TinyLlama token +2 %, tools/ab_ao.sh
 #endif
 #if KQ_ATTN_DIAG
 #define ADIAG(a) ((a).diag)

@@ -36,7 +36,8 @@ struct mi355x_backend {
     };
     std::vector<Captured> graphs;
     bool fuse = true;
-    bool attn_oproj = true;  // decode attention + o-proj GEMV in one launch (kq_attn_oproj.hip)
+    bool attn_oproj = false;  // decode attention + o-proj GEMV in one launch (kq_attn_oproj.hip): measured
+                              // slower than the two launches, so opt-in
     void *fx = nullptr;      // its arrival counters (zeroed at allocation) and records
     size_t fx_size = 0;
     int fx_nsb = 0;          // the superblock count the counters' rounds are aligned to
@@ -304,7 +305,8 @@ bool multi_types_ok(int a, int b) { return a == b || (is_kquant(a) && is_kquant(
 // A decode attention whose output only the next node, a GEMV (the o-proj), reads: both
 // run as one kq_attn_oproj launch when its shape allows (bit-identical: kq_attn_oproj.hip).
 bool attn_oproj_fusable(const mi355x_backend *b, const mi355x_tensor *t, const mi355x_tensor *mm, int readers) {
-    if (!b->attn_oproj || kq::knob(kq::KNOB_ATTN_OPROJ) == 0 || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] != 1) return false;
+    const int ko = (int)kq::knob(kq::KNOB_ATTN_OPROJ);  // A/B: 0 never, 2 every backend
+    if (ko == 0 || (ko == 1 && !b->attn_oproj) || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] != 1) return false;
     if (kq::attn_impl() != MI355X_ATTN_HEAD || !elidable(t, readers)) return false;
     if (!is_gemv_node(mm) || mm->src[1] != t || !is_kquant(mm->src[0]->type)) return false;
     const mi355x_tensor *w = mm->src[0];

@@ -124,7 +124,7 @@ enum Knob {
     KNOB_MMF_ORDER,        // kq_mmf tile order
     KNOB_ATTN_DIAG,        // timing stops of the KQ_ATTN_DIAG build
     KNOB_LOOPBACK_NOCOPY,  // emulated ALL_GATHERs skip their own-slice copy (timing only)
-    KNOB_ATTN_OPROJ,       // 0: no attention + o-proj fusion in any backend (A/B of kq_attn_oproj)
+    KNOB_ATTN_OPROJ,       // attention + o-proj fusion: 1 per backend (set_attn_oproj), 0 never, 2 always (A/B)
     KNOB_AO_NRB,           // kq_attn_oproj row blocks (0: by shape)
     KNOB_COUNT
 };

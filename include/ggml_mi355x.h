@@ -283,8 +283,8 @@ int mi355x_gemv_waves(int waves);
  * "GEMV_PF", "GEMV_XMODE", "GEMV_SMALL_MB", "GEMV_WPC", "GEMV_SMALL_WG", "GEMV_FQMAX",
  * "MMF_WAVES", "MMF_ORDER", "ATTN_DIAG", "LOOPBACK_NOCOPY", "ATTN_OPROJ", "AO_NRB"
  * (csrc/kq_internal.h). None changes numerics: the DIAG knobs act only in the diagnostic
- * builds (make variant), the others move launch shapes of bit-exact kernels (ATTN_OPROJ 0:
- * no attention + o-proj fusion in any backend), and LOOPBACK_NOCOPY (timing only)
+ * builds (make variant), the others move launch shapes of bit-exact kernels (ATTN_OPROJ: 1
+ * each backend's mi355x_backend_set_attn_oproj, 0 never, 2 in every backend), and LOOPBACK_NOCOPY (timing only)
  * leaves emulated all-gathers stale. value NaN restores the default; *previous (may be
  * NULL) receives the value in force before. 0, or MI355X_E_INVAL for an unknown name. */
 int mi355x_debug_knob(const char *name, double value, double *previous);
@@ -447,14 +447,16 @@ int mi355x_backend_supports_op(const mi355x_tensor *op); /* 1 / 0 */
  * kernel. Fused intermediates (not flagged OUTPUT, read by no other node) are not
  * written. Results are bit-identical with fusion off. Returns the previous value. */
 int mi355x_backend_set_fusion(mi355x_backend_t backend, int enable);
-/* Decode attention fused with the o-proj GEMV (default on, with fusion on): an ATTN_DECODE
+/* Decode attention fused with the o-proj GEMV (default OFF: bit-identical, but measured 6-10 %
+ * slower per token than the two launches; needs fusion on): an ATTN_DECODE
  * of one token whose output only the next node reads, a K-quant MUL_MAT (+ its residual
  * ADD), runs as ONE launch -- workgroup (s, rb) computes the heads of the o-proj's K
  * superblock s, quantizes them to that Q8_K superblock and writes the exact integer records
  * of rows block rb; the last workgroup of each row block replays every row's fp32 chain in
  * superblock order (csrc/kq_attn_oproj.hip). Bit-identical to the two launches. Applies with
  * the per-head attention kernel (mi355x_attn_impl ATTN_HEAD), head_dim 64 / 128, the heads
- * of one K superblock in one KV group and K <= 4096. Returns the previous value. */
+ * of one K superblock in one KV group, K <= 4096 and a KV cache of <= 256 cells. Returns
+ * the previous value. */
 int mi355x_backend_set_attn_oproj(mi355x_backend_t backend, int enable);
 /* Runs nodes in order on the backend stream. Consecutive MUL_MAT nodes with
  * ne11 == 1 that share src[1] are fused into one launch. When `use_graph` is

@@ -24,6 +24,7 @@ def _decoder(dev, hp, seed, n_ctx, mix="q4_k_m"):
     from ggml_mi355x.llama import LlamaDecoder
     w = LM.build(hp, seed, mix=mix)
     b = g.Backend()
+    assert b.set_attn_oproj(True) == 0  # opt-in (the product default is the two launches)
     dec = LlamaDecoder(b, hp, LM.to_device(w, dev), n_ctx, fuse=True)
     return w, b, dec
 

@@ -279,8 +279,8 @@ def test_llama_decode_tokens(dev, O, fuse, mix):
 
 
 def test_llama_fused_launch_count(dev):
-    """Fusion leaves 4 launches per layer (q/k/v, attention + o-proj + residual, gate/up,
-    down) + get_rows + the output GEMV; without the attention/o-proj fusion 5 per layer."""
+    """Fusion leaves 5 launches per layer (q/k/v, attention, o-proj + residual, gate/up,
+    down) + get_rows + the output GEMV; with the opt-in attention/o-proj fusion 4 per layer."""
     import ggml_mi355x as g
     from ggml_mi355x.llama import hparams
     hp = hparams(2048, 3, 32, 4, 5632, 1024)
@@ -291,13 +291,13 @@ def test_llama_fused_launch_count(dev):
     dec.step(6, 1, use_graph=False)
     rows = g.timing_read()
     g.timing_enable(False)
-    assert len(rows) == 4 * hp["n_layer"] + 2, [r[0] for r in rows]
-    assert b.set_attn_oproj(False) == 1
+    assert len(rows) == 5 * hp["n_layer"] + 2, [r[0] for r in rows]
+    assert b.set_attn_oproj(True) == 0
     g.timing_enable(True)
     dec.step(7, 2, use_graph=False)
     rows = g.timing_read()
     g.timing_enable(False)
-    assert len(rows) == 5 * hp["n_layer"] + 2, [r[0] for r in rows]
+    assert len(rows) == 4 * hp["n_layer"] + 2, [r[0] for r in rows]
     b.close()
 
 

@@ -1,6 +1,6 @@
 #!/bin/bash
 # Decode-token A/B on one box, interleaved ROUNDS times: the product, the attention + o-proj
-# fusion off (knob ATTN_OPROJ=0), row-block counts (knob AO_NRB), the timing ablations of
+# fusion forced on (knob ATTN_OPROJ=2; the product leaves it off), row-block counts (knob AO_NRB), the timing ablations of
 # `make variant-ao` (lib/variants/libaoN.so: 1 no attention, 2 stop after the attention,
 # 4 no hand-off, 8 no weight DMA) and other variant builds.
 #   usage (GPU box): bash tools/ab_ao.sh [CONFIG...]
@@ -10,8 +10,8 @@ cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 V=$PWD/ggml-neon-opt_amd/lib/variants
 CFGS=("$@")
-[ ${#CFGS[@]} -eq 0 ] && CFGS=(tiny 8b tiny,knob:ATTN_OPROJ=0 8b,knob:ATTN_OPROJ=0 tiny,knob:AO_NRB=16 tiny,lib:ao1
-                              tiny,lib:ao2 tiny,lib:ao4 tiny,lib:ao8)
+[ ${#CFGS[@]} -eq 0 ] && CFGS=(tiny 8b tiny,knob:ATTN_OPROJ=2 8b,knob:ATTN_OPROJ=2 tiny,knob:ATTN_OPROJ=2,knob:AO_NRB=16 tiny,lib:ao1,knob:ATTN_OPROJ=2
+                              tiny,lib:ao2,knob:ATTN_OPROJ=2 tiny,lib:ao4,knob:ATTN_OPROJ=2 tiny,lib:ao8,knob:ATTN_OPROJ=2)
 OUT=gpurun_out/ab_ao.log
 : > $OUT
 for r in $(seq 1 ${ROUNDS:-2}); do
