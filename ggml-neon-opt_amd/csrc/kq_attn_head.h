@@ -39,6 +39,20 @@ namespace kq {
 #ifndef KQ_ATTN_PFC
 #define KQ_ATTN_PFC 64  // 0 (all of them) -> 64: TinyLlama token +2 %, tools/ab_ao.sh
 #endif
+// a diagnostic stop's output: depends on every value it keeps live, always a float in [1, 2)
+// (garbage bits would send the next GEMV's rms_norm and soft_max down their slow paths)
+__device__ __forceinline__ float adiag_finite(uint32_t bits) { return __uint_as_float((bits & 0x007fffffu) | 0x3f800000u); }
+// Experiment build (KQ_ATTN_EARLY=1): the cells past the prefetched ones, up to the position,
+// requested as soon as the position is known (before rope, KQ and soft_max) instead of where
+// they are used: K rows up to the register path's TPH cells, V chunks of KQ_ATTN_VPOST more
+// 32-cell iterations. Measured neutral to -1 % on the TinyLlama / 8B tokens
+// (profiles/r04_attn_ab.txt), so off.
+#ifndef KQ_ATTN_EARLY
+#define KQ_ATTN_EARLY 0
+#endif
+#ifndef KQ_ATTN_VPOST
+#define KQ_ATTN_VPOST 2
+#endif
 #if KQ_ATTN_DIAG
 #define ADIAG(a) ((a).diag)
 #else
@@ -107,6 +121,25 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     const int pos = bad ? 0 : pos_in;
     int n_kv = (pos + 1 + 31) / 32 * 32;
     n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
+    constexpr int VPOST = KQ_ATTN_EARLY ? KQ_ATTN_VPOST : 0;
+    uint4 vpost[ITEMS][VPOST > 0 ? VPOST : 1] = {};
+    if (KQ_ATTN_EARLY && ADIAG(a) != 5) {
+        if (KPF < TPH && t >= KPF && t < pos && t < a.n_ctx) {  // this thread's K row, c = t < pos
+            const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)t * kvw + (int64_t)g * HD);
+#pragma unroll
+            for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
+        }
+#pragma unroll
+        for (int ii = 0; ii < ITEMS; ++ii) {
+            const int item = t + TPH * ii, d = item >> 2, j = item & 3;
+            const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx + 8 * j;
+#pragma unroll
+            for (int k = 0; k < VPOST; ++k) {
+                const int it = VPF + k;
+                if (32 * it <= pos) vpost[ii][k] = *(const uint4 *)(vr + 32 * it);  // (32 it <= pos < n_ctx)
+            }
+        }
+    }
     // LDS (attn_lds): q16 | k16 | v16 (HD f16 each) | w (n_ctx f32) | p16 (n_ctx f16) |
     // red (HD*32 f16 accumulators) | scal (max, 1/sum, 2 pad) [| gsum]; every piece 16-B aligned
     uint16_t *q16 = (uint16_t *)smem;
@@ -140,7 +173,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     }
     __syncthreads();
     if (ADIAG(a) == 1 || ADIAG(a) == 5) {  // diagnostics: stop after the loads and rope
-        if (t < HD) out[t] = x0 + __uint_as_float(kpre[0].x ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
+        if (t < HD) out[t] = adiag_finite(__float_as_uint(x0) ^ kpre[0].x ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
         return;
     }
 
@@ -152,11 +185,11 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             if (c == pos) {
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
-            } else if (KPF < TPH && c >= KPF) {  // a cell past the prefetched ones (below the position)
+            } else if (!KQ_ATTN_EARLY && KPF < TPH && c >= KPF) {  // a cell past the prefetched ones (below the position)
                 const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
-            } else {
+            } else {  // prefetched with the position, or (KQ_ATTN_EARLY) right after it
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
             }
@@ -166,7 +199,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         if ((t & 63) == 0) scal[t >> 6] = wmx;
         __syncthreads();
         if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
-            if (t < HD) out[t] = sc + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            if (t < HD) out[t] = adiag_finite(__float_as_uint(sc) ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
         const float mx = TPH == 256 ? fmaxf(fmaxf(scal[0], scal[1]), fmaxf(scal[2], scal[3])) : fmaxf(scal[0], scal[1]);
@@ -183,7 +216,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         if (c < n_kv) p16[c] = h2u(f2h_rne(ec * inv));
         __syncthreads();
         if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
-            if (t < HD) out[t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            if (t < HD) out[t] = adiag_finite((uint32_t)p16[t] ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
     } else {
@@ -195,7 +228,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 if (c == pos) {
 #pragma unroll
                     for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
-                } else if (c == t && t < KPF) {
+                } else if (c == t && (KQ_ATTN_EARLY || t < KPF)) {
 #pragma unroll
                     for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
                 } else {
@@ -209,7 +242,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         }
         __syncthreads();
         if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
-            if (t < HD) out[t] = w[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            if (t < HD) out[t] = adiag_finite(__float_as_uint(w[t]) ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
         // max (order-free), then exp + group sums
@@ -244,7 +277,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         for (int c = t; c < n_kv; c += TPH) p16[c] = h2u(f2h_rne(w[c] * inv));
         __syncthreads();
         if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
-            if (t < HD) out[t] = (float)p16[t] + __uint_as_float(vpre[0][0].x ^ vpre[0][VPF - 1].y);
+            if (t < HD) out[t] = adiag_finite((uint32_t)p16[t] ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
 
@@ -265,6 +298,10 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
 #pragma unroll
                 for (int k = 0; k < VPF; ++k)
                     if (k == it) vv = vpre[ii][k];
+            } else if (VPOST > 0 && it < VPF + VPOST) {
+#pragma unroll
+                for (int k = 0; k < (VPOST > 0 ? VPOST : 1); ++k)
+                    if (k == it - VPF) vv = vpost[ii][k];
             } else {
                 vv = *(const uint4 *)(vr + c0);
             }
