@@ -159,7 +159,7 @@ __host__ __device__ constexpr int mmq_buf_bytes(int type, int rt, int cw) {
     return 64 * cw * Q8L_STRIDE + rt * (type == Q6_K ? 224 : block_bytes(type));
 }
 __host__ __device__ constexpr int mmq_nbuf(int type, int rt, int cw) {
-    return KQ_MMQ_NBUF >= 3 && ((rt == 128 && cw == 1) || (rt == 64 && cw == 2)) &&
+    return KQ_MMQ_NBUF == 1 ? 1 : KQ_MMQ_NBUF >= 3 && ((rt == 128 && cw == 1) || (rt == 64 && cw == 2)) &&
                    3 * mmq_buf_bytes(type, rt, cw) + 16 + MMQ_PF_LDS <= 160 * 1024
                ? 3
                : 2;

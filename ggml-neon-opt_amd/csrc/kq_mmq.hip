@@ -296,11 +296,17 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sumf[ct][i] = 0.f;
 
-    issue(0);
+    if (NBUF > 1) issue(0);
     if (NBUF == 3 && nb > 1) issue(1);
 #pragma unroll 1
     for (int b = 0; b < nb; ++b) {
-        if (NBUF == 3) {
+        if (NBUF == 1) {
+            // one buffer (experiment: occupancy instead of double buffering): every wave
+            // finished reading b - 1 at the trailing barrier of the previous iteration
+            issue(b);
+            vm_wait<0>();
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        } else if (NBUF == 3) {
             // superblock b landed (b + 1's DMAs, younger, may be in flight); after the barrier
             // every wave has finished reading b - 1's buffer, where b + 2 goes
             if (b + 1 < nb) vm_wait<NWP>();
@@ -338,7 +344,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
 #pragma unroll
                 for (int i = 0; i < 16; ++i) yd[16 * ct + i] = yd_of(ct, i);
             q6_superblock<CW>(a, Bt, At, yd, row0 + 32 * wn + r, b, h, sumf);
-            if (!KQ_MMQ_ONEBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            if (!KQ_MMQ_ONEBAR || NBUF == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
             continue;
         }
         const u32x4 hdr = *(const u32x4 *)Bt;
@@ -492,7 +498,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                 }
             }
         }
-        if (!KQ_MMQ_ONEBAR) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer b&1 free for b+2
+        if (!KQ_MMQ_ONEBAR || NBUF == 1) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // buffer b&1 free for b+2
     }
 
     // ---- store: lane's weight row n, 16 activation columns per tile
