@@ -24,7 +24,8 @@
 //    (sc1 loads, EVERY load of them), adds the residual and stores y. No workgroup waits for
 //    another: nothing can deadlock, and placement only changes speed.
 // Counters are never reset: the round of row block rb is old / nsb, the last arriver the one
-// that draws old % nsb == nsb - 1 (zeroed once when the backend allocates them).
+// that draws old % nsb == nsb - 1 (zeroed once when the backend allocates them; nsb a power
+// of two, so the rounds stay aligned when a counter wraps).
 #include <string.h>
 
 #include <hip/hip_ext.h>
@@ -240,6 +241,9 @@ bool ao_shape(int hd, int n_head, int n_head_kv, int n_ctx, int type, int64_t K,
     if (K != (int64_t)n_head * hd || K % QK) return false;
     sh.nsb = (int)(K / QK);
     if (sh.nsb > 16 || n_rows <= 0 || n_rows > (1 << 24)) return false;
+    // the arrival counters are never reset and wrap at 2^32: rounds of nsb arrivals stay
+    // aligned across the wrap only when nsb divides 2^32
+    if (sh.nsb & (sh.nsb - 1)) return false;
     int n_rb = 256 / sh.nsb;
     const int nrb_knob = (int)knob(KNOB_AO_NRB);  // A/B only
     if (nrb_knob > 0) n_rb = nrb_knob;
