@@ -61,6 +61,9 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #ifndef KQ_MMQ_ONEBAR
 #define KQ_MMQ_ONEBAR 1
 #endif
+#ifndef KQ_MMQ_PKCHAIN
+#define KQ_MMQ_PKCHAIN 0  // experiment build: the Q4_K fp32 chain on packed f32 (v_pk_mul / v_pk_fma)
+#endif
 #ifndef KQ_MMQ_Q5_VALU
 #define KQ_MMQ_Q5_VALU 0  // experiment build: Q5_K sub-block scales on VALU (the round-2 kernel)
 #endif
@@ -484,6 +487,24 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             const f16x8 am = *(const f16x8 *)(At[ct] + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
             const f32x16 zero = {};
             const f32x16 mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
+            if (KQ_MMQ_PKCHAIN && TYPE == Q4_K && !(KQ_MMQ_DIAG & 1)) {
+                // two elements per packed f32 instruction (each lane an IEEE mul / fma: the
+                // scalar chain's bits)
+                typedef float f32x2 __attribute__((ext_vector_type(2)));
+                const f32x2 nxdm2 = {nxdm, nxdm}, xd2 = {xd, xd};
+#pragma unroll
+                for (int i = 0; i < 16; i += 2) {
+                    const f32x2 y2 = {yd_of(ct, i), yd_of(ct, i + 1)};
+                    const f32x2 m2 = {mins[i], mins[i + 1]};
+                    const f32x2 s2 = {(float)sumi[ct][i], (float)sumi[ct][i + 1]};
+                    f32x2 acc = {sumf[ct][i], sumf[ct][i + 1]};
+                    acc = __builtin_elementwise_fma(m2, y2 * nxdm2, acc);
+                    acc = __builtin_elementwise_fma(s2, y2 * xd2, acc);
+                    sumf[ct][i] = acc.x;
+                    sumf[ct][i + 1] = acc.y;
+                }
+                continue;
+            }
 #pragma unroll
             for (int i = 0; i < 16; ++i) {
                 const float y = yd_of(ct, i);
