@@ -62,7 +62,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #define KQ_MMQ_ONEBAR 1
 #endif
 #ifndef KQ_MMQ_PKCHAIN
-#define KQ_MMQ_PKCHAIN 0  // experiment build: the Q4_K fp32 chain on packed f32 (v_pk_mul / v_pk_fma)
+#define KQ_MMQ_PKCHAIN 0  // experiment build: the fp32 chain on packed f32 (bits: 1 Q4_K, 2 Q5_K, 4 Q6_K)
 #endif
 #ifndef KQ_MMQ_Q5_VALU
 #define KQ_MMQ_Q5_VALU 0  // experiment build: Q5_K sub-block scales on VALU (the round-2 kernel)
@@ -190,6 +190,22 @@ __device__ __forceinline__ void q6_superblock(const MmqArgs &a, const uint8_t *B
         }
     }
     const float xd = h2f(dh);
+    if (KQ_MMQ_PKCHAIN & 4) {  // experiment build: two elements per packed f32 instruction
+        typedef float f32x2 __attribute__((ext_vector_type(2)));
+        const f32x2 xd2 = {xd, xd};
+#pragma unroll
+        for (int ct = 0; ct < CW; ++ct)
+#pragma unroll
+            for (int i = 0; i < 16; i += 2) {
+                const f32x2 y2 = {yd[16 * ct + i], yd[16 * ct + i + 1]};
+                const f32x2 s2 = {(float)(256 * shi[ct][i] + slo[ct][i]), (float)(256 * shi[ct][i + 1] + slo[ct][i + 1])};
+                f32x2 acc = {sumf[ct][i], sumf[ct][i + 1]};
+                acc = __builtin_elementwise_fma(xd2 * y2, s2, acc);
+                sumf[ct][i] = acc.x;
+                sumf[ct][i + 1] = acc.y;
+            }
+        return;
+    }
 #pragma unroll
     for (int ct = 0; ct < CW; ++ct)
 #pragma unroll
@@ -487,7 +503,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             const f16x8 am = *(const f16x8 *)(At[ct] + 272 + 16 * h);  // [lo | hi] of bs_j (Q8L/mmq)
             const f32x16 zero = {};
             const f32x16 mins = (KQ_MMQ_DIAG & 8) ? zero : __builtin_amdgcn_mfma_f32_32x32x16_f16(am, bm, zero, 0, 0, 0);
-            if (KQ_MMQ_PKCHAIN && TYPE == Q4_K && !(KQ_MMQ_DIAG & 1)) {
+            if ((KQ_MMQ_PKCHAIN & 1) && TYPE == Q4_K && !(KQ_MMQ_DIAG & 1)) {
                 // two elements per packed f32 instruction (each lane an IEEE mul / fma: the
                 // scalar chain's bits)
                 typedef float f32x2 __attribute__((ext_vector_type(2)));
@@ -500,6 +516,22 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
                     f32x2 acc = {sumf[ct][i], sumf[ct][i + 1]};
                     acc = __builtin_elementwise_fma(m2, y2 * nxdm2, acc);
                     acc = __builtin_elementwise_fma(s2, y2 * xd2, acc);
+                    sumf[ct][i] = acc.x;
+                    sumf[ct][i + 1] = acc.y;
+                }
+                continue;
+            }
+            if ((KQ_MMQ_PKCHAIN & 2) && TYPE == Q5_K && !(KQ_MMQ_DIAG & 1)) {
+                typedef float f32x2 __attribute__((ext_vector_type(2)));
+                const f32x2 xd2 = {xd, xd}, xdm2 = {xdm, xdm};
+#pragma unroll
+                for (int i = 0; i < 16; i += 2) {
+                    const f32x2 y2 = {yd_of(ct, i), yd_of(ct, i + 1)};
+                    const f32x2 m2 = {mins[i], mins[i + 1]};
+                    const f32x2 s2 = {(float)sumi[ct][i], (float)sumi[ct][i + 1]};
+                    const f32x2 t = __builtin_elementwise_fma(y2 * xd2, s2, -((y2 * xdm2) * m2));
+                    f32x2 acc = {sumf[ct][i], sumf[ct][i + 1]};
+                    acc = acc + t;
                     sumf[ct][i] = acc.x;
                     sumf[ct][i + 1] = acc.y;
                 }
