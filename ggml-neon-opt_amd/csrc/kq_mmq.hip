@@ -62,7 +62,10 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 #define KQ_MMQ_ONEBAR 1
 #endif
 #ifndef KQ_MMQ_PKCHAIN
-#define KQ_MMQ_PKCHAIN 0  // experiment build: the fp32 chain on packed f32 (bits: 1 Q4_K, 2 Q5_K, 4 Q6_K)
+// The fp32 chain on packed f32 (v_pk_mul_f32 / v_pk_fma_f32, two elements per instruction,
+// each lane an IEEE op: the same bits). Bits: 1 Q4_K (product: 8B ffn_down 3-8 % faster, the
+// rest equal), 2 Q5_K, 4 Q6_K (no gain; experiment builds), profiles/r04_mmq_pkchain_ab.txt.
+#define KQ_MMQ_PKCHAIN 1
 #endif
 #ifndef KQ_MMQ_Q5_VALU
 #define KQ_MMQ_Q5_VALU 0  // experiment build: Q5_K sub-block scales on VALU (the round-2 kernel)
