@@ -4,6 +4,9 @@ Cache (MALL)? Times kq_rows on the TinyLlama shapes three ways:
   hot       the same buffer every call (MALL/L2 resident upper bound)
   prefetch  rotated, but a plain read of the buffer (torch sum) runs just before
             the GEMV, as a side-stream prefetcher would leave it
+  cold_fx / hot_fx  as cold / hot, but the activation is rewritten by another kernel just
+            before each GEMV (as in the token: x is the previous launch's output), so only
+            the weights' residency differs between the two
 Only the GEMV launches are timed (library launch-timing hook)."""
 import os
 import sys
@@ -32,13 +35,15 @@ def main(reps=30):
         y = torch.empty(1, N, device=dev)
         sink = torch.zeros(1, dtype=torch.int64, device=dev)
         res = {}
-        for mode in ("cold", "hot", "prefetch"):
+        for mode in ("cold", "hot", "prefetch", "cold_fx", "hot_fx"):
             for w in ws[:4]:
                 g.mul_mat(typ, w, K, x, out=y)
             torch.cuda.synchronize()
             g.timing_enable(True)
             for r in range(reps):
-                w = ws[0] if mode == "hot" else ws[r % nbuf]
+                w = ws[0] if mode.startswith("hot") else ws[r % nbuf]
+                if mode.endswith("_fx"):
+                    x.mul_(1.0)  # the activation freshly written by another kernel
                 if mode == "prefetch":
                     sink += w.view(torch.int32).sum(dtype=torch.int64)
                 g.mul_mat(typ, w, K, x, out=y)
