@@ -67,7 +67,19 @@
 #define KQ_ROWS_LINT_BREAK 0  // 1: drop the activation wait (a lint self-test build, never run)
 #endif
 
+// Experiment build (KQ_ROWS_YSC1=1): the GEMV's outputs (and the SWIGLU epilogue's) stored
+// write-through (sc1), so the next launch's activation is in memory-side caches before the
+// kernel boundary (tools/xfresh.hip: the consumer's fresh-read price 0.15 -> 0.03 us).
+#ifndef KQ_ROWS_YSC1
+#define KQ_ROWS_YSC1 0
+#endif
+
 namespace kq {
+
+__device__ __forceinline__ void store_y(float *p, float v) {
+    if (KQ_ROWS_YSC1) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+    else *p = v;
+}
 
 // Q8L quantization of whole rows (K > 8192 path): 16 superblocks per workgroup.
 // AM: the prefill GEMMs' layout (quant16_store<true>: the mins operand in place of bsums).
@@ -533,10 +545,10 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             asm volatile("" : "+v"(rv));
             for (int k = 0; k < ww.nrows; k += 64)
                 if (k + lane < ww.nrows)
-                    y[k + lane] = outs[k + lane] + (k == 0 ? __uint_as_float(rv) : res_p[ww.r0 + k + lane]);
+                    store_y(y + k + lane, outs[k + lane] + (k == 0 ? __uint_as_float(rv) : res_p[ww.r0 + k + lane]));
         } else {
             for (int k = 0; k < ww.nrows; k += 64)
-                if (k + lane < ww.nrows) y[k + lane] = outs[k + lane];
+                if (k + lane < ww.nrows) store_y(y + k + lane, outs[k + lane]);
         }
     }
     // ---- SWIGLU epilogue (the GLU node after the gate/up MUL_MATs): up wave and its
@@ -551,7 +563,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
                 if (k + lane < ww.nrows) {
                     const int r = ww.r0 + k + lane;
                     const float gv = gouts[k + lane], uv = outs[k + lane];
-                    a.epi_y[r] = r < n4 ? v_silu(gv) * uv : (gv / (1.0f + expf(-gv))) * uv;
+                    store_y(a.epi_y + r, r < n4 ? v_silu(gv) * uv : (gv / (1.0f + expf(-gv))) * uv);
                 }
         }
     }
