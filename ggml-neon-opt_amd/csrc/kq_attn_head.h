@@ -68,7 +68,9 @@ __device__ __forceinline__ float adiag_finite(uint32_t bits) { return __uint_as_
 // workgroup and 256 threads each would cap it at 128 VGPRs): the register path holds one
 // cell per thread (n_kv <= TPH), KQV runs HD * 4 / TPH (d, j) items per thread.
 // VPF0: V-cache iterations (32 cells each) prefetched with the position (0: 8 / ITEMS).
-template <int HD, int TPH = 256, int VPF0 = 0>
+// OUT_WT: out is global memory, stored write-through (sc1) for the next launch (kq_rows'
+// outputs likewise, KQ_ROWS_YSC1).
+template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false>
 __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8_t *smem, float *out,
                                           bool may_write) {
     static_assert(HD == 64 || HD == 128, "head_dim");
@@ -316,7 +318,11 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             for (int k = 0; k < 4; ++k) acc[k] = pk_fma_w(vw[k], pw[k], acc[k]);
         }
         const float o = f16x8_reduce_quad(acc);  // accumulators j = 0..3 of output d: one quad of lanes
-        if (j == 0) out[d] = bad ? __builtin_nanf("") : o;
+        if (j == 0) {
+            const float ov = bad ? __builtin_nanf("") : o;
+            if (OUT_WT) asm volatile("global_store_dword %0, %1, off sc1" ::"v"(out + d), "v"(ov) : "memory");
+            else out[d] = ov;
+        }
     }
 }
 

@@ -32,6 +32,10 @@
 #include "kq_ops_device.h"
 #include "kq_rows_device.h"
 
+#ifndef KQ_ATTN_OSC1
+#define KQ_ATTN_OSC1 0  // experiment build: the decode attention's output stored write-through (sc1)
+#endif
+
 namespace kq {
 
 // ------------------------------------------------------------ get_rows
@@ -202,7 +206,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     // the L2 of 8*gsz/n_head XCDs (TinyLlama: 2, Llama-3: 1) instead of all 8.
     int h = blockIdx.x;
     if ((a.n_head & 7) == 0) h = (h & 7) * (a.n_head >> 3) + (h >> 3);
-    attn_head<HD>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true);
+    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true);
 }
 
 // One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read

@@ -67,11 +67,11 @@
 #define KQ_ROWS_LINT_BREAK 0  // 1: drop the activation wait (a lint self-test build, never run)
 #endif
 
-// Experiment build (KQ_ROWS_YSC1=1): the GEMV's outputs (and the SWIGLU epilogue's) stored
-// write-through (sc1), so the next launch's activation is in memory-side caches before the
-// kernel boundary (tools/xfresh.hip: the consumer's fresh-read price 0.15 -> 0.03 us).
+// The GEMV's outputs (and the SWIGLU epilogue's) are stored write-through (sc1), so the next
+// launch's activation is in the memory-side caches before the kernel boundary
+// (tools/xfresh.hip: the consumer's fresh-read price 0.15 -> 0.03 us per edge).
 #ifndef KQ_ROWS_YSC1
-#define KQ_ROWS_YSC1 0
+#define KQ_ROWS_YSC1 1  // TinyLlama token +0.5-1.4 %, Llama-3-8B +0.7 % (profiles/r04_store_flavour_ab.txt)
 #endif
 
 namespace kq {
