@@ -5,12 +5,12 @@
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 export TMPDIR=/tmp
-OUT=gpurun_out/prof_decode_pmc
+OUT=gpurun_out/prof_decode_pmc${TAG:+_$TAG}
 mkdir -p $OUT
 timeout -s KILL 200 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_INSTS_VALU SQ_INSTS_LDS \
     SQ_INSTS_VMEM SQ_WAVES --output-format csv -d $OUT/pmc -o run -- \
     python3 bench.py --steps 16 --warmup 2 --no-graph --no-cpu-baseline --no-large --no-prefill --no-chain --no-8b --no-70b \
-    --tg 0 --no-collectives > $OUT/bench.log 2>&1 || exit $?
+    --tg 0 --no-collectives ${KNOBS:-} > $OUT/bench.log 2>&1 || exit $?
 python3 - $OUT/pmc/run_counter_collection.csv <<'PY'
 import collections, csv, sys
 agg = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.Counter()
@@ -27,3 +27,4 @@ for name, c in sorted(agg.items(), key=lambda kv: -kv[1]["SQ_WAVE_CYCLES"]):
     print(f"| `{name}` | {n[name]} | {w / max(n[name], 1):.0f} | {100 * c['SQ_WAIT_ANY'] / wc:.0f} % | {100 * c['SQ_WAIT_INST_ANY'] / wc:.0f} % | "
           f"{100 * c['SQ_ACTIVE_INST_ANY'] / wc:.0f} % | {c['SQ_INSTS_VALU'] / w:.0f} / {c['SQ_INSTS_LDS'] / w:.0f} / {c['SQ_INSTS_VMEM'] / w:.0f} |")
 PY
+rm -f $OUT/pmc/run_counter_collection.csv
