@@ -695,25 +695,48 @@ def spawn_ranks(n):
         time.sleep(0.2)
 
 
-def tg_side(tk, steps, barrier):
+def spread(ms):
+    """p10 / p50 / p90 (nearest rank) of per-step milliseconds, plus mean and sd."""
+    v = sorted(ms)
+    if not v:
+        return None
+    def pct(q):
+        return round(v[min(len(v) - 1, max(0, int(round(q * (len(v) - 1)))))], 4)
+    mean = sum(v) / len(v)
+    sd = (sum((x - mean) ** 2 for x in v) / (len(v) - 1)) ** 0.5 if len(v) > 1 else 0.0
+    return {"p10": pct(0.10), "p50": pct(0.50), "p90": pct(0.90), "mean": round(mean, 4), "sd": round(sd, 4),
+            "n": len(v)}
+
+
+def tg_side(tk, steps, barrier, reps=5):
     """llama-bench's tg128 on the same decoder: `steps` tokens from an empty KV cache
-    (positions 0 .. steps-1), hipGraph replay, whatever --steps the headline used.
-    Every rank runs it (the row split's gathers are collective)."""
-    tk.dec.reset()
-    torch.cuda.synchronize()
+    (positions 0 .. steps-1), hipGraph replay, whatever --steps the headline used; run
+    `reps` times, reported as llama-bench does (tok/s mean +- sd over the repetitions,
+    README.md:192-193) beside the first run's figures. Every rank runs it (the row split's
+    gathers are collective)."""
     st = torch.cuda.ExternalStream(tk.dec.b.stream)
-    barrier()
-    t0 = time.perf_counter()
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record(st)
-    for i in range(steps):
-        tk.dec.step(tk.tokens[i], i)
-    e1.record(st)
-    tk.dec.b.synchronize()
-    barrier()
-    el = time.perf_counter() - t0
+    runs = []
+    for r in range(reps):
+        tk.dec.reset()
+        torch.cuda.synchronize()
+        barrier()
+        t0 = time.perf_counter()
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record(st)
+        for i in range(steps):
+            tk.dec.step(tk.tokens[i], i)
+        e1.record(st)
+        tk.dec.b.synchronize()
+        barrier()
+        el = time.perf_counter() - t0
+        runs.append((el, e0.elapsed_time(e1)))
+    el, gms = runs[0]
+    rates = [steps / e for e, _ in runs]
+    mean = sum(rates) / len(rates)
+    sd = (sum((x - mean) ** 2 for x in rates) / (len(rates) - 1)) ** 0.5 if len(rates) > 1 else 0.0
     return {"tokens": steps, "tok_s": round(steps / el, 1), "ms_per_token": round(el / steps * 1e3, 4),
-            "gpu_ms_per_token": round(e0.elapsed_time(e1) / steps, 4)}
+            "gpu_ms_per_token": round(gms / steps, 4),
+            "reps": reps, "tok_s_mean": round(mean, 1), "tok_s_sd": round(sd, 1)}
 
 
 def connect(be, world, rank):
@@ -1034,16 +1057,21 @@ def main():
     barrier()
     torch.cuda.synchronize()
     ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    # one event after every step on the launch stream (a marker packet between two graph
+    # launches): the per-step spread p10/p50/p90 of the same timed steps
+    evs = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps)]
     t0 = time.perf_counter()
     ev0.record(stream)
-    for _ in range(args.steps):
+    for i in range(args.steps):
         step()
+        evs[i].record(stream)
     ev1.record(stream)
     torch.cuda.synchronize()
     be.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
     gpu_ms = ev0.elapsed_time(ev1)
+    step_ms = [(evs[i - 1] if i else ev0).elapsed_time(evs[i]) for i in range(args.steps)]
     t_max = elapsed
     if world > 1:
         import torch.distributed as dist
@@ -1176,6 +1204,7 @@ def main():
                        "parallelism": head["parallelism"],
                        "hipgraph": not args.no_graph},
             "gpu_ms_per_step": round(gpu_ms / args.steps, 4),
+            "step_ms": spread(step_ms),
             "effective_GBps": round(per_gpu_rate * local_bytes / 1e9, 1),
             # the whole token (every launch, gap and gather included) against the HBM roofline, per GPU
             "token_hbm_frac": round(per_gpu_rate * local_bytes / 1e9 / HBM_PEAK_GBS, 4),

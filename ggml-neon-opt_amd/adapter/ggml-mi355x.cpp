@@ -379,6 +379,37 @@ void shape_of(const ggml_tensor *t, mi355x_tensor &m) {
     }
 }
 
+// Through views / reshapes / permutes / transposes to the tensor that owns the bytes, or
+// to the op that computed them.
+const ggml_tensor *alias_root(const ggml_tensor *t) {
+    for (int hop = 0; t && hop < 64; ++hop) {
+        if (t->view_src) {
+            t = t->view_src;
+            continue;
+        }
+        if ((is_op(t, "RESHAPE") || is_op(t, "PERMUTE") || is_op(t, "TRANSPOSE") || is_op(t, "VIEW")) && t->src[0]) {
+            t = t->src[0];
+            continue;
+        }
+        break;
+    }
+    return t;
+}
+
+// The f16 MUL_MATs the lowering takes are the non-flash attention's KQ and KQV only
+// (kq_lower.cpp attention()): src0 a view from cell 0 of an f16 KV-cache leaf, src1 the
+// rope'd query (KQ) or the soft_max output (KQV). Any other f16 MUL_MAT (an f16 lm_head,
+// a tied embedding) stays with the CPU backend: claiming it would fail graph_compute.
+bool attn_f16_mul_mat(const ggml_tensor *op) {
+    const ggml_tensor *a = op->src[0], *b = op->src[1];
+    if (!a || !b || a->type != GGML_TYPE_F16 || b->type != GGML_TYPE_F32) return false;
+    if (!a->view_src || a->view_offs != 0) return false;
+    const ggml_tensor *cache = alias_root(a);
+    if (!cache || !is_op(cache, "NONE") || cache->type != GGML_TYPE_F16) return false;
+    const ggml_tensor *rb = alias_root(b);
+    return is_op(rb, "ROPE") || is_op(rb, "SOFT_MAX");
+}
+
 // What the lowering takes (mi355x_lower_ggml_graph): the scheduler places these nodes
 // here; a graph whose attention block is not the non-flash llm_build_llama pattern
 // fails in graph_compute (GGML_STATUS_FAILED), it is never computed wrongly.
@@ -396,7 +427,7 @@ bool dev_supports_op(ggml_backend_dev_t, const struct ggml_tensor *op) {
             return true;
         case MI355X_GOP_MUL_MAT: {
             if (!a || !b) return false;
-            if (a->type == GGML_TYPE_F16 && b->type == GGML_TYPE_F32) return true;  // KQ / KQV on the f16 cache
+            if (a->type == GGML_TYPE_F16) return attn_f16_mul_mat(op);  // KQ / KQV on the f16 cache only
             if (!is_kquant(a->type)) return false;
             mi355x_tensor w, x, y;
             shape_of(a, w);
@@ -429,9 +460,12 @@ bool dev_supports_op(ggml_backend_dev_t, const struct ggml_tensor *op) {
             return f32_rows(a) && max_bias == 0.0f &&
                    (!b || b->type == GGML_TYPE_F16 || b->type == GGML_TYPE_F32);
         }
-        case MI355X_GOP_CONT:
-        case MI355X_GOP_CPY:
-            return a && a->type == GGML_TYPE_F32 && op->type == GGML_TYPE_F32;
+        case MI355X_GOP_CONT: {  // only the attention block's last node: CONT(PERMUTE(KQV))
+            if (!a || a->type != GGML_TYPE_F32 || op->type != GGML_TYPE_F32 || !is_op(a, "PERMUTE")) return false;
+            const ggml_tensor *kqv = alias_root(a);
+            return is_op(kqv, "MUL_MAT") && attn_f16_mul_mat(kqv);
+        }
+        case MI355X_GOP_CPY:  // never lowered (the KV store is SET_ROWS)
         default:
             return false;
     }
@@ -502,7 +536,7 @@ Registry *registry() {
         const int n = mi355x_device_count();
         for (int i = 0; i < n; ++i) {
             auto *d = new Device();
-            d->index = i;
+            d->index = mi355x_device_ordinal(i);  // the HIP ordinal, not the position in the list
             d->name = "MI355X" + std::to_string(i);
             d->description = "AMD Instinct MI355X (gfx950): K-quant MUL_MAT + llama decode ops, libggml_mi355x";
             d->buft = ggml_backend_buffer_type{kBuftIface, &d->dev, d};

@@ -23,9 +23,9 @@
 //    workgroup whose add returns the last count of the round replays row r's nsb records
 //    (sc1 loads, EVERY load of them), adds the residual and stores y. No workgroup waits for
 //    another: nothing can deadlock, and placement only changes speed.
-// Counters are never reset: the round of row block rb is old / nsb, the last arriver the one
-// that draws old % nsb == nsb - 1 (zeroed once when the backend allocates them; nsb a power
-// of two, so the rounds stay aligned when a counter wraps).
+// Counters start every launch at 0: the last arriver is the one whose add returns nsb - 1,
+// and it stores 0 back (zeroed once when the backend allocates them), so an aborted launch
+// cannot misalign the next one.
 #include <string.h>
 
 #include <hip/hip_ext.h>
@@ -170,7 +170,11 @@ __global__ void __launch_bounds__(512) kq_attn_oproj(const AttnOprojArgs p) {
     __syncthreads();
     if (threadIdx.x == 0) {
         const uint32_t old = __hip_atomic_fetch_add(p.cnt + rb, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *flag = (int)(old % (uint32_t)nsb) == nsb - 1;
+        const bool last = old == (uint32_t)(nsb - 1);
+        // every arrival of this launch has happened: the last arriver re-arms the counter, so
+        // each launch starts at 0 whatever an earlier (aborted or diagnostic) launch left
+        if (last) __hip_atomic_store(p.cnt + rb, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *flag = last;
     }
     __syncthreads();
     if (!*flag) return;
@@ -241,9 +245,6 @@ bool ao_shape(int hd, int n_head, int n_head_kv, int n_ctx, int type, int64_t K,
     if (K != (int64_t)n_head * hd || K % QK) return false;
     sh.nsb = (int)(K / QK);
     if (sh.nsb > 16 || n_rows <= 0 || n_rows > (1 << 24)) return false;
-    // the arrival counters are never reset and wrap at 2^32: rounds of nsb arrivals stay
-    // aligned across the wrap only when nsb divides 2^32
-    if (sh.nsb & (sh.nsb - 1)) return false;
     int n_rb = 256 / sh.nsb;
     const int nrb_knob = (int)knob(KNOB_AO_NRB);  // A/B only
     if (nrb_knob > 0) n_rb = nrb_knob;

@@ -894,6 +894,20 @@ int mi355x_device_count(void) {
     return n;
 }
 
+int mi355x_device_ordinal(int i) {
+    int ndev = 0;
+    if (i < 0 || hipGetDeviceCount(&ndev) != hipSuccess) return -1;
+    for (int d = 0; d < ndev; ++d) {
+        bool ok;
+        {
+            DeviceGuard dg(d);
+            ok = kq::device_ok() != 0;
+        }
+        if (ok && i-- == 0) return d;
+    }
+    return -1;
+}
+
 int mi355x_device_memory(int device, size_t *free_bytes, size_t *total_bytes) {
     int ndev = 0;
     if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) return MI355X_E_NODEVICE;
@@ -1217,7 +1231,11 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
                 if (hipMalloc(&b->fx, need) != hipSuccess) return MI355X_E_WORKSPACE;
                 b->fx_size = need;
             }
-            if (hipMemset(b->fx, 0, kq::kAttnOprojCounterBytes) != hipSuccess) return MI355X_E_WORKSPACE;
+            // on the backend stream (non-blocking: a legacy-stream memset is not ordered
+            // before its next launch), then waited for
+            if (hipMemsetAsync(b->fx, 0, kq::kAttnOprojCounterBytes, b->stream) != hipSuccess ||
+                hipStreamSynchronize(b->stream) != hipSuccess)
+                return MI355X_E_WORKSPACE;
             b->fx_nsb = nsb;
         }
     }

@@ -58,7 +58,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_prefill_precision",
     "mi355x_gemv_waves",
     "mi355x_debug_knob",
-    "mi355x_device_count", "mi355x_device_memory", "mi355x_backend_memset", "mi355x_backend_set_attn_oproj",
+    "mi355x_device_count", "mi355x_device_ordinal", "mi355x_device_memory", "mi355x_backend_memset", "mi355x_backend_set_attn_oproj",
     "mi355x_attn_prompt",
     "mi355x_attn_prompt_impl",
 )
@@ -136,6 +136,8 @@ def lib():
     L.mi355x_version.restype = ctypes.c_char_p
     L.mi355x_device_available.restype = i32
     L.mi355x_device_count.restype = i32
+    L.mi355x_device_ordinal.restype = i32
+    L.mi355x_device_ordinal.argtypes = [i32]
     L.mi355x_device_memory.argtypes = [i32, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(ctypes.c_size_t)]
     L.mi355x_device_memory.restype = i32
     L.mi355x_backend_memset.argtypes = [ctypes.c_void_p, ctypes.c_void_p, i32, ctypes.c_size_t]

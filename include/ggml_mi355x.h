@@ -423,6 +423,10 @@ typedef struct mi355x_backend *mi355x_backend_t;
  * registration's get_device_count (ggml_backend_reg_i [U], ggml-backend-impl.h; the
  * CPU sibling registers one device, ggml-cpu.cpp). 0 without a GPU. */
 int mi355x_device_count(void);
+/* The HIP ordinal of the i-th device counted by mi355x_device_count (a host may list a
+ * non-gfx950 GPU at a lower ordinal): the `device` argument the calls below take; -1 if
+ * there is no such device. */
+int mi355x_device_ordinal(int i);
 /* Free / total device memory (ggml_backend_device_i.get_memory [U]): 0 or an error. */
 int mi355x_device_memory(int device, size_t *free_bytes, size_t *total_bytes);
 mi355x_backend_t mi355x_backend_init(int device);        /* NULL on failure */

@@ -120,6 +120,41 @@ static int supports_checks(ggml_backend_dev_t dev) {
     y.op = GGML_OP_GET_ROWS;
     y.src[0] = &w, y.src[1] = &ids;
     CHECK(dev->iface.supports_op(dev, &y));
+    // f16 MUL_MAT: only the attention's KQ / KQV on a view of the f16 KV cache is claimed;
+    // an F16 lm_head (or tied embedding) stays on the CPU backend
+    ggml_tensor hw{}, hx{}, hy{}, kc{}, kv{}, rq{}, rp{}, kq{}, ct{};
+    shape(hw, GGML_TYPE_F16, 2048, 32000, 2, 2048 * 2);
+    shape(hx, GGML_TYPE_F32, 2048, 1, 4, 2048 * 4);
+    shape(hy, GGML_TYPE_F32, 32000, 1, 4, 32000 * 4);
+    hy.op = GGML_OP_MUL_MAT;
+    hy.src[0] = &hw, hy.src[1] = &hx;
+    CHECK(!dev->iface.supports_op(dev, &hy));
+    shape(kc, GGML_TYPE_F16, 256, 128, 2, 256 * 2);  // K cache leaf [n_ctx][n_head_kv * hd]
+    shape(kv, GGML_TYPE_F16, 64, 128, 2, 256 * 2);   // one kv head's view from cell 0
+    kv.op = GGML_OP_VIEW;
+    kv.src[0] = &kc, kv.view_src = &kc;
+    shape(rq, GGML_TYPE_F32, 64, 32, 4, 64 * 4);
+    rq.op = GGML_OP_ROPE;
+    shape(rp, GGML_TYPE_F32, 64, 1, 4, 64 * 4);
+    rp.op = GGML_OP_PERMUTE;
+    rp.src[0] = &rq;
+    shape(kq, GGML_TYPE_F32, 128, 1, 4, 128 * 4);
+    kq.op = GGML_OP_MUL_MAT;
+    kq.src[0] = &kv, kq.src[1] = &rp;
+    CHECK(dev->iface.supports_op(dev, &kq));
+    kq.src[1] = &hx;  // the same view against a plain activation: not the attention pattern
+    CHECK(!dev->iface.supports_op(dev, &kq));
+    kv.view_offs = 512;  // a view that does not start at cell 0
+    kq.src[1] = &rp;
+    CHECK(!dev->iface.supports_op(dev, &kq));
+    // CONT / CPY: only CONT(PERMUTE(KQV)) is lowered
+    shape(ct, GGML_TYPE_F32, 64, 1, 4, 64 * 4);
+    ct.op = GGML_OP_CONT;
+    ct.src[0] = &rp;  // PERMUTE(ROPE): not an attention output
+    CHECK(!dev->iface.supports_op(dev, &ct));
+    ct.op = GGML_OP_CPY;
+    ct.src[0] = &hx;
+    CHECK(!dev->iface.supports_op(dev, &ct));
     return 0;
 }
 

@@ -278,3 +278,59 @@ def test_token_split_plan_reduce():
         TokenSplit(KSPLIT_HP, 8, 0, mode="reduce")  # 2 heads x 64 = half a superblock
     with pytest.raises(ValueError):
         TokenSplit(KSPLIT_HP, 2, 0, mode="bogus")
+
+
+# ------------------------------------------------ bench.py's N > 1 control plane
+def _bench_connect_worker(rank, world, port, fail_rank, results):
+    import types
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        import bench
+
+        class FakeBackend:  # the GPU backend's communicator entry point, failing on one rank
+            def __init__(self):
+                self.calls = []
+
+            def set_comm(self, r, n, uid):
+                self.calls.append((r, n, len(uid)))
+                if r == fail_rank:
+                    raise RuntimeError("ncclCommInitRank failed (test)")
+
+        bench.g = types.SimpleNamespace(lib=lambda: types.SimpleNamespace(mi355x_comm_id_size=lambda: 128),
+                                        comm_unique_id=lambda: bytes(range(128)))
+        be = FakeBackend()
+        err = bench.connect(be, world, rank)
+        # what main() does with the agreed error: every rank falls back to replicas
+        mode = bench.resolve_mode("auto", world)
+        rowsplit = mode != "replicas" and err is None
+        head = bench.headline_fields(mode if rowsplit else "replicas", world)
+        results[rank] = (err, be.calls, mode, head)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("fail_rank", [None, 1])
+def test_bench_connect_failure_falls_back_to_replicas(fail_rank):
+    """bench.py at N = 2 (gloo control plane, as the driver's scaling run):
+    the headline is the reduce row split; the RCCL id goes from rank 0 to every rank; when
+    the communicator fails on ANY rank, every rank agrees on the failure (so none waits in a
+    collective the others never enter) and the line falls back to replicas with the replicas
+    fields (weak scaling, N tokens per step)."""
+    import torch.multiprocessing as mp
+    world = 2
+    results = mp.Manager().dict()
+    mp.spawn(_bench_connect_worker, args=(world, free_port(), fail_rank, results), nprocs=world, join=True)
+    for r in range(world):
+        err, calls, mode, head = results[r]
+        assert mode == "rowsplit-reduce"
+        assert calls == [(r, world, 128)]
+        if fail_rank is None:
+            assert err is None
+            assert head == {"scaling": "strong", "parallelism": "rowsplit-reduce2", "tokens_per_step": 1}
+        else:
+            assert err is not None
+            assert ("ncclCommInitRank" in err) if r == fail_rank else err == "communicator setup failed on another rank"
+            assert head == {"scaling": "weak", "parallelism": "replicas x2", "tokens_per_step": 2}

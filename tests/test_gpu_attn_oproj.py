@@ -107,3 +107,45 @@ def test_attn_oproj_position_outside_cache(dev):
         outs.append(dec.logits.cpu().numpy().copy())
         b.close()
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+
+
+@pytest.mark.parametrize("nrb", [0, 12])
+def test_attn_oproj_long_cache_and_row_blocks(dev, nrb):
+    """the fused kernel admits KV caches of up to 256 cells. At head_dim 64 a head
+    runs on 128 threads, so n_kv > 128 takes attn_head's multi-pass branch: decode past
+    position 128 of a 256-cell cache, fused against unfused bit for bit (and against the
+    oracle at the positions around the 128-cell edge). nrb = 12 (AO_NRB): row blocks whose
+    workgroups are not a multiple of 8 apart, so one row block's workgroups sit on several
+    XCDs and the hand-off crosses them."""
+    from oracle import kq_ops_oracle as O
+    from tests import llama_model as LM
+    import ggml_mi355x as g
+    from ggml_mi355x.llama import hparams
+    O.lib()
+    hp = hparams(2048, 1, 32, 4, 1024, 1024)
+    n_ctx = 256
+    prev = g.debug_knob("AO_NRB", nrb) if nrb else None
+    try:
+        w, b, dec = _decoder(dev, hp, 29, n_ctx)
+        model, cache = LM.oracle_model(hp, w, n_ctx)
+        rng = np.random.default_rng(11)
+        tokens = rng.integers(0, hp["n_vocab"], size=150).tolist()
+        fused = []
+        for p, tok in enumerate(tokens):
+            dec.step(tok, p)
+            b.synchronize()
+            got = dec.logits.cpu().numpy().copy()
+            ref, _ = O.decode_token(model, tok, p, cache)
+            if p in (0, 1, 126, 127, 128, 129, 130, 149):
+                assert bits_equal(got, ref), (p, first_mismatch(got, ref))
+            fused.append(got)
+        assert b.set_attn_oproj(False) == 1
+        dec.reset()
+        for p, tok in enumerate(tokens):
+            dec.step(tok, p)
+            b.synchronize()
+            assert bits_equal(dec.logits.cpu().numpy(), fused[p]), p
+        b.close()
+    finally:
+        if nrb:
+            g.debug_knob("AO_NRB", prev if prev else float("nan"))
