@@ -374,6 +374,19 @@ static inline void q5K_block_ints(const kqo_block_q5_K *x, const kqo_block_q8_K 
     *summins_out = summins;
 }
 
+/* [U] contraction choices the reference's listings do not show: 0 is the
+ * restatement's choice (gcc -O2 -std=gnu11, whose default -ffp-contract=fast fuses a
+ * single-use product into the add/sub it feeds, README.md:649-677's compile line); the
+ * other values are the alternatives, selectable only here, so tests can measure how often
+ * each would change an output (tests/test_oracle.py::test_unpinned_choice_flip_rates).
+ *   which 0 (Q5_K update): 1 = fma(-dmin, mins, d*sumi); 2 = no fma; 3 = Q4_K's two fmas
+ *   which 1 (Q6_K update): 1 = sum + (d_all*y.d)*f, unfused */
+static int g_q5_variant = 0, g_q6_variant = 0;
+void kqo_set_contraction_variant(int which, int v) {
+    if (which == 0) g_q5_variant = v;
+    else g_q6_variant = v;
+}
+
 /* NEON ggml_vec_dot_q5_K_q8_K [U]: `sumf += d * sumi - dmin * sumi_mins;`
  * Contraction as gcc's FMA pass forms it (first product fused into the
  * subtraction, the add to sumf unfused) — tolerance-only: parity unpinned. */
@@ -390,8 +403,19 @@ void kqo_vec_dot_q5_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size
         const float dmin = y[i].d * kqo_fp16_to_fp32(x[i].dmin);
         int32_t sumi, summins;
         q5K_block_ints(&x[i], &y[i], &sumi, &summins);
-        const float t = fmaf(d, (float)sumi, -(dmin * (float)summins));
-        sumf = sumf + t;
+        if (g_q5_variant == 0) {
+            const float t = fmaf(d, (float)sumi, -(dmin * (float)summins));
+            sumf = sumf + t;
+        } else if (g_q5_variant == 1) {
+            const float t = fmaf(-dmin, (float)summins, d * (float)sumi);
+            sumf = sumf + t;
+        } else if (g_q5_variant == 2) {
+            const float t = d * (float)sumi - dmin * (float)summins;
+            sumf = sumf + t;
+        } else {
+            sumf = fmaf(-(float)summins, dmin, sumf);
+            sumf = fmaf((float)sumi, d, sumf);
+        }
     }
     *s = sumf;
 }
@@ -445,7 +469,8 @@ void kqo_vec_dot_q6_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size
         const float d_all = kqo_fp16_to_fp32(x[i].d);
         int32_t isum, isum_mins;
         q6K_block_ints(&x[i], &y[i], &isum, &isum_mins);
-        sum = fmaf(d_all * y[i].d, (float)(isum - 32 * isum_mins), sum);
+        if (g_q6_variant == 0) sum = fmaf(d_all * y[i].d, (float)(isum - 32 * isum_mins), sum);
+        else sum = sum + (d_all * y[i].d) * (float)(isum - 32 * isum_mins);
     }
     *s = sum;
 }

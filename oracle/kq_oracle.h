@@ -50,6 +50,7 @@ void kqo_vec_dot_q4_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size
                                 const void *vy, size_t by, int nrc);
 void kqo_vec_dot_q4_K_q8_K_generic(int n, float *s, size_t bs, const void *vx, size_t bx,
                                    const void *vy, size_t by, int nrc);
+void kqo_set_contraction_variant(int which, int v); /* tests only: DESIGN.md §2 [U] choices */
 void kqo_vec_dot_q5_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size_t bx,
                                 const void *vy, size_t by, int nrc);
 void kqo_vec_dot_q6_K_q8_K_neon(int n, float *s, size_t bs, const void *vx, size_t bx,

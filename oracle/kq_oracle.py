@@ -48,8 +48,26 @@ def lib():
         L.kqo_dequantize_row_q4_K.argtypes = [vp, vp, i64]
         L.kqo_dequantize_row_q5_K.argtypes = [vp, vp, i64]
         L.kqo_dequantize_row_q6_K.argtypes = [vp, vp, i64]
+        L.kqo_set_contraction_variant.argtypes = [i32, i32]
         _lib = L
     return _lib
+
+
+class contraction_variant:
+    """with contraction_variant(which, v): the Q5_K (which 0) or Q6_K (which 1) fp32 update
+    as one of the [U] alternatives of kq_oracle.c (0 = the restatement's gcc choice); tests
+    only."""
+
+    def __init__(self, which, v):
+        self.which, self.v = which, v
+
+    def __enter__(self):
+        lib().kqo_set_contraction_variant(self.which, self.v)
+        return self
+
+    def __exit__(self, *exc):
+        lib().kqo_set_contraction_variant(self.which, 0)
+        return False
 
 
 def _p(a):

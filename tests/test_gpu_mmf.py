@@ -173,9 +173,12 @@ def test_llama_prompt_f16_auto_then_exact_prologue(dev, f16path):
     Q4_K and stay on kq_mmq behind the fused rms_norm -> Q8L prologue. That prologue must
     publish int8 Q8L blocks even though the launch before it was an f16 GEMM (ADVICE r3:
     a stale `f16` flag made the q/k/v GEMMs re-quantize a never-written f32 buffer).
-    Checked: every layer's K cache within a relative L2 error of 2^-4 of the bit-exact
-    prompt's (garbage or zeros there would be ~1), layers 0-2 (no f16 GEMM before them)
-    bit-exact, and the logits within 2^-3 of the oracle's sequential llm_build_llama."""
+    Checked: layers 0-2 (no f16 GEMM before them) bit-exact; layer 3's K cache, the first
+    behind ONE f16 GEMM (layer 2's ffn_down), within a relative L2 error of 2^-7 of the
+    bit-exact prompt's (one GEMM's stated bound carried through a residual add, a norm and
+    the k projection: a regression of one layer shows there); every layer's K cache within
+    2^-5 (garbage or zeros there would be ~1); and the logits within 2^-5 of the oracle's
+    sequential llm_build_llama (VERDICT r4 #8: held to ADVICE r3's 2^-5)."""
     import torch
     from oracle import kq_ops_oracle as O
     from tests import llama_model as LM
@@ -204,7 +207,8 @@ def test_llama_prompt_f16_auto_then_exact_prologue(dev, f16path):
         errs.append(float(np.linalg.norm(k - ke) / np.linalg.norm(ke)))
     print("K-cache relative L2 per layer:", errs)
     assert errs[0] == errs[1] == errs[2] == 0.0, errs
-    assert max(errs) <= 2.0 ** -4, errs
+    assert errs[3] <= 2.0 ** -7, errs
+    assert max(errs) <= 2.0 ** -5, errs
     model, cache = LM.oracle_model(hp, w, n_ctx)
     for p, tok in enumerate(tokens):
         ref, _ = O.decode_token(model, tok, p, cache)
@@ -213,7 +217,7 @@ def test_llama_prompt_f16_auto_then_exact_prologue(dev, f16path):
     got = out["f16_auto"][0]
     rel = float(np.linalg.norm(got - ref) / np.linalg.norm(ref))
     print("logits relative L2:", rel)
-    assert np.isfinite(got).all() and rel <= 2.0 ** -3, rel
+    assert np.isfinite(got).all() and rel <= 2.0 ** -5, rel
     torch.cuda.synchronize()
 
 

@@ -167,3 +167,43 @@ def test_thread_pool_reuse_and_resize(oracle, npo):
     for nt in (4, 4, 7, 2, 7):
         got = oracle.mul_mat(12, w, x, n_threads=nt, variant="simd")
         assert (got.view(np.uint32) == ref.view(np.uint32)).all()
+
+
+def test_unpinned_choice_flip_rates(oracle, npo):
+    """the three bit-deciding fp choices the reference's listings do not show
+    ([U]), each against its alternatives at TinyLlama's shapes — how often
+    the alternative would change an output. Whoever holds llama.cpp a3cb0474 can then tell
+    which goldens an observed difference would force to be regenerated.
+      * quantize_row_q8_K's nearest_int(iscale * x): fused (fmadd) vs unfused — about 2e-6 of
+        the qs bytes (one activation row of 2048 in a few hundred), but a flipped byte changes
+        every output of the GEMV that reads the row;
+      * Q6_K `sum += d_all * y.d * (isum - 32 * isum_mins)`: fma vs no fma — half the rows;
+      * Q5_K `sumf += d * sumi - dmin * sumi_mins`: which product gcc fuses — half the rows."""
+    rng = np.random.default_rng(2024)
+    K = 2048
+    x = rng.standard_normal((1024, K)).astype(np.float32)
+    a, b = oracle.quantize_q8_K(x, fused=True), oracle.quantize_q8_K(x, fused=False)
+    A, B = a.reshape(1024, K // 256, 292), b.reshape(1024, K // 256, 292)
+    byte_frac = (A[..., 4:260] != B[..., 4:260]).mean()
+    assert 0 < byte_frac < 1e-4, byte_frac
+    row = int(np.flatnonzero((A != B).any((1, 2)))[0])
+    w = npo.random_blocks(rng, 12, 512, K)
+    ya, yb = oracle.mul_mat_q8(12, w, a[row], K)[0], oracle.mul_mat_q8(12, w, b[row], K)[0]
+    assert (ya.view(np.uint32) != yb.view(np.uint32)).mean() > 0.9
+
+    q = oracle.quantize_q8_K(x[:1])
+    w6 = npo.random_blocks(rng, 14, 1024, K)
+    y0 = oracle.mul_mat_q8(14, w6, q, K)[0]
+    with oracle.contraction_variant(1, 1):
+        y1 = oracle.mul_mat_q8(14, w6, q, K)[0]
+    f6 = (y0.view(np.uint32) != y1.view(np.uint32)).mean()
+    assert 0.3 < f6 < 0.8, f6
+    assert np.array_equal(oracle.mul_mat_q8(14, w6, q, K)[0].view(np.uint32), y0.view(np.uint32))  # restored
+
+    w5 = npo.random_blocks(rng, 13, 1024, K)
+    y0 = oracle.mul_mat_q8(13, w5, q, K)[0]
+    for v, lo, hi in ((1, 0.3, 0.7), (2, 0.3, 0.7), (3, 0.5, 0.9)):
+        with oracle.contraction_variant(0, v):
+            y1 = oracle.mul_mat_q8(13, w5, q, K)[0]
+        f5 = (y0.view(np.uint32) != y1.view(np.uint32)).mean()
+        assert lo < f5 < hi, (v, f5)
