@@ -70,9 +70,15 @@ __device__ __forceinline__ float adiag_finite(uint32_t bits) { return __uint_as_
 // VPF0: V-cache iterations (32 cells each) prefetched with the position (0: 8 / ITEMS).
 // OUT_WT: out is global memory, stored write-through (sc1) for the next launch (kq_rows'
 // outputs likewise, KQ_ROWS_YSC1).
-template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false>
+// SC1_IN: q / k / v were written in this launch by other workgroups (the persistent layer,
+// kq_layer.hip): every load of them is an agent-scope (sc1) load, as the hand-off requires.
+template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false, bool SC1_IN = false>
 __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8_t *smem, float *out,
                                           bool may_write) {
+    auto ldin = [](const float *p) {
+        if (SC1_IN) return __uint_as_float(__hip_atomic_load((const uint32_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        return *p;
+    };
     static_assert(HD == 64 || HD == 128, "head_dim");
     constexpr int KV4 = HD / 8;          // 16-B pieces of one K-cache row
     static_assert(TPH == 256 || (TPH == 128 && HD == 64), "threads per head");
@@ -96,12 +102,12 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         }
         const float *qp = a.q + (int64_t)h * HD + 2 * t;
         const float *kp = a.k + (int64_t)g * HD + 2 * t;
-        x0 = qp[0];
-        x1 = qp[1];
-        y0 = kp[0];
-        y1 = kp[1];
+        x0 = ldin(qp);
+        x1 = ldin(qp + 1);
+        y0 = ldin(kp);
+        y1 = ldin(kp + 1);
     } else if (t < HD / 2 + HD) {
-        x0 = a.v[(int64_t)g * HD + (t - HD / 2)];
+        x0 = ldin(a.v + (int64_t)g * HD + (t - HD / 2));
     }
     uint4 kpre[KV4] = {};
     if (t < a.n_ctx && t < KPF && ADIAG(a) != 5) {  // (diag 5: no cache loads, stop after rope; timing only)

@@ -221,7 +221,6 @@ KQ_AO_INST(128, Q5_K)
 KQ_AO_INST(128, Q6_K)
 
 // ------------------------------------------------------------------ host side
-namespace {
 size_t attn_lds16(int hd, int n_ctx) {
     // kq_ops.hip attn_lds (the per-head layout of attn_head), rounded to 16 B
     const size_t gsum = (size_t)(n_ctx / 4) * 8 <= (size_t)hd * 64 ? 0 : (size_t)(n_ctx / 4) * 8;
@@ -229,6 +228,7 @@ size_t attn_lds16(int hd, int n_ctx) {
     return (b + 15) & ~(size_t)15;
 }
 
+namespace {
 struct AoShape {
     int hps, nsb, n_rb, R;
     size_t lds, recs_bytes;

@@ -41,6 +41,10 @@ struct mi355x_backend {
     void *fx = nullptr;      // its arrival counters (zeroed at allocation) and records
     size_t fx_size = 0;
     int fx_nsb = 0;          // the superblock count the counters' rounds are aligned to
+    bool layer_engine = false;  // each decode layer as one persistent launch (kq_layer.hip)
+    uint32_t *ly_sync = nullptr;  // the persistent layers' counter blocks (zeroed at allocation), then err
+    int ly_blocks = 0;
+    std::vector<uint32_t> ly_sig;  // producers per edge and shard of every block: a change re-zeroes them
     ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
     bool loop_nocopy = false;   // emulated rank, timing only (MI355X_LOOPBACK_NOCOPY)
     int rank = 0, world = 0;
@@ -134,7 +138,8 @@ struct Launch {
     int first, count;  // nodes[first .. first+count): the MUL_MAT run, or the single node
     int kind = 0;      // 0 single node, 1 MUL_MAT run (GEMV), 2 prefill prologue -> Q8L, 3 batched MUL_MAT + ADD,
                        // 4 batched MUL_MATs of one type on one activation in one tile-GEMM launch,
-                       // 5 decode ATTN_DECODE -> MUL_MAT (-> ADD) in one launch (kq_attn_oproj)
+                       // 5 decode ATTN_DECODE -> MUL_MAT (-> ADD) in one launch (kq_attn_oproj),
+                       // 6 a whole decode layer (15 nodes) in one persistent launch (kq_layer)
     const mi355x_tensor *q8_of = nullptr;  // kind 2: the node whose (never written) output the Q8L blocks stand for
     int pro = MI355X_PRO_NONE;
     const float *x = nullptr, *x2 = nullptr;  // GEMV input (prologue source) and its second operand
@@ -144,6 +149,8 @@ struct Launch {
     const float *norm_w = nullptr;  // single RMS_NORM with its MUL fused
     float *norm_y = nullptr;
     float *epi_y = nullptr;  // GEMV run [gate, up] with the SWIGLU node fused as its epilogue
+    int ly_block = -1;       // kind 6: its counter block
+    kq::LayerArgs la;        // kind 6: the launch's arguments (sync / err set at enqueue)
 };
 
 float f_of(int32_t bits) {
@@ -315,6 +322,105 @@ bool attn_oproj_fusable(const mi355x_backend *b, const mi355x_tensor *t, const m
     return kq::attn_oproj_buffer(hd, nh, nkv, (int)t->src[4]->ne[1], w->type, w->ne[0], w->ne[1], nullptr) > 0;
 }
 
+// ---- kind 6: the 15 nodes of one llm_build_llama decode layer as one kq_layer launch
+bool contiguous_kq(const mi355x_tensor *w) {
+    return is_kquant(w->type) && w->ne[0] % MI355X_QK_K == 0 && w->ne[2] == 1 && w->ne[3] == 1 &&
+           w->nb[1] == (size_t)(w->ne[0] / MI355X_QK_K) * mi355x_row_size(w->type, MI355X_QK_K) &&
+           (w->type == MI355X_TYPE_Q6_K || ((uintptr_t)w->data & 15u) == 0);
+}
+bool f32_vec(const mi355x_tensor *t, int64_t n, bool aligned16) {
+    return t && t->type == MI355X_TYPE_F32 && nelem(t) == n && t->ne[0] == n && t->nb[0] == 4 && t->data &&
+           (!aligned16 || ((uintptr_t)t->data & 15u) == 0);
+}
+// ADD(a, b) where one operand is node `mm` and the other is `res`'s bytes: true
+bool add_of(const mi355x_tensor *ad, const mi355x_tensor *mm, const mi355x_tensor *res) {
+    if (!ad || ad->op != MI355X_OP_ADD) return false;
+    const int s = ad->src[0] == mm ? 0 : ad->src[1] == mm ? 1 : -1;
+    if (s < 0) return false;
+    const mi355x_tensor *o = ad->src[1 - s];
+    return o && o->data == res->data && o->type == MI355X_TYPE_F32 && nelem(o) == nelem(res);
+}
+bool spans_overlap(const mi355x_tensor *p, const mi355x_tensor *q) {
+    const Span a = span_of(p), c = span_of(q);
+    return a.lo < c.hi && c.lo < a.hi;
+}
+
+bool layer_match(const mi355x_backend *b, mi355x_tensor *const *nodes, int n, int i, const std::vector<int> &readers,
+                 kq::LayerArgs &la) {
+    if (!b->layer_engine || i + 15 > n) return false;
+    mi355x_tensor *const *t = nodes + i;
+    const mi355x_tensor *n1 = t[0], *m1 = t[1], *q = t[2], *k = t[3], *v = t[4], *at = t[5], *o = t[6], *x1 = t[7];
+    const mi355x_tensor *n2 = t[8], *m2 = t[9], *g = t[10], *u = t[11], *sw = t[12], *dn = t[13], *x2 = t[14];
+    if (n1->op != MI355X_OP_RMS_NORM || m1->op != MI355X_OP_MUL || m1->src[0] != n1) return false;
+    const mi355x_tensor *x = n1->src[0];
+    const int64_t E = n1->ne[0];
+    if (!f32_vec(x, E, true) || !f32_vec(n1, E, false) || !f32_vec(m1->src[1], E, true) || !f32_vec(m1, E, false))
+        return false;
+    if (!elidable(n1, readers[i]) || readers[i + 1] != 3 || (m1->flags & MI355X_TENSOR_FLAG_OUTPUT)) return false;
+    for (const mi355x_tensor *mm : {q, k, v})
+        if (!is_gemv_node(mm) || mm->src[1] != m1 || !contiguous_kq(mm->src[0]) || mm->src[0]->ne[0] != E ||
+            !f32_vec(mm, mm->src[0]->ne[1], true))
+            return false;
+    if (at->op != MI355X_OP_ATTN_DECODE || at->src[0] != q || at->src[1] != k || at->src[2] != v) return false;
+    if (at->src[6]->ne[1] != 1) return false;  // the position's rope row staged with the inputs
+    const int nh = at->op_params[0], nkv = at->op_params[1], hd = at->op_params[2];
+    if (k->src[0]->ne[1] != v->src[0]->ne[1] || (int64_t)nh * hd != q->src[0]->ne[1] || q->src[0]->ne[1] != E ||
+        (int64_t)nkv * hd != k->src[0]->ne[1] || !f32_vec(at, E, true))
+        return false;
+    if (!is_gemv_node(o) || o->src[1] != at || !contiguous_kq(o->src[0]) || o->src[0]->ne[0] != E ||
+        o->src[0]->ne[1] != E || !elidable(o, readers[i + 6]))
+        return false;
+    if (!add_of(x1, o, x) || !f32_vec(x1, E, true)) return false;
+    if (n2->op != MI355X_OP_RMS_NORM || n2->src[0] != x1 || !elidable(n2, readers[i + 8]) || m2->op != MI355X_OP_MUL ||
+        m2->src[0] != n2 || !f32_vec(m2->src[1], E, true) || readers[i + 9] != 2 ||
+        (m2->flags & MI355X_TENSOR_FLAG_OUTPUT))
+        return false;
+    if (f_of(n1->op_params[0]) != f_of(n2->op_params[0])) return false;  // one eps per layer (llama)
+    for (const mi355x_tensor *mm : {g, u})
+        if (!is_gemv_node(mm) || mm->src[1] != m2 || !contiguous_kq(mm->src[0]) || mm->src[0]->ne[0] != E)
+            return false;
+    const int64_t F = g->src[0]->ne[1];
+    if (u->src[0]->ne[1] != F || !elidable(g, readers[i + 10]) || !elidable(u, readers[i + 11])) return false;
+    if (sw->op != MI355X_OP_SWIGLU || sw->src[0] != g || sw->src[1] != u || !f32_vec(sw, F, true)) return false;
+    if (!is_gemv_node(dn) || dn->src[1] != sw || !contiguous_kq(dn->src[0]) || dn->src[0]->ne[0] != F ||
+        dn->src[0]->ne[1] != E || !elidable(dn, readers[i + 13]))
+        return false;
+    if (!add_of(x2, dn, x1) || !f32_vec(x2, E, false)) return false;
+    // written in the launch: q, k, v, att, x1, h, x2 -- none of them over an input or another
+    const mi355x_tensor *wr[6] = {q, k, v, at, x1, sw};
+    for (int a0 = 0; a0 < 6; ++a0) {
+        if (spans_overlap(wr[a0], x) || spans_overlap(wr[a0], x2)) return false;
+        for (int a1 = a0 + 1; a1 < 6; ++a1)
+            if (spans_overlap(wr[a0], wr[a1])) return false;
+    }
+    memset(&la, 0, sizeof(la));
+    la.E = (int)E;
+    la.F = (int)F;
+    la.nq = (int)q->src[0]->ne[1];
+    la.nkv = (int)k->src[0]->ne[1];
+    const mi355x_tensor *ws[7] = {q->src[0], k->src[0], v->src[0], o->src[0], g->src[0], u->src[0], dn->src[0]};
+    for (int m = 0; m < 7; ++m) {
+        la.type[m] = ws[m]->type;
+        la.w[m] = (const uint8_t *)ws[m]->data;
+    }
+    la.y[0] = (float *)q->data;
+    la.y[1] = (float *)k->data;
+    la.y[2] = (float *)v->data;
+    la.x = (const float *)x->data;
+    la.attn_norm = (const float *)m1->src[1]->data;
+    la.ffn_norm = (const float *)m2->src[1]->data;
+    la.eps = f_of(n1->op_params[0]);
+    la.att = (float *)at->data;
+    la.x1 = (float *)x1->data;
+    la.h = (float *)sw->data;
+    la.x2 = (float *)x2->data;
+    mi355x_attn_desc d;
+    attn_desc_of(at, d);
+    d.rope_row = 1;
+    if (kq::attn_args_from(&d, la.at) != 0) return false;
+    return kq::layer_plan(la, hd, nh) == MI355X_OK;
+}
+
 std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const *nodes, int n, bool fuse) {
     std::vector<Launch> out;
     const std::vector<int> readers = fuse ? count_readers(nodes, n) : std::vector<int>(n, 0);
@@ -323,13 +429,21 @@ std::vector<Launch> plan_launches(const mi355x_backend *b, mi355x_tensor *const 
             if (nodes[i] == u) return i;
         return -1;
     };
-    int i = 0;
+    int i = 0, ly_blocks = 0;
     while (i < n) {
         const mi355x_tensor *t = nodes[i];
         Launch l;
         l.first = i;
         l.count = 1;
         int head = i;  // first MUL_MAT of a run
+        if (fuse && layer_match(b, nodes, n, i, readers, l.la)) {
+            l.kind = 6;
+            l.count = 15;
+            l.ly_block = ly_blocks++;
+            out.push_back(l);
+            i += 15;
+            continue;
+        }
         if (fuse && i + 1 < n && attn_oproj_fusable(b, t, nodes[i + 1], readers[i])) {
             const mi355x_tensor *mm = nodes[i + 1];
             l.kind = 5;
@@ -696,6 +810,16 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
             q8.nb = m->nb[1];
             continue;
         }
+        if (l.kind == 6) {  // a decode layer: one persistent launch
+            kq::LayerArgs la = l.la;
+            if (!b->ly_sync || l.ly_block >= b->ly_blocks) return MI355X_E_WORKSPACE;
+            la.sync = b->ly_sync + (size_t)l.ly_block * kq::LAYER_SYNC_U32;
+            la.err = (int *)(b->ly_sync + (size_t)b->ly_blocks * kq::LAYER_SYNC_U32);
+            rc = kq::launch_layer(la, b->stream);
+            if (rc) return rc;
+            q8 = Q8State();
+            continue;
+        }
         if (l.kind == 5) {  // decode attention + o-proj (+ residual): one launch
             const mi355x_tensor *mm = nodes[l.first + 1];
             mi355x_attn_desc d;
@@ -943,6 +1067,7 @@ void mi355x_backend_free(mi355x_backend_t b) {
     drop_graph(b);
     if (b->workspace) hipFree(b->workspace);
     if (b->fx) hipFree(b->fx);
+    if (b->ly_sync) hipFree(b->ly_sync);
     if (b->comm) rccl().comm_destroy(b->comm);
     hipStreamDestroy(b->stream);
     }
@@ -1159,6 +1284,35 @@ int mi355x_backend_set_attn_oproj(mi355x_backend_t b, int enable) {
     return prev;
 }
 
+int mi355x_backend_set_layer_engine(mi355x_backend_t b, int enable) {
+    if (!b) return MI355X_E_INVAL;
+    DeviceGuard dg(b->device);
+    const int prev = b->layer_engine ? 1 : 0;
+    if ((enable != 0) != b->layer_engine) {
+        hipStreamSynchronize(b->stream);
+        drop_graph(b);
+        b->layer_engine = enable != 0;
+    }
+    return prev;
+}
+
+int mi355x_backend_layer_error(mi355x_backend_t b) {
+    if (!b) return MI355X_E_INVAL;
+    if (!b->ly_sync) return 0;
+    DeviceGuard dg(b->device);
+    if (hipStreamSynchronize(b->stream) != hipSuccess) return MI355X_E_NODEVICE;
+    int err = 0;
+    const size_t words = (size_t)b->ly_blocks * kq::LAYER_SYNC_U32 + 64;
+    if (hipMemcpy(&err, b->ly_sync + (size_t)b->ly_blocks * kq::LAYER_SYNC_U32, 4, hipMemcpyDeviceToHost) != hipSuccess)
+        return MI355X_E_NODEVICE;
+    if (err) {  // the counters of an abandoned launch are out of step: start every block again
+        if (hipMemsetAsync(b->ly_sync, 0, words * 4, b->stream) != hipSuccess ||
+            hipStreamSynchronize(b->stream) != hipSuccess)
+            return MI355X_E_NODEVICE;
+    }
+    return err ? 1 : 0;
+}
+
 int mi355x_backend_set_fusion(mi355x_backend_t b, int enable) {
     if (!b) return MI355X_E_INVAL;
     DeviceGuard dg(b->device);
@@ -1237,6 +1391,34 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
                 hipStreamSynchronize(b->stream) != hipSuccess)
                 return MI355X_E_WORKSPACE;
             b->fx_nsb = nsb;
+        }
+    }
+    {  // the persistent layers' counter blocks: one per kind-6 launch, zeroed outside any capture
+       // whenever they are (re)allocated or their producer counts change
+        std::vector<uint32_t> sig;
+        int nblk = 0;
+        for (const Launch &l : launches) {
+            if (l.kind != 6) continue;
+            nblk = l.ly_block + 1 > nblk ? l.ly_block + 1 : nblk;
+            for (int e = 0; e < 4; ++e)
+                for (int k = 0; k < 8; ++k) sig.push_back(l.la.expect[e][k]);
+        }
+        if (nblk && (nblk > b->ly_blocks || sig != b->ly_sig)) {
+            hipStreamSynchronize(b->stream);
+            drop_graph(b);
+            if (nblk > b->ly_blocks) {
+                if (b->ly_sync) hipFree(b->ly_sync);
+                b->ly_sync = nullptr;
+                b->ly_blocks = 0;
+                if (hipMalloc(&b->ly_sync, ((size_t)nblk * kq::LAYER_SYNC_U32 + 64) * 4) != hipSuccess)
+                    return MI355X_E_WORKSPACE;
+                b->ly_blocks = nblk;
+            }
+            if (hipMemsetAsync(b->ly_sync, 0, ((size_t)b->ly_blocks * kq::LAYER_SYNC_U32 + 64) * 4, b->stream) !=
+                    hipSuccess ||
+                hipStreamSynchronize(b->stream) != hipSuccess)
+                return MI355X_E_WORKSPACE;
+            b->ly_sig = sig;
         }
     }
     if (!use_graph) return enqueue(b, nodes, launches);

@@ -239,6 +239,33 @@ struct AttnOprojArgs {
     uint32_t *cnt;            // [n_rb] arrival counters (monotonic: last = old % nsb == nsb - 1)
 };
 
+// ---------------------------------------------------------------- persistent decode layer
+// kq_layer (kq_layer.hip): one llm_build_llama decode layer as ONE launch of one workgroup
+// per CU. Stages: 0 q/k/v (attn_norm prologue), attention, 1 o-proj (+ x -> x1),
+// 2 gate/up (ffn_norm prologue, SWIGLU -> h), 3 down (+ x1 -> x2). Matrices m: 0 q, 1 k,
+// 2 v, 3 o, 4 gate, 5 up, 6 down. Edges e (counter sets in `sync`): 0 q/k/v -> attention,
+// 1 attention -> o-proj, 2 x1 -> gate/up, 3 h -> down.
+constexpr int LAYER_WAVES = 8;       // 7 weight-stream waves + 1 control wave
+constexpr int LAYER_SYNC_U32 = 32 * 33;  // epoch + 4 edges x 8 shards, each on its own 128-B line
+struct LayerArgs {
+    int G;                           // workgroups (one per CU, all co-resident)
+    int E, F, nb_e, nb_f, nq, nkv;   // embd, ffn, K / 256 of each; rows of attn_q, attn_k (= attn_v)
+    int type[7];
+    const uint8_t *w[7];             // contiguous rows of K / 256 blocks
+    float *y[3];                     // q / k / v (written sc1: the attention's inputs)
+    const float *x;                  // layer input (written by the previous launch)
+    const float *attn_norm, *ffn_norm;
+    float eps;
+    float *att, *x1, *h, *x2;        // attention output, ffn_inp = o + x, swiglu(gate, up), layer output
+    AttnArgs at;                     // q / k / v = y[0..2], rope_row staged with the position
+    int n_attn, hpw, attn_stride, head_lds;  // attention workgroups, heads per workgroup, placement
+    uint32_t *sync;                  // this launch's counter block (LAYER_SYNC_U32 words, zeroed once)
+    int *err;                        // set when a wait timed out (co-residency lost): results invalid
+    uint32_t expect[4][8];           // producers per edge and shard
+    int D, slot;                     // ring slots per stream wave, bytes per slot
+    int o_aux, act_bytes, o_sums, o_res, o_tab, lds;  // LDS layout (ring at 0)
+};
+
 // ---------------------------------------------------------------- batched (prefill) MFMA GEMM
 // kq_mmq (M > 1): 64 x 64 output tiles, Q8L activations in a workspace.
 struct MmqArgs {

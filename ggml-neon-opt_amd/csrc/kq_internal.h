@@ -105,6 +105,12 @@ size_t attn_oproj_buffer(int hd, int n_head, int n_head_kv, int n_ctx, int type,
 int launch_attn_oproj(const AttnArgs &a, int type, const void *w, int64_t n_rows, size_t row_stride, const float *res,
                       float *y, uint8_t *buf, size_t buf_size, hipStream_t stream);
 int attn_impl();  // mi355x_attn_impl (kq_ops.hip)
+size_t attn_lds16(int hd, int n_ctx);  // attn_head's LDS per head, 16-B multiple (kq_attn_oproj.hip)
+// kq_layer.hip: one decode layer as one persistent launch. The caller fills E, F, nq, nkv,
+// type / w, y, x, the norms, eps, att / x1 / h / x2, at (rope_row 1), sync, err; layer_plan
+// checks the shape and fills the rest (grid, attention placement, ring depth, LDS layout).
+int layer_plan(LayerArgs &a, int hd, int n_head);
+int launch_layer(const LayerArgs &a, hipStream_t stream);
 // kq_api.hip
 void allow_lds(const void *fn, size_t lds);
 // Experiment / diagnostic knobs of A/B runs. The product reads no environment: a knob

@@ -59,6 +59,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_gemv_waves",
     "mi355x_debug_knob",
     "mi355x_device_count", "mi355x_device_ordinal", "mi355x_device_memory", "mi355x_backend_memset", "mi355x_backend_set_attn_oproj",
+    "mi355x_backend_set_layer_engine", "mi355x_backend_layer_error",
     "mi355x_attn_prompt",
     "mi355x_attn_prompt_impl",
 )
@@ -144,6 +145,10 @@ def lib():
     L.mi355x_backend_memset.restype = i32
     L.mi355x_backend_set_attn_oproj.argtypes = [ctypes.c_void_p, i32]
     L.mi355x_backend_set_attn_oproj.restype = i32
+    L.mi355x_backend_set_layer_engine.argtypes = [ctypes.c_void_p, i32]
+    L.mi355x_backend_set_layer_engine.restype = i32
+    L.mi355x_backend_layer_error.argtypes = [ctypes.c_void_p]
+    L.mi355x_backend_layer_error.restype = i32
     L.mi355x_quantize_row_q8_K.argtypes = [vp, vp, i64]
     for n in ("q4_K", "q5_K", "q6_K"):
         getattr(L, f"mi355x_vec_dot_{n}_q8_K").argtypes = [i32, vp, sz, vp, sz, vp, sz, i32]
@@ -612,8 +617,16 @@ class Backend:
         return int(lib().mi355x_backend_set_fusion(self.h, 1 if enable else 0))
 
     def set_attn_oproj(self, enable):
-        """Decode attention + o-proj GEMV in one launch (default on); returns the previous."""
+        """Decode attention + o-proj GEMV in one launch (default off); returns the previous."""
         return int(lib().mi355x_backend_set_attn_oproj(self.h, 1 if enable else 0))
+
+    def set_layer_engine(self, enable):
+        """Each decode layer as one persistent launch (csrc/kq_layer.hip); returns the previous."""
+        return int(lib().mi355x_backend_set_layer_engine(self.h, 1 if enable else 0))
+
+    def layer_error(self):
+        """Non-zero if a persistent-layer launch gave up waiting (results invalid); clears it."""
+        return int(lib().mi355x_backend_layer_error(self.h))
 
     def set_comm(self, rank, world, unique_id: bytes):
         """Join the RCCL communicator of a row split (every rank, same id bytes)."""

@@ -462,6 +462,21 @@ int mi355x_backend_set_fusion(mi355x_backend_t backend, int enable);
  * of one K superblock in one KV group, K <= 4096 and a KV cache of <= 256 cells. Returns
  * the previous value. */
 int mi355x_backend_set_attn_oproj(mi355x_backend_t backend, int enable);
+/* Persistent decode layer (default off; needs fusion on): the 15 nodes of one
+ * llm_build_llama decode layer -- RMS_NORM, MUL, MUL_MAT q / k / v, ATTN_DECODE, MUL_MAT o,
+ * ADD, RMS_NORM, MUL, MUL_MAT gate / up, SWIGLU, MUL_MAT down, ADD -- run as ONE launch of one
+ * workgroup per CU (csrc/kq_layer.hip): each workgroup owns rows of every matrix, streams
+ * the next stage's weights into LDS while the current stage's output is handed over
+ * between workgroups, and replays each row's fp32 chain in superblock order, so every
+ * output is bit-identical to the per-node path (ggml_compute_forward_mul_mat row by row,
+ * README.md:125-137). Applies to K-quant weights with contiguous rows, n_embd <= 4096,
+ * head_dim 64 / 128, the position's rope row staged with the inputs, and a KV cache whose
+ * attention LDS fits beside the weight ring. Returns the previous value. */
+int mi355x_backend_set_layer_engine(mi355x_backend_t backend, int enable);
+/* Non-zero when a persistent-layer launch since the last call gave up waiting for another
+ * workgroup (the device did not keep every workgroup resident): that graph's outputs are
+ * invalid. Clears the flag and re-arms the launches' counters. 0 without such launches. */
+int mi355x_backend_layer_error(mi355x_backend_t backend);
 /* Runs nodes in order on the backend stream. Consecutive MUL_MAT nodes with
  * ne11 == 1 that share src[1] are fused into one launch. When `use_graph` is
  * non-zero the launch sequence is captured once into a hipGraph and replayed
