@@ -1365,6 +1365,14 @@ int mi355x_gemv_waves(int waves) {
     return g_rows_waves.exchange(waves);
 }
 
+}  // extern "C"
+namespace kq {
+uint64_t *diag_stamps(int64_t *cap) {
+    if (cap) *cap = g_stamps_cap;
+    return g_stamps;
+}
+}  // namespace kq
+extern "C" {
 int mi355x_diag_stamps(void *buf, size_t bytes) {
     g_stamps = (uint64_t *)buf;
     g_stamps_cap = buf ? (int64_t)(bytes / 8) : 0;

@@ -45,6 +45,12 @@ struct mi355x_backend {
     uint32_t *ly_sync = nullptr;  // the persistent layers' counter blocks (zeroed at allocation), then err
     int ly_blocks = 0;
     std::vector<uint32_t> ly_sig;  // producers per edge and shard of every block: a change re-zeroes them
+    struct LyTab {                 // a block's step tables (kq::layer_table_fill), built for `key`
+        void *dev = nullptr;
+        int64_t stride = 0;
+        std::vector<uint64_t> key;
+    };
+    std::vector<LyTab> ly_tabs;
     ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
     bool loop_nocopy = false;   // emulated rank, timing only (MI355X_LOOPBACK_NOCOPY)
     int rank = 0, world = 0;
@@ -813,6 +819,9 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
         if (l.kind == 6) {  // a decode layer: one persistent launch
             kq::LayerArgs la = l.la;
             if (!b->ly_sync || l.ly_block >= b->ly_blocks) return MI355X_E_WORKSPACE;
+            if ((size_t)l.ly_block >= b->ly_tabs.size() || !b->ly_tabs[l.ly_block].dev) return MI355X_E_WORKSPACE;
+            la.tab = (const uint8_t *)b->ly_tabs[l.ly_block].dev;
+            la.tab_stride = b->ly_tabs[l.ly_block].stride;
             la.sync = b->ly_sync + (size_t)l.ly_block * kq::LAYER_SYNC_U32;
             la.err = (int *)(b->ly_sync + (size_t)b->ly_blocks * kq::LAYER_SYNC_U32);
             rc = kq::launch_layer(la, b->stream);
@@ -1068,6 +1077,8 @@ void mi355x_backend_free(mi355x_backend_t b) {
     if (b->workspace) hipFree(b->workspace);
     if (b->fx) hipFree(b->fx);
     if (b->ly_sync) hipFree(b->ly_sync);
+    for (auto &t : b->ly_tabs)
+        if (t.dev) hipFree(t.dev);
     if (b->comm) rccl().comm_destroy(b->comm);
     hipStreamDestroy(b->stream);
     }
@@ -1408,6 +1419,8 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
             drop_graph(b);
             if (nblk > b->ly_blocks) {
                 if (b->ly_sync) hipFree(b->ly_sync);
+    for (auto &t : b->ly_tabs)
+        if (t.dev) hipFree(t.dev);
                 b->ly_sync = nullptr;
                 b->ly_blocks = 0;
                 if (hipMalloc(&b->ly_sync, ((size_t)nblk * kq::LAYER_SYNC_U32 + 64) * 4) != hipSuccess)
@@ -1419,6 +1432,32 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
                 hipStreamSynchronize(b->stream) != hipSuccess)
                 return MI355X_E_WORKSPACE;
             b->ly_sig = sig;
+        }
+        // the step tables: built on the host once per (weights, shape) and kept
+        for (const Launch &l : launches) {
+            if (l.kind != 6) continue;
+            const kq::LayerArgs &la = l.la;
+            std::vector<uint64_t> key = {(uint64_t)la.G, (uint64_t)la.E, (uint64_t)la.F, (uint64_t)la.nq, (uint64_t)la.nkv};
+            for (int m = 0; m < 7; ++m) {
+                key.push_back((uint64_t)(uintptr_t)la.w[m]);
+                key.push_back((uint64_t)la.type[m]);
+            }
+            if ((size_t)l.ly_block >= b->ly_tabs.size()) b->ly_tabs.resize((size_t)l.ly_block + 1);
+            mi355x_backend::LyTab &tb = b->ly_tabs[l.ly_block];
+            if (tb.dev && tb.key == key) continue;
+            hipStreamSynchronize(b->stream);
+            drop_graph(b);  // a captured graph may read this block's old table
+            const int64_t stride = kq::layer_table_stride(la);
+            std::vector<uint8_t> host((size_t)(stride * la.G));
+            kq::layer_table_fill(la, host.data(), stride);
+            if (tb.dev) hipFree(tb.dev);
+            tb.dev = nullptr;
+            tb.key.clear();
+            if (hipMalloc(&tb.dev, host.size()) != hipSuccess) return MI355X_E_WORKSPACE;
+            if (hipMemcpy(tb.dev, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess)
+                return MI355X_E_WORKSPACE;
+            tb.stride = stride;
+            tb.key.swap(key);
         }
     }
     if (!use_graph) return enqueue(b, nodes, launches);

@@ -263,7 +263,11 @@ struct LayerArgs {
     int *err;                        // set when a wait timed out (co-residency lost): results invalid
     uint32_t expect[4][8];           // producers per edge and shard
     int D, slot;                     // ring slots per stream wave, bytes per slot
-    int o_aux, act_bytes, o_sums, o_res, o_tab, lds;  // LDS layout (ring at 0)
+    int o_aux, act_bytes, o_sums, o_res, lds;  // LDS layout (ring at 0)
+    const uint8_t *tab;              // every workgroup's step table (layer_table_fill), tab_stride bytes apart
+    int64_t tab_stride;
+    uint64_t *stamps;                // KQ_LAYER_STAMPS builds: 32 s_memrealtime stamps per workgroup
+    int64_t stamps_cap;
 };
 
 // ---------------------------------------------------------------- batched (prefill) MFMA GEMM

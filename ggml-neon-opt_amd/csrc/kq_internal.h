@@ -111,6 +111,9 @@ size_t attn_lds16(int hd, int n_ctx);  // attn_head's LDS per head, 16-B multipl
 // checks the shape and fills the rest (grid, attention placement, ring depth, LDS layout).
 int layer_plan(LayerArgs &a, int hd, int n_head);
 int launch_layer(const LayerArgs &a, hipStream_t stream);
+int64_t layer_table_stride(const LayerArgs &a);                  // bytes per workgroup's step lists (-1: too long)
+void layer_table_fill(const LayerArgs &a, uint8_t *buf, int64_t stride);  // G tables (host memory)
+uint64_t *diag_stamps(int64_t *cap);  // mi355x_diag_stamps' buffer (diagnostic builds)
 // kq_api.hip
 void allow_lds(const void *fn, size_t lds);
 // Experiment / diagnostic knobs of A/B runs. The product reads no environment: a knob

@@ -50,6 +50,24 @@ namespace kq {
 
 namespace {
 
+// Timing stamps (experiment builds only: make variant-layer NAME=lst VFLAGS=-DKQ_LAYER_STAMPS=1):
+// the control wave's lane 0 stores s_memrealtime at each phase boundary, slot i of
+// stamps[b * 32 + i] (tools/layer_stamps.py). The product build has none.
+#ifndef KQ_LAYER_STAMPS
+#define KQ_LAYER_STAMPS 0
+#endif
+#define LY_STAMP(i)                                                                                  \
+    do {                                                                                             \
+        if (KQ_LAYER_STAMPS && a.stamps && lane == 0 && (int64_t)b * 32 + (i) < a.stamps_cap)        \
+            a.stamps[(int64_t)b * 32 + (i)] = __builtin_amdgcn_s_memrealtime();                       \
+    } while (0)
+
+// Timing ablations (experiment builds only, outputs wrong): 1 no dot products in the stream
+// loop, 2 no weight DMA (the ring's stale bytes are used), 4 no wait for the weight DMA.
+#ifndef KQ_LAYER_DIAG
+#define KQ_LAYER_DIAG 0
+#endif
+
 constexpr int LY_STREAM = LAYER_WAVES - 1;  // stream waves 0..6; wave 7 is the control wave
 constexpr int LY_NI = 4;                    // DMA instructions per step, whatever its size
 constexpr int LY_POLL_LIMIT = 1 << 20;      // polls (with s_sleep) before a wait gives up (~1 s)
@@ -91,7 +109,7 @@ struct LySeg {
 struct LyRows {
     int qa, qb, ea, eb, fa, fb;  // [qa, qb) of [q | k | v], [ea, eb) of E, [fa, fb) of F
 };
-__device__ __forceinline__ LyRows ly_rows(const LayerArgs &a, int b) {
+__host__ __device__ __forceinline__ LyRows ly_rows(const LayerArgs &a, int b) {
     LyRows r;
     const int nqkv = a.nq + 2 * a.nkv;
     r.qa = (int)((int64_t)b * nqkv / a.G);
@@ -108,7 +126,7 @@ struct LyStage {
 };
 // Segment of matrix M: rows [row0, row0 + n) (n may be 0: an empty segment, no steps).
 template <int M>
-__device__ __forceinline__ LySeg ly_seg(const LayerArgs &a, int nb, int rbase, int row0, int n) {
+__host__ __device__ __forceinline__ LySeg ly_seg(const LayerArgs &a, int nb, int rbase, int row0, int n) {
     LySeg g;
     n = n > 0 ? n : 0;
     g.w = a.w[M];
@@ -124,7 +142,7 @@ __device__ __forceinline__ LySeg ly_seg(const LayerArgs &a, int nb, int rbase, i
 // The workgroup's segments of GEMV stage s (0 q/k/v, 1 o-proj, 2 gate/up, 3 down): always
 // three, the unused ones empty (no segment counter: a struct filled at a run-time index
 // would live in scratch).
-__device__ __forceinline__ void ly_stage(const LayerArgs &a, int s, const LyRows &rw, LyStage &st) {
+__host__ __device__ __forceinline__ void ly_stage(const LayerArgs &a, int s, const LyRows &rw, LyStage &st) {
     if (s == 0) {
         const int r0 = rw.qa, r1 = rw.qb;
         st.nb = a.nb_e;
@@ -151,56 +169,36 @@ __device__ __forceinline__ void ly_stage(const LayerArgs &a, int s, const LyRows
     st.T = st.s0.steps + st.s1.steps + st.s2.steps;
 }
 
-// ---------------------------------------------------------------- the workgroup's step table
-// Step j of stage s = 16 consecutive superblocks of one segment's stream (fewer at its end).
-// Every workgroup writes its table of steps once, at entry, lane-parallel (so the stream
-// waves' loop holds no stage geometry in scalar registers): 16 B per step in LDS,
-// {src16 (8 B), ngran | mis << 8 | type << 12 | cnt << 14 | sb0 << 19, rrow0}, where src16 is
-// the 16-B boundary below the step's first byte, mis the offset above it, ngran the 16-B
-// granules to fetch, (rrow0, sb0) the stage row and block of its first superblock. The
-// header (8 ints) holds T[s] and the table index of stage s's first step.
-constexpr int LY_HDR = 32;
-__device__ __forceinline__ int ly_tcode(int type) { return type == Q4_K ? 0 : type == Q5_K ? 1 : 2; }
+// ---------------------------------------------------------------- each stream wave's step list
+// Step = 16 consecutive superblocks of one segment's stream (fewer at its end). Stage s's
+// T steps of the workgroup go to stream wave w as [T*w/7, T*(w+1)/7). The host writes every
+// (workgroup, wave) list once per layer launch (layer_table_fill): a 16-B header
+// {count of stage 0, 1, 2, 3} and 16 B per step, {src16 (8 B), ngran | mis << 8 | type << 12 |
+// cnt << 14 | sb0 << 19, rrow0}: src16 is the 16-B boundary below the step's first byte, mis
+// the offset above it, ngran the 16-B granules to fetch, (rrow0, sb0) the stage row and
+// block of its first superblock. The wave loads its list into registers at entry (lane i
+// holds step i, and 64 + i) and reads a step with v_readlane: no memory access per step.
+constexpr int LY_LIST_MAX = 128;  // steps per wave and layer
+__host__ __device__ __forceinline__ int ly_tcode(int type) { return type == Q4_K ? 0 : type == Q5_K ? 1 : 2; }
 
-__device__ __forceinline__ void ly_build_table(const LayerArgs &a, const LyRows &rw, uint8_t *tab) {
-    int *const hdr = (int *)tab;
-    u32x4 *const ent = (u32x4 *)(tab + LY_HDR);
-    int base = 0;
-#pragma unroll
-    for (int s = 0; s < 4; ++s) {
-        LyStage st;
-        ly_stage(a, s, rw, st);
-        for (int j = (int)threadIdx.x; j < st.T; j += LAYER_WAVES * 64) {
-            const int k = j >= st.s0.steps ? (j >= st.s0.steps + st.s1.steps ? 2 : 1) : 0;
-            const int jj = k == 0 ? j : k == 1 ? j - st.s0.steps : j - st.s0.steps - st.s1.steps;
-            const uint8_t *w = k == 0 ? st.s0.w : k == 1 ? st.s1.w : st.s2.w;
-            const int type = k == 0 ? st.s0.type : k == 1 ? st.s1.type : st.s2.type;
-            const int row0 = k == 0 ? st.s0.row0 : k == 1 ? st.s1.row0 : st.s2.row0;
-            const int nrows = k == 0 ? st.s0.nrows : k == 1 ? st.s1.nrows : st.s2.nrows;
-            const int rbase = k == 0 ? st.s0.rbase : k == 1 ? st.s1.rbase : st.s2.rbase;
-            const int bsz = block_bytes(type);
-            const int g0 = ROWS_SB * jj;
-            const int G = nrows * st.nb;
-            const int cnt = G - g0 < ROWS_SB ? G - g0 : ROWS_SB;
-            const uint8_t *src = w + ((int64_t)row0 * st.nb + g0) * bsz;
-            const uint32_t mis = (uint32_t)((uintptr_t)src & 15u);
-            const uint64_t s16 = (uint64_t)(uintptr_t)(src - mis);
-            const int ngran = (int)((mis + (uint32_t)(cnt * bsz) + 15u) >> 4);
-            const int row = g0 / st.nb, sb0 = g0 - row * st.nb;
-            u32x4 e;
-            e.x = (uint32_t)s16;
-            e.y = (uint32_t)(s16 >> 32);
-            e.z = (uint32_t)ngran | (mis << 8) | ((uint32_t)ly_tcode(type) << 12) | ((uint32_t)cnt << 14) |
-                  ((uint32_t)sb0 << 19);
-            e.w = (uint32_t)(rbase + row);
-            ent[base + j] = e;
-        }
-        if (threadIdx.x == 0) {
-            hdr[s] = st.T;
-            hdr[4 + s] = base;
-        }
-        base += st.T;
-    }
+struct LyList {
+    u32x4 e0, e1;  // steps lane and 64 + lane
+    int c[4];      // steps of each stage
+    int n;
+};
+
+__device__ __forceinline__ void ly_list_load(const LayerArgs &a, int b, int w, int lane, LyList &L) {
+    const uint8_t *p = a.tab + (int64_t)b * a.tab_stride + (int64_t)w * (a.tab_stride / LY_STREAM);
+    const u32x4 h = *(const u32x4 *)p;
+    L.c[0] = __builtin_amdgcn_readfirstlane((int)h.x);
+    L.c[1] = __builtin_amdgcn_readfirstlane((int)h.y);
+    L.c[2] = __builtin_amdgcn_readfirstlane((int)h.z);
+    L.c[3] = __builtin_amdgcn_readfirstlane((int)h.w);
+    L.n = L.c[0] + L.c[1] + L.c[2] + L.c[3];
+    const u32x4 *e = (const u32x4 *)(p + 16);
+    const u32x4 z = {0u, 0u, 0u, 0u};
+    L.e0 = lane < L.n ? e[lane] : z;
+    L.e1 = 64 + lane < L.n ? e[64 + lane] : z;
 }
 
 struct LyStep {
@@ -208,11 +206,20 @@ struct LyStep {
     uint32_t mis;
     int ngran, type, cnt, rrow0, sb0;
 };
-__device__ __forceinline__ LyStep ly_step(const uint8_t *tab, int idx) {
-    const u32x4 e = *(const u32x4 *)(tab + LY_HDR + 16 * idx);
+__device__ __forceinline__ LyStep ly_step(const LyList &L, int idx) {
+    uint32_t lo, hi, z, w;
+    if (idx < 64) {
+        lo = __builtin_amdgcn_readlane(L.e0.x, idx);
+        hi = __builtin_amdgcn_readlane(L.e0.y, idx);
+        z = __builtin_amdgcn_readlane(L.e0.z, idx);
+        w = __builtin_amdgcn_readlane(L.e0.w, idx);
+    } else {
+        lo = __builtin_amdgcn_readlane(L.e1.x, idx - 64);
+        hi = __builtin_amdgcn_readlane(L.e1.y, idx - 64);
+        z = __builtin_amdgcn_readlane(L.e1.z, idx - 64);
+        w = __builtin_amdgcn_readlane(L.e1.w, idx - 64);
+    }
     LyStep d;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane(e.x), hi = __builtin_amdgcn_readfirstlane(e.y);
-    const uint32_t z = __builtin_amdgcn_readfirstlane(e.z);
     d.src16 = (const uint8_t *)(uintptr_t)(((uint64_t)hi << 32) | lo);
     d.ngran = (int)(z & 0xffu);
     d.mis = (z >> 8) & 15u;
@@ -220,18 +227,15 @@ __device__ __forceinline__ LyStep ly_step(const uint8_t *tab, int idx) {
     d.type = tc == 0 ? Q4_K : tc == 1 ? Q5_K : Q6_K;
     d.cnt = (int)((z >> 14) & 31u);
     d.sb0 = (int)((z >> 19) & 127u);
-    d.rrow0 = (int)__builtin_amdgcn_readfirstlane(e.w);
+    d.rrow0 = (int)w;
     d.last16 = d.src16 + 16 * (d.ngran - 1);
     return d;
 }
 
-// One LDS-DMA instruction (nt) for lanes [0, n) at LDS byte address m0 (both wave-uniform:
-// readfirstlane'd here, as the compiler cannot always prove it).
+// One LDS-DMA instruction (nt) for lanes [0, n) at LDS byte address m0 (wave-uniform).
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
 __device__ __forceinline__ void ly_dma(const void *src, uint32_t m0, int lane, int n) {
-    m0 = __builtin_amdgcn_readfirstlane(m0);
-    n = __builtin_amdgcn_readfirstlane(n);
     uint64_t save;
     asm volatile(
         "s_mov_b64 %0, exec\n\t"
@@ -242,16 +246,17 @@ __device__ __forceinline__ void ly_dma(const void *src, uint32_t m0, int lane, i
         "global_load_lds_dwordx4 %4, off nt\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(save)
-        : "s"(m0), "s"(n), "v"(lane), "v"(src)
+        : "s"(__builtin_amdgcn_readfirstlane(m0)), "s"(__builtin_amdgcn_readfirstlane(n)), "v"(lane), "v"(src)
         : "memory", "m0", "vcc");
 }
 #pragma clang diagnostic pop
 
-// The step's granules into a ring slot: exactly LY_NI DMA instructions on every path (an
-// instruction past the step's granules re-reads the last granule into its own place: the
-// same bytes, so the order in which the two land does not matter).
-__device__ __forceinline__ void ly_issue(const LyStep &d, uint8_t *slot, int lane) {
-    const uint32_t s0 = (uint32_t)(uintptr_t)(LDS void *)slot;
+// The step's granules into the ring at LDS byte address s0 (ngran * 16 bytes): exactly LY_NI
+// DMA instructions on every path (an instruction past the step's granules re-reads the last
+// granule into its own place: the same bytes, so the order in which the two land does not
+// matter).
+__device__ __forceinline__ void ly_issue(const LyStep &d, uint32_t s0, int lane) {
+    if (KQ_LAYER_DIAG & 2) return;
 #pragma unroll
     for (int i = 0; i < LY_NI; ++i) {
         const int n = d.ngran - 64 * i;
@@ -265,52 +270,60 @@ __device__ __forceinline__ void ly_issue(const LyStep &d, uint8_t *slot, int lan
 }
 
 // ---------------------------------------------------------------- one stream wave's ring
+// A byte ring of RB bytes per wave: a step takes exactly its ngran * 16 bytes, placed after
+// the previous one, or at the start when it would cross the end (the tail then idles until
+// the consumer passes it). Issue and consumption place the same steps by the same rule, so
+// the consumer finds each step where it was issued. At most LY_MAXQ steps in flight (the
+// counted wait covers 4 x (in flight - 1) DMA instructions).
+constexpr int LY_MAXQ = 10;
 struct LyRing {
-    uint8_t *base;
-    int is, ij, iend;  // next step to issue: stage, table index, end of this wave's steps there
-    int n_iss, n_con;  // steps issued / consumed
-    int islot, cslot;  // their ring slots
+    uint32_t base;    // LDS byte address of this wave's ring
+    int rb;           // its bytes
+    int ii;           // next list index to issue
+    int n_iss, n_con; // steps issued / consumed
+    int ipos, cpos, used;  // issue / consume byte positions, bytes held (steps + idle tails)
 };
 
-// this wave's table indices [j0, j1) of stage s
-__device__ __forceinline__ void ly_range(const uint8_t *tab, int s, int w, int &j0, int &j1) {
-    const int *hdr = (const int *)tab;
-    const int T = __builtin_amdgcn_readfirstlane(hdr[s]), base = __builtin_amdgcn_readfirstlane(hdr[4 + s]);
-    j0 = base + T * w / LY_STREAM;
-    j1 = base + T * (w + 1) / LY_STREAM;
-}
-
-// advance the issue pointer past stages where this wave has no steps
-__device__ __forceinline__ void ly_next_stage(const uint8_t *tab, LyRing &r, int w) {
-    while (r.is < 4 && r.ij >= r.iend) {
-        ++r.is;
-        if (r.is < 4) ly_range(tab, r.is, w, r.ij, r.iend);
-    }
-}
-
-__device__ __forceinline__ void ly_top_up(const LayerArgs &a, const uint8_t *tab, LyRing &r, int w, int lane) {
-    while (r.is < 4 && r.n_iss - r.n_con < a.D) {
-        const LyStep d = ly_step(tab, r.ij);
-        ly_issue(d, r.base + r.islot * a.slot, lane);
-        r.islot = r.islot + 1 == a.D ? 0 : r.islot + 1;
+__device__ __forceinline__ void ly_top_up(const LyList &L, LyRing &r, int lane) {
+    while (r.ii < L.n && r.n_iss - r.n_con < LY_MAXQ) {
+        const LyStep d = ly_step(L, r.ii);
+        const int B = d.ngran * 16;
+        const bool wrap = r.ipos + B > r.rb;  // (tail 0 when the last step ended at the ring's end)
+        const int tail = wrap ? r.rb - r.ipos : 0;
+        if (r.used + tail + B > r.rb) break;  // ring full
+        const int pos = wrap ? 0 : r.ipos;
+        ly_issue(d, r.base + (uint32_t)pos, lane);
+        r.used += tail + B;
+        r.ipos = pos + B;
         ++r.n_iss;
-        ++r.ij;
-        ly_next_stage(tab, r, w);
+        ++r.ii;
     }
 }
 
 // This wave's steps of stage s (nb superblocks per row, R stage rows in the workgroup):
 // each step's records into LDS (block-major [sb][row]).
-__device__ __forceinline__ void ly_consume(const LayerArgs &a, const uint8_t *tab, LyRing &r, int s, int nb, int R,
-                                          int w, int lane, const uint8_t *act, Rec *recs) {
-    int j0, j1;
-    ly_range(tab, s, w, j0, j1);
+__device__ __forceinline__ void ly_consume(const LyList &L, LyRing &r, int s, int nb, int R, int lane,
+                                          const uint8_t *smem, const uint8_t *act, Rec *recs) {
+    const int j0 = s == 0 ? 0 : s == 1 ? L.c[0] : s == 2 ? L.c[0] + L.c[1] : L.c[0] + L.c[1] + L.c[2];
+    const int j1 = j0 + (s == 0 ? L.c[0] : s == 1 ? L.c[1] : s == 2 ? L.c[2] : L.c[3]);
     const int q = lane >> 2, sl = lane & 3;
     for (int j = j0; j < j1; ++j) {
-        vm_wait_dyn(LY_NI * (r.n_iss - r.n_con - 1));  // this step's DMAs landed (younger ones may not)
-        const LyStep d = ly_step(tab, j);
-        const uint8_t *slot = r.base + r.cslot * a.slot;
-        if (q < d.cnt) {  // (uniform over the quad: DPP sums inside it)
+        if (!(KQ_LAYER_DIAG & 6)) vm_wait_dyn(LY_NI * (r.n_iss - r.n_con - 1));  // this step's DMAs landed (younger ones may not)
+        const LyStep d = ly_step(L, j);
+        const int B = d.ngran * 16;
+        const bool wrap = r.cpos + B > r.rb;
+        const int tail = wrap ? r.rb - r.cpos : 0;
+        const int pos = wrap ? 0 : r.cpos;
+        const uint8_t *slot = smem + (r.base - (uint32_t)(uintptr_t)(LDS void *)smem) + pos;
+        if ((KQ_LAYER_DIAG & 1) && q < d.cnt && sl == 0) {  // ablation: zero records, no dot products
+            int row = d.rrow0, sb = d.sb0 + q;
+            while (sb >= nb) {
+                sb -= nb;
+                ++row;
+            }
+            recs[sb * R + row] = Rec{0, 0, 0.f, 0.f};
+        }
+        if (!(KQ_LAYER_DIAG & 1) && q < d.cnt) {  // (uniform over the quad: DPP sums inside it)
             int row = d.rrow0, sb = d.sb0 + q;
             while (sb >= nb) {  // 16 consecutive superblocks span at most 16 / nb + 1 rows
                 sb -= nb;
@@ -340,9 +353,10 @@ __device__ __forceinline__ void ly_consume(const LayerArgs &a, const uint8_t *ta
                 recs[sb * R + row] = rec;
             }
         }
+        r.used -= tail + B;
+        r.cpos = pos + B;
         ++r.n_con;
-        r.cslot = r.cslot + 1 == a.D ? 0 : r.cslot + 1;
-        ly_top_up(a, tab, r, w, lane);
+        ly_top_up(L, r, lane);
     }
 }
 
@@ -371,17 +385,25 @@ __device__ __forceinline__ void ly_signal(const LayerArgs &a, int e, int b, int 
     if (lane == 0) __hip_atomic_fetch_add(cnt_of(a.sync, e, b & 7), 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// Row r's chain over its nb records, in superblock order (the reference's fp32 updates).
-__device__ __forceinline__ float ly_chain(const Rec *recs, int R, int nb, int r, int type) {
+// Row r's chain over its nb records, in superblock order (the reference's fp32 updates):
+// records read 8 ahead (independent LDS reads), the dependent fp32 updates after them.
+template <int TYPE>
+__device__ __forceinline__ float ly_chain_t(const Rec *recs, int R, int nb, int r) {
     float v = 0.f;
-    if (type == Q4_K) {
-        for (int i = 0; i < nb; ++i) v = chain_step(Q4_K, recs[i * R + r], v);
-    } else if (type == Q5_K) {
-        for (int i = 0; i < nb; ++i) v = chain_step(Q5_K, recs[i * R + r], v);
-    } else {
-        for (int i = 0; i < nb; ++i) v = chain_step(Q6_K, recs[i * R + r], v);
+    int i = 0;
+    for (; i + 8 <= nb; i += 8) {
+        Rec rc[8];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) rc[k] = recs[(i + k) * R + r];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v = chain_step(TYPE, rc[k], v);
     }
+    for (; i < nb; ++i) v = chain_step(TYPE, recs[i * R + r], v);
     return v;
+}
+__device__ __forceinline__ float ly_chain(const Rec *recs, int R, int nb, int r, int type) {
+    return type == Q4_K ? ly_chain_t<Q4_K>(recs, R, nb, r) : type == Q5_K ? ly_chain_t<Q5_K>(recs, R, nb, r)
+                                                                          : ly_chain_t<Q6_K>(recs, R, nb, r);
 }
 
 // ---------------------------------------------------------------- activation builds
@@ -395,7 +417,7 @@ __device__ __forceinline__ void ly_build(const float *src, int nb, const float *
                                          double *sums, int wave, int lane) {
     const __amdgpu_buffer_rsrc_t rs = rsrc_of(src, (uint32_t)nb * QK * 4u);
     const int np = (nb + 4 * LAYER_WAVES - 1) / (4 * LAYER_WAVES);  // passes (<= 2: nb <= 64)
-    u32x4 xv[2][4];
+    u32x4 xv[2][4], wv[2][4];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
         const int j = 4 * LAYER_WAVES * i + 4 * wave + (lane >> 4);
@@ -403,6 +425,11 @@ __device__ __forceinline__ void ly_build(const float *src, int nb, const float *
         if (i < np) {
 #pragma unroll
             for (int k = 0; k < 4; ++k) xv[i][k] = ld16_sc1(rs, (uint32_t)(jj * QK + 16 * (lane & 15) + 4 * k) * 4u);
+            if (NORM) {  // the norm weights with x: not behind the sum's barrier
+                const u32x4 *wp = (const u32x4 *)(norm_w + (int64_t)jj * QK + 16 * (lane & 15));
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wv[i][k] = wp[k];
+            }
         }
     }
     if (NORM) {
@@ -445,11 +472,8 @@ __device__ __forceinline__ void ly_build(const float *src, int nb, const float *
 #pragma unroll
         for (int i = 0; i < 2; ++i) {
             if (i >= np) continue;
-            const int j = 4 * LAYER_WAVES * i + 4 * wave + (lane >> 4);
-            const int jj = j < nb ? j : nb - 1;
-            const float *wp = norm_w + (int64_t)jj * QK + 16 * (lane & 15);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) xv[i][k] = normmul4(xv[i][k], *(const u32x4 *)(wp + 4 * k), scale);
+            for (int k = 0; k < 4; ++k) xv[i][k] = normmul4(xv[i][k], wv[i][k], scale);
         }
     }
 #pragma unroll
@@ -462,11 +486,12 @@ __device__ __forceinline__ void ly_build(const float *src, int nb, const float *
 
 // Stage 0's activation by the control wave alone (the stream waves are issuing the first
 // weight steps meanwhile): rms_norm(x) * attn_norm -> Q8L; x comes from the previous launch
-// (plain loads). nb <= 16: four passes of four superblocks, held in registers.
-__device__ __forceinline__ void ly_build0(const LayerArgs &a, uint8_t *act, double *sums, int lane) {
+// (plain loads). nb <= 16: four passes of four superblocks, held in registers. The loads are
+// issued at entry, ahead of every weight DMA of the workgroup (ly_load0, then a barrier):
+// behind the entry burst they took ~6 us.
+__device__ __forceinline__ void ly_load0(const LayerArgs &a, int lane, u32x4 (&xv)[4][4], u32x4 (&wv)[4][4]) {
     const int nb = a.nb_e;
     const int np = (nb + 3) / 4;
-    u32x4 xv[4][4], wv[4][4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (i < np) {
@@ -481,6 +506,12 @@ __device__ __forceinline__ void ly_build0(const LayerArgs &a, uint8_t *act, doub
             }
         }
     }
+}
+
+__device__ __forceinline__ void ly_quant0(const LayerArgs &a, uint8_t *act, double *sums, int lane,
+                                          const u32x4 (&xv)[4][4], const u32x4 (&wv)[4][4]) {
+    const int nb = a.nb_e;
+    const int np = (nb + 3) / 4;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         if (i >= np) continue;
@@ -531,31 +562,44 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
     const int ai = b / a.attn_stride;
     const bool attn_wg = ai < a.n_attn && b == ai * a.attn_stride + (ai & 7) % a.attn_stride;
     const LyRows rw = ly_rows(a, b);
-    uint8_t *const tab = smem + a.o_tab;
-    ly_build_table(a, rw, tab);
-    ly_bar();  // the step table
+    if (ctrl) LY_STAMP(0);
 
+    LyList L;
     LyRing ring;
-    ring.base = smem + wave * a.D * a.slot;
-    ring.n_iss = ring.n_con = 0;
-    ring.islot = ring.cslot = 0;
+    ring.rb = a.D * a.slot;
+    ring.base = (uint32_t)(uintptr_t)(LDS void *)smem + (uint32_t)(wave * ring.rb);
+    ring.ii = ring.n_iss = ring.n_con = 0;
+    ring.ipos = ring.cpos = ring.used = 0;
+    if (!ctrl) ly_list_load(a, b, wave, lane, L);
     uint32_t epoch = 0;
-    // ---- stage 0 (q/k/v): the stream waves issue their first steps at entry; the control
-    // wave builds the normed activation and stashes x of the rows it will add it to
-    if (!ctrl) {
-        ring.is = 0;
-        ly_range(tab, 0, wave, ring.ij, ring.iend);
-        ly_next_stage(tab, ring, wave);
-        ly_top_up(a, tab, ring, wave, lane);
-    } else {
+    // ---- stage 0 (q/k/v): the control wave's activation loads go first; then the stream
+    // waves issue their first steps while it builds the normed activation and stashes x of
+    // the rows it will add to
+    u32x4 xv[4][4], wv[4][4];
+    float xres = 0.f;
+    if (ctrl) {
+        ly_load0(a, lane, xv, wv);
+        if (lane < rw.eb - rw.ea) xres = a.x[rw.ea + lane];
         epoch = __builtin_amdgcn_readfirstlane(ld_sc1(a.sync));
-        ly_build0(a, act, sums, lane);
-        for (int r = lane; r < rw.eb - rw.ea; r += 64) res[r] = a.x[rw.ea + r];
+    }
+    ly_bar();  // A0: the activation requests are queued ahead of every weight DMA
+    if (!ctrl) {
+        ly_top_up(L, ring, lane);
+    } else {
+        if (KQ_LAYER_STAMPS) {  // the activation loads' latency (stamps builds only)
+            vm_wait<0>();
+            LY_STAMP(1);
+        }
+        ly_quant0(a, act, sums, lane, xv, wv);
+        if (lane < rw.eb - rw.ea) res[lane] = xres;
+        for (int r = lane + 64; r < rw.eb - rw.ea; r += 64) res[r] = a.x[rw.ea + r];
+        LY_STAMP(2);
     }
     ly_bar();  // B0: the Q8L activation in LDS
-    if (!ctrl) ly_consume(a, tab, ring, 0, a.nb_e, rw.qb - rw.qa, wave, lane, act, recs);
+    if (!ctrl) ly_consume(L, ring, 0, a.nb_e, rw.qb - rw.qa, lane, smem, act, recs);
     ly_bar();  // C0: every record of the workgroup's q/k/v rows
     if (ctrl) {
+        LY_STAMP(3);
         LyStage st;
         ly_stage(a, 0, rw, st);
         for (int r = lane; r < st.R; r += 64) {
@@ -568,11 +612,15 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
         }
         vm_wait<0>();
         ly_signal(a, 0, b, lane);
+        LY_STAMP(4);
     }
     // ---- attention (its workgroups only): heads [ai*hpw, ai*hpw + hpw), every thread
     if (attn_wg) {
-        if (!ctrl) ly_top_up(a, tab, ring, wave, lane);
-        else ly_poll(a, 0, epoch, lane);
+        if (!ctrl) ly_top_up(L, ring, lane);
+        else {
+            ly_poll(a, 0, epoch, lane);
+            LY_STAMP(5);
+        }
         ly_bar();  // A1: q / k / v of every head written
         constexpr int TPH = HD == 64 ? 128 : 256;
         const int hi = (int)threadIdx.x / TPH, t = (int)threadIdx.x % TPH;
@@ -580,17 +628,25 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
         attn_head<HD, TPH, 0, true, true>(a.at, h, t, smem + a.o_aux + hi * a.head_lds, a.att + (int64_t)h * HD, true);
         vm_wait<0>();  // this wave's sc1 output stores (and its weight DMAs) done
         ly_bar();      // D1
-        if (ctrl) ly_signal(a, 1, b, lane);
+        if (ctrl) {
+            ly_signal(a, 1, b, lane);
+            LY_STAMP(6);
+        }
     }
     // ---- stage 1: o-proj + x -> x1
-    if (!ctrl) ly_top_up(a, tab, ring, wave, lane);
-    else ly_poll(a, 1, epoch, lane);
+    if (!ctrl) ly_top_up(L, ring, lane);
+    else {
+        ly_poll(a, 1, epoch, lane);
+        LY_STAMP(7);
+    }
     ly_bar();  // A2
     ly_build<false>(a.att, a.nb_e, nullptr, 0.f, act, sums, wave, lane);
     ly_bar();  // B2
-    if (!ctrl) ly_consume(a, tab, ring, 1, a.nb_e, rw.eb - rw.ea, wave, lane, act, recs);
+    if (ctrl) LY_STAMP(8);
+    if (!ctrl) ly_consume(L, ring, 1, a.nb_e, rw.eb - rw.ea, lane, smem, act, recs);
     ly_bar();  // C2
     if (ctrl) {
+        LY_STAMP(9);
         LyStage st;
         ly_stage(a, 1, rw, st);
         for (int r = lane; r < st.R; r += 64) {
@@ -600,16 +656,22 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
         }
         vm_wait<0>();
         ly_signal(a, 2, b, lane);
+        LY_STAMP(10);
     }
     // ---- stage 2: ffn_norm(x1) -> gate / up -> SWIGLU -> h
-    if (!ctrl) ly_top_up(a, tab, ring, wave, lane);
-    else ly_poll(a, 2, epoch, lane);
+    if (!ctrl) ly_top_up(L, ring, lane);
+    else {
+        ly_poll(a, 2, epoch, lane);
+        LY_STAMP(11);
+    }
     ly_bar();  // A3
     ly_build<true>(a.x1, a.nb_e, a.ffn_norm, a.eps, act, sums, wave, lane);
     ly_bar();  // B3
-    if (!ctrl) ly_consume(a, tab, ring, 2, a.nb_e, 2 * (rw.fb - rw.fa), wave, lane, act, recs);
+    if (ctrl) LY_STAMP(12);
+    if (!ctrl) ly_consume(L, ring, 2, a.nb_e, 2 * (rw.fb - rw.fa), lane, smem, act, recs);
     ly_bar();  // C3
     if (ctrl) {
+        LY_STAMP(13);
         LyStage st;
         ly_stage(a, 2, rw, st);
         const int n = st.s0.nrows, r0 = st.s0.row0, n4 = a.F & ~3;
@@ -621,12 +683,14 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
         }
         vm_wait<0>();
         ly_signal(a, 3, b, lane);
+        LY_STAMP(14);
     }
     // ---- stage 3: down + x1 -> x2
     if (!ctrl) {
-        ly_top_up(a, tab, ring, wave, lane);
+        ly_top_up(L, ring, lane);
     } else {
         ly_poll(a, 3, epoch, lane);
+        LY_STAMP(15);
         // every workgroup has passed its last edge's arrival, so every one of them read
         // `epoch` at entry: the next launch of this block may count from epoch + 1
         if (b == 0 && lane == 0) __hip_atomic_store(a.sync, epoch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -634,13 +698,17 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
     ly_bar();  // A4
     ly_build<false>(a.h, a.nb_f, nullptr, 0.f, act, sums, wave, lane);
     ly_bar();  // B4
-    if (!ctrl) ly_consume(a, tab, ring, 3, a.nb_f, rw.eb - rw.ea, wave, lane, act, recs);
+    if (ctrl) LY_STAMP(16);
+    if (!ctrl) ly_consume(L, ring, 3, a.nb_f, rw.eb - rw.ea, lane, smem, act, recs);
     ly_bar();  // C4
     if (ctrl) {
+        LY_STAMP(17);
         LyStage st;
         ly_stage(a, 3, rw, st);
         for (int r = lane; r < st.R; r += 64)
             st_sc1(a.x2 + st.s0.row0 + r, ly_chain(recs, st.R, st.nb, r, st.s0.type) + res[r]);
+        vm_wait<0>();
+        LY_STAMP(18);
     }
 }
 
@@ -685,22 +753,18 @@ int layer_plan(LayerArgs &a, int hd, int n_head) {
     int64_t aux = (int64_t)a.act_bytes + recs * 16;
     const int64_t attn = (int64_t)a.hpw * a.head_lds;
     aux = aux > attn ? aux : attn;
-    // the step table: every stage's steps of the largest workgroup (+ a partial step per segment)
-    const int64_t steps = (int64_t)(R0 * a.nb_e + 15) / 16 + 3 + (int64_t)(R1 * a.nb_e + 15) / 16 + 1 +
-                          (int64_t)(R2 * a.nb_e + 15) / 16 + 2 + (int64_t)(R1 * a.nb_f + 15) / 16 + 1;
-    const int64_t tab = LY_HDR + 16 * steps;
-    const int64_t fixed = ((aux + 15) & ~(int64_t)15) + (int64_t)nb_max * 8 + (int64_t)R1 * 4 + tab + 64;
+    const int64_t fixed = ((aux + 15) & ~(int64_t)15) + (int64_t)nb_max * 8 + (int64_t)R1 * 4 + 64;
     const int64_t budget = 160 * 1024 - 16 - fixed;
     int D = (int)(budget / ((int64_t)LY_STREAM * a.slot));
     if (D > 10) D = 10;
     if (D < 2) return MI355X_E_UNSUPPORTED;
     a.D = D;
+    a.stamps = diag_stamps(&a.stamps_cap);
     const int ring = LY_STREAM * D * a.slot + 16;  // + slack for Q6_K's realigning reads
     a.o_aux = (ring + 15) & ~15;
     a.o_sums = a.o_aux + (int)((aux + 15) & ~(int64_t)15);
     a.o_res = a.o_sums + nb_max * 8;
-    a.o_tab = (a.o_res + R1 * 4 + 15) & ~15;
-    a.lds = a.o_tab + (int)tab + 16;
+    a.lds = a.o_res + R1 * 4 + 64;
     if (a.lds > 160 * 1024) return MI355X_E_UNSUPPORTED;
     // producers per edge and shard (shard = workgroup index & 7)
     memset(a.expect, 0, sizeof(a.expect));
@@ -713,10 +777,74 @@ int layer_plan(LayerArgs &a, int hd, int n_head) {
         const int b = i * a.attn_stride + (i & 7) % a.attn_stride;
         a.expect[1][b & 7] += 1;
     }
+    if (layer_table_stride(a) < 0) return MI355X_E_UNSUPPORTED;  // a wave's list past LY_LIST_MAX
     return MI355X_OK;
 }
 
+// Every (workgroup, stream wave) step list (see LyList): bytes per workgroup, LY_STREAM
+// lists of 16 + 16 x (the most steps any wave gets) bytes ...
+int64_t layer_table_stride(const LayerArgs &a) {
+    int most = 0;
+    for (int b = 0; b < a.G; ++b) {
+        const LyRows rw = ly_rows(a, b);
+        for (int w = 0; w < LY_STREAM; ++w) {
+            int n = 0;
+            for (int s = 0; s < 4; ++s) {
+                LyStage st;
+                ly_stage(a, s, rw, st);
+                n += st.T * (w + 1) / LY_STREAM - st.T * w / LY_STREAM;
+            }
+            most = n > most ? n : most;
+        }
+    }
+    if (most > LY_LIST_MAX) return -1;
+    return (int64_t)LY_STREAM * (16 + 16 * most);
+}
+
+// ... and the lists themselves (G x stride bytes at buf). Stage s's T steps of the
+// workgroup: wave w takes [T w / 7, T (w + 1) / 7), in stream order.
+void layer_table_fill(const LayerArgs &a, uint8_t *buf, int64_t stride) {
+    memset(buf, 0, (size_t)(a.G * stride));
+    const int64_t wstride = stride / LY_STREAM;
+    for (int b = 0; b < a.G; ++b) {
+        const LyRows rw = ly_rows(a, b);
+        for (int w = 0; w < LY_STREAM; ++w) {
+            uint8_t *list = buf + (int64_t)b * stride + (int64_t)w * wstride;
+            int32_t *hdr = (int32_t *)list;
+            uint32_t *ent = (uint32_t *)(list + 16);
+            int n = 0;
+            for (int s = 0; s < 4; ++s) {
+                LyStage st;
+                ly_stage(a, s, rw, st);
+                const int j0 = st.T * w / LY_STREAM, j1 = st.T * (w + 1) / LY_STREAM;
+                for (int j = j0; j < j1; ++j, ++n) {
+                    const int k = j >= st.s0.steps ? (j >= st.s0.steps + st.s1.steps ? 2 : 1) : 0;
+                    const LySeg g = k == 0 ? st.s0 : k == 1 ? st.s1 : st.s2;
+                    const int jj = k == 0 ? j : k == 1 ? j - st.s0.steps : j - st.s0.steps - st.s1.steps;
+                    const int bsz = block_bytes(g.type);
+                    const int g0 = ROWS_SB * jj;
+                    const int G = g.nrows * st.nb;
+                    const int cnt = G - g0 < ROWS_SB ? G - g0 : ROWS_SB;
+                    const uint8_t *src = g.w + ((int64_t)g.row0 * st.nb + g0) * bsz;
+                    const uint32_t mis = (uint32_t)((uintptr_t)src & 15u);
+                    const uint64_t s16 = (uint64_t)(uintptr_t)(src - mis);
+                    const uint32_t ngran = (mis + (uint32_t)(cnt * bsz) + 15u) >> 4;
+                    const int row = g0 / st.nb, sb0 = g0 - row * st.nb;
+                    uint32_t *e = ent + 4 * n;
+                    e[0] = (uint32_t)s16;
+                    e[1] = (uint32_t)(s16 >> 32);
+                    e[2] = ngran | (mis << 8) | ((uint32_t)ly_tcode(g.type) << 12) | ((uint32_t)cnt << 14) |
+                           ((uint32_t)sb0 << 19);
+                    e[3] = (uint32_t)(g.rbase + row);
+                }
+                hdr[s] = j1 - j0;
+            }
+        }
+    }
+}
+
 int launch_layer(const LayerArgs &a, hipStream_t stream) {
+    if (!a.tab || a.tab_stride <= 0) return MI355X_E_INVAL;
     const void *fn = a.at.head_dim == 64 ? (const void *)kq_layer<64> : (const void *)kq_layer<128>;
     allow_lds(fn, (size_t)a.lds);
     void *args[] = {const_cast<LayerArgs *>(&a)};
