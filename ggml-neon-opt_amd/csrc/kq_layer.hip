@@ -40,6 +40,8 @@
 // within ~1 s sets *err and gives up (never a hang; the backend reports it).
 #include <string.h>
 
+#include <vector>
+
 #include <hip/hip_ext.h>
 
 #include "kq_attn_head.h"
@@ -174,15 +176,20 @@ __host__ __device__ __forceinline__ void ly_stage(const LayerArgs &a, int s, con
 // T steps of the workgroup go to stream wave w as [T*w/7, T*(w+1)/7). The host writes every
 // (workgroup, wave) list once per layer launch (layer_table_fill): a 16-B header
 // {count of stage 0, 1, 2, 3} and 16 B per step, {src16 (8 B), ngran | mis << 8 | type << 12 |
-// cnt << 14 | sb0 << 19, rrow0}: src16 is the 16-B boundary below the step's first byte, mis
+// cnt << 14 | sb0 << 19, rrow0 | need << 8 | pos16 << 16}: src16 is the 16-B boundary below the step's first byte, mis
 // the offset above it, ngran the 16-B granules to fetch, (rrow0, sb0) the stage row and
-// block of its first superblock. The wave loads its list into registers at entry (lane i
-// holds step i, and 64 + i) and reads a step with v_readlane: no memory access per step.
-constexpr int LY_LIST_MAX = 128;  // steps per wave and layer
+// block of its first superblock; the last word also holds the step's place in the wave's
+// weight ring (pos16 << 16) and its issue gate (need << 8, see layer_table_fill). The wave
+// loads its list into registers at entry (lane i
+// holds step i) and reads a step with v_readlane: no memory access and no branch per step.
+// (Measured: the scalar bookkeeping of a step cost ~0.4 us when it branched on the list
+// half, looped over the row wrap and searched a 37-case wait switch, as much as the dot
+// products of the step's 16 superblocks.)
+constexpr int LY_LIST_MAX = 64;  // steps per wave and layer
 __host__ __device__ __forceinline__ int ly_tcode(int type) { return type == Q4_K ? 0 : type == Q5_K ? 1 : 2; }
 
 struct LyList {
-    u32x4 e0, e1;  // steps lane and 64 + lane
+    u32x4 e;       // step `lane`
     int c[4];      // steps of each stage
     int n;
 };
@@ -197,28 +204,17 @@ __device__ __forceinline__ void ly_list_load(const LayerArgs &a, int b, int w, i
     L.n = L.c[0] + L.c[1] + L.c[2] + L.c[3];
     const u32x4 *e = (const u32x4 *)(p + 16);
     const u32x4 z = {0u, 0u, 0u, 0u};
-    L.e0 = lane < L.n ? e[lane] : z;
-    L.e1 = 64 + lane < L.n ? e[64 + lane] : z;
+    L.e = lane < L.n ? e[lane] : z;
 }
 
 struct LyStep {
     const uint8_t *src16, *last16;
     uint32_t mis;
-    int ngran, type, cnt, rrow0, sb0;
+    int ngran, type, cnt, rrow0, sb0, pos;
 };
 __device__ __forceinline__ LyStep ly_step(const LyList &L, int idx) {
-    uint32_t lo, hi, z, w;
-    if (idx < 64) {
-        lo = __builtin_amdgcn_readlane(L.e0.x, idx);
-        hi = __builtin_amdgcn_readlane(L.e0.y, idx);
-        z = __builtin_amdgcn_readlane(L.e0.z, idx);
-        w = __builtin_amdgcn_readlane(L.e0.w, idx);
-    } else {
-        lo = __builtin_amdgcn_readlane(L.e1.x, idx - 64);
-        hi = __builtin_amdgcn_readlane(L.e1.y, idx - 64);
-        z = __builtin_amdgcn_readlane(L.e1.z, idx - 64);
-        w = __builtin_amdgcn_readlane(L.e1.w, idx - 64);
-    }
+    const uint32_t lo = __builtin_amdgcn_readlane(L.e.x, idx), hi = __builtin_amdgcn_readlane(L.e.y, idx);
+    const uint32_t z = __builtin_amdgcn_readlane(L.e.z, idx), w = __builtin_amdgcn_readlane(L.e.w, idx);
     LyStep d;
     d.src16 = (const uint8_t *)(uintptr_t)(((uint64_t)hi << 32) | lo);
     d.ngran = (int)(z & 0xffu);
@@ -227,26 +223,44 @@ __device__ __forceinline__ LyStep ly_step(const LyList &L, int idx) {
     d.type = tc == 0 ? Q4_K : tc == 1 ? Q5_K : Q6_K;
     d.cnt = (int)((z >> 14) & 31u);
     d.sb0 = (int)((z >> 19) & 127u);
-    d.rrow0 = (int)w;
+    d.rrow0 = (int)(w & 0xffu);
+    d.pos = (int)(w >> 16) * 16;
     d.last16 = d.src16 + 16 * (d.ngran - 1);
     return d;
 }
 
-// One LDS-DMA instruction (nt) for lanes [0, n) at LDS byte address m0 (wave-uniform).
+// LY_NI (4) LDS-DMA instructions (nt), instruction i for lanes [0, n[i]) at LDS byte address
+// m0[i]: one exec save / restore around the four.
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winline-asm"
-__device__ __forceinline__ void ly_dma(const void *src, uint32_t m0, int lane, int n) {
+__device__ __forceinline__ void ly_dma4(const void *const (&src)[4], const uint32_t (&m0)[4], const int (&n)[4], int lane) {
     uint64_t save;
     asm volatile(
         "s_mov_b64 %0, exec\n\t"
-        "v_cmp_gt_i32_e32 vcc, %2, %3\n\t"
-        "s_and_b64 exec, exec, vcc\n\t"
+        "v_cmp_gt_i32_e32 vcc, %5, %9\n\t"
+        "s_and_b64 exec, %0, vcc\n\t"
         "s_mov_b32 m0, %1\n\t"
         "s_nop 0\n\t"
-        "global_load_lds_dwordx4 %4, off nt\n\t"
+        "global_load_lds_dwordx4 %10, off nt\n\t"
+        "v_cmp_gt_i32_e32 vcc, %6, %9\n\t"
+        "s_and_b64 exec, %0, vcc\n\t"
+        "s_mov_b32 m0, %2\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %11, off nt\n\t"
+        "v_cmp_gt_i32_e32 vcc, %7, %9\n\t"
+        "s_and_b64 exec, %0, vcc\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %12, off nt\n\t"
+        "v_cmp_gt_i32_e32 vcc, %8, %9\n\t"
+        "s_and_b64 exec, %0, vcc\n\t"
+        "s_mov_b32 m0, %4\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %13, off nt\n\t"
         "s_mov_b64 exec, %0"
         : "=&s"(save)
-        : "s"(__builtin_amdgcn_readfirstlane(m0)), "s"(__builtin_amdgcn_readfirstlane(n)), "v"(lane), "v"(src)
+        : "s"(m0[0]), "s"(m0[1]), "s"(m0[2]), "s"(m0[3]), "s"(n[0]), "s"(n[1]), "s"(n[2]), "s"(n[3]), "v"(lane),
+          "v"(src[0]), "v"(src[1]), "v"(src[2]), "v"(src[3])
         : "memory", "m0", "vcc");
 }
 #pragma clang diagnostic pop
@@ -257,16 +271,18 @@ __device__ __forceinline__ void ly_dma(const void *src, uint32_t m0, int lane, i
 // matter).
 __device__ __forceinline__ void ly_issue(const LyStep &d, uint32_t s0, int lane) {
     if (KQ_LAYER_DIAG & 2) return;
+    const void *src[LY_NI];
+    uint32_t m0[LY_NI];
+    int n[LY_NI];
 #pragma unroll
     for (int i = 0; i < LY_NI; ++i) {
-        const int n = d.ngran - 64 * i;
-        if (n > 0) {
-            const uint8_t *p = d.src16 + 1024 * i + 16 * lane;
-            ly_dma(p < d.last16 ? p : d.last16, s0 + 1024 * i, lane, n < 64 ? n : 64);
-        } else {
-            ly_dma(d.last16, s0 + 16 * (d.ngran - 1), lane, 1);
-        }
+        const int k = d.ngran - 64 * i;
+        const uint8_t *p = d.src16 + 1024 * i + 16 * lane;
+        src[i] = k > 0 ? (const void *)(p < d.last16 ? p : d.last16) : (const void *)d.last16;
+        m0[i] = __builtin_amdgcn_readfirstlane(k > 0 ? s0 + 1024u * (uint32_t)i : s0 + 16u * (uint32_t)(d.ngran - 1));
+        n[i] = __builtin_amdgcn_readfirstlane(k > 0 ? (k < 64 ? k : 64) : 1);
     }
+    ly_dma4(src, m0, n, lane);
 }
 
 // ---------------------------------------------------------------- one stream wave's ring
@@ -276,26 +292,35 @@ __device__ __forceinline__ void ly_issue(const LyStep &d, uint32_t s0, int lane)
 // the consumer finds each step where it was issued. At most LY_MAXQ steps in flight (the
 // counted wait covers 4 x (in flight - 1) DMA instructions).
 constexpr int LY_MAXQ = 10;
+// s_waitcnt until at most k younger steps' DMAs (LY_NI each) are in flight, 0 <= k < LY_MAXQ
+__device__ __forceinline__ void ly_wait(int k) {
+    switch (k) {
+        case 0: vm_wait<0>(); break;
+        case 1: vm_wait<LY_NI>(); break;
+        case 2: vm_wait<2 * LY_NI>(); break;
+        case 3: vm_wait<3 * LY_NI>(); break;
+        case 4: vm_wait<4 * LY_NI>(); break;
+        case 5: vm_wait<5 * LY_NI>(); break;
+        case 6: vm_wait<6 * LY_NI>(); break;
+        case 7: vm_wait<7 * LY_NI>(); break;
+        case 8: vm_wait<8 * LY_NI>(); break;
+        default: vm_wait<9 * LY_NI>(); break;
+    }
+}
 struct LyRing {
-    uint32_t base;    // LDS byte address of this wave's ring
-    int rb;           // its bytes
-    int ii;           // next list index to issue
-    int n_iss, n_con; // steps issued / consumed
-    int ipos, cpos, used;  // issue / consume byte positions, bytes held (steps + idle tails)
+    uint32_t base;  // LDS byte address of this wave's ring
+    int ii;         // steps issued (the next list index to issue)
+    int nc;         // steps consumed
 };
 
+// Issue every step whose gate has opened: step k may go once `need` (its list field) steps
+// are consumed, the host's placement (layer_table_fill) having checked that it then
+// overwrites nothing still held and that at most LY_MAXQ steps are in flight.
 __device__ __forceinline__ void ly_top_up(const LyList &L, LyRing &r, int lane) {
-    while (r.ii < L.n && r.n_iss - r.n_con < LY_MAXQ) {
-        const LyStep d = ly_step(L, r.ii);
-        const int B = d.ngran * 16;
-        const bool wrap = r.ipos + B > r.rb;  // (tail 0 when the last step ended at the ring's end)
-        const int tail = wrap ? r.rb - r.ipos : 0;
-        if (r.used + tail + B > r.rb) break;  // ring full
-        const int pos = wrap ? 0 : r.ipos;
-        ly_issue(d, r.base + (uint32_t)pos, lane);
-        r.used += tail + B;
-        r.ipos = pos + B;
-        ++r.n_iss;
+    while (r.ii < L.n) {
+        const uint32_t w = __builtin_amdgcn_readlane(L.e.w, r.ii);
+        if ((int)((w >> 8) & 0xffu) > r.nc) break;
+        ly_issue(ly_step(L, r.ii), r.base + ((w >> 16) << 4), lane);
         ++r.ii;
     }
 }
@@ -303,32 +328,21 @@ __device__ __forceinline__ void ly_top_up(const LyList &L, LyRing &r, int lane) 
 // This wave's steps of stage s (nb superblocks per row, R stage rows in the workgroup):
 // each step's records into LDS (block-major [sb][row]).
 __device__ __forceinline__ void ly_consume(const LyList &L, LyRing &r, int s, int nb, int R, int lane,
-                                          const uint8_t *smem, const uint8_t *act, Rec *recs) {
+                                          const uint8_t *smem, const uint8_t *act, Rec *recs, uint64_t *stp = nullptr) {
     const int j0 = s == 0 ? 0 : s == 1 ? L.c[0] : s == 2 ? L.c[0] + L.c[1] : L.c[0] + L.c[1] + L.c[2];
     const int j1 = j0 + (s == 0 ? L.c[0] : s == 1 ? L.c[1] : s == 2 ? L.c[2] : L.c[3]);
     const int q = lane >> 2, sl = lane & 3;
+    const uint32_t inv_nb = (65536u + (uint32_t)nb - 1u) / (uint32_t)nb;  // (x * inv_nb) >> 16 == x / nb for x < 128
     for (int j = j0; j < j1; ++j) {
-        if (!(KQ_LAYER_DIAG & 6)) vm_wait_dyn(LY_NI * (r.n_iss - r.n_con - 1));  // this step's DMAs landed (younger ones may not)
+        if (KQ_LAYER_STAMPS && stp && lane == 0 && j - j0 < 12) stp[j - j0] = __builtin_amdgcn_s_memrealtime();
+        if (!(KQ_LAYER_DIAG & 6)) ly_wait(r.ii - j - 1);  // this step's DMAs landed (younger ones may not)
         const LyStep d = ly_step(L, j);
-        const int B = d.ngran * 16;
-        const bool wrap = r.cpos + B > r.rb;
-        const int tail = wrap ? r.rb - r.cpos : 0;
-        const int pos = wrap ? 0 : r.cpos;
-        const uint8_t *slot = smem + (r.base - (uint32_t)(uintptr_t)(LDS void *)smem) + pos;
-        if ((KQ_LAYER_DIAG & 1) && q < d.cnt && sl == 0) {  // ablation: zero records, no dot products
-            int row = d.rrow0, sb = d.sb0 + q;
-            while (sb >= nb) {
-                sb -= nb;
-                ++row;
-            }
-            recs[sb * R + row] = Rec{0, 0, 0.f, 0.f};
-        }
+        const uint8_t *slot = smem + (r.base - (uint32_t)(uintptr_t)(LDS void *)smem) + d.pos;
+        // this quad's superblock: 16 consecutive ones span at most 16 / nb + 1 rows
+        const int sbq = d.sb0 + q, dr = (int)(((uint32_t)sbq * inv_nb) >> 16);
+        const int row = d.rrow0 + dr, sb = sbq - dr * nb;
+        if ((KQ_LAYER_DIAG & 1) && q < d.cnt && sl == 0) recs[sb * R + row] = Rec{0, 0, 0.f, 0.f};  // ablation
         if (!(KQ_LAYER_DIAG & 1) && q < d.cnt) {  // (uniform over the quad: DPP sums inside it)
-            int row = d.rrow0, sb = d.sb0 + q;
-            while (sb >= nb) {  // 16 consecutive superblocks span at most 16 / nb + 1 rows
-                sb -= nb;
-                ++row;
-            }
             const int bsz = block_bytes(d.type);
             const uint8_t *blk = slot + d.mis + q * bsz;
             const uint8_t *ab = act + sb * Q8L_STRIDE;
@@ -353,9 +367,7 @@ __device__ __forceinline__ void ly_consume(const LyList &L, LyRing &r, int s, in
                 recs[sb * R + row] = rec;
             }
         }
-        r.used -= tail + B;
-        r.cpos = pos + B;
-        ++r.n_con;
+        r.nc = j + 1;
         ly_top_up(L, r, lane);
     }
 }
@@ -508,8 +520,10 @@ __device__ __forceinline__ void ly_load0(const LayerArgs &a, int lane, u32x4 (&x
     }
 }
 
-__device__ __forceinline__ void ly_quant0(const LayerArgs &a, uint8_t *act, double *sums, int lane,
-                                          const u32x4 (&xv)[4][4], const u32x4 (&wv)[4][4]) {
+// ... the sum, the scale and (x * scale) * w into `stg` (nb x 256 floats, superblock-major);
+// the Q8L blocks are then made by every wave (ly_quant0_all) after a barrier.
+__device__ __forceinline__ void ly_norm0(const LayerArgs &a, uint8_t *stg, double *sums, int lane,
+                                         const u32x4 (&xv)[4][4], const u32x4 (&wv)[4][4]) {
     const int nb = a.nb_e;
     const int np = (nb + 3) / 4;
 #pragma unroll
@@ -539,10 +553,23 @@ __device__ __forceinline__ void ly_quant0(const LayerArgs &a, uint8_t *act, doub
     for (int i = 0; i < 4; ++i) {
         if (i >= np) continue;
         const int j = 4 * i + (lane >> 4);
+        if (j < nb) {
+            u32x4 *d = (u32x4 *)(stg + j * (QK * 4) + 64 * (lane & 15));
+#pragma unroll
+            for (int k = 0; k < 4; ++k) d[k] = normmul4(xv[i][k], wv[i][k], scale);
+        }
+    }
+}
+
+// staged floats -> Q8L blocks: wave w, lane l: superblock 4 w + (l >> 4) (nb <= 16: one pass)
+__device__ __forceinline__ void ly_quant0_all(int nb, const uint8_t *stg, uint8_t *act, int wave, int lane) {
+    const int j = 4 * wave + (lane >> 4);
+    if (j < nb) {
+        const u32x4 *sp = (const u32x4 *)(stg + j * (QK * 4) + 64 * (lane & 15));
         u32x4 v[4];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = normmul4(xv[i][k], wv[i][k], scale);
-        if (j < nb) quant16_store(v, lane & 15, act + j * Q8L_STRIDE);
+        for (int k = 0; k < 4; ++k) v[k] = sp[k];
+        quant16_store(v, lane & 15, act + j * Q8L_STRIDE);
     }
 }
 
@@ -566,10 +593,8 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
 
     LyList L;
     LyRing ring;
-    ring.rb = a.D * a.slot;
-    ring.base = (uint32_t)(uintptr_t)(LDS void *)smem + (uint32_t)(wave * ring.rb);
-    ring.ii = ring.n_iss = ring.n_con = 0;
-    ring.ipos = ring.cpos = ring.used = 0;
+    ring.base = (uint32_t)(uintptr_t)(LDS void *)smem + (uint32_t)(wave * a.D * a.slot);
+    ring.ii = ring.nc = 0;
     if (!ctrl) ly_list_load(a, b, wave, lane, L);
     uint32_t epoch = 0;
     // ---- stage 0 (q/k/v): the control wave's activation loads go first; then the stream
@@ -590,11 +615,15 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
             vm_wait<0>();
             LY_STAMP(1);
         }
-        ly_quant0(a, act, sums, lane, xv, wv);
+        ly_norm0(a, (uint8_t *)recs, sums, lane, xv, wv);
         if (lane < rw.eb - rw.ea) res[lane] = xres;
         for (int r = lane + 64; r < rw.eb - rw.ea; r += 64) res[r] = a.x[rw.ea + r];
-        LY_STAMP(2);
     }
+    ly_bar();  // S0: the normed activation staged (in the records' space)
+    // (a wave with a quad-quarter j >= nb has nothing to do; the quant needs every lane of
+    // its 16-lane row, which ly_quant0_all's uniform-per-row condition keeps)
+    ly_quant0_all(a.nb_e, (const uint8_t *)recs, act, wave, lane);
+    if (ctrl) LY_STAMP(2);
     ly_bar();  // B0: the Q8L activation in LDS
     if (!ctrl) ly_consume(L, ring, 0, a.nb_e, rw.qb - rw.qa, lane, smem, act, recs);
     ly_bar();  // C0: every record of the workgroup's q/k/v rows
@@ -668,7 +697,9 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
     ly_build<true>(a.x1, a.nb_e, a.ffn_norm, a.eps, act, sums, wave, lane);
     ly_bar();  // B3
     if (ctrl) LY_STAMP(12);
-    if (!ctrl) ly_consume(L, ring, 2, a.nb_e, 2 * (rw.fb - rw.fa), lane, smem, act, recs);
+    if (!ctrl)
+        ly_consume(L, ring, 2, a.nb_e, 2 * (rw.fb - rw.fa), lane, smem, act, recs,
+                   KQ_LAYER_STAMPS && a.stamps && wave == 0 && (int64_t)b * 32 + 32 <= a.stamps_cap ? a.stamps + (int64_t)b * 32 + 20 : nullptr);
     ly_bar();  // C3
     if (ctrl) {
         LY_STAMP(13);
@@ -743,10 +774,12 @@ int layer_plan(LayerArgs &a, int hd, int n_head) {
     // workgroup rows (the most any workgroup gets) and the records they need
     auto cdiv = [](int64_t x, int64_t y) { return (int)((x + y - 1) / y); };
     const int R0 = cdiv(a.nq + 2 * a.nkv, G) + 2, R1 = cdiv(a.E, G), R2 = 2 * cdiv(a.F, G);
+    if (R0 > 255 || R1 > 255 || R2 > 255) return MI355X_E_UNSUPPORTED;  // a step's row field: 8 bits
     int64_t recs = (int64_t)R0 * a.nb_e;
     recs = recs > (int64_t)R1 * a.nb_e ? recs : (int64_t)R1 * a.nb_e;
     recs = recs > (int64_t)R2 * a.nb_e ? recs : (int64_t)R2 * a.nb_e;
     recs = recs > (int64_t)R1 * a.nb_f ? recs : (int64_t)R1 * a.nb_f;
+    recs = recs > (int64_t)a.nb_e * QK * 4 / 16 ? recs : (int64_t)a.nb_e * QK * 4 / 16;  // stage 0's staged floats
     const int nb_max = a.nb_e > a.nb_f ? a.nb_e : a.nb_f;
     a.act_bytes = nb_max * Q8L_STRIDE;
     a.head_lds = (int)attn_lds16(hd, a.at.n_ctx);
@@ -813,6 +846,13 @@ void layer_table_fill(const LayerArgs &a, uint8_t *buf, int64_t stride) {
             int32_t *hdr = (int32_t *)list;
             uint32_t *ent = (uint32_t *)(list + 16);
             int n = 0;
+            // the wave's byte ring: a step takes its ngran * 16 bytes after the previous one,
+            // or from 0 when it would cross the end (the tail idles until consumed past);
+            // held[k] = its bytes plus that tail. Step k may issue once steps [0, need) are
+            // consumed: the held bytes of need..k fit the ring, and k - need < LY_MAXQ.
+            const int rb = a.D * a.slot;
+            int end = 0;
+            std::vector<int> held;
             for (int s = 0; s < 4; ++s) {
                 LyStage st;
                 ly_stage(a, s, rw, st);
@@ -830,12 +870,25 @@ void layer_table_fill(const LayerArgs &a, uint8_t *buf, int64_t stride) {
                     const uint64_t s16 = (uint64_t)(uintptr_t)(src - mis);
                     const uint32_t ngran = (mis + (uint32_t)(cnt * bsz) + 15u) >> 4;
                     const int row = g0 / st.nb, sb0 = g0 - row * st.nb;
+                    const int B = (int)ngran * 16;
+                    const bool wrap = end + B > rb;
+                    const int pos = wrap ? 0 : end;
+                    held.push_back((wrap ? rb - end : 0) + B);
+                    end = pos + B;
+                    int need = n + 1 - LY_MAXQ > 0 ? n + 1 - LY_MAXQ : 0, sum = 0;
+                    for (int k = n; k >= need; --k) {
+                        if (sum + held[k] > rb) {
+                            need = k + 1;
+                            break;
+                        }
+                        sum += held[k];
+                    }
                     uint32_t *e = ent + 4 * n;
                     e[0] = (uint32_t)s16;
                     e[1] = (uint32_t)(s16 >> 32);
                     e[2] = ngran | (mis << 8) | ((uint32_t)ly_tcode(g.type) << 12) | ((uint32_t)cnt << 14) |
                            ((uint32_t)sb0 << 19);
-                    e[3] = (uint32_t)(g.rbase + row);
+                    e[3] = (uint32_t)(g.rbase + row) | ((uint32_t)need << 8) | ((uint32_t)(pos >> 4) << 16);
                 }
                 hdr[s] = j1 - j0;
             }

@@ -52,7 +52,8 @@ def main():
         tk.dec.step(tk.tokens[4 + t], 4 + t, use_graph=False)
         be.synchronize()
         g.lib().mi355x_diag_stamps(None, 0)
-        s = buf.cpu().numpy().reshape(G, 32)[:, :19].astype(np.int64)
+        full = buf.cpu().numpy().reshape(G, 32).astype(np.int64)
+        s = full[:, :19]
         t0 = s[:, 0][s[:, 0] > 0].min()
         rel = np.where(s > 0, (s - t0) / 100.0, np.nan)  # 100 MHz -> us
         row = {}
@@ -61,6 +62,10 @@ def main():
             col = col[~np.isnan(col)]
             if col.size:
                 row[nm] = (round(float(np.median(col)), 2), round(float(col.max()), 2), int(col.size))
+        # slots 20..31: stream wave 0's first 12 gate/up steps (start of each)
+        st = full[:, 20:32].astype(np.float64)
+        d = np.diff(np.where(st > 0, st, np.nan), axis=1) / 100.0
+        row["gate/up step us"] = [round(float(v), 3) for v in np.nanmedian(d, axis=0)] if np.isfinite(d).any() else []
         out.append(row)
     assert be.layer_error() == 0
     print(json.dumps({"model": args.model, "layers": L, "note": "last layer of each eager token; (median, max, n) us",
@@ -71,6 +76,7 @@ def main():
             med = np.median([v[0] for v in vals])
             mx = np.median([v[1] for v in vals])
             print(f"{nm:8s} median {med:7.2f} us   max {mx:7.2f} us   (workgroups {vals[0][2]})")
+    print("gate/up per-step (stream wave 0, median over workgroups):", out[-1].get("gate/up step us"))
 
 
 if __name__ == "__main__":
