@@ -292,6 +292,7 @@ __device__ __forceinline__ void ly_issue(const LyStep &d, uint32_t s0, int lane)
 // the consumer finds each step where it was issued. At most LY_MAXQ steps in flight (the
 // counted wait covers 4 x (in flight - 1) DMA instructions).
 constexpr int LY_MAXQ = 10;
+constexpr int LY_PRE = 2;  // steps a stream wave issues before the stage-0 activation barriers
 // s_waitcnt until at most k younger steps' DMAs (LY_NI each) are in flight, 0 <= k < LY_MAXQ
 __device__ __forceinline__ void ly_wait(int k) {
     switch (k) {
@@ -316,8 +317,8 @@ struct LyRing {
 // Issue every step whose gate has opened: step k may go once `need` (its list field) steps
 // are consumed, the host's placement (layer_table_fill) having checked that it then
 // overwrites nothing still held and that at most LY_MAXQ steps are in flight.
-__device__ __forceinline__ void ly_top_up(const LyList &L, LyRing &r, int lane) {
-    while (r.ii < L.n) {
+__device__ __forceinline__ void ly_top_up(const LyList &L, LyRing &r, int lane, int most = LY_LIST_MAX) {
+    while (r.ii < L.n && r.ii < most) {
         const uint32_t w = __builtin_amdgcn_readlane(L.e.w, r.ii);
         if ((int)((w >> 8) & 0xffu) > r.nc) break;
         ly_issue(ly_step(L, r.ii), r.base + ((w >> 16) << 4), lane);
@@ -608,8 +609,12 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
         epoch = __builtin_amdgcn_readfirstlane(ld_sc1(a.sync));
     }
     ly_bar();  // A0: the activation requests are queued ahead of every weight DMA
+    // Before the stage-0 barriers the stream waves issue only LY_PRE steps: a whole ring
+    // issued there stalls on the memory queue's back-pressure and holds the barrier (stamps:
+    // the activation +2.7 us at 8B, +4.9 us at TinyLlama). The rest goes out after the
+    // staging barrier, by the waves without a superblock to quantize first.
     if (!ctrl) {
-        ly_top_up(L, ring, lane);
+        ly_top_up(L, ring, lane, LY_PRE);
     } else {
         if (KQ_LAYER_STAMPS) {  // the activation loads' latency (stamps builds only)
             vm_wait<0>();
@@ -622,7 +627,10 @@ __global__ void __launch_bounds__(LAYER_WAVES * 64) kq_layer(const LayerArgs a) 
     ly_bar();  // S0: the normed activation staged (in the records' space)
     // (a wave with a quad-quarter j >= nb has nothing to do; the quant needs every lane of
     // its 16-lane row, which ly_quant0_all's uniform-per-row condition keeps)
+    const bool quants = 4 * wave < a.nb_e;
+    if (!ctrl && !quants) ly_top_up(L, ring, lane);
     ly_quant0_all(a.nb_e, (const uint8_t *)recs, act, wave, lane);
+    if (!ctrl && quants) ly_top_up(L, ring, lane);
     if (ctrl) LY_STAMP(2);
     ly_bar();  // B0: the Q8L activation in LDS
     if (!ctrl) ly_consume(L, ring, 0, a.nb_e, rw.qb - rw.qa, lane, smem, act, recs);
