@@ -53,6 +53,19 @@ __device__ __forceinline__ float adiag_finite(uint32_t bits) { return __uint_as_
 #ifndef KQ_ATTN_VPOST
 #define KQ_ATTN_VPOST 2
 #endif
+// V-cache iterations (32 cells each) requested together in KQV, past the prefetched ones
+#ifndef KQ_ATTN_VB
+#define KQ_ATTN_VB 8
+#endif
+#ifndef KQ_ATTN_VB64  // head_dim 64: half the registers per K row, twice the batch
+#define KQ_ATTN_VB64 8
+#endif
+#ifndef KQ_ATTN_KR64
+#define KQ_ATTN_KR64 2
+#endif
+#ifndef KQ_ATTN_VLDS  // 1: experiment build with the LDS-staged V rows (launch_attn): measured neutral
+#define KQ_ATTN_VLDS 0
+#endif
 #if KQ_ATTN_DIAG
 #define ADIAG(a) ((a).diag)
 #else
@@ -72,6 +85,32 @@ __device__ __forceinline__ float adiag_finite(uint32_t bits) { return __uint_as_
 // outputs likewise, KQ_ROWS_YSC1).
 // SC1_IN: q / k / v were written in this launch by other workgroups (the persistent layer,
 // kq_layer.hip): every load of them is an agent-scope (sc1) load, as the hand-off requires.
+// One LDS-DMA instruction (default cache policy: the V cache is re-read token after token)
+// for lanes [0, n) at LDS byte address m0 (wave-uniform), the lane mask set inside the asm.
+#pragma clang diagnostic push
+#pragma clang diagnostic ignored "-Winline-asm"
+__device__ __forceinline__ void attn_dma16_lanes(const void *src, uint32_t m0, int lane, int n) {
+    uint64_t save;
+    asm volatile(
+        "s_mov_b64 %0, exec\n\t"
+        "v_cmp_gt_i32_e32 vcc, %2, %3\n\t"
+        "s_and_b64 exec, exec, vcc\n\t"
+        "s_mov_b32 m0, %1\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %4, off\n\t"
+        "s_mov_b64 exec, %0"
+        : "=&s"(save)
+        : "s"(m0), "s"(n), "v"(lane), "v"(src)
+        : "memory", "m0", "vcc");
+}
+#pragma clang diagnostic pop
+
+// attn_lds (kq_ops.hip) on the device: the per-head LDS layout below, before any staged V rows
+__device__ __forceinline__ int attn_lds_dev(int hd, int n_ctx) {
+    const int gsum = (n_ctx / 4) * 8 <= hd * 64 ? 0 : (n_ctx / 4) * 8;
+    return 6 * hd + n_ctx * 6 + hd * 64 + 16 + gsum;
+}
+
 template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false, bool SC1_IN = false>
 __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8_t *smem, float *out,
                                           bool may_write) {
@@ -82,10 +121,17 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     static_assert(HD == 64 || HD == 128, "head_dim");
     constexpr int KV4 = HD / 8;          // 16-B pieces of one K-cache row
     static_assert(TPH == 256 || (TPH == 128 && HD == 64), "threads per head");
+    // the standalone kernel batches its cache loads (KR K rows per round, 1-2 x KQ_ATTN_VB V chunks);
+    // the fused kernels' register budgets keep one K row and 4 V chunks (PAIR off)
+    constexpr bool PAIR = TPH == 256 && !SC1_IN;
+    constexpr int VB = PAIR ? (HD == 64 ? KQ_ATTN_VB64 : KQ_ATTN_VB) : 4;
+    constexpr int KR = HD == 64 ? KQ_ATTN_KR64 : 2;  // K rows per thread per round (register budget)
     constexpr int ITEMS = HD * 4 / TPH;  // KQV (d, j) items per thread
     constexpr int VPF = VPF0 > 0 ? VPF0 : KQ_ATTN_PFC > 0 ? (KQ_ATTN_PFC / 32 < 8 / ITEMS ? KQ_ATTN_PFC / 32 : 8 / ITEMS)
                                                          : 8 / ITEMS;  // prefetched 32-cell iterations per item
     constexpr int KPF = KQ_ATTN_PFC > 0 && KQ_ATTN_PFC < TPH ? KQ_ATTN_PFC : TPH;  // K rows prefetched (thread t < KPF)
+    static_assert(VPF + (KQ_ATTN_EARLY ? KQ_ATTN_VPOST : 0) <= (TPH == 256 && !SC1_IN ? KQ_ATTN_VB : 4),
+                  "KQV's first batch holds the prefetched V iterations");
     const int gsz = a.n_head / a.n_head_kv;
     const int g = h / gsz;
     const int kvw = a.n_head_kv * HD;
@@ -115,9 +161,10 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
 #pragma unroll
         for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
     }
+    const bool vl = PAIR && a.v_lds;  // V rows staged in LDS (launch_attn): no register prefetch
     uint4 vpre[ITEMS][VPF] = {};
 #pragma unroll
-    for (int ii = 0; ii < ITEMS; ++ii) {
+    for (int ii = 0; ii < ITEMS && !vl; ++ii) {
         const int item = t + TPH * ii, d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx + 8 * j;
 #pragma unroll
@@ -161,6 +208,26 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     // KQV) when it fits, past scal otherwise
     double *gsum = (a.n_ctx / 4) * 8 <= HD * 64 ? (double *)red : (double *)(scal + 4);
 
+    // V rows of the head's kv group, cells [0, n_kv), into LDS (vl): wave w takes rows
+    // [w HD / 4, (w + 1) HD / 4); row d at vlds + d * VSTR; completion: vmcnt(0) + barrier
+    // before KQV. A cell past pos holds whatever the cache holds (its weight is an exact 0);
+    // the new cell is patched from v16 as on the register path.
+    const int VSTR = 2 * a.n_ctx + 16;
+    uint8_t *const vlds = smem + (attn_lds_dev(HD, a.n_ctx) + 15) / 16 * 16;
+    if (vl && !bad) {
+        const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+        const int gran = n_kv / 8;  // 16-B granules of a row
+#pragma unroll 1
+        for (int d = wv * (HD / 4); d < (wv + 1) * (HD / 4); ++d) {
+            const uint8_t *src = (const uint8_t *)(a.v_cache + (int64_t)(g * HD + d) * a.n_ctx);
+#pragma unroll 1
+            for (int i = 0; 64 * i < gran; ++i) {
+                const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS void *)(vlds + d * VSTR + 1024 * i));
+                const int n = __builtin_amdgcn_readfirstlane(gran - 64 * i);
+                attn_dma16_lanes(src + 1024 * i + 16 * ln, m0, ln, n < 64 ? n : 64);
+            }
+        }
+    }
     const float *tc = a.rope_table + (a.rope_row ? 0 : (int64_t)pos * (HD / 2) * 2);
     const bool writer = may_write && !bad && (h % gsz) == 0;
     if (t < HD / 2) {
@@ -181,6 +248,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     }
     __syncthreads();
     if (ADIAG(a) == 1 || ADIAG(a) == 5) {  // diagnostics: stop after the loads and rope
+        vm_wait<0>();  // (staged V DMAs, vl) land before the wave ends
         if (t < HD) out[t] = adiag_finite(__float_as_uint(x0) ^ kpre[0].x ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
         return;
     }
@@ -207,6 +275,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         if ((t & 63) == 0) scal[t >> 6] = wmx;
         __syncthreads();
         if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
+            vm_wait<0>();  // (staged V DMAs, vl) land before the wave ends
             if (t < HD) out[t] = adiag_finite(__float_as_uint(sc) ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
@@ -224,32 +293,65 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         if (c < n_kv) p16[c] = h2u(f2h_rne(ec * inv));
         __syncthreads();
         if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
+            vm_wait<0>();  // (staged V DMAs, vl) land before the wave ends
             if (t < HD) out[t] = adiag_finite((uint32_t)p16[t] ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
     } else {
-        // KQ + scale + mask; the first pass (c == t) scores the prefetched row
-        for (int c = t; c < n_kv; c += TPH) {
-            float s = -INFINITY;
-            if (c <= pos) {
-                uint4 kv[KV4];
-                if (c == pos) {
+        if constexpr (PAIR) {
+            // KQ + scale + mask; the first pass (c == t) scores the prefetched row. KR cells per
+            // thread per round, every row requested before any is used.
+            for (int c0 = t; c0 < n_kv; c0 += KR * TPH) {
+                uint4 kv[KR][KV4];  // (branches, not selects: a select of the three sources takes
+                                    // kpre's address and puts it in scratch)
 #pragma unroll
-                    for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
-                } else if (c == t && (KQ_ATTN_EARLY || t < KPF)) {
+                for (int r = 0; r < KR; ++r) {
+                    const int c = c0 + r * TPH;
+                    if (c < n_kv && c <= pos) {
+                        if (c == pos) {
 #pragma unroll
-                    for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
-                } else {
-                    const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+                            for (int i = 0; i < KV4; ++i) kv[r][i] = ((const uint4 *)k16)[i];
+                        } else if (r == 0 && c == t && (KQ_ATTN_EARLY || t < KPF)) {
 #pragma unroll
-                    for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
+                            for (int i = 0; i < KV4; ++i) kv[r][i] = kpre[i];
+                        } else {
+                            const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+#pragma unroll
+                            for (int i = 0; i < KV4; ++i) kv[r][i] = kr[i];
+                        }
+                    }
                 }
-                s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+#pragma unroll
+                for (int r = 0; r < KR; ++r) {
+                    const int c = c0 + r * TPH;
+                    if (c < n_kv) w[c] = c <= pos ? vec_dot_f16_rows<HD>(kv[r], (const uint4 *)q16) * a.scale : -INFINITY;
+                }
             }
-            w[c] = s;
+        } else {
+            // KQ + scale + mask; the first pass (c == t) scores the prefetched row
+            for (int c = t; c < n_kv; c += TPH) {
+                float s = -INFINITY;
+                if (c <= pos) {
+                    uint4 kv[KV4];
+                    if (c == pos) {
+#pragma unroll
+                        for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+                    } else if (c == t && (KQ_ATTN_EARLY || t < KPF)) {
+#pragma unroll
+                        for (int i = 0; i < KV4; ++i) kv[i] = kpre[i];
+                    } else {
+                        const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
+#pragma unroll
+                        for (int i = 0; i < KV4; ++i) kv[i] = kr[i];
+                    }
+                    s = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
+                }
+                w[c] = s;
+            }
         }
         __syncthreads();
         if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
+            vm_wait<0>();  // (staged V DMAs, vl) land before the wave ends
             if (t < HD) out[t] = adiag_finite(__float_as_uint(w[t]) ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
@@ -285,13 +387,20 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         for (int c = t; c < n_kv; c += TPH) p16[c] = h2u(f2h_rne(w[c] * inv));
         __syncthreads();
         if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
+            vm_wait<0>();  // (staged V DMAs, vl) land before the wave ends
             if (t < HD) out[t] = adiag_finite((uint32_t)p16[t] ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
 
     }
 
-    // KQV: thread (d, j) -> accumulator j of output d
+    // KQV: thread (d, j) -> accumulator j of output d. The V chunks past the prefetched ones
+    // are requested KQ_ATTN_VB iterations at a time before any of them is used (a loop that
+    // loads and then uses each chunk pays one memory latency per 32 cells: tg1024 -18 %).
+    if (vl) {  // the staged V rows landed (every wave's DMAs)
+        vm_wait<0>();
+        __syncthreads();
+    }
     const int n_it = (pos + 32) / 32;  // iterations holding a cell <= pos; later ones add exact zeros
 #pragma unroll
     for (int ii = 0; ii < ITEMS; ++ii) {
@@ -299,29 +408,63 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         const int d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
         uint32_t acc[4] = {};  // lanes 2k, 2k+1 of accumulator j in word k
-        for (int it = 0; it < n_it; ++it) {  // VPF prefetched iterations, then global loads
-            const int c0 = 32 * it + 8 * j;
-            uint4 vv;
-            if (it < VPF) {
+        if constexpr (PAIR) {
+            for (int it0 = 0; it0 < n_it; it0 += VB) {
+                uint4 vb[VB];
 #pragma unroll
-                for (int k = 0; k < VPF; ++k)
-                    if (k == it) vv = vpre[ii][k];
-            } else if (VPOST > 0 && it < VPF + VPOST) {
+                for (int k = 0; k < VB; ++k) {
+                    const int it = it0 + k;
+                    if (!vl && it0 == 0 && k < VPF) {
+                        vb[k] = vpre[ii][k < VPF ? k : 0];
+                    } else if (VPOST > 0 && it0 == 0 && k < VPF + VPOST) {
+                        vb[k] = vpost[ii][k - VPF < (VPOST > 0 ? VPOST : 1) ? k - VPF : 0];
+                    } else if (it < n_it) {
+                        vb[k] = vl ? *(const uint4 *)(vlds + d * VSTR + 2 * (32 * it + 8 * j))
+                                   : *(const uint4 *)(vr + 32 * it + 8 * j);
+                    }
+                }
 #pragma unroll
-                for (int k = 0; k < (VPOST > 0 ? VPOST : 1); ++k)
-                    if (k == it - VPF) vv = vpost[ii][k];
-            } else {
-                vv = *(const uint4 *)(vr + c0);
+                for (int k = 0; k < VB; ++k) {
+                    const int it = it0 + k;
+                    if (it < n_it) {
+                        const int c0 = 32 * it + 8 * j;
+                        const uint4 pp = *(const uint4 *)(p16 + c0);
+                        uint32_t vw[4] = {vb[k].x, vb[k].y, vb[k].z, vb[k].w};
+                        const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+                        if (pos >= c0 && pos < c0 + 8) {  // the new cell: LDS copy
+                            const int l = pos - c0;
+                            vw[l >> 1] = (vw[l >> 1] & (0xffff0000u >> (16 * (l & 1)))) | ((uint32_t)v16[d] << (16 * (l & 1)));
+                        }
+#pragma unroll
+                        for (int q = 0; q < 4; ++q) acc[q] = pk_fma_w(vw[q], pw[q], acc[q]);
+                    }
+                }
             }
-            const uint4 pp = *(const uint4 *)(p16 + c0);
-            uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
-            const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
-            if (pos >= c0 && pos < c0 + 8) {  // the new cell: LDS copy
-                const int l = pos - c0;
-                vw[l >> 1] = (vw[l >> 1] & (0xffff0000u >> (16 * (l & 1)))) | ((uint32_t)v16[d] << (16 * (l & 1)));
-            }
+        } else {  // one V chunk per iteration (the fused kernels)
+            for (int it = 0; it < n_it; ++it) {  // VPF prefetched iterations, then global loads
+                const int c0 = 32 * it + 8 * j;
+                uint4 vv;
+                if (it < VPF) {
 #pragma unroll
-            for (int k = 0; k < 4; ++k) acc[k] = pk_fma_w(vw[k], pw[k], acc[k]);
+                    for (int k = 0; k < VPF; ++k)
+                        if (k == it) vv = vpre[ii][k];
+                } else if (VPOST > 0 && it < VPF + VPOST) {
+#pragma unroll
+                    for (int k = 0; k < (VPOST > 0 ? VPOST : 1); ++k)
+                        if (k == it - VPF) vv = vpost[ii][k];
+                } else {
+                    vv = *(const uint4 *)(vr + c0);
+                }
+                const uint4 pp = *(const uint4 *)(p16 + c0);
+                uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
+                const uint32_t pw[4] = {pp.x, pp.y, pp.z, pp.w};
+                if (pos >= c0 && pos < c0 + 8) {  // the new cell: LDS copy
+                    const int l = pos - c0;
+                    vw[l >> 1] = (vw[l >> 1] & (0xffff0000u >> (16 * (l & 1)))) | ((uint32_t)v16[d] << (16 * (l & 1)));
+                }
+#pragma unroll
+                for (int k = 0; k < 4; ++k) acc[k] = pk_fma_w(vw[k], pw[k], acc[k]);
+            }
         }
         const float o = f16x8_reduce_quad(acc);  // accumulators j = 0..3 of output d: one quad of lanes
         if (j == 0) {

@@ -221,6 +221,8 @@ struct AttnArgs {
     int no_store;     // prompt batch: the KV cells are already stored (the k/v GEMM's epilogue)
     uint8_t *q8_out;  // prompt batch (kq_attn_prompt_group): also the output rows as Q8L blocks
                       // for the next GEMM (row i's superblock b at (i*nb + b)*304), or null
+    int v_lds;        // kq_attn_decode only, set by launch_attn: the head's V rows are staged in
+                      // LDS by LDS-DMA as soon as the position is known (attn_lds_v bytes)
 };
 
 // Decode attention fused with the o-proj GEMV (kq_attn_oproj.hip): workgroup (s, rb) runs the

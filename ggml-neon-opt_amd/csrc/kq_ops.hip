@@ -512,6 +512,10 @@ size_t attn_lds(int hd, int n_ctx) {
     const size_t gsum = (size_t)(n_ctx / 4) * 8 <= (size_t)hd * 64 ? 0 : (size_t)(n_ctx / 4) * 8;
     return (size_t)6 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + gsum;
 }
+// ... plus the head's V rows (v_lds): head_dim rows of n_ctx f16, 16 B of padding each
+size_t attn_lds_v(int hd, int n_ctx) {
+    return (attn_lds(hd, n_ctx) + 15) / 16 * 16 + (size_t)hd * ((size_t)n_ctx * 2 + 16);
+}
 
 // ------------------------------------------------------------ launch helpers
 int check_launch() {
@@ -592,10 +596,19 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
         return timed_launch("kq::kq_attn_group<128>", bytes, kq_attn_group<128>, dim3(a.n_head_kv), dim3(64 * nw),
                             glds, s, a);
     }
-    const size_t lds = attn_lds(a.head_dim, a.n_ctx);
-    if (a.head_dim == 64)
-        return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64>, dim3(a.n_head), dim3(256), lds, s, a);
-    return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128>, dim3(a.n_head), dim3(256), lds, s, a);
+    // Past the register path's 256 cells the V rows go to LDS by LDS-DMA as soon as the position
+    // is known (all of them in flight under KQ and soft_max) where they fit; shorter caches keep
+    // the register prefetch, which issues V with the position itself.
+    AttnArgs b = a;
+    b.v_lds = a.n_ctx > 256 && a.n_ctx % 8 == 0 && attn_lds_v(a.head_dim, a.n_ctx) <= 160 * 1024 &&
+              ((uintptr_t)a.v_cache & 15u) == 0 && KQ_ATTN_VLDS;
+    const size_t lds = b.v_lds ? attn_lds_v(a.head_dim, a.n_ctx) : attn_lds(a.head_dim, a.n_ctx);
+    if (a.head_dim == 64) {
+        if (b.v_lds) allow_lds((const void *)kq_attn_decode<64>, lds);
+        return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64>, dim3(a.n_head), dim3(256), lds, s, b);
+    }
+    if (b.v_lds) allow_lds((const void *)kq_attn_decode<128>, lds);
+    return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128>, dim3(a.n_head), dim3(256), lds, s, b);
 }
 
 // mi355x_attn_prompt_impl: MI355X_ATTN_GROUP (default: one workgroup per kv group and token

@@ -15,16 +15,19 @@ def child():
     import numpy as np
     import torch
     import ggml_mi355x as g
+    sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+    import knobs
+    knobs.apply_env()  # MI355X_ATTN_DIAG -> the library knob (KQ_ATTN_DIAG builds only)
     dev = torch.device("cuda:0")
     out = []
-    for hd, nh, nkv, n_ctx in ((64, 32, 4, 128), (128, 32, 8, 512)):
+    for hd, nh, nkv, n_ctx in ((64, 32, 4, 128), (64, 32, 4, 1024), (128, 32, 8, 512)):
         kvw = nkv * hd
         tab = g.rope_table(n_ctx, hd, 10000.0, 1.0, device=dev)
         kc = (torch.randn((n_ctx, kvw), device=dev) * 0.5).half().view(torch.int16)
         vc = (torch.randn((kvw, n_ctx), device=dev) * 0.5).half().view(torch.int16)
         q, k, v = (torch.randn(n * hd, device=dev) for n in (nh, nkv, nkv))
         y = torch.empty(nh * hd, device=dev)
-        for p in (0, 63, n_ctx - 1):
+        for p in sorted({0, 63, n_ctx // 2 - 1, n_ctx - 1}):
             pos = torch.tensor([p], dtype=torch.int32, device=dev)
             for _ in range(20):
                 g.attn_decode(q, k, v, pos, tab, kc, vc, nh, nkv, hd, 0.125, out=y)
