@@ -111,7 +111,7 @@ __device__ __forceinline__ int attn_lds_dev(int hd, int n_ctx) {
     return 6 * hd + n_ctx * 6 + hd * 64 + 16 + gsum;
 }
 
-template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false, bool SC1_IN = false>
+template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false, bool SC1_IN = false, bool BATCH = false>
 __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8_t *smem, float *out,
                                           bool may_write) {
     auto ldin = [](const float *p) {
@@ -121,16 +121,17 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     static_assert(HD == 64 || HD == 128, "head_dim");
     constexpr int KV4 = HD / 8;          // 16-B pieces of one K-cache row
     static_assert(TPH == 256 || (TPH == 128 && HD == 64), "threads per head");
-    // the standalone kernel batches its cache loads (KR K rows per round, 1-2 x KQ_ATTN_VB V chunks);
-    // the fused kernels' register budgets keep one K row and 4 V chunks (PAIR off)
-    constexpr bool PAIR = TPH == 256 && !SC1_IN;
+    // BATCH (kq_attn_decode): the cache loads past the prefetched cells are batched (KR K rows
+    // per round, KQ_ATTN_VB V chunks); the fused kernels' register budgets keep one K row and
+    // one V chunk per step (PAIR off)
+    constexpr bool PAIR = BATCH && TPH == 256 && !SC1_IN;
     constexpr int VB = PAIR ? (HD == 64 ? KQ_ATTN_VB64 : KQ_ATTN_VB) : 4;
     constexpr int KR = HD == 64 ? KQ_ATTN_KR64 : 2;  // K rows per thread per round (register budget)
     constexpr int ITEMS = HD * 4 / TPH;  // KQV (d, j) items per thread
     constexpr int VPF = VPF0 > 0 ? VPF0 : KQ_ATTN_PFC > 0 ? (KQ_ATTN_PFC / 32 < 8 / ITEMS ? KQ_ATTN_PFC / 32 : 8 / ITEMS)
                                                          : 8 / ITEMS;  // prefetched 32-cell iterations per item
     constexpr int KPF = KQ_ATTN_PFC > 0 && KQ_ATTN_PFC < TPH ? KQ_ATTN_PFC : TPH;  // K rows prefetched (thread t < KPF)
-    static_assert(VPF + (KQ_ATTN_EARLY ? KQ_ATTN_VPOST : 0) <= (TPH == 256 && !SC1_IN ? KQ_ATTN_VB : 4),
+    static_assert(VPF + (KQ_ATTN_EARLY ? KQ_ATTN_VPOST : 0) <= (BATCH && TPH == 256 && !SC1_IN ? KQ_ATTN_VB : 4),
                   "KQV's first batch holds the prefetched V iterations");
     const int gsz = a.n_head / a.n_head_kv;
     const int g = h / gsz;

@@ -206,7 +206,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     // the L2 of 8*gsz/n_head XCDs (TinyLlama: 2, Llama-3: 1) instead of all 8.
     int h = blockIdx.x;
     if ((a.n_head & 7) == 0) h = (h & 7) * (a.n_head >> 3) + (h >> 3);
-    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true);
+    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0, false, true>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true);
 }
 
 // One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read
@@ -813,6 +813,7 @@ int attn_args_from(const mi355x_attn_desc *d, AttnArgs &a) {
     a.rope_row = d->rope_row ? 1 : 0;
     a.q8_out = nullptr;
     a.no_store = 0;
+    a.v_lds = 0;  // launch_attn decides
     a.diag = (int)knob(KNOB_ATTN_DIAG);  // KQ_ATTN_DIAG builds only
     return check_attn(a);
 }
