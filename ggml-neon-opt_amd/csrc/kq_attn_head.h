@@ -63,6 +63,9 @@ __device__ __forceinline__ float adiag_finite(uint32_t bits) { return __uint_as_
 #ifndef KQ_ATTN_KR64
 #define KQ_ATTN_KR64 2
 #endif
+#ifndef KQ_ATTN_KR128  // head_dim 128: a K row is 64 VGPRs; two per round cost the short-context
+#define KQ_ATTN_KR128 1  // launch 0.7 us at Llama-3-8B (247 VGPRs, profiles/r05q_token8b_summary.md)
+#endif
 #ifndef KQ_ATTN_VLDS  // 1: experiment build with the LDS-staged V rows (launch_attn): measured neutral
 #define KQ_ATTN_VLDS 0
 #endif
@@ -126,7 +129,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     // one V chunk per step (PAIR off)
     constexpr bool PAIR = BATCH && TPH == 256 && !SC1_IN;
     constexpr int VB = PAIR ? (HD == 64 ? KQ_ATTN_VB64 : KQ_ATTN_VB) : 4;
-    constexpr int KR = HD == 64 ? KQ_ATTN_KR64 : 2;  // K rows per thread per round (register budget)
+    constexpr int KR = HD == 64 ? KQ_ATTN_KR64 : KQ_ATTN_KR128;  // K rows per thread per round (register budget)
     constexpr int ITEMS = HD * 4 / TPH;  // KQV (d, j) items per thread
     constexpr int VPF = VPF0 > 0 ? VPF0 : KQ_ATTN_PFC > 0 ? (KQ_ATTN_PFC / 32 < 8 / ITEMS ? KQ_ATTN_PFC / 32 : 8 / ITEMS)
                                                          : 8 / ITEMS;  // prefetched 32-cell iterations per item
