@@ -476,6 +476,12 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     }
     for (int i = n_desc; i <= MI355X_MAX_FUSED; ++i) a.wave_prefix[i] = (int)waves;
     a.waves_total = (int)waves;
+    a.prio_bytes = 0;
+    for (int i = 0; i < n_desc; ++i)
+        if (wv[i] > 0) {
+            const int64_t b = (int64_t)(a.rbase[i] + (a.rrem[i] ? 1 : 0)) * nb * block_bytes(d[i].type);
+            a.prio_bytes = b > a.prio_bytes ? b : a.prio_bytes;
+        }
     if (rpw > 0x7fffffff / 64) return MI355X_E_UNSUPPORTED;
     a.rpw = (int)(rpw > 0 ? rpw : 1);
     // rows per chain batch: ~ROWS_RECS records, batch ends on a step boundary (bR*nb % 16 == 0)

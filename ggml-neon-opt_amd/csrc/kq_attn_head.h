@@ -66,6 +66,9 @@ __device__ __forceinline__ float adiag_finite(uint32_t bits) { return __uint_as_
 #ifndef KQ_ATTN_KR128  // head_dim 128: a K row is 64 VGPRs; two per round cost the short-context
 #define KQ_ATTN_KR128 1  // launch 0.7 us at Llama-3-8B (247 VGPRs, profiles/r05q_token8b_summary.md)
 #endif
+#ifndef KQ_ATTN_EARLYV  // 1: head_dim 64, KQV's first V batch requested with the position (measured -1 % tg1024)
+#define KQ_ATTN_EARLYV 0
+#endif
 #ifndef KQ_ATTN_VLDS  // 1: experiment build with the LDS-staged V rows (launch_attn): measured neutral
 #define KQ_ATTN_VLDS 0
 #endif
@@ -165,7 +168,9 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
 #pragma unroll
         for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
     }
-    const bool vl = PAIR && a.v_lds;  // V rows staged in LDS (launch_attn): no register prefetch
+    // V rows staged in LDS (launch_attn sets a.v_lds) only in the KQ_ATTN_VLDS build: as a run-time
+    // choice its LDS / global select turned KQV's cache loads into flat loads (tg1024 -4 %, r5t)
+    const bool vl = PAIR && KQ_ATTN_VLDS && a.v_lds;
     uint4 vpre[ITEMS][VPF] = {};
 #pragma unroll
     for (int ii = 0; ii < ITEMS && !vl; ++ii) {
@@ -230,6 +235,21 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 const int n = __builtin_amdgcn_readfirstlane(gran - 64 * i);
                 attn_dma16_lanes(src + 1024 * i + 16 * ln, m0, ln, n < 64 ? n : 64);
             }
+        }
+    }
+    // EARLYV (head_dim 64, kq_attn_decode): KQV's first batch of V chunks past the prefetched
+    // ones requested as soon as the position is known, under KQ and soft_max
+    constexpr bool EARLYV = PAIR && HD == 64 && KQ_ATTN_EARLYV;
+    uint4 vb0[ITEMS][EARLYV ? VB : 1];
+    if (EARLYV && !vl) {
+        const int n_it0 = (pos + 32) / 32;
+#pragma unroll
+        for (int ii = 0; ii < ITEMS; ++ii) {
+            const int item = t + TPH * ii, d = item >> 2, j = item & 3;
+            const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
+#pragma unroll
+            for (int k = VPF + VPOST; k < (EARLYV ? VB : 1); ++k)
+                if (k < n_it0) vb0[ii][k] = *(const uint4 *)(vr + 32 * k + 8 * j);
         }
     }
     const float *tc = a.rope_table + (a.rope_row ? 0 : (int64_t)pos * (HD / 2) * 2);
@@ -422,6 +442,8 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                         vb[k] = vpre[ii][k < VPF ? k : 0];
                     } else if (VPOST > 0 && it0 == 0 && k < VPF + VPOST) {
                         vb[k] = vpost[ii][k - VPF < (VPOST > 0 ? VPOST : 1) ? k - VPF : 0];
+                    } else if (EARLYV && !vl && it0 == 0) {
+                        vb[k] = vb0[ii][k < (EARLYV ? VB : 1) ? k : 0];  // requested with the position (it < n_it)
                     } else if (it < n_it) {
                         vb[k] = vl ? *(const uint4 *)(vlds + d * VSTR + 2 * (32 * it + 8 * j))
                                    : *(const uint4 *)(vr + 32 * it + 8 * j);

@@ -127,6 +127,7 @@ struct RowsArgs {
     // (identical row ranges); epi_y[r] = swiglu(gate[r], up[r]) for r < epi_n
     int epi, epi_n, epi_wave_off;
     float *epi_y;
+    int64_t prio_bytes;  // the most weight bytes any wave streams (KQ_ROWS_PRIO: remaining-work priority)
 };
 constexpr int ROWS_PRO_NONE = 0, ROWS_PRO_NORM = 1, ROWS_PRO_SWIGLU = 2;
 // Prologue of the fused quantization (a.xmode bits):

@@ -67,6 +67,11 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 // rest equal), 2 Q5_K, 4 Q6_K (no gain; experiment builds), profiles/r04_mmq_pkchain_ab.txt.
 #define KQ_MMQ_PKCHAIN 1
 #endif
+// Experiment build: static issue priority 1 for the second half of the workgroup's waves (the
+// arbitration losers of every two-waves-per-SIMD pair, MI355X_MICROARCH.md item 4).
+#ifndef KQ_MMQ_PRIO
+#define KQ_MMQ_PRIO 0
+#endif
 #ifndef KQ_MMQ_Q5_VALU
 #define KQ_MMQ_Q5_VALU 0  // experiment build: Q5_K sub-block scales on VALU (the round-2 kernel)
 #endif
@@ -318,6 +323,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
 #pragma unroll
         for (int i = 0; i < 16; ++i) sumf[ct][i] = 0.f;
 
+    if (KQ_MMQ_PRIO && NWV >= 8 && wave >= NWV / 2) __builtin_amdgcn_s_setprio(1);
     if (NBUF > 1) issue(0);
     if (NBUF == 3 && nb > 1) issue(1);
 #pragma unroll 1

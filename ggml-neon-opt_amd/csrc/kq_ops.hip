@@ -32,6 +32,9 @@
 #include "kq_ops_device.h"
 #include "kq_rows_device.h"
 
+#ifndef KQ_ATTN_BATCH_CTX
+#define KQ_ATTN_BATCH_CTX 256  // caches above this many cells take kq_attn_decode<HD, true>
+#endif
 #ifndef KQ_ATTN_OSC1
 #define KQ_ATTN_OSC1 0  // experiment build: the decode attention's output stored write-through (sc1)
 #endif
@@ -198,7 +201,10 @@ __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, floa
 
 // ------------------------------------------------------------ decode attention
 // One workgroup per query head (kq_attn_head.h).
-template <int HD>
+// BATCH: the cache loads past the prefetched cells requested in batches (kq_attn_head.h); the
+// launch takes it for caches of more than KQ_ATTN_BATCH_CTX cells only: at short context its
+// code costs the head_dim-128 launch ~0.3 us (profiles/r05_attn_ab_batch_ctx.txt).
+template <int HD, bool BATCH>
 __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // XCD-aware head order (speed only): workgroup b runs on XCD b % 8, so XCD x takes the
@@ -206,7 +212,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     // the L2 of 8*gsz/n_head XCDs (TinyLlama: 2, Llama-3: 1) instead of all 8.
     int h = blockIdx.x;
     if ((a.n_head & 7) == 0) h = (h & 7) * (a.n_head >> 3) + (h >> 3);
-    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0, false, true>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true);
+    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0, false, BATCH>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true);
 }
 
 // One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read
@@ -600,15 +606,18 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     // is known (all of them in flight under KQ and soft_max) where they fit; shorter caches keep
     // the register prefetch, which issues V with the position itself.
     AttnArgs b = a;
-    b.v_lds = a.n_ctx > 256 && a.n_ctx % 8 == 0 && attn_lds_v(a.head_dim, a.n_ctx) <= 160 * 1024 &&
+    b.v_lds = a.n_ctx > KQ_ATTN_BATCH_CTX && a.n_ctx % 8 == 0 && attn_lds_v(a.head_dim, a.n_ctx) <= 160 * 1024 &&
               ((uintptr_t)a.v_cache & 15u) == 0 && KQ_ATTN_VLDS;
     const size_t lds = b.v_lds ? attn_lds_v(a.head_dim, a.n_ctx) : attn_lds(a.head_dim, a.n_ctx);
+    const bool batch = a.n_ctx > KQ_ATTN_BATCH_CTX;
     if (a.head_dim == 64) {
-        if (b.v_lds) allow_lds((const void *)kq_attn_decode<64>, lds);
-        return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64>, dim3(a.n_head), dim3(256), lds, s, b);
+        if (!batch) return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64, false>, dim3(a.n_head), dim3(256), lds, s, b);
+        if (b.v_lds) allow_lds((const void *)kq_attn_decode<64, true>, lds);
+        return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64, true>, dim3(a.n_head), dim3(256), lds, s, b);
     }
-    if (b.v_lds) allow_lds((const void *)kq_attn_decode<128>, lds);
-    return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128>, dim3(a.n_head), dim3(256), lds, s, b);
+    if (!batch) return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128, false>, dim3(a.n_head), dim3(256), lds, s, b);
+    if (b.v_lds) allow_lds((const void *)kq_attn_decode<128, true>, lds);
+    return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128, true>, dim3(a.n_head), dim3(256), lds, s, b);
 }
 
 // mi355x_attn_prompt_impl: MI355X_ATTN_GROUP (default: one workgroup per kv group and token

@@ -70,6 +70,15 @@
 // The GEMV's outputs (and the SWIGLU epilogue's) are stored write-through (sc1), so the next
 // launch's activation is in the memory-side caches before the kernel boundary
 // (tools/xfresh.hip: the consumer's fresh-read price 0.15 -> 0.03 us per edge).
+// Issue priority by remaining work (MI355X_MICROARCH.md "Two waves per SIMD": VALU and memory
+// issue go by priority, then age, so with three waves per SIMD the older ones stream faster
+// and the middle one ends last, r05 stamps): every few steps a wave sets s_setprio from the
+// weight bytes it still has to stream, relative to the most any wave streams, so the waves
+// behind catch up.
+#ifndef KQ_ROWS_PRIO
+#define KQ_ROWS_PRIO 0
+#endif
+
 #ifndef KQ_ROWS_YSC1
 #define KQ_ROWS_YSC1 1  // TinyLlama token +0.5-1.4 %, Llama-3-8B +0.7 % (profiles/r04_store_flavour_ab.txt)
 #endif
@@ -467,8 +476,21 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
     int bend = bR * nb < G ? bR * nb : G;  // superblock index ending the current batch
     int brow = 0;
     const uint8_t *cslot = ring;
+    int prio = -1;
 #pragma unroll 1
     for (int t = 0; t < T; ++t) {
+        if (KQ_ROWS_PRIO && (t & 3) == 0) {
+            const int64_t rem = (int64_t)(T - t) * (ROWS_SB * BSZ);
+            int p = (int)(rem * 4 / (a.prio_bytes + 1));
+            p = __builtin_amdgcn_readfirstlane(p > 3 ? 3 : p);
+            if (p != prio) {
+                prio = p;
+                if (p == 3) __builtin_amdgcn_s_setprio(3);
+                else if (p == 2) __builtin_amdgcn_s_setprio(2);
+                else if (p == 1) __builtin_amdgcn_s_setprio(1);
+                else __builtin_amdgcn_s_setprio(0);
+            }
+        }
         if (pf_on && t < pre0) {  // the prefetch touches sit between steps pre0-1 and pre0
             if (T - t >= D) vm_wait<NI * (D - 1) + ROWS_PF>();
             else vm_wait_kp<NI, ROWS_PF>(T - t - 1);
@@ -531,6 +553,7 @@ __device__ __forceinline__ void rows_body(const RowsArgs &a, const WaveWork &ww,
             wave_lds_fence();
         }
     }
+    if (KQ_ROWS_PRIO) __builtin_amdgcn_s_setprio(0);
     const uint64_t st2 = RSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
     if (pf_on) {  // every touch has landed (they are older than step pre0): release the register
         asm volatile("" ::"v"(pf_sink));
