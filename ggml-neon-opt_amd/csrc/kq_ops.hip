@@ -611,13 +611,13 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     const size_t lds = b.v_lds ? attn_lds_v(a.head_dim, a.n_ctx) : attn_lds(a.head_dim, a.n_ctx);
     const bool batch = a.n_ctx > KQ_ATTN_BATCH_CTX;
     if (a.head_dim == 64) {
-        if (!batch) return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64, false>, dim3(a.n_head), dim3(256), lds, s, b);
+        if (!batch) return timed_launch("kq::kq_attn_decode<64, false>", bytes, kq_attn_decode<64, false>, dim3(a.n_head), dim3(256), lds, s, b);
         if (b.v_lds) allow_lds((const void *)kq_attn_decode<64, true>, lds);
-        return timed_launch("kq::kq_attn_decode<64>", bytes, kq_attn_decode<64, true>, dim3(a.n_head), dim3(256), lds, s, b);
+        return timed_launch("kq::kq_attn_decode<64, true>", bytes, kq_attn_decode<64, true>, dim3(a.n_head), dim3(256), lds, s, b);
     }
-    if (!batch) return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128, false>, dim3(a.n_head), dim3(256), lds, s, b);
+    if (!batch) return timed_launch("kq::kq_attn_decode<128, false>", bytes, kq_attn_decode<128, false>, dim3(a.n_head), dim3(256), lds, s, b);
     if (b.v_lds) allow_lds((const void *)kq_attn_decode<128, true>, lds);
-    return timed_launch("kq::kq_attn_decode<128>", bytes, kq_attn_decode<128, true>, dim3(a.n_head), dim3(256), lds, s, b);
+    return timed_launch("kq::kq_attn_decode<128, true>", bytes, kq_attn_decode<128, true>, dim3(a.n_head), dim3(256), lds, s, b);
 }
 
 // mi355x_attn_prompt_impl: MI355X_ATTN_GROUP (default: one workgroup per kv group and token
