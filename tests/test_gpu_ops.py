@@ -145,6 +145,37 @@ def test_attn_decode_sequence(dev, O, attn_impl, hd, nh, nkv, n_ctx, rope_row):
     assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
 
 
+@pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 1024), (128, 16, 4, 512), (64, 8, 2, 256), (64, 8, 2, 288)])
+def test_attn_decode_long_random_cache(dev, O, hd, nh, nkv, n_ctx):
+    """Every cell of both caches random (not only the cells this test wrote), then positions
+    across the whole cache: the batched loads of kq_attn_decode<HD, true> (caches past 256
+    cells: two K rows per round at head_dim 64, eight V chunks per batch) and the boundary
+    cache sizes on either side of that choice, bit-exact with the oracle."""
+    import torch
+    import ggml_mi355x as g
+    rng = np.random.default_rng(n_ctx + hd)
+    kvw = nkv * hd
+    tab = g.rope_table(n_ctx, hd, 10000.0, 1.0, device=dev)
+    tref = O.rope_table(n_ctx, hd, 10000.0)
+    kc_ref = rng.standard_normal((n_ctx, kvw)).astype(np.float16).view(np.uint16)
+    vc_ref = rng.standard_normal((kvw, n_ctx)).astype(np.float16).view(np.uint16)
+    kc = torch.from_numpy(kc_ref.view(np.int16).copy()).to(dev)
+    vc = torch.from_numpy(vc_ref.view(np.int16).copy()).to(dev)
+    scale = float(np.float32(1.0) / np.sqrt(np.float32(hd)))
+    for p in sorted(x for x in {0, 31, 32, 255, 256, 257, n_ctx // 2 + 7, n_ctx - 9, n_ctx - 1} if x < n_ctx):
+        q = (rng.standard_normal(nh * hd) * 2).astype(np.float32)
+        k = (rng.standard_normal(kvw) * 2).astype(np.float32)
+        v = rng.standard_normal(kvw).astype(np.float32)
+        pos = torch.tensor([p], dtype=torch.int32, device=dev)
+        got = g.attn_decode(t(q, dev), t(k, dev), t(v, dev), pos, tab[p].contiguous(), kc, vc, nh, nkv, hd, scale,
+                            rope_row=True).cpu().numpy()
+        ref = O.attn_decode(O.rope(q, hd, hd, p, tref), O.rope(k, hd, hd, p, tref), v, kc_ref, vc_ref, p, nh, nkv,
+                            hd, scale)
+        assert bits_equal(got, ref), (p, first_mismatch(got, ref))
+    assert (kc.cpu().numpy().view(np.uint16) == kc_ref).all()
+    assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
+
+
 @pytest.mark.parametrize("qscale", [0.05, 2.0, 40.0], ids=["flat", "normal", "peaked"])
 def test_attn_softmax_sum_tree_and_fallback(dev, O, attn_impl, qscale):
     """soft_max's double sum runs as a wave tree where every partial sum is exact (then it
