@@ -582,6 +582,7 @@ MmqShape mmq_shape(int type, int64_t rows, int64_t M) {
     if (impl == MI355X_MMQ_TILE128W) return {128, 2};
     if (impl == MI355X_MMQ_TILE64W) return {64, 2};
     if (impl == MI355X_MMQ_TILE64) return {64, 1};
+    if (impl == MI355X_MMQ_TILE128X) return {128, type == Q6_K ? 2 : 4};
     const int64_t rt128 = (rows + 127) / 128;
     if (rt128 * ((M + 127) / 128) >= 160) return {128, 2};
     if (type == Q6_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
@@ -594,13 +595,15 @@ const void *mmq_fn(int type, bool mixed, MmqShape sh) {
          : type == Q5_K ? (const void *)kq_mmq<Q5_K, RT, CW>                   \
          : type == Q6_K ? (const void *)kq_mmq<Q6_K, RT, CW>                   \
                         : (const void *)kq_mmq<Q4_K, RT, CW>;
+    if (sh.rt == 128 && sh.cw == 4 && !mixed && type != Q6_K)
+        return type == Q5_K ? (const void *)kq_mmq<Q5_K, 128, 4> : (const void *)kq_mmq<Q4_K, 128, 4>;
     if (sh.rt == 128 && sh.cw == 2) KQ_MMQ_PICK(128, 2)
     if (sh.rt == 64 && sh.cw == 2) KQ_MMQ_PICK(64, 2)
     if (sh.rt == 128) KQ_MMQ_PICK(128, 1)
     KQ_MMQ_PICK(64, 1)
 #undef KQ_MMQ_PICK
 }
-// two superblock buffers: 64 * cw Q8L columns + rt weight rows (Q6_K: 224-B granule span),
+// two superblock buffers: mmq_cols(cw) Q8L columns + rt weight rows (Q6_K: 224-B granule span),
 // +16 B for the Q6_K realign reads past the last row
 size_t mmq_lds(int type, MmqShape sh) {
     return (size_t)mmq_nbuf(type, sh.rt, sh.cw) * (size_t)mmq_buf_bytes(type, sh.rt, sh.cw) + 16 + MMQ_PF_LDS;
@@ -625,8 +628,9 @@ int launch_mmq(int type, const void *w, int64_t K, int64_t N, size_t row_stride,
     const MmqShape sh = mmq_shape(type, N, M);
     const void *fn = mmq_fn(type, false, sh);
     const size_t lds = mmq_lds(type, sh);
-    dim3 grid((unsigned)((M + 64 * sh.cw - 1) / (64 * sh.cw)), (unsigned)((N + sh.rt - 1) / sh.rt), 1);
-    dim3 block((unsigned)(4 * sh.rt));
+    const int cols = mmq_cols(sh.cw);
+    dim3 grid((unsigned)((M + cols - 1) / cols), (unsigned)((N + sh.rt - 1) / sh.rt), 1);
+    dim3 block((unsigned)(64 * mmq_waves(sh.rt, sh.cw)));
     std::string name = std::string("kq::kq_mmq<") + std::to_string(type) + ">";
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
@@ -857,6 +861,7 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     bool has_q5 = false;
     for (int d = 0; d < n_mat; ++d) has_q5 |= types[d] == Q5_K;
     if (mixed && has_q5 && sh.rt == 128 && sh.cw == 2) sh = {128, 1};  // kq_mmq_mixed<128, 2> has no Q5_K body
+    if (sh.cw == 4 && (mixed || type == Q6_K)) sh = {128, 2};  // the 4-wave 128 x 128 tile: Q4_K / Q5_K only
     const int rt = sh.rt;
     MmqArgs a;
     memset(&a, 0, sizeof(a));
@@ -897,17 +902,17 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     const void *fn = mmq_fn(type, mixed, sh);
     size_t lds = mmq_lds(mixed ? Q6_K : type, sh);  // mixed: the largest tile of its bodies
     if (mixed) lds = std::max(lds, std::max(mmq_lds(Q4_K, sh), mmq_lds(Q5_K, sh)));
-    const dim3 grid((unsigned)((M + 64 * sh.cw - 1) / (64 * sh.cw)), (unsigned)tiles, 1);
+    const dim3 grid((unsigned)((M + mmq_cols(sh.cw) - 1) / mmq_cols(sh.cw)), (unsigned)tiles, 1);
     allow_lds(fn, lds);
     hipEvent_t e0, e1;
     void *args[] = {&a};
     hipError_t e;
     if (timing_slot(stream, e0, e1)) {
-        e = hipExtLaunchKernel(fn, grid, dim3((unsigned)(4 * rt)), args, lds, stream, e0, e1, 0);
+        e = hipExtLaunchKernel(fn, grid, dim3((unsigned)(64 * mmq_waves(rt, sh.cw))), args, lds, stream, e0, e1, 0);
         timing_log(mixed ? std::string("kq::kq_mmq_mixed") : std::string("kq::kq_mmq<") + std::to_string(type) + ">", wbytes + (double)M * a.nb * Q8L_STRIDE + ybytes,
                    e0, e1);
     } else {
-        e = hipLaunchKernel(fn, grid, dim3((unsigned)(4 * rt)), args, lds, stream);
+        e = hipLaunchKernel(fn, grid, dim3((unsigned)(64 * mmq_waves(rt, sh.cw))), args, lds, stream);
     }
     if (e != hipSuccess) return (int)e;
     e = hipGetLastError();
@@ -1352,7 +1357,7 @@ int mi355x_debug_knob(const char *name, double value, double *previous) {
 }
 
 int mi355x_mmq_impl(int impl) {
-    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE64W) return MI355X_E_INVAL;
+    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE128X) return MI355X_E_INVAL;
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
     return prev;

@@ -156,8 +156,14 @@ constexpr int Q8L_STRIDE = 304; // LDS/workspace Q8_K block: d @0, qs @16, bsums
 // Superblock buffers of a kq_mmq tile (RT weight rows x 64*CW columns): KQ_MMQ_NBUF where the
 // tile already runs one workgroup per CU (128 x 64 at two waves per SIMD, 64 x 128) and the
 // buffers fit the CU's LDS; else 2.
+// Column groups of waves: 2 (a wave takes 32 x CW of the tile's 64 x CW columns), or 1 for
+// CW = 4 (the 4-wave 128 x 128 tile: every wave all 128 columns of its 32 rows, one wave per
+// SIMD with every register: each weight operand feeds four MFMA column tiles).
+__host__ __device__ constexpr int mmq_cgroups(int cw) { return cw == 4 ? 1 : 2; }
+__host__ __device__ constexpr int mmq_cols(int cw) { return 32 * cw * mmq_cgroups(cw); }
+__host__ __device__ constexpr int mmq_waves(int rt, int cw) { return rt / 32 * mmq_cgroups(cw); }
 __host__ __device__ constexpr int mmq_buf_bytes(int type, int rt, int cw) {
-    return 64 * cw * Q8L_STRIDE + rt * (type == Q6_K ? 224 : block_bytes(type));
+    return mmq_cols(cw) * Q8L_STRIDE + rt * (type == Q6_K ? 224 : block_bytes(type));
 }
 __host__ __device__ constexpr int mmq_nbuf(int type, int rt, int cw) {
     return KQ_MMQ_NBUF == 1 ? 1 : KQ_MMQ_NBUF >= 3 && ((rt == 128 && cw == 1) || (rt == 64 && cw == 2)) &&

@@ -260,8 +260,9 @@ __device__ __forceinline__ int mmq_tile_of(const MmqArgs &a0, MmqArgs &a, int &t
 template <int TYPE, int RT, int CW>
 __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     constexpr int BSZ = block_bytes(TYPE);
-    constexpr int NWV = RT / 16;  // waves
-    constexpr int COLS = 64 * CW;
+    constexpr int NWV = mmq_waves(RT, CW);  // waves
+    constexpr int CG = mmq_cgroups(CW);     // column groups of waves
+    constexpr int COLS = mmq_cols(CW);
     constexpr int A_BYTES = COLS * Q8L_STRIDE;
     constexpr int A_INSTR = A_BYTES / 1024;  // 19 per 64 columns (exact)
     constexpr int NB_I = mmq_b_instr(TYPE, RT);
@@ -273,7 +274,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int wm = wave & 1, wn = wave >> 1;
+    const int wm = CG == 2 ? wave & 1 : 0, wn = CG == 2 ? wave >> 1 : wave;
     const int r = lane & 31, h = lane >> 5;
     const int col0 = tx * COLS, row0 = ty * RT;
     const int nb = a.nb;
@@ -600,9 +601,9 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
 }
 
 // (64 x 128: one 4-wave workgroup per CU by LDS, so one wave per SIMD and every register)
-#define KQ_MMQ_WPE_OF(RT, CW) __attribute__((amdgpu_waves_per_eu((RT) == 64 && (CW) == 2 ? 1 : KQ_MMQ_WPE)))
+#define KQ_MMQ_WPE_OF(RT, CW) __attribute__((amdgpu_waves_per_eu(((RT) == 64 && (CW) == 2) || (CW) == 4 ? 1 : KQ_MMQ_WPE)))
 template <int TYPE, int RT, int CW>
-__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_OF(RT, CW) kq_mmq(const MmqArgs a0) {
+__global__ void __launch_bounds__(mmq_waves(RT, CW) * 64) KQ_MMQ_WPE_OF(RT, CW) kq_mmq(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     mmq_tile_of(a0, a, tx, ty);
@@ -612,7 +613,7 @@ __global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_OF(RT, CW) kq_mmq(const Mmq
 // Q4_K / Q5_K and Q6_K matrices on one activation in one launch (a prompt batch's q/k with a
 // Q6_K attn_v): each row tile runs its matrix's kernel body (a0.mtype), LDS sized for Q6_K.
 template <int RT, int CW>
-__global__ void __launch_bounds__(RT * 4) KQ_MMQ_WPE_OF(RT, CW) kq_mmq_mixed(const MmqArgs a0) {
+__global__ void __launch_bounds__(mmq_waves(RT, CW) * 64) KQ_MMQ_WPE_OF(RT, CW) kq_mmq_mixed(const MmqArgs a0) {
     MmqArgs a = a0;
     int tx, ty;
     const int d = mmq_tile_of(a0, a, tx, ty);
@@ -636,5 +637,7 @@ KQ_MMQ_INST(64, 1)
 KQ_MMQ_INST(128, 1)
 KQ_MMQ_INST(128, 2)
 KQ_MMQ_INST(64, 2)
+template __global__ void kq_mmq<Q4_K, 128, 4>(const MmqArgs a);
+template __global__ void kq_mmq<Q5_K, 128, 4>(const MmqArgs a);
 
 }  // namespace kq

@@ -446,7 +446,7 @@ def prompt_impl(request):
     g.attn_prompt_impl(prev)
 
 
-@pytest.fixture(params=[0, 2, 3], ids=["mmq_auto", "mmq_tile128", "mmq_tile128w"])
+@pytest.fixture(params=[0, 2, 3, 5], ids=["mmq_auto", "mmq_tile128", "mmq_tile128w", "mmq_tile128x"])
 def prompt_mmq(request):
     """The prompt's GEMMs on the default choice and on the 128-row tiles (the streamed
     Q4_K kernel was removed in round 3)."""
