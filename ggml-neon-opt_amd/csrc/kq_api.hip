@@ -583,6 +583,7 @@ MmqShape mmq_shape(int type, int64_t rows, int64_t M) {
     if (impl == MI355X_MMQ_TILE64W) return {64, 2};
     if (impl == MI355X_MMQ_TILE64) return {64, 1};
     if (impl == MI355X_MMQ_TILE128X) return {128, type == Q6_K ? 2 : 4};
+    if (impl == MI355X_MMQ_TILE192) return type == Q6_K ? MmqShape{128, 1} : MmqShape{192, 1};
     const int64_t rt128 = (rows + 127) / 128;
     if (rt128 * ((M + 127) / 128) >= 160) return {128, 2};
     if (type == Q6_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
@@ -595,6 +596,8 @@ const void *mmq_fn(int type, bool mixed, MmqShape sh) {
          : type == Q5_K ? (const void *)kq_mmq<Q5_K, RT, CW>                   \
          : type == Q6_K ? (const void *)kq_mmq<Q6_K, RT, CW>                   \
                         : (const void *)kq_mmq<Q4_K, RT, CW>;
+    if (sh.rt == 192 && !mixed && type != Q6_K)
+        return type == Q5_K ? (const void *)kq_mmq<Q5_K, 192, 1> : (const void *)kq_mmq<Q4_K, 192, 1>;
     if (sh.rt == 128 && sh.cw == 4 && !mixed && type != Q6_K)
         return type == Q5_K ? (const void *)kq_mmq<Q5_K, 128, 4> : (const void *)kq_mmq<Q4_K, 128, 4>;
     if (sh.rt == 128 && sh.cw == 2) KQ_MMQ_PICK(128, 2)
@@ -862,6 +865,7 @@ int launch_mmq_multi(const int *types, int n_mat, const void *const *w, const in
     for (int d = 0; d < n_mat; ++d) has_q5 |= types[d] == Q5_K;
     if (mixed && has_q5 && sh.rt == 128 && sh.cw == 2) sh = {128, 1};  // kq_mmq_mixed<128, 2> has no Q5_K body
     if (sh.cw == 4 && (mixed || type == Q6_K)) sh = {128, 2};  // the 4-wave 128 x 128 tile: Q4_K / Q5_K only
+    if (sh.rt == 192 && (mixed || type == Q6_K)) sh = {128, 1};  // the 12-wave 192-row tile: Q4_K / Q5_K only
     const int rt = sh.rt;
     MmqArgs a;
     memset(&a, 0, sizeof(a));
@@ -1357,7 +1361,7 @@ int mi355x_debug_knob(const char *name, double value, double *previous) {
 }
 
 int mi355x_mmq_impl(int impl) {
-    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE128X) return MI355X_E_INVAL;
+    if (impl < MI355X_MMQ_AUTO || impl > MI355X_MMQ_TILE192) return MI355X_E_INVAL;
     const int prev = mmq_impl();
     g_mmq_impl.store(impl);
     return prev;

@@ -601,7 +601,7 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
 }
 
 // (64 x 128: one 4-wave workgroup per CU by LDS, so one wave per SIMD and every register)
-#define KQ_MMQ_WPE_OF(RT, CW) __attribute__((amdgpu_waves_per_eu(((RT) == 64 && (CW) == 2) || (CW) == 4 ? 1 : KQ_MMQ_WPE)))
+#define KQ_MMQ_WPE_OF(RT, CW) __attribute__((amdgpu_waves_per_eu(((RT) == 64 && (CW) == 2) || (CW) == 4 ? 1 : (RT) == 192 ? 3 : KQ_MMQ_WPE)))
 template <int TYPE, int RT, int CW>
 __global__ void __launch_bounds__(mmq_waves(RT, CW) * 64) KQ_MMQ_WPE_OF(RT, CW) kq_mmq(const MmqArgs a0) {
     MmqArgs a = a0;
@@ -638,6 +638,8 @@ KQ_MMQ_INST(128, 1)
 KQ_MMQ_INST(128, 2)
 KQ_MMQ_INST(64, 2)
 template __global__ void kq_mmq<Q4_K, 128, 4>(const MmqArgs a);
+template __global__ void kq_mmq<Q4_K, 192, 1>(const MmqArgs a);
+template __global__ void kq_mmq<Q5_K, 192, 1>(const MmqArgs a);
 template __global__ void kq_mmq<Q5_K, 128, 4>(const MmqArgs a);
 
 }  // namespace kq

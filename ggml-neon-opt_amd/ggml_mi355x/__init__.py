@@ -30,7 +30,7 @@ E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM = 0, -1, -2, -3, -
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 ATTN_GROUP, ATTN_HEAD = 0, 1
-MMQ_AUTO, MMQ_TILE64, MMQ_TILE128, MMQ_TILE128W, MMQ_TILE64W, MMQ_TILE128X = 0, 1, 2, 3, 4, 5
+MMQ_AUTO, MMQ_TILE64, MMQ_TILE128, MMQ_TILE128W, MMQ_TILE64W, MMQ_TILE128X, MMQ_TILE192 = 0, 1, 2, 3, 4, 5, 6
 PREFILL_EXACT, PREFILL_F16, PREFILL_F16_ALL = 0, 1, 2
 
 # Every symbol include/ggml_mi355x.h declares (checked by tests/test_abi.py).

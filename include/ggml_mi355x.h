@@ -256,6 +256,7 @@ int mi355x_gemv_impl(int impl);
 #define MI355X_MMQ_TILE64W 4 /* 64 rows x 128 columns, 4 waves (two column tiles per wave) */
 #define MI355X_MMQ_TILE128X 5 /* 128 rows x 128 columns, 4 waves (each wave 32 rows x all 128 columns,
                                  one wave per SIMD); Q4_K / Q5_K (Q6_K takes TILE128W) */
+#define MI355X_MMQ_TILE192 6 /* 192 rows x 64 columns, 12 waves (three per SIMD); Q4_K / Q5_K (Q6_K takes TILE128) */
 int mi355x_mmq_impl(int impl);
 /* Prefill (ne11 >= 16) precision: MI355X_PREFILL_EXACT (kq_mmq, int8 MFMA, bit-exact
  * against ggml's per-(row, column) vec_dot loop; the default), MI355X_PREFILL_F16 (within

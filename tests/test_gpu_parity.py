@@ -291,7 +291,7 @@ def test_fused_ragged_partition(dev, oracle, npo, impl):
 
 
 # ---------------------------------------------------------------- batched (prefill) MFMA path
-@pytest.fixture(params=[0, 1, 2, 3, 4, 5], ids=["auto", "tile64", "tile128", "tile128w", "tile64w", "tile128x"])
+@pytest.fixture(params=[0, 1, 2, 3, 4, 5, 6], ids=["auto", "tile64", "tile128", "tile128w", "tile64w", "tile128x", "tile192"])
 def mmq(request):
     """Runs a prefill test on every GEMM variant (64 or 128 weight rows per workgroup)."""
     import ggml_mi355x as g

@@ -22,7 +22,7 @@ def apply_env(environ=None):
     sel = {
         "MI355X_GEMV_IMPL": (g.gemv_impl, {"tasks": g.GEMV_TASKS, "rows": g.GEMV_ROWS, "auto": g.GEMV_AUTO}),
         "MI355X_MMQ_IMPL": (g.mmq_impl, {"tile64": g.MMQ_TILE64, "tile128": g.MMQ_TILE128,
-                                         "tile128w": g.MMQ_TILE128W, "tile64w": g.MMQ_TILE64W, "tile128x": g.MMQ_TILE128X,
+                                         "tile128w": g.MMQ_TILE128W, "tile64w": g.MMQ_TILE64W, "tile128x": g.MMQ_TILE128X, "tile192": g.MMQ_TILE192,
                                          "auto": g.MMQ_AUTO}),
         "MI355X_PREFILL": (g.prefill_precision, {"f16": g.PREFILL_F16, "f16_all": g.PREFILL_F16_ALL,
                                                  "exact": g.PREFILL_EXACT}),
