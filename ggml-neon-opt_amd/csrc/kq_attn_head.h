@@ -109,7 +109,29 @@ __device__ __forceinline__ void attn_dma16_lanes(const void *src, uint32_t m0, i
         : "s"(m0), "s"(n), "v"(lane), "v"(src)
         : "memory", "m0", "vcc");
 }
+// ... all 64 lanes
+__device__ __forceinline__ void attn_dma16(const void *src, uint32_t m0) {
+    asm volatile(
+        "s_mov_b32 m0, %0\n\t"
+        "s_nop 0\n\t"
+        "global_load_lds_dwordx4 %1, off"
+        :
+        : "s"(m0), "v"(src)
+        : "memory", "m0");
+}
 #pragma clang diagnostic pop
+
+// K-cache ring of the split head_dim-64 kernel (KDMA below): per wave KQ_ATTN_KD slots of 64
+// rows (8 KiB)
+#ifndef KQ_ATTN_KD
+#define KQ_ATTN_KD 2
+#endif
+// 1: KDMA's soft_max on the cells each thread scored (max kept from KQ, group sums across the
+// quad's lanes, every wave summing the groups itself): three barriers instead of five
+#ifndef KQ_ATTN_KSM
+#define KQ_ATTN_KSM 1
+#endif
+constexpr int ATTN_KSLOT = 64 * 128;
 
 // attn_lds (kq_ops.hip) on the device: the per-head LDS layout below, before any staged V rows
 __device__ __forceinline__ int attn_lds_dev(int hd, int n_ctx) {
@@ -117,9 +139,17 @@ __device__ __forceinline__ int attn_lds_dev(int hd, int n_ctx) {
     return 6 * hd + n_ctx * 6 + hd * 64 + 16 + gsum;
 }
 
-template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false, bool SC1_IN = false, bool BATCH = false>
+// DS > 1 (kq_attn_decode past KQ_ATTN_BATCH_CTX cells, BATCH): the head is split over DS
+// workgroups by output dimension; workgroup ds computes the whole KQ and soft_max (every slice
+// needs every weight) and KQV for outputs [ds HD/DS, (ds + 1) HD/DS) only, from its slice of
+// the V rows, staged in LDS by LDS-DMA as soon as the position is known. One workgroup's
+// cache reads for KQV drop to 1/DS and arrive in one round under KQ and soft_max, where the
+// unsplit head waits for them in n_kv / (32 VB) dependent batches after soft_max. The
+// accumulation order of every output is unchanged (bit-exact).
+template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false, bool SC1_IN = false, bool BATCH = false,
+          int DS = 1>
 __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8_t *smem, float *out,
-                                          bool may_write) {
+                                          bool may_write, int ds = 0) {
     auto ldin = [](const float *p) {
         if (SC1_IN) return __uint_as_float(__hip_atomic_load((const uint32_t *)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
         return *p;
@@ -131,6 +161,17 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     // per round, KQ_ATTN_VB V chunks); the fused kernels' register budgets keep one K row and
     // one V chunk per step (PAIR off)
     constexpr bool PAIR = BATCH && TPH == 256 && !SC1_IN;
+    static_assert(DS == 1 || (PAIR && (HD / DS) % 4 == 0 && HD / DS * 4 <= TPH), "output slices");
+    constexpr int RS = HD / DS;  // V rows (outputs) of this workgroup
+    // KDMA (split head_dim-64 kernel, caches past the register path): KQ's K rows arrive by
+    // LDS-DMA in chunks of 256 cells, each wave loading the 64 rows its own lanes score, eight
+    // whole rows (1 KiB, 8 lanes per row) per instruction. The per-thread row loads of the
+    // other paths put 64 different rows under every load instruction, which the texture
+    // path serves at about one cache line per cycle (measured: ~0.85 us per 256 cells per
+    // workgroup); here an instruction touches 8 rows' lines. Within a row the 16-B chunks are
+    // stored at position k ^ ((lane >> 1) & 7) so that each thread's row reads are free of
+    // bank conflicts; the dot product itself is unchanged (bit-exact).
+    constexpr bool KDMA = PAIR && HD == 64 && DS > 1;
     constexpr int VB = PAIR ? (HD == 64 ? KQ_ATTN_VB64 : KQ_ATTN_VB) : 4;
     constexpr int KR = HD == 64 ? KQ_ATTN_KR64 : KQ_ATTN_KR128;  // K rows per thread per round (register budget)
     constexpr int ITEMS = HD * 4 / TPH;  // KQV (d, j) items per thread
@@ -170,7 +211,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     }
     // V rows staged in LDS (launch_attn sets a.v_lds) only in the KQ_ATTN_VLDS build: as a run-time
     // choice its LDS / global select turned KQV's cache loads into flat loads (tg1024 -4 %, r5t)
-    const bool vl = PAIR && KQ_ATTN_VLDS && a.v_lds;
+    const bool vl = DS > 1 || (PAIR && KQ_ATTN_VLDS && a.v_lds);
     uint4 vpre[ITEMS][VPF] = {};
 #pragma unroll
     for (int ii = 0; ii < ITEMS && !vl; ++ii) {
@@ -217,26 +258,37 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     // KQV) when it fits, past scal otherwise
     double *gsum = (a.n_ctx / 4) * 8 <= HD * 64 ? (double *)red : (double *)(scal + 4);
 
-    // V rows of the head's kv group, cells [0, n_kv), into LDS (vl): wave w takes rows
-    // [w HD / 4, (w + 1) HD / 4); row d at vlds + d * VSTR; completion: vmcnt(0) + barrier
-    // before KQV. A cell past pos holds whatever the cache holds (its weight is an exact 0);
-    // the new cell is patched from v16 as on the register path.
+    // V rows of the head's kv group (DS > 1: the slice's RS rows), cells [0, n_kv), into LDS
+    // (vl): wave w takes rows [w RS / 4, (w + 1) RS / 4); local row r at vlds + r * VSTR;
+    // completion: vmcnt(0) + barrier before KQV. Issued once KQ's cache loads have been used:
+    // vmcnt retires in issue order, so a wait for any load issued after the DMAs (rope's inputs,
+    // KQ's K rows) would wait for them too; soft_max issues no memory loads and runs under them.
+    // A cell past pos holds whatever the cache holds (its weight is an exact 0); the new cell is
+    // patched from v16 as on the register path.
     const int VSTR = 2 * a.n_ctx + 16;
     uint8_t *const vlds = smem + (attn_lds_dev(HD, a.n_ctx) + 15) / 16 * 16;
-    if (vl && !bad) {
+    uint8_t *const kring = vlds + RS * VSTR;  // (KDMA) after the V rows
+    auto issue_v_rows = [&]() {
+        if (!vl) return;
+        // every earlier load has been used; the builtin (unlike an asm wait) tells the compiler,
+        // which would otherwise wait vmcnt(0) later for loads it cannot prove consumed (a kpre
+        // row on a path that skipped it) — and so for these DMAs behind them. On every path.
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        if (bad) return;
         const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
         const int gran = n_kv / 8;  // 16-B granules of a row
 #pragma unroll 1
-        for (int d = wv * (HD / 4); d < (wv + 1) * (HD / 4); ++d) {
-            const uint8_t *src = (const uint8_t *)(a.v_cache + (int64_t)(g * HD + d) * a.n_ctx);
+        for (int r = wv * (RS / 4); r < (wv + 1) * (RS / 4); ++r) {
+            const uint8_t *src = (const uint8_t *)(a.v_cache + (int64_t)(g * HD + ds * RS + r) * a.n_ctx);
 #pragma unroll 1
             for (int i = 0; 64 * i < gran; ++i) {
-                const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS void *)(vlds + d * VSTR + 1024 * i));
+                const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS void *)(vlds + r * VSTR + 1024 * i));
                 const int n = __builtin_amdgcn_readfirstlane(gran - 64 * i);
                 attn_dma16_lanes(src + 1024 * i + 16 * ln, m0, ln, n < 64 ? n : 64);
             }
         }
-    }
+    };
+
     // EARLYV (head_dim 64, kq_attn_decode): KQV's first batch of V chunks past the prefetched
     // ones requested as soon as the position is known, under KQ and soft_max
     constexpr bool EARLYV = PAIR && HD == 64 && KQ_ATTN_EARLYV;
@@ -253,7 +305,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         }
     }
     const float *tc = a.rope_table + (a.rope_row ? 0 : (int64_t)pos * (HD / 2) * 2);
-    const bool writer = may_write && !bad && (h % gsz) == 0;
+    const bool writer = may_write && !bad && (h % gsz) == 0 && ds == 0;
     if (t < HD / 2) {
         const float c = a.rope_row ? rc : tc[2 * t], s = a.rope_row ? rs : tc[2 * t + 1];
         const float2 rq = rope_pair(x0, x1, c, s);
@@ -295,6 +347,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             }
             sc = vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale;
         }
+        issue_v_rows();
         const float wmx = wave_fmax(sc);  // max (order-free): per wave, then over the 4 waves
         if ((t & 63) == 0) scal[t >> 6] = wmx;
         __syncthreads();
@@ -322,7 +375,90 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             return;
         }
     } else {
-        if constexpr (PAIR) {
+        if constexpr (KDMA) {
+            const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+            const int n_ch = (n_kv + 255) / 256;  // chunks of 256 cells; wave wv scores cells 256 c + 64 wv + ln
+            const int sw = (ln >> 1) & 7;         // this lane's row: chunk k at position k ^ sw
+            auto issue_k = [&](int c) {
+                const uint32_t slot = (uint32_t)(uintptr_t)(LDS void *)(kring + (wv * KQ_ATTN_KD + c % KQ_ATTN_KD) * ATTN_KSLOT);
+                const int r = ln >> 3, pp = ln & 7;
+#pragma unroll
+                for (int i = 0; i < 8; ++i) {
+                    const int lr = 8 * i + r;  // the lane that scores this row
+                    int row = 256 * c + 64 * wv + lr;
+                    row = row < n_kv ? row : n_kv - 1;  // (rows past n_kv are never read)
+                    const int k = pp ^ ((lr >> 1) & 7);
+                    const uint8_t *src = (const uint8_t *)(a.k_cache + (int64_t)row * kvw + (int64_t)g * HD) + 16 * k;
+                    attn_dma16(src, __builtin_amdgcn_readfirstlane(slot + 1024 * i));
+                }
+            };
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // (nothing of the compiler's in flight past here)
+            issue_k(0);
+            if (n_ch > 1) issue_k(1);
+            static_assert(KQ_ATTN_KD == 2, "the waits below assume two slots per wave");
+            float mloc = -INFINITY;  // (KQ_ATTN_KSM) the max over this thread's cells
+            for (int c = 0; c < n_ch; ++c) {
+                if (c + 1 < n_ch) __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): chunk c landed, c + 1 in flight
+                else __builtin_amdgcn_s_waitcnt(0x0F70);
+                const int cell = 256 * c + t;
+                if (cell < n_kv) {
+                    uint4 kv[KV4];
+                    if (cell == pos) {
+#pragma unroll
+                        for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+                    } else {
+                        const uint8_t *rowp = kring + (wv * KQ_ATTN_KD + c % KQ_ATTN_KD) * ATTN_KSLOT + 128 * ln;
+#pragma unroll
+                        for (int i = 0; i < KV4; ++i) kv[i] = *(const uint4 *)(rowp + 16 * (i ^ sw));
+                    }
+                    const float sc = cell <= pos ? vec_dot_f16_rows<HD>(kv, (const uint4 *)q16) * a.scale : -INFINITY;
+                    w[cell] = sc;
+                    mloc = fmaxf(mloc, sc);
+                }
+                if (c + KQ_ATTN_KD < n_ch) issue_k(c + KQ_ATTN_KD);  // (this slot's reads were used above)
+            }
+            if constexpr (KQ_ATTN_KSM != 0) {
+                // soft_max over the thread's own cells 256 c + t (written by this thread: no
+                // barrier before reading them back). max: per wave, then over the 4 waves
+                const float wmx = wave_fmax(mloc);
+                if ((t & 63) == 0) scal[t >> 6] = wmx;
+                issue_v_rows();
+                __syncthreads();
+                if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
+                    vm_wait<0>();
+                    if (t < HD) out[t] = adiag_finite(__float_as_uint(w[t]));
+                    return;
+                }
+                const float mx = fmaxf(fmaxf(scal[0], scal[1]), fmaxf(scal[2], scal[3]));
+                for (int c = 0; c < n_ch; ++c) {  // (uniform trip count: every lane in the quad sums)
+                    const int cell = 256 * c + t;
+                    const float sv = cell < n_kv ? w[cell] : -INFINITY;
+                    const float ec = sv == -INFINITY ? 0.0f : v_expf(sv - mx);
+                    // group of cells 4g..4g+3 (lanes 4g..4g+3) in the vaddvq order (e0 + e1) + (e2 + e3)
+                    const float s01 = ec + dpp_mov_f32<0xB1>(ec);
+                    const float g4 = s01 + dpp_mov_f32<0x4E>(s01);
+                    if (cell < n_kv) {
+                        w[cell] = ec;
+                        if ((t & 3) == 0) gsum[cell >> 2] = (double)g4;
+                    }
+                }
+                __syncthreads();
+                // every wave computes the same sum (no barrier to publish it): ggml's in-order
+                // double sum, as a tree where that is exact (softmax_group_sum)
+                const double sum = softmax_group_sum(gsum, n_kv / 4, t & 63);
+                const float inv = (float)(1.0 / sum);
+                for (int c = 0; c < n_ch; ++c) {
+                    const int cell = 256 * c + t;
+                    if (cell < n_kv) p16[cell] = h2u(f2h_rne(w[cell] * inv));
+                }
+                __syncthreads();
+                if (ADIAG(a) == 3) {  // diagnostics: stop after soft_max
+                    vm_wait<0>();
+                    if (t < HD) out[t] = adiag_finite((uint32_t)p16[t]);
+                    return;
+                }
+            }
+        } else if constexpr (PAIR) {
             // KQ + scale + mask; the first pass (c == t) scores the prefetched row. KR cells per
             // thread per round, every row requested before any is used.
             for (int c0 = t; c0 < n_kv; c0 += KR * TPH) {
@@ -373,6 +509,8 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 w[c] = s;
             }
         }
+        if constexpr (!KDMA || KQ_ATTN_KSM == 0) {
+        issue_v_rows();
         __syncthreads();
         if (ADIAG(a) == 2) {  // diagnostics: stop after KQ
             vm_wait<0>();  // (staged V DMAs, vl) land before the wave ends
@@ -415,24 +553,60 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             if (t < HD) out[t] = adiag_finite((uint32_t)p16[t] ^ vpre[0][0].x ^ vpre[0][VPF - 1].y);
             return;
         }
-
+        }
     }
 
     // KQV: thread (d, j) -> accumulator j of output d. The V chunks past the prefetched ones
     // are requested KQ_ATTN_VB iterations at a time before any of them is used (a loop that
     // loads and then uses each chunk pays one memory latency per 32 cells: tg1024 -18 %).
-    if (vl) {  // the staged V rows landed (every wave's DMAs)
-        vm_wait<0>();
+    if (vl) {  // the staged V rows landed (every wave's DMAs); then the new cell patched into
+               // them from v16, so the loop below reads LDS only, without per-cell branches
+        __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0), seen by the compiler (no stale waits below)
         __syncthreads();
+        if (!bad)
+            for (int r = t; r < RS; r += TPH) *(uint16_t *)(vlds + r * VSTR + 2 * pos) = v16[ds * RS + r];
+        __syncthreads();
+    }
+    if (ADIAG(a) == 6) {  // diagnostics: stop before KQV's arithmetic (the staged V rows landed)
+        if (t < HD) out[t] = adiag_finite((uint32_t)p16[t] ^ *(const uint32_t *)(vlds + 16 * t));
+        return;
     }
     const int n_it = (pos + 32) / 32;  // iterations holding a cell <= pos; later ones add exact zeros
 #pragma unroll
-    for (int ii = 0; ii < ITEMS; ++ii) {
+    for (int ii = 0; ii < (DS > 1 ? 1 : ITEMS); ++ii) {
         const int item = t + TPH * ii;
-        const int d = item >> 2, j = item & 3;
+        const int vr_l = item >> 2, j = item & 3;  // (DS > 1: the local V row; threads past RS * 4 idle)
+        if (DS > 1 && vr_l >= RS) break;
+        const int d = DS > 1 ? ds * RS + vr_l : vr_l;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * a.n_ctx;
         uint32_t acc[4] = {};  // lanes 2k, 2k+1 of accumulator j in word k
-        if constexpr (PAIR) {
+        if (PAIR && vl) {  // V rows in LDS (new cell patched): 8 iterations' reads, then their FMAs
+            const uint8_t *vrow = vlds + vr_l * VSTR + 16 * j;
+            const uint8_t *prow = (const uint8_t *)p16 + 16 * j;
+            int it = 0;
+            for (; it + 8 <= n_it; it += 8) {
+                uint4 vb[8], pb[8];
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    vb[k] = *(const uint4 *)(vrow + 64 * (it + k));
+                    pb[k] = *(const uint4 *)(prow + 64 * (it + k));
+                }
+#pragma unroll
+                for (int k = 0; k < 8; ++k) {
+                    acc[0] = pk_fma_w(vb[k].x, pb[k].x, acc[0]);
+                    acc[1] = pk_fma_w(vb[k].y, pb[k].y, acc[1]);
+                    acc[2] = pk_fma_w(vb[k].z, pb[k].z, acc[2]);
+                    acc[3] = pk_fma_w(vb[k].w, pb[k].w, acc[3]);
+                }
+            }
+            for (; it < n_it; ++it) {
+                const uint4 vv = *(const uint4 *)(vrow + 64 * it), pp = *(const uint4 *)(prow + 64 * it);
+                acc[0] = pk_fma_w(vv.x, pp.x, acc[0]);
+                acc[1] = pk_fma_w(vv.y, pp.y, acc[1]);
+                acc[2] = pk_fma_w(vv.z, pp.z, acc[2]);
+                acc[3] = pk_fma_w(vv.w, pp.w, acc[3]);
+            }
+        } else if constexpr (PAIR) {
             for (int it0 = 0; it0 < n_it; it0 += VB) {
                 uint4 vb[VB];
 #pragma unroll
@@ -445,7 +619,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                     } else if (EARLYV && !vl && it0 == 0) {
                         vb[k] = vb0[ii][k < (EARLYV ? VB : 1) ? k : 0];  // requested with the position (it < n_it)
                     } else if (it < n_it) {
-                        vb[k] = vl ? *(const uint4 *)(vlds + d * VSTR + 2 * (32 * it + 8 * j))
+                        vb[k] = vl ? *(const uint4 *)(vlds + vr_l * VSTR + 2 * (32 * it + 8 * j))
                                    : *(const uint4 *)(vr + 32 * it + 8 * j);
                     }
                 }

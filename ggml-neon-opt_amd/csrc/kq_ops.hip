@@ -204,15 +204,22 @@ __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, floa
 // BATCH: the cache loads past the prefetched cells requested in batches (kq_attn_head.h); the
 // launch takes it for caches of more than KQ_ATTN_BATCH_CTX cells only: at short context its
 // code costs the head_dim-128 launch ~0.3 us (profiles/r05_attn_ab_batch_ctx.txt).
-template <int HD, bool BATCH>
+// DS > 1: DS workgroups per head, one slice of the head's outputs each (kq_attn_head.h).
+template <int HD, bool BATCH, int DS = 1>
 __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // XCD-aware head order (speed only): workgroup b runs on XCD b % 8, so XCD x takes the
-    // consecutive heads [x*n_head/8, (x+1)*n_head/8) and a KV group's cells are fetched into
-    // the L2 of 8*gsz/n_head XCDs (TinyLlama: 2, Llama-3: 1) instead of all 8.
-    int h = blockIdx.x;
-    if ((a.n_head & 7) == 0) h = (h & 7) * (a.n_head >> 3) + (h >> 3);
-    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0, false, BATCH>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true);
+    // consecutive heads [x*n_head/8, (x+1)*n_head/8) (every slice of a head on one XCD) and a
+    // KV group's cells are fetched into the L2 of 8*gsz/n_head XCDs (TinyLlama: 2, Llama-3: 1)
+    // instead of all 8.
+    int h = blockIdx.x / DS, ds = blockIdx.x % DS;
+    if ((a.n_head & 7) == 0) {
+        const int x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        h = x * (a.n_head >> 3) + i / DS;
+        ds = i % DS;
+    }
+    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0, false, BATCH, DS>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true,
+                                                                ds);
 }
 
 // One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read
@@ -518,9 +525,21 @@ size_t attn_lds(int hd, int n_ctx) {
     const size_t gsum = (size_t)(n_ctx / 4) * 8 <= (size_t)hd * 64 ? 0 : (size_t)(n_ctx / 4) * 8;
     return (size_t)6 * hd + (size_t)n_ctx * 6 + (size_t)hd * 64 + 16 + gsum;
 }
-// ... plus the head's V rows (v_lds): head_dim rows of n_ctx f16, 16 B of padding each
-size_t attn_lds_v(int hd, int n_ctx) {
-    return (attn_lds(hd, n_ctx) + 15) / 16 * 16 + (size_t)hd * ((size_t)n_ctx * 2 + 16);
+// ... plus the head's V rows (v_lds, or a 1/ds slice of them): rows of n_ctx f16, 16 B of
+// padding each
+size_t attn_lds_v(int hd, int n_ctx, int ds = 1) {
+    return (attn_lds(hd, n_ctx) + 15) / 16 * 16 + (size_t)(hd / ds) * ((size_t)n_ctx * 2 + 16) +
+           (hd == 64 && ds > 1 ? (size_t)4 * KQ_ATTN_KD * ATTN_KSLOT : 0);  // + the K ring (KDMA)
+}
+// Output slices per head for a cache of n_ctx cells (1: no split): past the register path's
+// KQ_ATTN_BATCH_CTX cells, the fewest of 4 / 8 whose V slice fits the LDS beside the rest
+int attn_slices(const AttnArgs &a) {
+    if (attn_impl() != MI355X_ATTN_SPLIT || a.n_ctx <= KQ_ATTN_BATCH_CTX || a.n_ctx % 8 ||
+        ((uintptr_t)a.v_cache & 15u))
+        return 1;
+    for (int ds = 4; ds <= 8; ds *= 2)
+        if (attn_lds_v(a.head_dim, a.n_ctx, ds) <= 160 * 1024) return ds;
+    return 1;
 }
 
 // ------------------------------------------------------------ launch helpers
@@ -585,7 +604,10 @@ bool attn_group_ok(const AttnArgs &a, int nwaves) {
 // MI355X_ATTN_GROUP (one workgroup per kv group: each group's cells read once, 1/gsz of the
 // cache traffic, +2.3 us per launch on the TinyLlama token: profiles/r02_attention_ab.md);
 // Set only through mi355x_attn_impl().
-std::atomic<int> g_attn_impl{MI355X_ATTN_HEAD};
+#ifndef KQ_ATTN_DEFAULT_IMPL  // (experiment builds: the selector's initial value)
+#define KQ_ATTN_DEFAULT_IMPL MI355X_ATTN_SPLIT
+#endif
+std::atomic<int> g_attn_impl{KQ_ATTN_DEFAULT_IMPL};
 int attn_impl() { return g_attn_impl.load(); }
 
 int launch_attn(const AttnArgs &a, hipStream_t s) {
@@ -606,6 +628,23 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     // is known (all of them in flight under KQ and soft_max) where they fit; shorter caches keep
     // the register prefetch, which issues V with the position itself.
     AttnArgs b = a;
+    const int ds = attn_slices(a);
+    if (ds > 1) {
+        const size_t lds = attn_lds_v(a.head_dim, a.n_ctx, ds);
+        const dim3 grid((unsigned)(a.n_head * ds));
+#define KQ_ATTN_SPLIT_LAUNCH(HD, DS)                                                                        \
+    if (a.head_dim == HD && ds == DS) {                                                                    \
+        allow_lds((const void *)kq_attn_decode<HD, true, DS>, lds);                                        \
+        return timed_launch("kq::kq_attn_decode<" #HD ", true, " #DS ">", bytes, kq_attn_decode<HD, true, DS>, \
+                            grid, dim3(256), lds, s, b);                                                   \
+    }
+        KQ_ATTN_SPLIT_LAUNCH(64, 4)
+        KQ_ATTN_SPLIT_LAUNCH(64, 8)
+        KQ_ATTN_SPLIT_LAUNCH(128, 4)
+        KQ_ATTN_SPLIT_LAUNCH(128, 8)
+#undef KQ_ATTN_SPLIT_LAUNCH
+        return MI355X_E_INVAL;
+    }
     b.v_lds = a.n_ctx > KQ_ATTN_BATCH_CTX && a.n_ctx % 8 == 0 && attn_lds_v(a.head_dim, a.n_ctx) <= 160 * 1024 &&
               ((uintptr_t)a.v_cache & 15u) == 0 && KQ_ATTN_VLDS;
     const size_t lds = b.v_lds ? attn_lds_v(a.head_dim, a.n_ctx) : attn_lds(a.head_dim, a.n_ctx);
@@ -794,7 +833,7 @@ int mi355x_attn_prompt_impl(int impl) {
 }
 
 int mi355x_attn_impl(int impl) {
-    if (impl != MI355X_ATTN_GROUP && impl != MI355X_ATTN_HEAD) return MI355X_E_INVAL;
+    if (impl != MI355X_ATTN_GROUP && impl != MI355X_ATTN_HEAD && impl != MI355X_ATTN_SPLIT) return MI355X_E_INVAL;
     const int prev = attn_impl();
     g_attn_impl.store(impl);
     return prev;

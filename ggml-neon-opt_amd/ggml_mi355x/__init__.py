@@ -29,7 +29,7 @@ FLAG_OUTPUT = 1
 E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM = 0, -1, -2, -3, -4, -6
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
-ATTN_GROUP, ATTN_HEAD = 0, 1
+ATTN_GROUP, ATTN_HEAD, ATTN_SPLIT = 0, 1, 2
 MMQ_AUTO, MMQ_TILE64, MMQ_TILE128, MMQ_TILE128W, MMQ_TILE64W, MMQ_TILE128X, MMQ_TILE192 = 0, 1, 2, 3, 4, 5, 6
 PREFILL_EXACT, PREFILL_F16, PREFILL_F16_ALL = 0, 1, 2
 
@@ -430,7 +430,8 @@ def attn_prompt_impl(impl):
 
 
 def attn_impl(impl):
-    """ATTN_GROUP (one workgroup per kv group, default) / ATTN_HEAD; returns the previous."""
+    """ATTN_SPLIT (default: per query head, split by output past 256 cache cells) / ATTN_HEAD
+    (per query head) / ATTN_GROUP (per kv group); returns the previous."""
     return int(lib().mi355x_attn_impl(impl))
 
 

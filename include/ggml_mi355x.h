@@ -355,13 +355,15 @@ int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
  * the tokens before it, bit for bit. A position outside the cache gives a NaN row and no
  * cell. */
 int mi355x_attn_prompt(const mi355x_attn_desc *a, int n_tokens, void *stream);
-/* Attention kernel selector (A/B runs, parity of both): MI355X_ATTN_HEAD (default: one
- * workgroup per query head, the fastest launch) or MI355X_ATTN_GROUP (one workgroup per KV
- * group where its cells fit in LDS: cells [0, n_kv) read once and shared by the group's
- * n_head/n_head_kv query heads, 1/gsz of the cache reads). Returns the previous value, or
- * MI355X_E_INVAL. */
+/* Attention kernel selector (A/B runs, parity of all): MI355X_ATTN_SPLIT (default: one
+ * workgroup per query head; for caches past 256 cells each head split over 4 or 8 workgroups
+ * by output dimension, where the slice's LDS fits), MI355X_ATTN_HEAD (one workgroup per query
+ * head at every cache size) or MI355X_ATTN_GROUP (one workgroup per KV group where its cells
+ * fit in LDS: cells [0, n_kv) read once and shared by the group's n_head/n_head_kv query
+ * heads, 1/gsz of the cache reads). Returns the previous value, or MI355X_E_INVAL. */
 #define MI355X_ATTN_GROUP 0
 #define MI355X_ATTN_HEAD 1
+#define MI355X_ATTN_SPLIT 2
 int mi355x_attn_impl(int impl);
 /* Prompt attention selector (A/B runs, parity of both): MI355X_ATTN_GROUP (default: one
  * workgroup per kv group and token, the group's query heads sharing every K/V load, where

@@ -101,10 +101,11 @@ def test_rope(dev, O, hd, nh, base):
 
 
 # ---------------------------------------------------------------- attention
-@pytest.fixture(params=[0, 1], ids=["group", "head"])
+@pytest.fixture(params=[0, 1, 2], ids=["group", "head", "split"])
 def attn_impl(request):
-    """Runs an attention test on both kernels: one workgroup per kv group (default; the
-    per-head kernel where the group's slice does not fit in LDS) and one per query head."""
+    """Runs an attention test on every kernel: one workgroup per kv group (the per-head
+    kernel where the group's slice does not fit in LDS), one per query head, and (past 256
+    cache cells) each head split over 4 or 8 workgroups by output."""
     import ggml_mi355x as g
     prev = g.attn_impl(request.param)
     yield request.param
@@ -146,7 +147,7 @@ def test_attn_decode_sequence(dev, O, attn_impl, hd, nh, nkv, n_ctx, rope_row):
 
 
 @pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 1024), (128, 16, 4, 512), (64, 8, 2, 256), (64, 8, 2, 288)])
-def test_attn_decode_long_random_cache(dev, O, hd, nh, nkv, n_ctx):
+def test_attn_decode_long_random_cache(dev, O, attn_impl, hd, nh, nkv, n_ctx):
     """Every cell of both caches random (not only the cells this test wrote), then positions
     across the whole cache: the batched loads of kq_attn_decode<HD, true> (caches past 256
     cells: two K rows per round at head_dim 64, eight V chunks per batch) and the boundary

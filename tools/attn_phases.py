@@ -1,6 +1,7 @@
 """Where the time of one decode-attention launch goes (diagnostic): kq_attn_decode at
 TinyLlama / Llama-3 head shapes, stopped after its loads (MI355X_ATTN_DIAG=1), after KQ
-(2), after soft_max (3), empty (4) or complete (0). Per-launch kernel time from the
+(2), after soft_max (3), empty (4) or complete (0) (ATTN_PHASES_DIAGS: which of them; the
+stops need the KQ_ATTN_DIAG build). Per-launch kernel time from the
 library's launch events, and back-to-back launches per microsecond of stream time."""
 import json
 import os
@@ -52,7 +53,7 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "child":
         child()
         sys.exit(0)
-    for diag in ("4", "1", "2", "3", "0"):
+    for diag in os.environ.get("ATTN_PHASES_DIAGS", "4 1 2 3 0").split():
         env = dict(os.environ, MI355X_ATTN_DIAG=diag)
         r = subprocess.run([sys.executable, __file__, "child"], env=env, capture_output=True, text=True, timeout=300)
         if r.returncode:

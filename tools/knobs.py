@@ -4,7 +4,7 @@ library reads no environment (tests/test_abi.py); tools call apply_env() at star
 
   MI355X_<KNOB>=v          -> ggml_mi355x.debug_knob("<KNOB>", v)   (DEBUG_KNOBS)
   MI355X_GEMV_IMPL=tasks|rows, MI355X_MMQ_IMPL=tile64|..., MI355X_PREFILL=f16|f16_all,
-  MI355X_ATTN_IMPL=group|head -> the matching selector call
+  MI355X_ATTN_IMPL=group|head|split -> the matching selector call
 """
 import os
 
@@ -26,7 +26,7 @@ def apply_env(environ=None):
                                          "auto": g.MMQ_AUTO}),
         "MI355X_PREFILL": (g.prefill_precision, {"f16": g.PREFILL_F16, "f16_all": g.PREFILL_F16_ALL,
                                                  "exact": g.PREFILL_EXACT}),
-        "MI355X_ATTN_IMPL": (g.attn_impl, {"group": g.ATTN_GROUP, "head": g.ATTN_HEAD}),
+        "MI355X_ATTN_IMPL": (g.attn_impl, {"group": g.ATTN_GROUP, "head": g.ATTN_HEAD, "split": g.ATTN_SPLIT}),
     }
     for name, (fn, table) in sel.items():
         v = env.get(name)
