@@ -320,7 +320,7 @@ bool multi_types_ok(int a, int b) { return a == b || (is_kquant(a) && is_kquant(
 bool attn_oproj_fusable(const mi355x_backend *b, const mi355x_tensor *t, const mi355x_tensor *mm, int readers) {
     const int ko = (int)kq::knob(kq::KNOB_ATTN_OPROJ);  // A/B: 0 never, 2 every backend
     if (ko == 0 || (ko == 1 && !b->attn_oproj) || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] != 1) return false;
-    if (kq::attn_impl() != MI355X_ATTN_HEAD || !elidable(t, readers)) return false;
+    if (kq::attn_impl() == MI355X_ATTN_GROUP || !elidable(t, readers)) return false;  // (per-head kernels)
     if (!is_gemv_node(mm) || mm->src[1] != t || !is_kquant(mm->src[0]->type)) return false;
     const mi355x_tensor *w = mm->src[0];
     if (w->ne[0] != t->ne[0] || w->ne[2] != 1 || w->ne[3] != 1 || mm->nb[0] != 4) return false;

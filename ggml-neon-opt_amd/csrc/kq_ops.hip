@@ -600,10 +600,11 @@ bool attn_group_ok(const AttnArgs &a, int nwaves) {
     return (m & 7u) == 0 && a.diag == 0 && attn_group_bytes(a, nwaves) <= 160 * 1024;
 }
 
-// MI355X_ATTN_HEAD (one workgroup per query head: the default, the fastest launch) or
-// MI355X_ATTN_GROUP (one workgroup per kv group: each group's cells read once, 1/gsz of the
-// cache traffic, +2.3 us per launch on the TinyLlama token: profiles/r02_attention_ab.md);
-// Set only through mi355x_attn_impl().
+// MI355X_ATTN_SPLIT (the default: one workgroup per query head, split by output past 256
+// cells: profiles/r05_attn_split_ab.txt), MI355X_ATTN_HEAD (one workgroup per query head at
+// every size) or MI355X_ATTN_GROUP (one workgroup per kv group: each group's cells read
+// once, 1/gsz of the cache traffic, +2.3 us per launch on the TinyLlama token:
+// profiles/r02_attention_ab.md). Set only through mi355x_attn_impl().
 #ifndef KQ_ATTN_DEFAULT_IMPL  // (experiment builds: the selector's initial value)
 #define KQ_ATTN_DEFAULT_IMPL MI355X_ATTN_SPLIT
 #endif

@@ -197,6 +197,18 @@ __device__ __forceinline__ float wave_fmax(float v) {
     const float r3 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 48));
     return fmaxf(fmaxf(r0, r1), fmaxf(r2, r3));
 }
+__device__ __forceinline__ double readlane_f64(double v, int l) {
+    const uint64_t u = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)u, l);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(u >> 32), l);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// The wave's sum of v, for callers whose every partial sum is exact (then any order gives
+// the same bits): DPP within rows of 16, then the four row sums.
+__device__ __forceinline__ double wave_sum_exact_f64(double v) {
+    v = row16_sum(v);
+    return (readlane_f64(v, 0) + readlane_f64(v, 16)) + (readlane_f64(v, 32) + readlane_f64(v, 48));
+}
 
 // sum / n in double, correctly rounded (ggml_float mean = sum/ne00): for n a power of
 // two the quotient is the exact product sum * 2^-k (both correctly rounded results of
