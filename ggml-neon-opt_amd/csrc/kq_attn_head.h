@@ -185,11 +185,58 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     const int kvw = a.n_head_kv * HD;
     if (ADIAG(a) == 4) return;  // diagnostics (MI355X_ATTN_DIAG): empty launch
 
+    // LDS (attn_lds): q16 | k16 | v16 (HD f16 each) | w (n_ctx f32) | p16 (n_ctx f16) |
+    // red (HD*32 f16 accumulators) | scal (max, 1/sum, 2 pad) [| gsum]; every piece 16-B aligned
+    uint16_t *q16 = (uint16_t *)smem;
+    uint16_t *k16 = q16 + HD;
+    uint16_t *v16 = k16 + HD;
+    float *w = (float *)(smem + 6 * HD);
+    uint16_t *p16 = (uint16_t *)(w + a.n_ctx);
+    h16 *red = (h16 *)(p16 + a.n_ctx);
+    float *scal = (float *)(red + HD * 32);
+    // per group of 4 cells: (double)((e0 + e1) + (e2 + e3)); lives in `red` (free until
+    // KQV) when it fits, past scal otherwise
+    double *gsum = (a.n_ctx / 4) * 8 <= HD * 64 ? (double *)red : (double *)(scal + 4);
+    const int VSTR = 2 * a.n_ctx + 16;
+    uint8_t *const vlds = smem + (attn_lds_dev(HD, a.n_ctx) + 15) / 16 * 16;
+    uint8_t *const kring = vlds + RS * VSTR;  // (KDMA) after the V rows
+    // (KDMA) chunk c of K rows, cells [256 c, 256 c + 256) clamped to lim - 1, into this
+    // wave's ring slot: wave wv's 64 rows, 8 whole rows per instruction
+    auto issue_k = [&](int c, int lim) {
+        const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
+        const uint32_t slot = (uint32_t)(uintptr_t)(LDS void *)(kring + (wv * KQ_ATTN_KD + c % KQ_ATTN_KD) * ATTN_KSLOT);
+        const int r = ln >> 3, pp = ln & 7;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) {
+            const int lr = 8 * i + r;  // the lane that scores this row
+            int row = 256 * c + 64 * wv + lr;
+            row = row < lim ? row : lim - 1;  // (rows past n_kv are never read)
+            const int k = pp ^ ((lr >> 1) & 7);
+            const uint8_t *src = (const uint8_t *)(a.k_cache + (int64_t)row * kvw + (int64_t)g * HD) + 16 * k;
+            attn_dma16(src, __builtin_amdgcn_readfirstlane(slot + 1024 * i));
+        }
+    };
+
     // ---- 0. position-independent loads, issued with the position
     const int pos_in = *a.pos;
     float x0 = 0.f, x1 = 0.f, y0 = 0.f, y1 = 0.f;
     float rc = 0.f, rs = 0.f;  // rope_row: cos/sin of the thread's pair, staged with the position
-    if (t < HD / 2) {
+    if constexpr (KDMA) {
+        // q | k | v | the rope row (rope_row) by one LDS-DMA of wave 0 into the first KiB of the
+        // V-row area (free until KQ is done), then the first chunk of K rows, all before the
+        // position is known. Every memory operation of this path is then an LDS-DMA whose
+        // waits are counted here, so rope waits for its inputs only (vmcnt retires in order:
+        // a compiler-visible load here would make every later wait cover the K rows too).
+        if (t < 64) {
+            const float *src = t < 16   ? a.q + (int64_t)h * HD + 4 * t
+                               : t < 32 ? a.k + (int64_t)g * HD + 4 * (t - 16)
+                               : t < 48 ? a.v + (int64_t)g * HD + 4 * (t - 32)
+                               : a.rope_row ? a.rope_table + 4 * (t - 48)
+                                            : a.q + (int64_t)h * HD;
+            attn_dma16(src, (uint32_t)(uintptr_t)(LDS void *)vlds);
+        }
+        issue_k(0, a.n_ctx);
+    } else if (t < HD / 2) {
         if (a.rope_row) {
             rc = a.rope_table[2 * t];
             rs = a.rope_table[2 * t + 1];
@@ -204,7 +251,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         x0 = ldin(a.v + (int64_t)g * HD + (t - HD / 2));
     }
     uint4 kpre[KV4] = {};
-    if (t < a.n_ctx && t < KPF && ADIAG(a) != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
+    if (!KDMA && t < a.n_ctx && t < KPF && ADIAG(a) != 5) {  // (diag 5: no cache loads, stop after rope; timing only)
         const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)t * kvw + (int64_t)g * HD);
 #pragma unroll
         for (int i = 0; i < KV4; ++i) kpre[i] = kr[i];
@@ -245,19 +292,6 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             }
         }
     }
-    // LDS (attn_lds): q16 | k16 | v16 (HD f16 each) | w (n_ctx f32) | p16 (n_ctx f16) |
-    // red (HD*32 f16 accumulators) | scal (max, 1/sum, 2 pad) [| gsum]; every piece 16-B aligned
-    uint16_t *q16 = (uint16_t *)smem;
-    uint16_t *k16 = q16 + HD;
-    uint16_t *v16 = k16 + HD;
-    float *w = (float *)(smem + 6 * HD);
-    uint16_t *p16 = (uint16_t *)(w + a.n_ctx);
-    h16 *red = (h16 *)(p16 + a.n_ctx);
-    float *scal = (float *)(red + HD * 32);
-    // per group of 4 cells: (double)((e0 + e1) + (e2 + e3)); lives in `red` (free until
-    // KQV) when it fits, past scal otherwise
-    double *gsum = (a.n_ctx / 4) * 8 <= HD * 64 ? (double *)red : (double *)(scal + 4);
-
     // V rows of the head's kv group (DS > 1: the slice's RS rows), cells [0, n_kv), into LDS
     // (vl): wave w takes rows [w RS / 4, (w + 1) RS / 4); local row r at vlds + r * VSTR;
     // completion: vmcnt(0) + barrier before KQV. Issued once KQ's cache loads have been used:
@@ -265,9 +299,6 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     // KQ's K rows) would wait for them too; soft_max issues no memory loads and runs under them.
     // A cell past pos holds whatever the cache holds (its weight is an exact 0); the new cell is
     // patched from v16 as on the register path.
-    const int VSTR = 2 * a.n_ctx + 16;
-    uint8_t *const vlds = smem + (attn_lds_dev(HD, a.n_ctx) + 15) / 16 * 16;
-    uint8_t *const kring = vlds + RS * VSTR;  // (KDMA) after the V rows
     auto issue_v_rows = [&]() {
         if (!vl) return;
         // every earlier load has been used; the builtin (unlike an asm wait) tells the compiler,
@@ -304,10 +335,32 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 if (k < n_it0) vb0[ii][k] = *(const uint4 *)(vr + 32 * k + 8 * j);
         }
     }
+    if constexpr (KDMA) {  // the staged q | k | v | rope row landed (wave 0: all but chunk 0's 8 DMAs)
+        if (t < 64) __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8)
+        __syncthreads();
+        const float *stg = (const float *)vlds;
+        if (t < HD / 2) {
+            x0 = stg[2 * t], x1 = stg[2 * t + 1];
+            y0 = stg[HD + 2 * t], y1 = stg[HD + 2 * t + 1];
+            rc = stg[3 * HD + 2 * t], rs = stg[3 * HD + 2 * t + 1];  // (used with rope_row only)
+        } else if (t < HD / 2 + HD) {
+            x0 = stg[2 * HD + (t - HD / 2)];
+        }
+        if (!a.rope_row) {  // the position's row of the whole table: loaded now and waited for
+                            // here (with chunk 0: the slow path), so no load of the compiler's
+                            // is pending where this branch rejoins the rope_row path
+            if (t < HD / 2) {
+                const float *row = a.rope_table + (int64_t)pos * HD;
+                rc = row[2 * t];
+                rs = row[2 * t + 1];
+            }
+            __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+        }
+    }
     const float *tc = a.rope_table + (a.rope_row ? 0 : (int64_t)pos * (HD / 2) * 2);
     const bool writer = may_write && !bad && (h % gsz) == 0 && ds == 0;
     if (t < HD / 2) {
-        const float c = a.rope_row ? rc : tc[2 * t], s = a.rope_row ? rs : tc[2 * t + 1];
+        const float c = (KDMA || a.rope_row) ? rc : tc[2 * t], s = (KDMA || a.rope_row) ? rs : tc[2 * t + 1];
         const float2 rq = rope_pair(x0, x1, c, s);
         q16[2 * t] = h2u(f2h_rne(rq.x));
         q16[2 * t + 1] = h2u(f2h_rne(rq.y));
@@ -332,11 +385,17 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     if (n_kv <= TPH) {  // one cell per thread: score, max, exp and group sum stay in registers
         const int c = t;
         float sc = -INFINITY;
+        if (KDMA) __builtin_amdgcn_s_waitcnt(0x0F70);  // (KDMA) chunk 0 of the K rows landed
         if (c < n_kv && c <= pos) {
             uint4 kv[KV4];
             if (c == pos) {
 #pragma unroll
                 for (int i = 0; i < KV4; ++i) kv[i] = ((const uint4 *)k16)[i];
+            } else if (KDMA) {  // chunk 0's ring slot of this wave: cell t at lane t & 63
+                const int ln = t & 63, sw = (ln >> 1) & 7;
+                const uint8_t *rowp = kring + (__builtin_amdgcn_readfirstlane(t >> 6) * KQ_ATTN_KD) * ATTN_KSLOT + 128 * ln;
+#pragma unroll
+                for (int i = 0; i < KV4; ++i) kv[i] = *(const uint4 *)(rowp + 16 * (i ^ sw));
             } else if (!KQ_ATTN_EARLY && KPF < TPH && c >= KPF) {  // a cell past the prefetched ones (below the position)
                 const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
 #pragma unroll
@@ -379,22 +438,9 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
             const int n_ch = (n_kv + 255) / 256;  // chunks of 256 cells; wave wv scores cells 256 c + 64 wv + ln
             const int sw = (ln >> 1) & 7;         // this lane's row: chunk k at position k ^ sw
-            auto issue_k = [&](int c) {
-                const uint32_t slot = (uint32_t)(uintptr_t)(LDS void *)(kring + (wv * KQ_ATTN_KD + c % KQ_ATTN_KD) * ATTN_KSLOT);
-                const int r = ln >> 3, pp = ln & 7;
-#pragma unroll
-                for (int i = 0; i < 8; ++i) {
-                    const int lr = 8 * i + r;  // the lane that scores this row
-                    int row = 256 * c + 64 * wv + lr;
-                    row = row < n_kv ? row : n_kv - 1;  // (rows past n_kv are never read)
-                    const int k = pp ^ ((lr >> 1) & 7);
-                    const uint8_t *src = (const uint8_t *)(a.k_cache + (int64_t)row * kvw + (int64_t)g * HD) + 16 * k;
-                    attn_dma16(src, __builtin_amdgcn_readfirstlane(slot + 1024 * i));
-                }
-            };
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // (nothing of the compiler's in flight past here)
-            issue_k(0);
-            if (n_ch > 1) issue_k(1);
+            // chunk 0 was issued with the position (prologue); the cache stores of the new cell,
+            // issued since, are older than chunk 1 and covered by its waits
+            if (n_ch > 1) issue_k(1, n_kv);
             static_assert(KQ_ATTN_KD == 2, "the waits below assume two slots per wave");
             float mloc = -INFINITY;  // (KQ_ATTN_KSM) the max over this thread's cells
             for (int c = 0; c < n_ch; ++c) {
@@ -415,7 +461,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                     w[cell] = sc;
                     mloc = fmaxf(mloc, sc);
                 }
-                if (c + KQ_ATTN_KD < n_ch) issue_k(c + KQ_ATTN_KD);  // (this slot's reads were used above)
+                if (c + KQ_ATTN_KD < n_ch) issue_k(c + KQ_ATTN_KD, n_kv);  // (this slot's reads were used above)
             }
             if constexpr (KQ_ATTN_KSM != 0) {
                 // soft_max over the thread's own cells 256 c + t (written by this thread: no

@@ -30,18 +30,21 @@ def child():
         y = torch.empty(nh * hd, device=dev)
         for p in sorted({0, 63, n_ctx // 2 - 1, n_ctx - 1}):
             pos = torch.tensor([p], dtype=torch.int32, device=dev)
+            # ATTN_PHASES_ROPE_ROW=1: only the position's rope row (as the model's graph passes it)
+            rr = os.environ.get("ATTN_PHASES_ROPE_ROW", "0") == "1"
+            tb = tab[p].contiguous() if rr else tab
             for _ in range(20):
-                g.attn_decode(q, k, v, pos, tab, kc, vc, nh, nkv, hd, 0.125, out=y)
+                g.attn_decode(q, k, v, pos, tb, kc, vc, nh, nkv, hd, 0.125, out=y, rope_row=rr)
             g.timing_enable(True)
             for _ in range(50):
-                g.attn_decode(q, k, v, pos, tab, kc, vc, nh, nkv, hd, 0.125, out=y)
+                g.attn_decode(q, k, v, pos, tb, kc, vc, nh, nkv, hd, 0.125, out=y, rope_row=rr)
             rows = g.timing_read()
             g.timing_enable(False)
             torch.cuda.synchronize()
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             e0.record()
             for _ in range(200):
-                g.attn_decode(q, k, v, pos, tab, kc, vc, nh, nkv, hd, 0.125, out=y)
+                g.attn_decode(q, k, v, pos, tb, kc, vc, nh, nkv, hd, 0.125, out=y, rope_row=rr)
             e1.record()
             torch.cuda.synchronize()
             out.append({"hd": hd, "n_ctx": n_ctx, "pos": p, "kernel_us": float(np.median([r[2] for r in rows]) * 1e3),
