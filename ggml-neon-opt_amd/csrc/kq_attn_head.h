@@ -441,10 +441,13 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
             // chunk 0 was issued with the position (prologue); the cache stores of the new cell,
             // issued since, are older than chunk 1 and covered by its waits
             if (n_ch > 1) issue_k(1, n_kv);
-            static_assert(KQ_ATTN_KD == 2, "the waits below assume two slots per wave");
+            static_assert(KQ_ATTN_KD == 2 || KQ_ATTN_KD == 3, "the waits below cover two or three slots per wave");
+            if (KQ_ATTN_KD == 3 && n_ch > 2) issue_k(2, n_kv);
             float mloc = -INFINITY;  // (KQ_ATTN_KSM) the max over this thread's cells
             for (int c = 0; c < n_ch; ++c) {
-                if (c + 1 < n_ch) __builtin_amdgcn_s_waitcnt(0x0F78);  // vmcnt(8): chunk c landed, c + 1 in flight
+                // chunk c landed: the younger chunks in flight (8 DMAs each) may still be
+                if (KQ_ATTN_KD == 3 && c + 2 < n_ch) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
+                else if (c + 1 < n_ch) __builtin_amdgcn_s_waitcnt(0x0F78);               // vmcnt(8)
                 else __builtin_amdgcn_s_waitcnt(0x0F70);
                 const int cell = 256 * c + t;
                 if (cell < n_kv) {
