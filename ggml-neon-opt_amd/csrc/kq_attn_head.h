@@ -171,7 +171,12 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     // workgroup); here an instruction touches 8 rows' lines. Within a row the 16-B chunks are
     // stored at position k ^ ((lane >> 1) & 7) so that each thread's row reads are free of
     // bank conflicts; the dot product itself is unchanged (bit-exact).
-    constexpr bool KDMA = PAIR && HD == 64 && DS > 1;
+    // head_dim 128: a row is 256 B, two lanes per cell (each holding half the row; the odd
+    // lane continues the even lane's accumulators: the NEON order), 128 cells per chunk.
+    constexpr bool KDMA = PAIR && DS > 1;
+    constexpr int CPC = HD == 64 ? 256 : 128;  // (KDMA) cells per chunk, CPC / 4 per wave
+    // (KDMA) soft_max on each thread's own cells: head_dim 64 (one cell per lane)
+    constexpr bool KSM = KDMA && HD == 64 && KQ_ATTN_KSM != 0;
     constexpr int VB = PAIR ? (HD == 64 ? KQ_ATTN_VB64 : KQ_ATTN_VB) : 4;
     constexpr int KR = HD == 64 ? KQ_ATTN_KR64 : KQ_ATTN_KR128;  // K rows per thread per round (register budget)
     constexpr int ITEMS = HD * 4 / TPH;  // KQV (d, j) items per thread
@@ -200,18 +205,20 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     const int VSTR = 2 * a.n_ctx + 16;
     uint8_t *const vlds = smem + (attn_lds_dev(HD, a.n_ctx) + 15) / 16 * 16;
     uint8_t *const kring = vlds + RS * VSTR;  // (KDMA) after the V rows
-    // (KDMA) chunk c of K rows, cells [256 c, 256 c + 256) clamped to lim - 1, into this
-    // wave's ring slot: wave wv's 64 rows, 8 whole rows per instruction
+    // (KDMA) chunk c of K rows, cells [CPC c, CPC c + CPC) clamped to lim - 1, into this
+    // wave's ring slot: wave wv's CPC / 4 rows, 1 KiB (8 or 4 whole rows) per instruction.
+    // Lane ln of the wave reads the 128 B at slot + 128 ln: a whole row (head_dim 64) or half
+    // of one (128: row ln / 2, half ln & 1), its 16-B chunk k at position k ^ ((ln >> 1) & 7)
     auto issue_k = [&](int c, int lim) {
         const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
         const uint32_t slot = (uint32_t)(uintptr_t)(LDS void *)(kring + (wv * KQ_ATTN_KD + c % KQ_ATTN_KD) * ATTN_KSLOT);
         const int r = ln >> 3, pp = ln & 7;
 #pragma unroll
         for (int i = 0; i < 8; ++i) {
-            const int lr = 8 * i + r;  // the lane that scores this row
-            int row = 256 * c + 64 * wv + lr;
+            const int lr = 8 * i + r;  // the lane that reads these 128 B
+            int row = CPC * c + (CPC / 4) * wv + (HD == 64 ? lr : lr >> 1);
             row = row < lim ? row : lim - 1;  // (rows past n_kv are never read)
-            const int k = pp ^ ((lr >> 1) & 7);
+            const int k = (HD == 64 ? 0 : 8 * (lr & 1)) + (pp ^ ((lr >> 1) & 7));
             const uint8_t *src = (const uint8_t *)(a.k_cache + (int64_t)row * kvw + (int64_t)g * HD) + 16 * k;
             attn_dma16(src, __builtin_amdgcn_readfirstlane(slot + 1024 * i));
         }
@@ -227,13 +234,18 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         // position is known. Every memory operation of this path is then an LDS-DMA whose
         // waits are counted here, so rope waits for its inputs only (vmcnt retires in order:
         // a compiler-visible load here would make every later wait cover the K rows too).
-        if (t < 64) {
-            const float *src = t < 16   ? a.q + (int64_t)h * HD + 4 * t
-                               : t < 32 ? a.k + (int64_t)g * HD + 4 * (t - 16)
-                               : t < 48 ? a.v + (int64_t)g * HD + 4 * (t - 32)
-                               : a.rope_row ? a.rope_table + 4 * (t - 48)
-                                            : a.q + (int64_t)h * HD;
-            attn_dma16(src, (uint32_t)(uintptr_t)(LDS void *)vlds);
+        if (t < 64) {  // (head_dim 128: two instructions, q | k then v | rope)
+            constexpr int L = HD / 4;  // lanes per vector
+#pragma unroll
+            for (int i = 0; i < HD / 64; ++i) {
+                const int e = 64 * i + t;  // 16-B piece of the 4 HD floats
+                const float *src = e < L       ? a.q + (int64_t)h * HD + 4 * e
+                                   : e < 2 * L ? a.k + (int64_t)g * HD + 4 * (e - L)
+                                   : e < 3 * L ? a.v + (int64_t)g * HD + 4 * (e - 2 * L)
+                                   : a.rope_row ? a.rope_table + 4 * (e - 3 * L)
+                                                : a.q + (int64_t)h * HD;
+                attn_dma16(src, (uint32_t)(uintptr_t)(LDS void *)(vlds + 1024 * i));
+            }
         }
         issue_k(0, a.n_ctx);
     } else if (t < HD / 2) {
@@ -382,7 +394,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
         return;
     }
 
-    if (n_kv <= TPH) {  // one cell per thread: score, max, exp and group sum stay in registers
+    if ((!KDMA || HD == 64) && n_kv <= TPH) {  // one cell per thread: score, max, exp and group sum stay in registers
         const int c = t;
         float sc = -INFINITY;
         if (KDMA) __builtin_amdgcn_s_waitcnt(0x0F70);  // (KDMA) chunk 0 of the K rows landed
@@ -436,8 +448,14 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     } else {
         if constexpr (KDMA) {
             const int wv = __builtin_amdgcn_readfirstlane(t >> 6), ln = t & 63;
-            const int n_ch = (n_kv + 255) / 256;  // chunks of 256 cells; wave wv scores cells 256 c + 64 wv + ln
-            const int sw = (ln >> 1) & 7;         // this lane's row: chunk k at position k ^ sw
+            const int n_ch = (n_kv + CPC - 1) / CPC;  // chunks; wave wv scores cells CPC c + (CPC / 4) wv + ...
+            const int sw = (ln >> 1) & 7;             // this lane's 128 B: chunk k at position k ^ sw
+            // head_dim 128: this lane's half of q (chunks 8 (ln & 1) + k)
+            uint4 qh[8];
+            if (HD == 128) {
+#pragma unroll
+                for (int i = 0; i < 8; ++i) qh[i] = ((const uint4 *)q16)[8 * (ln & 1) + i];
+            }
             // chunk 0 was issued with the position (prologue); the cache stores of the new cell,
             // issued since, are older than chunk 1 and covered by its waits
             if (n_ch > 1) issue_k(1, n_kv);
@@ -449,6 +467,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 if (KQ_ATTN_KD == 3 && c + 2 < n_ch) __builtin_amdgcn_s_waitcnt(0x4F70);  // vmcnt(16)
                 else if (c + 1 < n_ch) __builtin_amdgcn_s_waitcnt(0x0F78);               // vmcnt(8)
                 else __builtin_amdgcn_s_waitcnt(0x0F70);
+                if constexpr (HD == 64) {
                 const int cell = 256 * c + t;
                 if (cell < n_kv) {
                     uint4 kv[KV4];
@@ -464,9 +483,50 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                     w[cell] = sc;
                     mloc = fmaxf(mloc, sc);
                 }
+                } else {  // head_dim 128: lanes 2m, 2m + 1 score cell 128 c + 32 wv + m
+                    const int cell = 128 * c + 32 * wv + (ln >> 1);
+                    const bool live = cell < n_kv;  // (uniform per lane pair: both or neither)
+                    uint4 kv[8];
+                    if (cell == pos) {
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) kv[i] = ((const uint4 *)k16)[8 * (ln & 1) + i];
+                    } else {
+                        const uint8_t *rowp = kring + (wv * KQ_ATTN_KD + c % KQ_ATTN_KD) * ATTN_KSLOT + 128 * ln;
+#pragma unroll
+                        for (int i = 0; i < 8; ++i) kv[i] = *(const uint4 *)(rowp + 16 * (i ^ sw));
+                    }
+                    // ggml_vec_dot_f16 (NEON FP16), accumulator j over chunks j, 4+j, 8+j, 12+j:
+                    // every lane runs its own two chunks per accumulator from 0 (the even lane's
+                    // are the first two steps), then again from the even lane's result (the odd
+                    // lane's are the last two); the odd lane reduces (acc0 + acc2) + (acc1 + acc3)
+                    uint32_t x[4][4], y[4][4];
+#pragma unroll
+                    for (int j = 0; j < 4; ++j) {
+                        const uint32_t c0[4] = {kv[j].x, kv[j].y, kv[j].z, kv[j].w};
+                        const uint32_t c1[4] = {kv[4 + j].x, kv[4 + j].y, kv[4 + j].z, kv[4 + j].w};
+                        const uint32_t q0[4] = {qh[j].x, qh[j].y, qh[j].z, qh[j].w};
+                        const uint32_t q1[4] = {qh[4 + j].x, qh[4 + j].y, qh[4 + j].z, qh[4 + j].w};
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) x[j][k] = pk_fma_w(c1[k], q1[k], pk_fma_w(c0[k], q0[k], 0u));
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            const uint32_t e = dpp_w<0xA0>(x[j][k]);  // quad_perm [0,0,2,2]: the even lane's
+                            y[j][k] = pk_fma_w(c1[k], q1[k], pk_fma_w(c0[k], q0[k], e));
+                        }
+                    }
+                    h16 sv[8];
+#pragma unroll
+                    for (int l = 0; l < 8; ++l) {
+                        const h16 s0 = lane_of(y[0], l) + lane_of(y[2], l);
+                        const h16 s1 = lane_of(y[1], l) + lane_of(y[3], l);
+                        sv[l] = s0 + s1;
+                    }
+                    const float dot = f16x8_reduce(sv);
+                    if (live && (ln & 1)) w[cell] = cell <= pos ? dot * a.scale : -INFINITY;
+                }
                 if (c + KQ_ATTN_KD < n_ch) issue_k(c + KQ_ATTN_KD, n_kv);  // (this slot's reads were used above)
             }
-            if constexpr (KQ_ATTN_KSM != 0) {
+            if constexpr (KSM) {
                 // soft_max over the thread's own cells 256 c + t (written by this thread: no
                 // barrier before reading them back). max: per wave, then over the 4 waves
                 const float wmx = wave_fmax(mloc);
@@ -581,7 +641,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 w[c] = s;
             }
         }
-        if constexpr (!KDMA || KQ_ATTN_KSM == 0) {
+        if constexpr (!KSM) {
         issue_v_rows();
         __syncthreads();
         if (ADIAG(a) == 2) {  // diagnostics: stop after KQ

@@ -529,7 +529,7 @@ size_t attn_lds(int hd, int n_ctx) {
 // padding each
 size_t attn_lds_v(int hd, int n_ctx, int ds = 1) {
     return (attn_lds(hd, n_ctx) + 15) / 16 * 16 + (size_t)(hd / ds) * ((size_t)n_ctx * 2 + 16) +
-           (hd == 64 && ds > 1 ? (size_t)4 * KQ_ATTN_KD * ATTN_KSLOT : 0);  // + the K ring (KDMA)
+           (ds > 1 ? (size_t)4 * KQ_ATTN_KD * ATTN_KSLOT : 0);  // + the K ring (KDMA)
 }
 // Output slices per head for a cache of n_ctx cells (1: no split): past the register path's
 // KQ_ATTN_BATCH_CTX cells, the fewest of 4 / 8 whose V slice fits the LDS beside the rest

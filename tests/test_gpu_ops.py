@@ -146,12 +146,14 @@ def test_attn_decode_sequence(dev, O, attn_impl, hd, nh, nkv, n_ctx, rope_row):
     assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
 
 
-@pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 1024), (128, 16, 4, 512), (64, 8, 2, 256), (64, 8, 2, 288)])
+@pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 1024), (128, 16, 4, 512), (64, 8, 2, 256), (64, 8, 2, 288),
+                                             (128, 8, 2, 2048), (128, 8, 2, 288)])
 def test_attn_decode_long_random_cache(dev, O, attn_impl, hd, nh, nkv, n_ctx):
     """Every cell of both caches random (not only the cells this test wrote), then positions
     across the whole cache: the batched loads of kq_attn_decode<HD, true> (caches past 256
     cells: two K rows per round at head_dim 64, eight V chunks per batch) and the boundary
-    cache sizes on either side of that choice, bit-exact with the oracle."""
+    cache sizes on either side of that choice, bit-exact with the oracle. The split kernel
+    (past 256 cells) at both head sizes, with 4 slices and (head_dim 128 at 2048 cells) 8."""
     import torch
     import ggml_mi355x as g
     rng = np.random.default_rng(n_ctx + hd)
