@@ -532,7 +532,10 @@ size_t attn_lds_v(int hd, int n_ctx, int ds = 1) {
            (ds > 1 ? (size_t)4 * KQ_ATTN_KD * ATTN_KSLOT : 0);  // + the K ring (KDMA)
 }
 // Output slices per head for a cache of n_ctx cells (1: no split): past the register path's
-// KQ_ATTN_BATCH_CTX cells, the fewest of 4 / 8 whose V slice fits the LDS beside the rest
+// KQ_ATTN_BATCH_CTX cells, the fewest of 4 / 8 whose V slice fits the LDS beside the rest.
+// Every slice scores every cell, so the K reads grow with the slices: 16 slices at 4096 cells
+// (head_dim 64) measured slower than one workgroup per head (tg4096 894 against 925 tok/s,
+// profiles/r05_attn_split_ab.txt).
 int attn_slices(const AttnArgs &a) {
     if (attn_impl() != MI355X_ATTN_SPLIT || a.n_ctx <= KQ_ATTN_BATCH_CTX || a.n_ctx % 8 ||
         ((uintptr_t)a.v_cache & 15u))
