@@ -531,6 +531,9 @@ size_t attn_lds_v(int hd, int n_ctx, int ds = 1) {
     return (attn_lds(hd, n_ctx) + 15) / 16 * 16 + (size_t)(hd / ds) * ((size_t)n_ctx * 2 + 16) +
            (ds > 1 ? (size_t)4 * KQ_ATTN_KD * ATTN_KSLOT : 0);  // + the K ring (KDMA)
 }
+#ifndef KQ_ATTN_DSMIN
+#define KQ_ATTN_DSMIN 4  // (experiment builds: 8)
+#endif
 // Output slices per head for a cache of n_ctx cells (1: no split): past the register path's
 // KQ_ATTN_BATCH_CTX cells, the fewest of 4 / 8 whose V slice fits the LDS beside the rest.
 // Every slice scores every cell, so the K reads grow with the slices: 16 slices at 4096 cells
@@ -540,7 +543,7 @@ int attn_slices(const AttnArgs &a) {
     if (attn_impl() != MI355X_ATTN_SPLIT || a.n_ctx <= KQ_ATTN_BATCH_CTX || a.n_ctx % 8 ||
         ((uintptr_t)a.v_cache & 15u))
         return 1;
-    for (int ds = 4; ds <= 8; ds *= 2)
+    for (int ds = KQ_ATTN_DSMIN; ds <= 8; ds *= 2)
         if (attn_lds_v(a.head_dim, a.n_ctx, ds) <= 160 * 1024) return ds;
     return 1;
 }
