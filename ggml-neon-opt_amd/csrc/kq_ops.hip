@@ -378,14 +378,19 @@ size_t attn_prompt_group_lds(int hd, int n_ctx, int gsz) {
     return (size_t)gsz * ((size_t)2 * hd + (size_t)n_ctx * 6 + 16);
 }
 
-template <int HD>
+// GSZ: the group size fixed at compile time (4: Llama-3-8B, 8: TinyLlama / 70B), or 0 for
+// any gsz <= PROMPT_GMAX: with it fixed, the per-head loops have no exits and hipcc keeps
+// several LDS reads of KQV in flight (with the run-time exit it waited lgkmcnt(0) before
+// every probability read).
+template <int HD, int GSZ = 0>
 __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
     constexpr int KV4 = HD / 8;
     constexpr int ITEMS = HD * 4 / 256;
+    constexpr int GM = GSZ > 0 ? GSZ : PROMPT_GMAX;  // heads the unrolled loops cover
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // the latest tokens (the most cells) are dispatched first: a shorter tail
     const int g = blockIdx.x, i = (int)gridDim.y - 1 - (int)blockIdx.y, t = threadIdx.x;
-    const int gsz = a.n_head / a.n_head_kv;  // <= PROMPT_GMAX (host check)
+    const int gsz = GSZ > 0 ? GSZ : a.n_head / a.n_head_kv;  // <= PROMPT_GMAX (host check)
     const int kvw = a.n_head_kv * HD;
     const int64_t qrow = (int64_t)i * a.n_head * HD;
     const int pos_in = a.pos[i];
@@ -417,8 +422,8 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
 #pragma unroll
             for (int k = 0; k < KV4; ++k) kv[k] = kr[k];
 #pragma unroll
-            for (int hh = 0; hh < PROMPT_GMAX; ++hh)
-                if (hh < gsz)
+            for (int hh = 0; hh < GM; ++hh)
+                if (GSZ > 0 || hh < gsz)
                     w[hh * nc + c] = (KQ_PROMPT_DIAG & 1) ? __uint_as_float(kv[0].x ^ kv[KV4 - 1].w) * 1e-30f
                                                           : vec_dot_f16_rows<HD>(kv, (const uint4 *)(q16 + hh * HD)) * a.scale;
         } else {
@@ -472,31 +477,34 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
         const int item = t + 256 * ii;
         const int d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * nc;
-        uint32_t acc[PROMPT_GMAX][4] = {};  // lanes 2k, 2k+1 of head hh's accumulator j in word k
-        for (int it0 = 0; it0 < n_it; it0 += 4) {  // 4 V chunks in flight per round trip
+        uint32_t acc[GM][4] = {};  // lanes 2k, 2k+1 of head hh's accumulator j in word k
+        // one 32-cell iteration: its V chunk against every head's probabilities
+        auto step = [&](const uint4 &vv, int it) {
+            const int c0 = 32 * it + 8 * j;
+            const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
+#pragma unroll
+            for (int hh = 0; hh < GM; ++hh) {
+                if (GSZ == 0 && hh >= gsz) break;
+                const uint4 pp = *(const uint4 *)(p16 + hh * nc + c0);
+                acc[hh][0] = pk_fma_w(vw[0], pp.x, acc[hh][0]);
+                acc[hh][1] = pk_fma_w(vw[1], pp.y, acc[hh][1]);
+                acc[hh][2] = pk_fma_w(vw[2], pp.z, acc[hh][2]);
+                acc[hh][3] = pk_fma_w(vw[3], pp.w, acc[hh][3]);
+            }
+        };
+        int it = 0;
+        for (; it + 4 <= n_it; it += 4) {  // whole batches: 4 V chunks in flight, no guards
             uint4 vq[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) vq[k] = it0 + k < n_it ? *(const uint4 *)(vr + 32 * (it0 + k) + 8 * j) : uint4{};
+            for (int k = 0; k < 4; ++k) vq[k] = *(const uint4 *)(vr + 32 * (it + k) + 8 * j);
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                if (it0 + k >= n_it) break;
-                const int c0 = 32 * (it0 + k) + 8 * j;
-                const uint32_t vw[4] = {vq[k].x, vq[k].y, vq[k].z, vq[k].w};
-#pragma unroll
-                for (int hh = 0; hh < PROMPT_GMAX; ++hh) {
-                    if (hh >= gsz) break;
-                    const uint4 pp = *(const uint4 *)(p16 + hh * nc + c0);
-                    acc[hh][0] = pk_fma_w(vw[0], pp.x, acc[hh][0]);
-                    acc[hh][1] = pk_fma_w(vw[1], pp.y, acc[hh][1]);
-                    acc[hh][2] = pk_fma_w(vw[2], pp.z, acc[hh][2]);
-                    acc[hh][3] = pk_fma_w(vw[3], pp.w, acc[hh][3]);
-                }
-            }
+            for (int k = 0; k < 4; ++k) step(vq[k], it + k);
         }
+        for (; it < n_it; ++it) step(*(const uint4 *)(vr + 32 * it + 8 * j), it);
         // the 4 accumulators of output d sit in the 4 lanes of a quad (j = t & 3)
 #pragma unroll
-        for (int hh = 0; hh < PROMPT_GMAX; ++hh) {
-            if (hh >= gsz) break;
+        for (int hh = 0; hh < GM; ++hh) {
+            if (GSZ == 0 && hh >= gsz) break;
             const float o = bad ? __builtin_nanf("") : f16x8_reduce_quad(acc[hh]);
             if (j == 0) {
                 a.out[qrow + (int64_t)(g * gsz + hh) * HD + d] = o;
@@ -697,8 +705,15 @@ int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
         rc = a.no_store ? 0 : timed_launch("kq::kq_kv_store<64>", 0.0, kq_kv_store<64>, gs, dim3(256), 0, s, a);
         if (rc) return rc;
         if (group) {
-            allow_lds((const void *)kq_attn_prompt_group<64>, glds);
-            return timed_launch("kq::kq_attn_prompt_group<64>", 0.0, kq_attn_prompt_group<64>, gg, dim3(256), glds, s, a);
+#define KQ_PROMPT_GROUP_LAUNCH(HD, G)                                                                     \
+    {                                                                                                   \
+        allow_lds((const void *)kq_attn_prompt_group<HD, G>, glds);                                     \
+        return timed_launch("kq::kq_attn_prompt_group<" #HD ">", 0.0, kq_attn_prompt_group<HD, G>, gg, dim3(256), \
+                            glds, s, a);                                                                \
+    }
+            if (gsz == 8) KQ_PROMPT_GROUP_LAUNCH(64, 8)
+            if (gsz == 4) KQ_PROMPT_GROUP_LAUNCH(64, 4)
+            KQ_PROMPT_GROUP_LAUNCH(64, 0)
         }
         allow_lds((const void *)kq_attn_prompt<64>, lds);
         return timed_launch("kq::kq_attn_prompt<64>", 0.0, kq_attn_prompt<64>, ga, dim3(256), lds, s, a);
@@ -706,8 +721,10 @@ int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
     rc = a.no_store ? 0 : timed_launch("kq::kq_kv_store<128>", 0.0, kq_kv_store<128>, gs, dim3(256), 0, s, a);
     if (rc) return rc;
     if (group) {
-        allow_lds((const void *)kq_attn_prompt_group<128>, glds);
-        return timed_launch("kq::kq_attn_prompt_group<128>", 0.0, kq_attn_prompt_group<128>, gg, dim3(256), glds, s, a);
+        if (gsz == 8) KQ_PROMPT_GROUP_LAUNCH(128, 8)
+        if (gsz == 4) KQ_PROMPT_GROUP_LAUNCH(128, 4)
+        KQ_PROMPT_GROUP_LAUNCH(128, 0)
+#undef KQ_PROMPT_GROUP_LAUNCH
     }
     allow_lds((const void *)kq_attn_prompt<128>, lds);
     return timed_launch("kq::kq_attn_prompt<128>", 0.0, kq_attn_prompt<128>, ga, dim3(256), lds, s, a);
