@@ -585,7 +585,13 @@ MmqShape mmq_shape(int type, int64_t rows, int64_t M) {
     if (impl == MI355X_MMQ_TILE128X) return {128, type == Q6_K ? 2 : 4};
     if (impl == MI355X_MMQ_TILE192) return type == Q6_K ? MmqShape{128, 1} : MmqShape{192, 1};
     const int64_t rt128 = (rows + 127) / 128;
-    if (rt128 * ((M + 127) / 128) >= 160) return {128, 2};
+    const int64_t g128x128 = rt128 * ((M + 127) / 128), g128x64 = rt128 * ((M + 63) / 64);
+    // a 128 x 128 grid that fills under ~3/4 of two workgroups per CU, where the 128 x 64 one
+    // has two per CU: 128 x 64 (TinyLlama's 11264-row gate+up at M = 512: 352 against 704
+    // workgroups, 49.8 -> 41.6 us; Llama-3-8B ffn_up's 448 keep 128 x 128, 95 against 97 us;
+    // profiles/r05_mmq_tl_tiles.txt)
+    if (type != Q6_K && g128x128 >= 160 && g128x128 < 384 && g128x64 >= 512) return {128, 1};
+    if (g128x128 >= 160) return {128, 2};
     if (type == Q6_K && ((rows + 63) / 64) * ((M + 127) / 128) >= 192) return {64, 2};
     if (type != Q6_K && rt128 * ((M + 63) / 64) >= 256) return {128, 1};
     return {64, 1};
