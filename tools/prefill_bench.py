@@ -20,7 +20,7 @@ SHAPES = [("l3 q/o", 12, 4096, 4096), ("l3 up", 12, 4096, 14336), ("l3 down", 12
           ("tl gate", 12, 2048, 5632), ("l3 v q5", 13, 4096, 1024), ("tl out q6", 14, 2048, 32000),
           ("l3 down q6", 14, 14336, 4096), ("l3 q/o q5", 13, 4096, 4096), ("l3 up q5", 13, 4096, 14336),
           ("l3 down q5", 13, 14336, 4096), ("tl q/o", 12, 2048, 2048), ("tl gate+up", 12, 2048, 11264),
-          ("tl down", 12, 5632, 2048)]
+          ("tl down", 12, 5632, 2048), ("tl down q6", 14, 5632, 2048), ("tl v q6", 14, 2048, 256)]
 
 
 def main(M=512, reps=10, only=None):
