@@ -85,7 +85,10 @@ __host__ __device__ inline LdsLayout lds_layout(int ncol, int nb, int out_per_wg
 constexpr int ROWS_WAVES = KQ_ROWS_WAVES;  // the most waves per workgroup (LDS layout, launch bounds)
 // Small launches run ROWS_WAVES_SMALL waves per workgroup (the wave count is a launch
 // parameter: blockDim.x / 64): fewer waves to dispatch for a stream that is short anyway.
-constexpr int ROWS_WAVES_SMALL = 6;
+#ifndef KQ_ROWS_WAVES_SMALL
+#define KQ_ROWS_WAVES_SMALL 6
+#endif
+constexpr int ROWS_WAVES_SMALL = KQ_ROWS_WAVES_SMALL;
 constexpr int ROWS_QPASS = 3;  // fused-quantization passes of 4*ROWS_WAVES superblocks
 // L2 prefetch issued with the first weight step (waves whose stream outlasts the
 // ring): while the activation is fetched and quantized, each wave touches the next
