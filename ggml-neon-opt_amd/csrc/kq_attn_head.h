@@ -29,6 +29,11 @@ namespace kq {
 //  4. kqv[d] = vec_dot_f16(v_cache[g*hd+d][0..n_kv), p16): thread (d, j) runs
 //     accumulator j (8 lanes) over cells 32it+8j+l, then the f16 reduce tree.
 // A position outside the cache fails loudly: NaN output, caches untouched.
+// Caches past KQ_ATTN_BATCH_CTX cells (kq_attn_decode<HD, true, DS>, DS = 4 or 8): the head
+// is split over DS workgroups by output; q/k/v, the rope row and the first chunk of K rows
+// arrive by LDS-DMA with the position, K whole rows per instruction into a two-slot ring
+// per wave (KDMA below), soft_max on each thread's own cells (head_dim 64), and the
+// workgroup's V rows by LDS-DMA under soft_max ("Split by output").
 // Timing diagnostics (MI355X_ATTN_DIAG stops) only in experiment builds
 // (make variant-ops NAME=adiag VFLAGS=-DKQ_ATTN_DIAG=1); the product kernel has none.
 #ifndef KQ_ATTN_DIAG
