@@ -11,6 +11,7 @@
 #include <stdio.h>
 #include <stdlib.h>
 #include <algorithm>
+#include <chrono>
 #include <vector>
 
 __global__ void __launch_bounds__(768) probe(unsigned long long *rec, int spin_ticks, int slow_xcc, int extra_ticks) {
@@ -44,8 +45,8 @@ int main() {
     // waited for the previous launch per XCC rather than for all of it, the next launch
     // would start later on that XCC only.
     struct Cfg {
-        int spin_us, lds_kb, graph, slow, extra_us;
-    } cfgs[] = {{0, 0, 0, -1, 0}, {2, 0, 0, -1, 0}, {5, 0, 0, -1, 0}, {10, 0, 0, -1, 0}, {2, 64, 0, -1, 0},
+        int spin_us, lds_kb, graph, slow, extra_us, gap_us = 0;
+    } cfgs[] = {{5, 0, 0, -1, 0, 10}, {5, 0, 0, -1, 0, 30}, {5, 96, 0, -1, 0, 30}, {5, 0, 0, -1, 0, 100}, {0, 0, 0, -1, 0}, {2, 0, 0, -1, 0}, {5, 0, 0, -1, 0}, {10, 0, 0, -1, 0}, {2, 64, 0, -1, 0},
                 {5, 96, 0, -1, 0}, {2, 0, 1, -1, 0}, {5, 0, 1, -1, 0}, {5, 96, 1, -1, 0}, {5, 0, 0, 4, 3},
                 {5, 0, 1, 4, 3}, {5, 0, 0, 0, 3}};
     std::vector<unsigned long long> h((size_t)launches * wgs * 2);
@@ -53,9 +54,15 @@ int main() {
         const int ticks = c.spin_us * 100;  // 100 MHz
         const size_t lds = (size_t)c.lds_kb << 10;
         auto issue = [&]() {
-            for (int l = 0; l < launches; ++l)
+            for (int l = 0; l < launches; ++l) {
                 hipLaunchKernelGGL(probe, dim3(wgs), dim3(768), lds, s, rec + (size_t)l * wgs * 2, ticks, c.slow,
                                    c.extra_us * 100);
+                if (c.gap_us) {  // host-side gap: the GPU goes idle between launches (as eager Python launches do)
+                    const auto t = std::chrono::steady_clock::now();
+                    while (std::chrono::steady_clock::now() - t < std::chrono::microseconds(c.gap_us)) {
+                    }
+                }
+            }
         };
         if (c.graph) {
             hipGraph_t g;
@@ -90,8 +97,8 @@ int main() {
             }
         }
         std::sort(spread.begin(), spread.end());
-        printf("spin %2d us lds %3d KB %s slow xcc %2d +%d us: launch start spread med %.2f us | per-XCC median entry (us):",
-               c.spin_us, c.lds_kb, c.graph ? "graph" : "eager", c.slow, c.extra_us, spread[spread.size() / 2]);
+        printf("gap %3d us spin %2d us lds %3d KB %s slow xcc %2d +%d us: launch start spread med %.2f us | per-XCC median entry (us):",
+               c.gap_us, c.spin_us, c.lds_kb, c.graph ? "graph" : "eager", c.slow, c.extra_us, spread[spread.size() / 2]);
         for (int x = 0; x < 8; ++x) {
             if (per[x].empty()) {
                 printf("  x%d -", x);
