@@ -24,6 +24,11 @@ SHAPES = [("tl q", 12, 2048, 2048), ("tl 8rows", 12, 2048, 8), ("tl gate+up", 12
 
 
 PRO = os.environ.get("STAMPS_PRO", "none")  # none | norm | swiglu: fused prologue (kq_rows only)
+# STAMPS_SLEEP=1: a spin kernel (torch.cuda._sleep, ~10 ms) ahead of the burst, so the burst's
+# launches queue behind it and run back to back, as in the graph-replayed token. Without it
+# the GPU idles between the eager launches of a short kernel and its XCDs wake in turn
+# (tools/xcd_skew.hip: 0.1 .. 1.4 us apart), which the entry stamps then show.
+SLEEP = os.environ.get("STAMPS_SLEEP", "0") == "1"
 
 
 def main(impl):
@@ -51,6 +56,8 @@ def main(impl):
         for r in range(5):
             buf.zero_()
             torch.cuda.synchronize()
+            if SLEEP:
+                torch.cuda._sleep(20_000_000)
             # warm the clocks with a burst; stamps of the LAST launch of the burst survive
             for i in range(60):
                 if i == 59:

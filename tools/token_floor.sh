@@ -6,6 +6,8 @@
 # the last is the launch chain's floor (every launch kept, each returning at entry).
 #   build: make -C ggml-neon-opt_amd variant NAME=fdiag VFLAGS="-DKQ_ROWS_DIAG=1 -DKQ_GEMV_DIAG=1 -DKQ_ATTN_DIAG=1"
 #          plus kq_ops.hip with the same flags (tools/token_floor.sh's header in DESIGN §7)
+# LIST="tag lib knob=v ..." lines replace the default variants (e.g. the attention's
+# diagnostic stops: ATTN_DIAG=5 q/k/v + rope only, 1 + the cache loads, 2 + KQ, 3 + soft_max).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
@@ -21,11 +23,11 @@ for model in ${MODELS:-tinyllama-1.1b llama-3-8b}; do
       rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc $tag"; tail -5 gpurun_out/tf_tmp.err; exit $rc; }
       tail -1 gpurun_out/tf_tmp.json | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$model', '$r', '$tag', d['value'], d['ms_per_step'], d['config']['stages_per_token'])"
     done <<LIST
-product $P -
+${LIST:-product $P -
 diag $D -
 attn_empty $D ATTN_DIAG=4
 gemv_empty $D GEMV_DIAG=256
-all_empty $D GEMV_DIAG=256 ATTN_DIAG=4
+all_empty $D GEMV_DIAG=256 ATTN_DIAG=4}
 LIST
   done
 done
