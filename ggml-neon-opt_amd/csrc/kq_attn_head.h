@@ -42,7 +42,9 @@ namespace kq {
 // Cells whose K row / V chunk is loaded with the position, before it is known (the rest,
 // up to the position, after it): 0 = every cell of the register path (TPH) / 8 V iterations.
 #ifndef KQ_ATTN_PFC
-#define KQ_ATTN_PFC 64  // 0 (all of them) -> 64: TinyLlama token +2 %, tools/ab_ao.sh
+// 0 (all of them) -> 64: TinyLlama token +2 % (tools/ab_ao.sh); 64 -> 32: +0.5 % (tg128, three
+// interleaved rounds), 8B equal; 128: -1 % (tools/attn_pfc_ab.sh, profiles/r05_attn_pfc_ab.txt)
+#define KQ_ATTN_PFC 32
 #endif
 // a diagnostic stop's output: depends on every value it keeps live, always a float in [1, 2)
 // (garbage bits would send the next GEMV's rms_norm and soft_max down their slow paths)
