@@ -205,8 +205,13 @@ __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, floa
 // launch takes it for caches of more than KQ_ATTN_BATCH_CTX cells only: at short context its
 // code costs the head_dim-128 launch ~0.3 us (profiles/r05_attn_ab_batch_ctx.txt).
 // DS > 1: DS workgroups per head, one slice of the head's outputs each (kq_attn_head.h).
-template <int HD, bool BATCH, int DS = 1>
-__global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
+// TPH: threads per head (experiment builds: KQ_ATTN_TPH64 = 128 for the short-context head_dim
+// 64 launch; the register path then holds 128 cells, the fused attention + o-proj's shape).
+#ifndef KQ_ATTN_TPH64
+#define KQ_ATTN_TPH64 256
+#endif
+template <int HD, bool BATCH, int DS = 1, int TPH = 256>
+__global__ void __launch_bounds__(TPH) kq_attn_decode(const AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // XCD-aware head order (speed only): workgroup b runs on XCD b % 8, so XCD x takes the
     // consecutive heads [x*n_head/8, (x+1)*n_head/8) (every slice of a head on one XCD) and a
@@ -218,7 +223,7 @@ __global__ void __launch_bounds__(256) kq_attn_decode(const AttnArgs a) {
         h = x * (a.n_head >> 3) + i / DS;
         ds = i % DS;
     }
-    attn_head<HD, 256, 0, KQ_ATTN_OSC1 != 0, false, BATCH, DS>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true,
+    attn_head<HD, TPH, 0, KQ_ATTN_OSC1 != 0, false, BATCH, DS>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true,
                                                                 ds);
 }
 
@@ -665,7 +670,9 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     const size_t lds = b.v_lds ? attn_lds_v(a.head_dim, a.n_ctx) : attn_lds(a.head_dim, a.n_ctx);
     const bool batch = a.n_ctx > KQ_ATTN_BATCH_CTX;
     if (a.head_dim == 64) {
-        if (!batch) return timed_launch("kq::kq_attn_decode<64, false>", bytes, kq_attn_decode<64, false>, dim3(a.n_head), dim3(256), lds, s, b);
+        if (!batch)
+            return timed_launch("kq::kq_attn_decode<64, false>", bytes, kq_attn_decode<64, false, 1, KQ_ATTN_TPH64>,
+                                dim3(a.n_head), dim3(KQ_ATTN_TPH64), lds, s, b);
         if (b.v_lds) allow_lds((const void *)kq_attn_decode<64, true>, lds);
         return timed_launch("kq::kq_attn_decode<64, true>", bytes, kq_attn_decode<64, true>, dim3(a.n_head), dim3(256), lds, s, b);
     }
