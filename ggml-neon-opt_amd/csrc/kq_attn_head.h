@@ -154,7 +154,7 @@ __device__ __forceinline__ int attn_lds_dev(int hd, int n_ctx) {
 // unsplit head waits for them in n_kv / (32 VB) dependent batches after soft_max. The
 // accumulation order of every output is unchanged (bit-exact).
 template <int HD, int TPH = 256, int VPF0 = 0, bool OUT_WT = false, bool SC1_IN = false, bool BATCH = false,
-          int DS = 1>
+          int DS = 1, bool KD1 = false>
 __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8_t *smem, float *out,
                                           bool may_write, int ds = 0) {
     auto ldin = [](const float *p) {
@@ -180,7 +180,9 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     // bank conflicts; the dot product itself is unchanged (bit-exact).
     // head_dim 128: a row is 256 B, two lanes per cell (each holding half the row; the odd
     // lane continues the even lane's accumulators: the NEON order), 128 cells per chunk.
-    constexpr bool KDMA = PAIR && DS > 1;
+    // KD1 (experiment builds, KQ_ATTN_KDMA1): the unsplit head of a short cache (<= 256 cells)
+    // on the same LDS-DMA path: K ring, staged q | k | v, V rows in LDS
+    constexpr bool KDMA = PAIR && (DS > 1 || KD1);
     constexpr int CPC = HD == 64 ? 256 : 128;  // (KDMA) cells per chunk, CPC / 4 per wave
     // (KDMA) soft_max on each thread's own cells: head_dim 64 (one cell per lane)
     constexpr bool KSM = KDMA && HD == 64 && KQ_ATTN_KSM != 0;
@@ -277,7 +279,7 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
     }
     // V rows staged in LDS (launch_attn sets a.v_lds) only in the KQ_ATTN_VLDS build: as a run-time
     // choice its LDS / global select turned KQV's cache loads into flat loads (tg1024 -4 %, r5t)
-    const bool vl = DS > 1 || (PAIR && KQ_ATTN_VLDS && a.v_lds);
+    const bool vl = KDMA || (PAIR && KQ_ATTN_VLDS && a.v_lds);
     uint4 vpre[ITEMS][VPF] = {};
 #pragma unroll
     for (int ii = 0; ii < ITEMS && !vl; ++ii) {

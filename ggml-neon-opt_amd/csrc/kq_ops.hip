@@ -210,7 +210,10 @@ __global__ void __launch_bounds__(256) kq_rope(const float *__restrict__ x, floa
 #ifndef KQ_ATTN_TPH64
 #define KQ_ATTN_TPH64 256
 #endif
-template <int HD, bool BATCH, int DS = 1, int TPH = 256>
+#ifndef KQ_ATTN_KDMA1  // 1: experiment build, caches of <= 256 cells on the LDS-DMA path (attn_head KD1)
+#define KQ_ATTN_KDMA1 0
+#endif
+template <int HD, bool BATCH, int DS = 1, int TPH = 256, bool KD1 = false>
 __global__ void __launch_bounds__(TPH) kq_attn_decode(const AttnArgs a) {
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
     // XCD-aware head order (speed only): workgroup b runs on XCD b % 8, so XCD x takes the
@@ -223,8 +226,8 @@ __global__ void __launch_bounds__(TPH) kq_attn_decode(const AttnArgs a) {
         h = x * (a.n_head >> 3) + i / DS;
         ds = i % DS;
     }
-    attn_head<HD, TPH, 0, KQ_ATTN_OSC1 != 0, false, BATCH, DS>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD, true,
-                                                                ds);
+    attn_head<HD, TPH, 0, KQ_ATTN_OSC1 != 0, false, BATCH, DS, KD1>(a, h, threadIdx.x, smem, a.out + (int64_t)h * HD,
+                                                                     true, ds);
 }
 
 // One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read
@@ -540,9 +543,9 @@ size_t attn_lds(int hd, int n_ctx) {
 }
 // ... plus the head's V rows (v_lds, or a 1/ds slice of them): rows of n_ctx f16, 16 B of
 // padding each
-size_t attn_lds_v(int hd, int n_ctx, int ds = 1) {
+size_t attn_lds_v(int hd, int n_ctx, int ds = 1, bool ring = false) {
     return (attn_lds(hd, n_ctx) + 15) / 16 * 16 + (size_t)(hd / ds) * ((size_t)n_ctx * 2 + 16) +
-           (ds > 1 ? (size_t)4 * KQ_ATTN_KD * ATTN_KSLOT : 0);  // + the K ring (KDMA)
+           (ds > 1 || ring ? (size_t)4 * KQ_ATTN_KD * ATTN_KSLOT : 0);  // + the K ring (KDMA)
 }
 #ifndef KQ_ATTN_DSMIN
 #define KQ_ATTN_DSMIN 4  // (experiment builds: 8)
@@ -664,6 +667,18 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
         KQ_ATTN_SPLIT_LAUNCH(128, 8)
 #undef KQ_ATTN_SPLIT_LAUNCH
         return MI355X_E_INVAL;
+    }
+    if (KQ_ATTN_KDMA1 && a.n_ctx <= KQ_ATTN_BATCH_CTX && a.n_ctx % 8 == 0 && ((uintptr_t)a.v_cache & 15u) == 0 &&
+        ((uintptr_t)a.k_cache & 15u) == 0) {
+        const size_t lds = attn_lds_v(a.head_dim, a.n_ctx, 1, true);
+        if (a.head_dim == 64) {
+            allow_lds((const void *)kq_attn_decode<64, true, 1, 256, true>, lds);
+            return timed_launch("kq::kq_attn_decode<64, true, 1, kd1>", bytes, kq_attn_decode<64, true, 1, 256, true>,
+                                dim3(a.n_head), dim3(256), lds, s, b);
+        }
+        allow_lds((const void *)kq_attn_decode<128, true, 1, 256, true>, lds);
+        return timed_launch("kq::kq_attn_decode<128, true, 1, kd1>", bytes, kq_attn_decode<128, true, 1, 256, true>,
+                            dim3(a.n_head), dim3(256), lds, s, b);
     }
     b.v_lds = a.n_ctx > KQ_ATTN_BATCH_CTX && a.n_ctx % 8 == 0 && attn_lds_v(a.head_dim, a.n_ctx) <= 160 * 1024 &&
               ((uintptr_t)a.v_cache & 15u) == 0 && KQ_ATTN_VLDS;
