@@ -98,7 +98,10 @@ constexpr size_t kMaxLds = 160 * 1024;   // LDS per CU (one workgroup may use it
 constexpr size_t kTargetLds = 80 * 1024; // aim for >= 2 resident workgroups per CU
 constexpr int64_t kFusedQMaxNb = 32;      // kq_gemv: in-kernel quantization up to K = 8192
 constexpr int64_t kRowsFusedMaxNb = ROWS_QPASS * 4 * ROWS_WAVES;  // kq_rows: up to K = 36864
-constexpr double kRowsSmallBytes = 10e6;  // launches below this many weight bytes: ROWS_WAVES_SMALL waves
+// launches below this many weight bytes: ROWS_WAVES_SMALL waves. 10 MB -> 5 MB in round 5
+// (TinyLlama's 6.5 / 9.5 MB ffn_down and the 8B's 9.4 MB o-proj on 12 waves): both tokens
+// +0.3 %, six of six interleaved comparisons; 0 (never) -0.8 % (profiles/r05_gemv_small_mb_ab.txt)
+constexpr double kRowsSmallBytes = 5e6;
 std::atomic<int> g_rows_waves{0};         // mi355x_gemv_waves: 0 = by size, else fixed
 
 // ------------------------------------------------------------------ debug knobs
