@@ -26,6 +26,8 @@
 // [0, pos], an op outside the list) returns GGML_STATUS_FAILED rather than a wrong result.
 #include <cmath>
 #include <cstdint>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -194,7 +196,16 @@ void be_get_async(ggml_backend_t backend, const struct ggml_tensor *t, void *dat
     mi355x_backend_get_tensor(ctx->be, data, (const char *)t->data + off, n);
 }
 
-void be_synchronize(ggml_backend_t backend) { mi355x_backend_synchronize(((Backend *)backend->context)->be); }
+// ggml's synchronize returns nothing: like ggml-cuda's CUDA_CHECK, a failed wait aborts
+// (a persistent-layer launch that lost co-residency left invalid outputs: MI355X_E_LAYER)
+void be_synchronize(ggml_backend_t backend) {
+    const int rc = mi355x_backend_synchronize(((Backend *)backend->context)->be);
+    if (rc != 0) {
+        std::fprintf(stderr, "ggml-mi355x: synchronize failed (%d)%s\n", rc,
+                     rc == MI355X_E_LAYER ? ": persistent layer lost co-residency, outputs invalid" : "");
+        std::abort();
+    }
+}
 
 const char *op_name(const ggml_tensor *t) { return ggml_op_name(t->op); }
 

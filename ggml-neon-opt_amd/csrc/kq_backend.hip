@@ -8,6 +8,7 @@
 // walks every node (ggml_graph_compute_thread, ggml-cpu.c:2883), this backend
 // enqueues one kernel per (fused) node on its HIP stream; repeated graphs
 // (decode steps) are replayed from a captured hipGraph.
+#include <algorithm>
 #include <dlfcn.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -44,13 +45,13 @@ struct mi355x_backend {
     bool layer_engine = false;  // each decode layer as one persistent launch (kq_layer.hip)
     uint32_t *ly_sync = nullptr;  // the persistent layers' counter blocks (zeroed at allocation), then err
     int ly_blocks = 0;
-    std::vector<uint32_t> ly_sig;  // producers per edge and shard of every block: a change re-zeroes them
-    struct LyTab {                 // a block's step tables (kq::layer_table_fill), built for `key`
+    std::vector<std::vector<uint32_t>> ly_keys;  // block i's (layer index, producers per edge and shard)
+    struct LyTab {                 // step tables (kq::layer_table_fill) built for one full geometry `key`
         void *dev = nullptr;
         int64_t stride = 0;
         std::vector<uint64_t> key;
     };
-    std::vector<LyTab> ly_tabs;
+    std::vector<LyTab> ly_tabs;    // one entry per distinct key (several models / cache sizes coexist)
     ncclComm_t comm = nullptr;  // row split: one RCCL communicator per backend (rank of a world)
     bool loop_nocopy = false;   // emulated rank, timing only (MI355X_LOOPBACK_NOCOPY)
     int rank = 0, world = 0;
@@ -72,6 +73,25 @@ struct DeviceGuard {
         if (prev >= 0) hipSetDevice(prev);
     }
 };
+
+// The persistent layers' step tables depend on every field layer_table_fill reads: the
+// weights and their types, the stage shapes, the ring geometry (D, slot: byte positions
+// and issue gates) and the attention placement and LDS layout (which move with n_ctx).
+constexpr size_t kMaxLyTabs = 256;
+
+std::vector<uint64_t> ly_tab_key(const kq::LayerArgs &la) {
+    std::vector<uint64_t> key = {(uint64_t)la.G,      (uint64_t)la.E,           (uint64_t)la.F,
+                                 (uint64_t)la.nb_e,   (uint64_t)la.nb_f,        (uint64_t)la.nq,
+                                 (uint64_t)la.nkv,    (uint64_t)la.n_attn,      (uint64_t)la.hpw,
+                                 (uint64_t)la.attn_stride, (uint64_t)la.head_lds, (uint64_t)la.D,
+                                 (uint64_t)la.slot,   (uint64_t)la.o_aux,       (uint64_t)la.act_bytes,
+                                 (uint64_t)la.o_sums, (uint64_t)la.o_res,       (uint64_t)la.lds};
+    for (int m = 0; m < 7; ++m) {
+        key.push_back((uint64_t)(uintptr_t)la.w[m]);
+        key.push_back((uint64_t)la.type[m]);
+    }
+    return key;
+}
 
 // ---- RCCL, resolved at run time: the copy already loaded in the process (torch
 // bundles one) or /opt/rocm's. Only the entry points the row split uses.
@@ -138,6 +158,12 @@ mi355x_backend::Captured *find_graph(mi355x_backend *b, const std::vector<uint64
     return nullptr;
 }
 
+const mi355x_backend::LyTab *find_ly_tab(const mi355x_backend *b, const std::vector<uint64_t> &key) {
+    for (const auto &t : b->ly_tabs)
+        if (t.dev && t.key == key) return &t;
+    return nullptr;
+}
+
 // One launch: a MUL_MAT node, or a run of ne11 == 1 MUL_MAT nodes sharing src1
 // (kind GEMV, with its fused neighbours), or any other single node.
 struct Launch {
@@ -158,6 +184,20 @@ struct Launch {
     int ly_block = -1;       // kind 6: its counter block
     kq::LayerArgs la;        // kind 6: the launch's arguments (sync / err set at enqueue)
 };
+
+// a persistent layer launch's counter block key (see graph_compute)
+std::vector<uint32_t> ly_block_key(const Launch &l) {
+    std::vector<uint32_t> k = {(uint32_t)l.ly_block};
+    for (int e = 0; e < 4; ++e)
+        for (int q = 0; q < 8; ++q) k.push_back(l.la.expect[e][q]);
+    return k;
+}
+
+int find_ly_block(const mi355x_backend *b, const std::vector<uint32_t> &k) {
+    for (size_t i = 0; i < b->ly_keys.size(); ++i)
+        if (b->ly_keys[i] == k) return (int)i;
+    return -1;
+}
 
 float f_of(int32_t bits) {
     float f;
@@ -818,11 +858,13 @@ int enqueue(mi355x_backend *b, mi355x_tensor *const *nodes, const std::vector<La
         }
         if (l.kind == 6) {  // a decode layer: one persistent launch
             kq::LayerArgs la = l.la;
-            if (!b->ly_sync || l.ly_block >= b->ly_blocks) return MI355X_E_WORKSPACE;
-            if ((size_t)l.ly_block >= b->ly_tabs.size() || !b->ly_tabs[l.ly_block].dev) return MI355X_E_WORKSPACE;
-            la.tab = (const uint8_t *)b->ly_tabs[l.ly_block].dev;
-            la.tab_stride = b->ly_tabs[l.ly_block].stride;
-            la.sync = b->ly_sync + (size_t)l.ly_block * kq::LAYER_SYNC_U32;
+            const int blk = find_ly_block(b, ly_block_key(l));
+            if (!b->ly_sync || blk < 0 || blk >= b->ly_blocks) return MI355X_E_WORKSPACE;
+            const mi355x_backend::LyTab *tb = find_ly_tab(b, ly_tab_key(la));
+            if (!tb) return MI355X_E_WORKSPACE;
+            la.tab = (const uint8_t *)tb->dev;
+            la.tab_stride = tb->stride;
+            la.sync = b->ly_sync + (size_t)blk * kq::LAYER_SYNC_U32;
             la.err = (int *)(b->ly_sync + (size_t)b->ly_blocks * kq::LAYER_SYNC_U32);
             rc = kq::launch_layer(la, b->stream);
             if (rc) return rc;
@@ -1133,7 +1175,14 @@ int mi355x_backend_synchronize(mi355x_backend_t b) {
     if (!b) return MI355X_E_INVAL;
     DeviceGuard dg(b->device);
     const hipError_t e = hipStreamSynchronize(b->stream);
-    return e == hipSuccess ? 0 : (int)e;
+    if (e != hipSuccess) return (int)e;
+    // a persistent-layer launch that gave up waiting left invalid outputs: report it here,
+    // where every caller that reads results already stops (and re-arm the counters)
+    if (b->layer_engine && b->ly_sync) {
+        const int le = mi355x_backend_layer_error(b);
+        if (le) return le > 0 ? MI355X_E_LAYER : le;
+    }
+    return 0;
 }
 
 // ggml_backend_device_i::supports_op for this device: MUL_MAT of a contiguous-row
@@ -1406,58 +1455,69 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
     }
     {  // the persistent layers' counter blocks: one per kind-6 launch, zeroed outside any capture
        // whenever they are (re)allocated or their producer counts change
-        std::vector<uint32_t> sig;
-        int nblk = 0;
+        // A launch's counters are monotonic over its launches with ITS producer counts, so a
+        // block is keyed by (layer index in the graph, producers per edge and shard): graphs
+        // with other counts (another cache size or model on this backend) get blocks of their
+        // own instead of inheriting counters stepped by other counts.
+        size_t need = b->ly_keys.size();
+        std::vector<std::vector<uint32_t>> fresh;
         for (const Launch &l : launches) {
             if (l.kind != 6) continue;
-            nblk = l.ly_block + 1 > nblk ? l.ly_block + 1 : nblk;
-            for (int e = 0; e < 4; ++e)
-                for (int k = 0; k < 8; ++k) sig.push_back(l.la.expect[e][k]);
+            const std::vector<uint32_t> k = ly_block_key(l);
+            if (find_ly_block(b, k) < 0 && std::find(fresh.begin(), fresh.end(), k) == fresh.end())
+                fresh.push_back(k);
         }
-        if (nblk && (nblk > b->ly_blocks || sig != b->ly_sig)) {
+        need += fresh.size();
+        if (!fresh.empty()) {
             hipStreamSynchronize(b->stream);
-            drop_graph(b);
-            if (nblk > b->ly_blocks) {
+            if ((int)need > b->ly_blocks) {  // grow (capacity doubles): every counter restarts at 0
+                drop_graph(b);
+                int cap = b->ly_blocks ? b->ly_blocks : 8;
+                while (cap < (int)need) cap *= 2;
                 if (b->ly_sync) hipFree(b->ly_sync);
-    for (auto &t : b->ly_tabs)
-        if (t.dev) hipFree(t.dev);
                 b->ly_sync = nullptr;
                 b->ly_blocks = 0;
-                if (hipMalloc(&b->ly_sync, ((size_t)nblk * kq::LAYER_SYNC_U32 + 64) * 4) != hipSuccess)
+                if (hipMalloc(&b->ly_sync, ((size_t)cap * kq::LAYER_SYNC_U32 + 64) * 4) != hipSuccess) {
+                    b->ly_keys.clear();
                     return MI355X_E_WORKSPACE;
-                b->ly_blocks = nblk;
+                }
+                b->ly_blocks = cap;
+                if (hipMemsetAsync(b->ly_sync, 0, ((size_t)cap * kq::LAYER_SYNC_U32 + 64) * 4, b->stream) !=
+                        hipSuccess ||
+                    hipStreamSynchronize(b->stream) != hipSuccess)
+                    return MI355X_E_WORKSPACE;
             }
-            if (hipMemsetAsync(b->ly_sync, 0, ((size_t)b->ly_blocks * kq::LAYER_SYNC_U32 + 64) * 4, b->stream) !=
-                    hipSuccess ||
-                hipStreamSynchronize(b->stream) != hipSuccess)
-                return MI355X_E_WORKSPACE;
-            b->ly_sig = sig;
+            // new blocks are still zero: blocks past ly_keys.size() were zeroed when allocated
+            // and never launched on
+            for (auto &k : fresh) b->ly_keys.push_back(std::move(k));
         }
-        // the step tables: built on the host once per (weights, shape) and kept
+        // the step tables: built on the host once per full geometry (weights, shape, ring depth,
+        // attention placement, LDS layout) and kept; a table is never rebuilt in place, so a
+        // captured graph never reads a table that changed under it
         for (const Launch &l : launches) {
             if (l.kind != 6) continue;
-            const kq::LayerArgs &la = l.la;
-            std::vector<uint64_t> key = {(uint64_t)la.G, (uint64_t)la.E, (uint64_t)la.F, (uint64_t)la.nq, (uint64_t)la.nkv};
-            for (int m = 0; m < 7; ++m) {
-                key.push_back((uint64_t)(uintptr_t)la.w[m]);
-                key.push_back((uint64_t)la.type[m]);
+            std::vector<uint64_t> key = ly_tab_key(l.la);
+            if (find_ly_tab(b, key)) continue;
+            if (b->ly_tabs.size() >= kMaxLyTabs) {  // bound the cache: start over (graphs may read them)
+                hipStreamSynchronize(b->stream);
+                drop_graph(b);
+                for (auto &t : b->ly_tabs)
+                    if (t.dev) hipFree(t.dev);
+                b->ly_tabs.clear();
             }
-            if ((size_t)l.ly_block >= b->ly_tabs.size()) b->ly_tabs.resize((size_t)l.ly_block + 1);
-            mi355x_backend::LyTab &tb = b->ly_tabs[l.ly_block];
-            if (tb.dev && tb.key == key) continue;
-            hipStreamSynchronize(b->stream);
-            drop_graph(b);  // a captured graph may read this block's old table
-            const int64_t stride = kq::layer_table_stride(la);
-            std::vector<uint8_t> host((size_t)(stride * la.G));
-            kq::layer_table_fill(la, host.data(), stride);
-            if (tb.dev) hipFree(tb.dev);
-            tb.dev = nullptr;
-            tb.key.clear();
+            const int64_t stride = kq::layer_table_stride(l.la);
+            if (stride <= 0) return MI355X_E_UNSUPPORTED;
+            std::vector<uint8_t> host((size_t)(stride * l.la.G));
+            kq::layer_table_fill(l.la, host.data(), stride);
+            mi355x_backend::LyTab tb;
             if (hipMalloc(&tb.dev, host.size()) != hipSuccess) return MI355X_E_WORKSPACE;
-            if (hipMemcpy(tb.dev, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess)
+            if (hipMemcpy(tb.dev, host.data(), host.size(), hipMemcpyHostToDevice) != hipSuccess) {
+                hipFree(tb.dev);
                 return MI355X_E_WORKSPACE;
+            }
             tb.stride = stride;
             tb.key.swap(key);
+            b->ly_tabs.push_back(std::move(tb));
         }
     }
     if (!use_graph) return enqueue(b, nodes, launches);

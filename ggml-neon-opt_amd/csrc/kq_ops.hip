@@ -555,9 +555,13 @@ size_t attn_lds_v(int hd, int n_ctx, int ds = 1, bool ring = false) {
 // Every slice scores every cell, so the K reads grow with the slices: 16 slices at 4096 cells
 // (head_dim 64) measured slower than one workgroup per head (tg4096 894 against 925 tok/s,
 // profiles/r05_attn_split_ab.txt).
+// The split path LDS-DMAs K-cache rows and V rows and stages q / k / v and the rope row
+// with 16-B transfers (attn_dma16): every one of those operands must be 16-B aligned,
+// otherwise the per-head kernel runs.
 int attn_slices(const AttnArgs &a) {
-    if (attn_impl() != MI355X_ATTN_SPLIT || a.n_ctx <= KQ_ATTN_BATCH_CTX || a.n_ctx % 8 ||
-        ((uintptr_t)a.v_cache & 15u))
+    const uintptr_t mis = (uintptr_t)a.v_cache | (uintptr_t)a.k_cache | (uintptr_t)a.q | (uintptr_t)a.k |
+                          (uintptr_t)a.v | (uintptr_t)a.rope_table;
+    if (attn_impl() != MI355X_ATTN_SPLIT || a.n_ctx <= KQ_ATTN_BATCH_CTX || a.n_ctx % 8 || (mis & 15u))
         return 1;
     for (int ds = KQ_ATTN_DSMIN; ds <= 8; ds *= 2)
         if (attn_lds_v(a.head_dim, a.n_ctx, ds) <= 160 * 1024) return ds;

@@ -26,7 +26,7 @@ OP_NONE, OP_MUL_MAT, OP_GET_ROWS, OP_RMS_NORM, OP_MUL, OP_ADD, OP_SWIGLU, OP_ROP
     OP_ALL_REDUCE = range(11)
 MAX_SRC = 8
 FLAG_OUTPUT = 1
-E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM = 0, -1, -2, -3, -4, -6
+E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM, E_LAYER = 0, -1, -2, -3, -4, -6, -7
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 ATTN_GROUP, ATTN_HEAD, ATTN_SPLIT = 0, 1, 2
@@ -289,6 +289,9 @@ def row_size(type_: int, k: int) -> int:
 
 
 def _check(rc: int, what: str):
+    if rc == E_LAYER:
+        raise Mi355xError(f"{what}: a persistent-layer launch lost co-residency; that step's outputs "
+                          "are invalid (counters re-armed)")
     if rc != 0:
         raise Mi355xError(f"{what} failed with status {rc}")
 

@@ -90,6 +90,8 @@ enum mi355x_status {
     MI355X_E_WORKSPACE  = -3,  /* workspace missing or too small               */
     MI355X_E_NODEVICE   = -4,  /* no gfx950 device / HIP runtime unavailable   */
     MI355X_E_COMM       = -6,  /* RCCL missing / communicator error            */
+    MI355X_E_LAYER      = -7,  /* a persistent-layer launch lost co-residency:
+                                  that step's outputs are invalid (re-armed)   */
 };
 
 /* Bytes of one row of `type` with `k` elements (ggml_row_size). k % 256 == 0. */
@@ -447,6 +449,9 @@ int mi355x_backend_get_tensor(mi355x_backend_t backend, void *host_dst, const vo
 /* async device memset of `size` bytes to (uint8_t)value (ggml_backend_buffer_i.memset_tensor
  * / clear [U]) */
 int mi355x_backend_memset(mi355x_backend_t backend, void *dst, int value, size_t size);
+/* Waits for the backend stream. With the persistent layer on (set_layer_engine) it also
+ * returns MI355X_E_LAYER when a layer launch since the last check gave up waiting for
+ * another workgroup (outputs invalid; the counters are re-armed, as layer_error does). */
 int mi355x_backend_synchronize(mi355x_backend_t backend);
 int mi355x_backend_supports_op(const mi355x_tensor *op); /* 1 / 0 */
 /* Node fusion in graph_compute (default on): RMS_NORM -> MUL(norm weight) ->

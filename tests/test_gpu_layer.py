@@ -113,3 +113,52 @@ def test_layer_engine_long_cache(dev):
         b.synchronize()
         assert bits_equal(dec.logits.cpu().numpy(), eng[p]), p
     b.close()
+
+
+def _per_node_logits(dev, hp, wdev, n_ctx, tokens):
+    import ggml_mi355x as g
+    from ggml_mi355x.llama import LlamaDecoder
+    b = g.Backend()
+    dec = LlamaDecoder(b, hp, wdev, n_ctx, fuse=True)
+    out = []
+    for p, tok in enumerate(tokens):
+        dec.step(tok, p)
+        b.synchronize()
+        out.append(dec.logits.cpu().numpy().copy())
+    b.close()
+    return out
+
+
+def test_layer_engine_tables_across_graphs(dev):
+    """one backend, the engine on, graphs that (a) match MORE layers than the first
+    one did (the counter blocks grow; every step table stays valid) and (b) share weights at a
+    different KV-cache size (another ring depth and LDS layout, so another step table), steps
+    of the three decoders interleaved: every token bit-exact with the per-node launches."""
+    import ggml_mi355x as g
+    from tests import llama_model as LM
+    from ggml_mi355x.llama import LlamaDecoder, hparams
+    hp1 = hparams(2048, 1, 32, 4, 1024, 1024)
+    hp2 = hparams(2048, 2, 32, 4, 1024, 1024)
+    w1 = LM.to_device(LM.build(hp1, 11), dev)
+    w2 = LM.to_device(LM.build(hp2, 12), dev)
+    rng = np.random.default_rng(9)
+    tokens = rng.integers(0, hp1["n_vocab"], size=10).tolist()
+    b = g.Backend()
+    assert b.set_layer_engine(True) == 0
+    decs = [LlamaDecoder(b, hp1, w1, 64, fuse=True),    # 1 layer
+            LlamaDecoder(b, hp2, w2, 64, fuse=True),    # 2 layers: the blocks grow
+            LlamaDecoder(b, hp2, w2, 256, fuse=True)]   # same weights, another cache size
+    names = _launch_names(decs[2], 5, 0)
+    assert sum("kq_layer" in n for n in names) == 2, names
+    for d in decs:
+        d.reset()
+    refs = [_per_node_logits(dev, hp1, w1, 64, tokens), _per_node_logits(dev, hp2, w2, 64, tokens),
+            _per_node_logits(dev, hp2, w2, 256, tokens)]
+    for p, tok in enumerate(tokens):
+        for i, d in enumerate(decs):
+            d.step(tok, p, use_graph=(p % 3 != 1))
+            b.synchronize()  # raises on a lost-co-residency error (MI355X_E_LAYER)
+            got = d.logits.cpu().numpy()
+            assert bits_equal(got, refs[i][p]), (i, p, first_mismatch(got, refs[i][p]))
+    assert b.layer_error() == 0
+    b.close()
