@@ -557,10 +557,18 @@ def cpu_baseline_token(tk, seconds):
     a persistent worker pool with 64-row chunks, the NEON-order vec_dot with AVX2
     integer parts (bit-identical to the scalar restatement); f16 attention, soft_max,
     rope, rms_norm, swiglu) on the same weights, tokens 0, 1, 2 ... from an empty cache.
-    Two legs as llama-bench runs them: -t 1 (BASELINE config 1) and -t N with N the
-    host threads available to this process (at most 16, the box's CPU share); each
-    leg gets about half of `seconds` after an untimed warm-up token."""
+    Legs as llama-bench runs them (BASELINE config 1 is `llama-bench -p 512 -n 128 -t 1`,
+    README.md:186-195):
+      * tg128 -t 1: all 128 tokens (config 1's -n 128 on one thread);
+      * pp512 -t 1: the prompt's mul_mats at M = 512 (the restated batched
+        ggml_compute_forward_mul_mat on one thread, q/k/v/o/gate/up/down of each layer), timed on
+        as many whole layers as fit a bounded share of `seconds` and scaled to the model's layers
+        (the output head runs on the batch's last token only, as llama-bench's pp does: one
+        M = 1 mul_mat); attention, norms and rope of the prompt are not in the sample;
+      * tg -t N with N the host threads available to this process (at most 16, the box's CPU
+        share per GPU): the reported value."""
     from oracle import kq_ops_oracle as OO
+    from oracle import kq_oracle as KO
     model_name, ncpu, aff = host_cpu()
     threads_n = max(1, min(16, aff))
     hp = tk.hp
@@ -577,7 +585,7 @@ def cpu_baseline_token(tk, seconds):
     kvw = hp["n_head_kv"] * hp["head_dim"]
     OO.lib()
 
-    def leg(threads, budget):
+    def leg(threads, budget, n_max=128):
         cache = [(np.zeros((tk.n_ctx, kvw), np.uint16), np.zeros((kvw, tk.n_ctx), np.uint16))
                  for _ in range(hp["n_layer"])]
         t0 = time.perf_counter()  # warm-up: workers started, host threads at speed
@@ -590,18 +598,47 @@ def cpu_baseline_token(tk, seconds):
             c[1][:] = 0
         tokens, t0 = 0, time.perf_counter()
         while True:
-            OO.decode_token(model, tk.tokens[tokens], tokens, cache, n_threads=threads, variant="simd")
+            OO.decode_token(model, tk.tokens[tokens % len(tk.tokens)], tokens, cache, n_threads=threads,
+                            variant="simd")
             tokens += 1
             el = time.perf_counter() - t0
-            if el >= budget or tokens >= 128 or tokens >= tk.n_ctx:
+            if el >= budget or tokens >= n_max or tokens >= tk.n_ctx:
                 break
         return tokens, el
 
+    def pp_leg(budget, n_tok=512):
+        """pp512 at -t 1: whole layers' mul_mats at M = n_tok until the budget, scaled."""
+        rng = np.random.default_rng(7)
+        E, F = hp["n_embd"], hp["n_ff"]
+        x_e = rng.standard_normal((n_tok, E)).astype(np.float32)
+        x_f = rng.standard_normal((n_tok, F)).astype(np.float32)
+        x_q = rng.standard_normal((n_tok, hp["n_head"] * hp["head_dim"])).astype(np.float32)
+        done, t0 = 0, time.perf_counter()
+        for L in layers:
+            for key, x in (("wq", x_e), ("wk", x_e), ("wv", x_e), ("wo", x_q), ("w_gate", x_e), ("w_up", x_e),
+                           ("w_down", x_f)):
+                KO.mul_mat(L[key][0], L[key][1], x, 1, "simd")
+            done += 1
+            if time.perf_counter() - t0 >= budget:
+                break
+        per_layer = (time.perf_counter() - t0) / done
+        t1 = time.perf_counter()
+        KO.mul_mat(model["output"][0], model["output"][1], x_e[-1:], 1, "simd")  # the last token's logits
+        head = time.perf_counter() - t1
+        total = per_layer * hp["n_layer"] + head
+        return {"tok_s": round(n_tok / total, 3), "tokens": n_tok, "layers_timed": done,
+                "seconds_timed": round(per_layer * done + head, 2), "seconds_scaled": round(total, 2),
+                "note": f"mul_mats of {done} of {hp['n_layer']} layers at M = {n_tok} on one thread, scaled to "
+                        f"{hp['n_layer']} layers, plus the output head on the last token"}
+
     phys = physical_cores()
     quota = cpu_quota()
-    n1, e1 = leg(1, seconds * 0.4)
+    n1, e1 = leg(1, max(seconds, 12.0) * 2.0)  # tg128 -t 1 in full (config 1's -n 128)
+    pp1 = pp_leg(seconds * 0.5)
     nn, en = leg(threads_n, seconds * 0.35)
-    legs = {"t1": {"tok_s": round(n1 / e1, 3), "tokens": n1, "seconds": round(e1, 2)},
+    legs = {"t1": {"tok_s": round(n1 / e1, 3), "tokens": n1, "seconds": round(e1, 2),
+                   "note": "tg128 -t 1 (BASELINE config 1's -n 128 -t 1)"},
+            "pp512_t1": pp1,
             f"t{threads_n}": {"tok_s": round(nn / en, 3), "tokens": nn, "seconds": round(en, 2)}}
     if phys > threads_n and (quota is None or quota >= phys):  # one thread per physical core (a short leg)
         npn, epn = leg(phys, seconds * 0.25)
@@ -615,13 +652,14 @@ def cpu_baseline_token(tk, seconds):
     return {"value": round(nn / en, 3), "unit": "tok/s", "cores": threads_n, "kind": "port",
             "legs": legs, "host_cpu": model_name, "host_logical_cpus": ncpu, "affinity_cpus": aff,
             "affinity_physical_cores": phys, "cgroup_cpu_quota": quota,
+            "config1": {"pp512_t1_tok_s": pp1["tok_s"], "tg128_t1_tok_s": round(n1 / e1, 3), "tg_tokens": n1},
             "thread_cap": f"value is the -t {threads_n} leg: min(16, affinity) threads, the GPU box's CPU share "
                           f"per GPU; the -t {phys} leg uses every physical core of the affinity",
             "sample": f"tokens 0..n-1 from an empty KV cache of the full {tk.model} Q4_K_M decode graph through "
                       f"the oracle's restated llm_build_llama / ggml-cpu ops (mul_mat: quantize_row_q8_K_ref + "
                       f"NEON-order vec_dot with AVX2 integer parts, bit-identical to the scalar restatement, "
-                      f"persistent pool); legs -t 1 ({n1} tokens, {e1:.1f} s), -t {threads_n} ({nn} tokens, "
-                      f"{en:.1f} s)" + (f", -t {phys}" if phys > threads_n else "") +
+                      f"persistent pool); legs tg -t 1 ({n1} tokens, {e1:.1f} s), pp512 -t 1 ({pp1['note']}), "
+                      f"-t {threads_n} ({nn} tokens, {en:.1f} s)" + (f", -t {phys}" if phys > threads_n else "") +
                       f"; value is the -t {threads_n} leg"}
 
 

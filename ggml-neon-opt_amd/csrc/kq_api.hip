@@ -1,6 +1,7 @@
 // kq_api.hip — C-ABI of libggml_mi355x.so: argument checking, launch planning and
 // the ggml-surface mirrors (vec_dot / from_float / mul_mat). Declared in
 // include/ggml_mi355x.h.
+#include <algorithm>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -22,6 +23,8 @@ __global__ void kq_gemv(const GemvArgs a);
 __global__ void kq_quantize_q8K(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TMASK, bool FUSEDQ, int PRO>
 __global__ void kq_rows(const RowsArgs a);
+template <int TMASK, bool FUSEDQ, int PRO>
+__global__ void kq_rows_dyn(const RowsArgs a);
 template <bool AM>
 __global__ void kq_quantize_q8L(const float *x, int64_t x_stride, uint8_t *y, int nb, int64_t nblocks);
 template <int TYPE, int RT, int CW>
@@ -115,7 +118,7 @@ const KnobDef kKnobs[KNOB_COUNT] = {
     {"GEMV_XMODE", 0}, {"GEMV_SMALL_MB", kRowsSmallBytes / 1e6},      {"GEMV_WPC", 0},
     {"GEMV_SMALL_WG", 0}, {"GEMV_FQMAX", (double)kRowsFusedMaxNb},   {"MMF_WAVES", 0},
     {"MMF_ORDER", 0},  {"ATTN_DIAG", 0},     {"LOOPBACK_NOCOPY", 0}, {"ATTN_OPROJ", 1},
-    {"AO_NRB", 0},
+    {"AO_NRB", 0},     {"GEMV_DYN", 8},    {"GEMV_DYN_P", 0},
 };
 std::atomic<double> g_knob[KNOB_COUNT];
 std::atomic<bool> g_knob_set[KNOB_COUNT];
@@ -355,23 +358,27 @@ bool rows_enabled() {
 
 
 template <int TM, bool FQ, int PR>
-rows_fn rows_inst() {
-    return kq_rows<TM, FQ, PR>;
+rows_fn rows_inst(bool dyn) {
+    if constexpr (TM == 7) {
+        return kq_rows<TM, FQ, PR>;
+    } else {
+        return dyn ? kq_rows_dyn<TM, FQ, PR> : kq_rows<TM, FQ, PR>;
+    }
 }
 
 template <int TM>
-rows_fn rows_pick_pro(bool fusedq, int pro) {
-    if (!fusedq) return rows_inst<TM, false, 0>();
-    return pro == ROWS_PRO_NORM ? rows_inst<TM, true, 1>() : pro == ROWS_PRO_SWIGLU ? rows_inst<TM, true, 2>()
-                                                                                     : rows_inst<TM, true, 0>();
+rows_fn rows_pick_pro(bool fusedq, int pro, bool dyn) {
+    if (!fusedq) return rows_inst<TM, false, 0>(dyn);
+    return pro == ROWS_PRO_NORM ? rows_inst<TM, true, 1>(dyn) : pro == ROWS_PRO_SWIGLU ? rows_inst<TM, true, 2>(dyn)
+                                                                                       : rows_inst<TM, true, 0>(dyn);
 }
 
-rows_fn pick_rows(int tmask, bool fusedq, int pro) {
+rows_fn pick_rows(int tmask, bool fusedq, int pro, bool dyn = false) {
     switch (tmask) {
-        case 1: return rows_pick_pro<1>(fusedq, pro);
-        case 2: return rows_pick_pro<2>(fusedq, pro);
-        case 4: return rows_pick_pro<4>(fusedq, pro);
-        default: return rows_pick_pro<7>(fusedq, pro);
+        case 1: return rows_pick_pro<1>(fusedq, pro, dyn);
+        case 2: return rows_pick_pro<2>(fusedq, pro, dyn);
+        case 4: return rows_pick_pro<4>(fusedq, pro, dyn);
+        default: return rows_pick_pro<7>(fusedq, pro, false);
     }
 }
 
@@ -409,6 +416,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
         a.type[i] = d[i].type;
         a.w[i] = (const uint8_t *)d[i].w;
         a.y[i] = d[i].y;
+        a.n_rows[i] = (int)d[i].n_rows;
     }
     {
         a.pf = (int)knob(KNOB_GEMV_PF);
@@ -499,18 +507,66 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
     pl.lds = (size_t)L.total;
     const int64_t grid = waves < n_wg ? waves : n_wg;
     pl.grid = dim3((unsigned)(grid > 0 ? grid : 1), 1, 1);
+    // Claimed rows (kq_rows_dyn) for one-type launches whose waves get enough units to balance
+    // (GEMV_DYN units per wave on average; MI355X_GEMV_DYN: every one-type launch). A unit is
+    // U whole rows of at least one 16-superblock step; each wave's first P units (a ring's
+    // worth) are static.
+    pl.dyn = false;
+    const double dyn_min = knob(KNOB_GEMV_DYN);
+    const bool force = g_impl.load() == MI355X_GEMV_DYN;
+    bool same_rows = true;  // kq_rows_dyn: one workgroup row range for every matrix
+    for (int i = 1; i < n_desc; ++i) same_rows = same_rows && d[i].n_rows == d[0].n_rows;
+    if (tmask != 7 && same_rows && (force || dyn_min > 0)) {
+        // U: whole rows, a power of two, at least one 16-superblock step; two steps where every
+        // wave streams many (a claim and a unit's bookkeeping per two steps)
+        int ush = 0;
+        while ((int64_t)(1 << ush) * nb < ROWS_SB) ++ush;
+        const double steps_per_wave = (double)n_desc * d[0].n_rows * nb / ROWS_SB / n_wg / pl.nwv;
+        if ((int64_t)(1 << ush) * nb == ROWS_SB && steps_per_wave >= 16) ++ush;
+        const int U = 1 << ush;
+        const int Tu = (int)((U * nb + ROWS_SB - 1) / ROWS_SB);
+        const int D = rows_depth(tmask == 1 ? Q4_K : tmask == 2 ? Q5_K : Q6_K);
+        // flat output slots per workgroup: its row units (strided placement) or rows, per matrix
+        const int64_t flat = (int64_t)n_desc * ((d[0].n_rows + n_wg - 1) / n_wg);
+        const int64_t rows = (int64_t)n_desc * d[0].n_rows;
+        // replay batch: ~ROWS_RECS records, whole units
+        int bRd = (int)(ROWS_RECS / nb) / U * U;
+        if (bRd < U) bRd = U;
+        // AUTO (profiles/r06_dyn_ab.txt): claimed rows paid where every wave streams many steps
+        // in many units (the Q6_K heads, 70B gate + up: -1 to -3 %); with few units per wave
+        // (8B ffn_up, 70B ffn_down: +5 to +10 %) the units' bookkeeping costs more than the
+        // balance gains
+        const double per_wave = (double)rows / (double)n_wg / U / pl.nwv;
+        const bool auto_ok = per_wave >= dyn_min && steps_per_wave >= 16;
+        const RowsDynLayout DL = rows_dyn_layout((int)nb, tmask, bRd, (int)flat, pl.nwv);
+        if ((force || auto_ok) && rows > 0 && (size_t)DL.total <= kMaxLds && flat < 0x7fffffff / 64) {
+            pl.dyn = true;
+            a.dyn_u = U;
+            a.dyn_ush = ush;
+            a.rbase[0] = (int)(d[0].n_rows / n_wg);
+            a.rrem[0] = (int)(d[0].n_rows % n_wg);
+            a.dyn_p = (D + Tu - 1) / Tu;
+            const int p_knob = (int)knob(KNOB_GEMV_DYN_P);
+            if (p_knob > 0) a.dyn_p = p_knob;
+            a.bR = bRd;
+            a.rpw = (int)flat;
+            pl.lds = (size_t)DL.total;
+            pl.grid = dim3((unsigned)n_wg, 1, 1);
+            pl.fn = pick_rows(tmask, fusedq, ROWS_PRO_NONE, true);
+        }
+    }
     return MI355X_OK;
 }
 
 std::string rows_name(const RowsPlan &pl) {
-    return std::string("kq::kq_rows<") + std::to_string(pl.tmask) + ", " + (pl.fusedq ? "true" : "false") + ", " +
+    return std::string(pl.dyn ? "kq::kq_rows_dyn<" : "kq::kq_rows<") + std::to_string(pl.tmask) + ", " + (pl.fusedq ? "true" : "false") + ", " +
            std::to_string(pl.a.pro) + ">";
 }
 
 double rows_bytes(const RowsArgs &a, bool fusedq) {
     double w = 0, y = 0;
     for (int i = 0; i < a.n_desc; ++i) {
-        const double rows = (double)a.rbase[i] * (a.wave_prefix[i + 1] - a.wave_prefix[i]) + a.rrem[i];
+        const double rows = (double)a.n_rows[i];
         w += rows * a.nb * block_bytes(a.type[i]);
         y += rows * 4.0;
     }
@@ -992,7 +1048,7 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
                                                                 : ROWS_PRO_NONE;
                 rp.a.x2 = ext->x2;
                 rp.a.eps = ext->eps;
-                rp.fn = pick_rows(rp.tmask, true, rp.a.pro);
+                rp.fn = pick_rows(rp.tmask, true, rp.a.pro, rp.dyn);
                 for (int i = 0; i < n; ++i) {
                     rp.a.res[i] = ext->residual[i];
                     rp.a.n_rows[i] = (int)d[i].n_rows;
@@ -1001,9 +1057,10 @@ int gemv_m1(const mi355x_gemv_desc *d, int n, const float *x, int64_t k, void *w
                 // workgroup with the same rows: equal wave counts, up's first wave on a
                 // workgroup boundary (gw = wave * grid + block)
                 const int g = (int)rp.grid.x;
-                const bool paired = epi && rp.a.wave_prefix[2] == 2 * rp.a.wave_prefix[1] &&
-                                    rp.a.wave_prefix[1] % g == 0 && rp.a.rbase[0] == rp.a.rbase[1] &&
-                                    rp.a.rrem[0] == rp.a.rrem[1];
+                // (kq_rows_dyn: a workgroup owns the same rows of both by construction)
+                const bool paired = epi && (rp.dyn || (rp.a.wave_prefix[2] == 2 * rp.a.wave_prefix[1] &&
+                                                       rp.a.wave_prefix[1] % g == 0 && rp.a.rbase[0] == rp.a.rbase[1] &&
+                                                       rp.a.rrem[0] == rp.a.rrem[1]));
                 if (!epi || paired) {
                     if (paired) {
                         rp.a.epi = 1;
@@ -1348,7 +1405,7 @@ int mi355x_debug_block_partials(int src0_type, const void *src0, int64_t ne00, i
 }
 
 int mi355x_gemv_impl(int impl) {
-    if (impl < MI355X_GEMV_AUTO || impl > MI355X_GEMV_ROWS) return MI355X_E_INVAL;
+    if (impl < MI355X_GEMV_AUTO || impl > MI355X_GEMV_DYN) return MI355X_E_INVAL;
     return g_impl.exchange(impl);
 }
 

@@ -131,6 +131,10 @@ struct RowsArgs {
     int epi, epi_n, epi_wave_off;
     float *epi_y;
     int64_t prio_bytes;  // the most weight bytes any wave streams (KQ_ROWS_PRIO: remaining-work priority)
+    // kq_rows_dyn (claimed rows): workgroup b owns rows [b*N/G, (b+1)*N/G) of every matrix
+    // (rpw = the most such rows over the matrices, summed); its waves claim units of dyn_u
+    // rows from an LDS counter, the first dyn_p units of each wave assigned statically
+    int dyn_u, dyn_p, dyn_ush;  // (dyn_u = 1 << dyn_ush; rbase[0] / rrem[0]: the rows N / G split)
 };
 constexpr int ROWS_PRO_NONE = 0, ROWS_PRO_NORM = 1, ROWS_PRO_SWIGLU = 2;
 // Prologue of the fused quantization (a.xmode bits):
@@ -213,6 +217,25 @@ __host__ __device__ inline RowsLayout rows_layout(int nb, int tmask, int bR, int
     L.outs_stride = (rpw * 4 + 15) & ~15;
     L.sums = L.outs + nwv * L.outs_stride;  // ROWS_PRO_NORM: per-superblock sums of squares (double)
     L.total = L.sums + nb * 8;
+    return L;
+}
+
+// kq_rows_dyn: act | ring (per wave) | recs (per wave: a batch of bR rows, bR x nb records) |
+// outs (the workgroup's rows of every matrix, flat) | sums | claim counter
+struct RowsDynLayout {
+    int act, ring, ring_stride, recs, recs_stride, outs, sums, cnt, total;
+};
+__host__ __device__ inline RowsDynLayout rows_dyn_layout(int nb, int tmask, int bR, int flat_rows, int nwv) {
+    RowsDynLayout L;
+    L.act = 0;
+    L.ring = nb * Q8L_STRIDE;
+    L.ring_stride = rows_ring(tmask);
+    L.recs = L.ring + nwv * L.ring_stride;
+    L.recs_stride = bR * nb * 16;
+    L.outs = L.recs + nwv * L.recs_stride;
+    L.sums = L.outs + ((flat_rows * 4 + 15) & ~15);
+    L.cnt = L.sums + nb * 8;
+    L.total = L.cnt + 16;
     return L;
 }
 

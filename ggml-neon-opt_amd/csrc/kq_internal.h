@@ -34,6 +34,7 @@ struct RowsPlan {
     int tmask;
     bool fusedq;
     int nwv;  // waves per workgroup (one workgroup per CU): ROWS_WAVES, or ROWS_WAVES_SMALL
+    bool dyn = false;  // kq_rows_dyn: rows claimed from a per-workgroup counter
 };
 // Row-stream decode GEMV (kq_rows): returns MI355X_E_UNSUPPORTED when the rows are
 // not contiguous or not aligned for it (callers then use kq_gemv). waves_per_cu = 0:
@@ -135,6 +136,8 @@ enum Knob {
     KNOB_LOOPBACK_NOCOPY,  // emulated ALL_GATHERs skip their own-slice copy (timing only)
     KNOB_ATTN_OPROJ,       // attention + o-proj fusion: 1 per backend (set_attn_oproj), 0 never, 2 always (A/B)
     KNOB_AO_NRB,           // kq_attn_oproj row blocks (0: by shape)
+    KNOB_GEMV_DYN,         // kq_rows_dyn when a wave gets at least this many units (and 16 steps) on average (0: never)
+    KNOB_GEMV_DYN_P,       // kq_rows_dyn: static units per wave (0: a ring's worth; A/B only)
     KNOB_COUNT
 };
 double knob(Knob k);

@@ -650,4 +650,416 @@ KQ_ROWS_INST_T(2)
 KQ_ROWS_INST_T(4)
 KQ_ROWS_INST_T(7)
 
+// ---------------------------------------------------------------- claimed rows (kq_rows_dyn)
+// The static split above gives every wave a fixed share of whole rows; in the large GEMVs the
+// last wave to finish sets the launch time, and which one that is follows the wave's age on
+// its SIMD (issue goes by priority, then age: profiles/r05_rows_agew.txt), not its row count.
+// Here workgroup b owns the rows [b*N/G, (b+1)*N/G) of every matrix and its waves CLAIM units
+// of U rows from an LDS counter (MI355X_MICROARCH.md **dequeue**, kept inside the CU: one
+// ds_add per unit), a ring depth ahead of their compute: the first P units of each wave are
+// assigned statically (the ring fill before the prologue's barrier claims nothing), every
+// later one is taken when the wave has issued its previous unit's last step. A unit's rows
+// stay whole in one wave, so each row's fp32 chain is still replayed in superblock order by
+// one lane (bit-identical to the static split and to ggml_vec_dot_q4_K_q8_K row by row,
+// README.md:137). Results go to the workgroup's LDS rows and are stored coalesced, with the
+// residual ADD and the SWIGLU epilogue, after one workgroup barrier.
+#ifndef KQ_ROWS_DYN_RR
+#define KQ_ROWS_DYN_RR 0
+#endif
+namespace {
+static_assert(MI355X_MAX_FUSED == 4, "four matrices at most");
+struct DynUnit {
+    const uint8_t *src;
+    int rows, flat, G, T;
+};
+}  // namespace
+
+// Every matrix of a kq_rows_dyn launch has the same rows and type (plan_rows), so one
+// workgroup row range [r0, r0 + nr) serves them all: unit u is matrix u / nu's rows
+// [r0 + (u % nu) U, ...), flat output index m * nr + local row. Records of consecutive
+// units go into one batch of bR rows, replayed together (lane r <-> batch row r).
+template <int TYPE, bool FUSEDQ, int PRO>
+__device__ __forceinline__ void rows_dyn_body(const RowsArgs &a, uint8_t *smem, const RowsDynLayout &L, int wave,
+                                              int lane, uint64_t st0) {
+    uint64_t sx = 0, sq = 0, sf = 0;  // diagnostics (KQ_ROWS_DIAG builds): x landed, quantized, first step
+    constexpr int BSZ = block_bytes(TYPE);
+    constexpr int GRAN = rows_gran(TYPE);
+    constexpr int NI = rows_ni(TYPE);
+    constexpr int SLOT = rows_slot(TYPE);
+    constexpr int D = rows_depth(TYPE);
+    static_assert(D >= 2 && D <= 4, "vm_wait_k covers 3 steps in flight");
+    const int nb = a.nb, U = a.dyn_u, P = a.dyn_p, bR = a.bR;
+    const int nwv = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6));
+    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int q = lane >> 2, s = lane & 3;
+    uint8_t *const ring = smem + L.ring + wave * L.ring_stride;
+    uint8_t *const ring_end = ring + D * SLOT;
+    Rec *const recs = (Rec *)(smem + L.recs + wave * L.recs_stride);
+    float *const outs = (float *)(smem + L.outs);
+    uint32_t *const cnt = (uint32_t *)(smem + L.cnt);
+    const uint8_t *const actq = smem + L.act;
+
+    // ---- the workgroup's rows and units: rows [r0, r0 + nr) of every matrix (the host's
+    // N / G split, a.rbase[0] / a.rrem[0]); unit u = matrix u / nu, rows r0 + (u % nu) U ..
+    const int N = a.n_rows[0];
+    const int ush = a.dyn_ush;  // U = 1 << ush
+    const int rbase = a.rbase[0], rrem = a.rrem[0];
+    const int r0 = b * rbase + (b < rrem ? b : rrem);
+    const int nr = rbase + (b < rrem ? 1 : 0);
+    const int nu = (nr + U - 1) >> ush;
+    const int units = a.n_desc * nu, nflat = a.n_desc * nr;
+    const int64_t rowb = (int64_t)nb * BSZ;
+    auto row_of = [&](int f) { return r0 + f; };
+    // unit u's stream (its first byte), rows and flat output index: computed once, when the
+    // unit is taken, and kept for its consumption in lane (k & 7) of four registers
+    auto unit_of = [&](int u) {
+        DynUnit d;
+        const int m = (u >= nu ? 1 : 0) + (u >= 2 * nu ? 1 : 0) + (u >= 3 * nu ? 1 : 0);
+        const int lr = (u - m * nu) << ush;
+        d.rows = nr - lr < U ? nr - lr : U;
+        d.flat = m * nr + lr;
+        const uint8_t *w = m == 0 ? a.w[0] : m == 1 ? a.w[1] : m == 2 ? a.w[2] : a.w[3];
+        d.src = w + (int64_t)(r0 + lr) * rowb;
+        d.G = d.rows * nb;
+        d.T = (d.G + ROWS_SB - 1) / ROWS_SB;
+        return d;
+    };
+    const int nstat = nwv * P < units ? nwv * P : units;  // statically assigned unit ids [0, nstat)
+
+    // ---- issue side: the unit being issued, its next step, the claimed-unit list
+    uint32_t ul = 0, uh = 0, ug = 0, uf = 0;  // lane k & 7: the k-th unit's src (lo, hi), G | rows << 16, flat
+    int ki = -1, is = 0, iT = 0, issued = 0;
+    bool idone = false, iwait = false;
+    const uint8_t *is16 = nullptr, *il16 = nullptr;
+    uint8_t *islot = ring;
+    auto take = [&](int u) {
+        ++ki;
+        const DynUnit d = unit_of(u);
+        const bool mine = lane == (ki & 7);
+        ul = mine ? (uint32_t)(uintptr_t)d.src : ul;
+        uh = mine ? (uint32_t)((uintptr_t)d.src >> 32) : uh;
+        ug = mine ? (uint32_t)(d.G | (d.rows << 16)) : ug;
+        uf = mine ? (uint32_t)d.flat : uf;
+        is16 = (const uint8_t *)((uintptr_t)d.src & ~(uintptr_t)15);
+        il16 = (const uint8_t *)((uintptr_t)(d.src + (int64_t)d.G * BSZ - 1) & ~(uintptr_t)15);
+        iT = d.T;
+        is = 0;
+    };
+    // the next unit: static ones first; a claim only once the counter is set (claim_ok)
+    auto next_unit = [&](bool claim_ok) {
+        const int k = ki + 1;
+        if (k < P) {
+            const int u = wave * P + k;
+            if (u < nstat) take(u);
+            else idone = true;
+            return;
+        }
+        if (!claim_ok) {
+            iwait = true;
+            return;
+        }
+        iwait = false;
+#if KQ_ROWS_DYN_RR  // experiment builds: the same units dealt round-robin, no claim (cost isolation)
+        const int uu = nwv * P + (k - P) * nwv + wave;
+#else
+        uint32_t u = 0;
+        if (lane == 0) u = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const int uu = __builtin_amdgcn_readfirstlane((int)u);
+#endif
+        if (uu < units) take(uu);
+        else idone = true;
+    };
+    auto issue = [&](bool claim_ok) {  // one step (NI DMA instructions), then the next unit if this one is done
+        const uint8_t *base = is16 + (int64_t)is * (ROWS_SB * BSZ) + 16 * lane;
+        if (is + 1 < iT) {
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+                if (i + 1 < NI || lane < GRAN - 64 * (NI - 1)) dma16_nt(base + 1024 * i, (LDS void *)(islot + 1024 * i));
+        } else {
+#pragma unroll
+            for (int i = 0; i < NI; ++i) {
+                const uint8_t *p = base + 1024 * i;
+                if (i + 1 < NI || lane < GRAN - 64 * (NI - 1))
+                    dma16_nt(p < il16 ? p : il16, (LDS void *)(islot + 1024 * i));
+            }
+        }
+        islot = islot + SLOT == ring_end ? ring : islot + SLOT;
+        ++is;
+        ++issued;
+        if (is == iT) next_unit(claim_ok);
+    };
+    next_unit(false);  // the first static unit (or none)
+
+    // residual of the fused ADD for flat row 64 * wave + lane, fetched with the activation
+    // (issued on every path: a dummy read of x without one; kept live until the flush waits)
+    const int f0 = 64 * wave + lane;
+    const int fm = (f0 >= nr ? 1 : 0) + (f0 >= 2 * nr ? 1 : 0) + (f0 >= 3 * nr ? 1 : 0);
+    const float *fres = fm == 0 ? a.res[0] : fm == 1 ? a.res[1] : fm == 2 ? a.res[2] : a.res[3];
+    const int frow = row_of(f0 - fm * nr);
+    uint32_t rv = 0;
+
+    // ---- prologue (the product kq_rows prologue: one step before the activation wait)
+    if (FUSEDQ) {
+        const int PASS = 4 * nwv;
+        u32x4 xv[ROWS_QPASS][4] = {};
+        u32x4 x2v[ROWS_QPASS][4] = {};
+        const int qiters = (nb + PASS - 1) / PASS;
+        int qw = 0;
+#pragma unroll
+        for (int i = 0; i < ROWS_QPASS; ++i) qw += (i < qiters && PASS * i + 4 * wave < nb) ? 1 : 0;
+#pragma unroll
+        for (int i = 0; i < ROWS_QPASS; ++i) {
+            if (i < qw) {
+                const int j = PASS * i + 4 * wave + (lane >> 4);
+                const int bb = j < nb ? j : nb - 1;
+                const float *xp = a.x + (int64_t)bb * QK + 16 * (lane & 15);
+#pragma unroll
+                for (int k = 0; k < 4; ++k) xv[i][k] = gload16_asm(xp + 4 * k);
+                if (PRO != ROWS_PRO_NONE) {
+                    const float *x2p = a.x2 + (int64_t)bb * QK + 16 * (lane & 15);
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) x2v[i][k] = gload16_asm(x2p + 4 * k);
+                }
+            }
+        }
+        rv = gload4_asm(fres && f0 < nflat && frow < N ? fres + frow : a.x);
+        // exactly one step's NI DMA instructions on every path (the constant wait below)
+        if (ki < 0) {  // no unit: from the activation, into a slot never read
+            const uint8_t *xb = (const uint8_t *)a.x + 16 * lane;
+#pragma unroll
+            for (int i = 0; i < NI; ++i)
+                if (i + 1 == NI) dma16_nt_lanes(xb, (LDS void *)(islot + 1024 * i), lane, GRAN - 64 * (NI - 1));
+                else dma16_nt(xb, (LDS void *)(islot + 1024 * i));
+        } else {  // the first unit's first step, its partial DMA masked in asm
+            const uint8_t *base = is16 + 16 * lane;
+            const uint8_t *lim = iT > 1 ? base + 1024 * (NI - 1) : base + 1024 * (NI - 1) < il16 ? base + 1024 * (NI - 1) : il16;
+#pragma unroll
+            for (int i = 0; i + 1 < NI; ++i) {
+                const uint8_t *p = base + 1024 * i;
+                dma16_nt(iT > 1 || p < il16 ? p : il16, (LDS void *)(islot + 1024 * i));
+            }
+            dma16_nt_lanes(lim, (LDS void *)(islot + 1024 * (NI - 1)), lane, GRAN - 64 * (NI - 1));
+            islot = islot + SLOT == ring_end ? ring : islot + SLOT;
+            ++is;
+            ++issued;
+            if (is == iT) next_unit(false);
+        }
+        vm_wait<NI + 1>();  // x landed; the residual load and the step's DMAs may be in flight
+        if (RSTAMPS(a)) sx = __builtin_amdgcn_s_memrealtime();
+        asm volatile("" : "+v"(xv[0][0]), "+v"(xv[0][1]), "+v"(xv[0][2]), "+v"(xv[0][3]), "+v"(xv[1][0]),
+                     "+v"(xv[1][1]), "+v"(xv[1][2]), "+v"(xv[1][3]), "+v"(xv[2][0]), "+v"(xv[2][1]),
+                     "+v"(xv[2][2]), "+v"(xv[2][3]));
+        if (PRO != ROWS_PRO_NONE) {
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i)
+#pragma unroll
+                for (int k = 0; k < 4; ++k) asm volatile("" : "+v"(x2v[i][k]));
+        }
+        if (PRO == ROWS_PRO_SWIGLU) {
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i)
+                if (i < qw)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) xv[i][k] = swiglu4(xv[i][k], x2v[i][k]);
+        } else if (PRO == ROWS_PRO_NORM) {
+            double *sums = (double *)(smem + L.sums);
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i) {
+                if (i < qw) {
+                    const int j = PASS * i + 4 * wave + (lane >> 4);
+                    double sq = 0.0;
+                    if (j < nb) {
+                        float v[16];
+#pragma unroll
+                        for (int k = 0; k < 4; ++k) {
+                            v[4 * k] = __uint_as_float(xv[i][k].x), v[4 * k + 1] = __uint_as_float(xv[i][k].y);
+                            v[4 * k + 2] = __uint_as_float(xv[i][k].z), v[4 * k + 3] = __uint_as_float(xv[i][k].w);
+                        }
+                        sq = sumsq16(v);
+                    }
+                    sq = row16_sum(sq);
+                    if (j < nb && (lane & 15) == 0) sums[j] = sq;
+                }
+            }
+            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+            double tot = seq_sum_lanes(sums, nb, lane);
+            if (rms_mean_ambiguous(div_by_count(tot, (int64_t)nb * QK), (int64_t)nb * QK))
+                tot = seq_sumsq_wave(a.x, (int64_t)nb * QK, lane);
+            const float mean = (float)div_by_count(tot, (int64_t)nb * QK);
+            const float scale = 1.0f / sqrtf(mean + a.eps);
+#pragma unroll
+            for (int i = 0; i < ROWS_QPASS; ++i)
+                if (i < qw)
+#pragma unroll
+                    for (int k = 0; k < 4; ++k) xv[i][k] = normmul4(xv[i][k], x2v[i][k], scale);
+        }
+#pragma unroll 1
+        for (int i = 0; i < qw; ++i) {
+            u32x4 cur[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) cur[k] = i == 0 ? xv[0][k] : i == 1 ? xv[1][k] : xv[2][k];
+            const int j = PASS * i + 4 * wave + (lane >> 4);
+            if (j < nb) quant16_store(cur, lane & 15, smem + L.act + Q8L_STRIDE * j);
+        }
+        if (RSTAMPS(a)) {
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+            sq = __builtin_amdgcn_s_memrealtime();
+        }
+    } else {
+        const int ng = nb * (Q8L_STRIDE / 16);
+        for (int j = wave; 64 * j < ng; j += nwv) {
+            const int k = 64 * j + lane;
+            if (k < ng) dma16(a.xq + 16 * k, (LDS void *)(smem + L.act + 1024 * j));
+        }
+        rv = gload4_asm(fres && f0 < nflat && frow < N ? fres + frow : (const float *)a.xq);
+        if (!idone && !iwait && ki >= 0) issue(false);
+        vm_wait_k<NI>(issued);
+    }
+    while (!idone && !iwait && ki >= 0 && issued < D) issue(false);  // the rest of the ring: static units only
+    if (wave == 0 && lane == 0) *cnt = (uint32_t)(nwv * P);            // claims start after the static ids
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");   // Q8_K row complete, counter set
+    if (iwait) next_unit(true);
+    while (!idone && ki >= 0 && issued < D) issue(true);
+    const uint64_t st1 = RSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
+
+    // ---- main loop: the oldest step in flight, then one more issued
+    int kc = 0, cs = 0, cT = 0, cG = 0, cmis = 0, crows = 0, io = 0, rr = 0;
+    int bro = 0;        // batch rows before the current unit
+    uint32_t bfl = 0;   // lane r: flat output index of batch row r
+    auto consume_unit = [&](int k) {
+        const uint32_t gr = (uint32_t)__builtin_amdgcn_readlane((int)ug, k & 7);
+        const int flat = __builtin_amdgcn_readlane((int)uf, k & 7);
+        cG = (int)(gr & 0xffffu);
+        crows = (int)(gr >> 16);
+        cT = (cG + ROWS_SB - 1) / ROWS_SB;
+        cmis = (int)((uint32_t)__builtin_amdgcn_readlane((int)ul, k & 7) & 15u);
+        bfl = lane >= bro && lane < bro + crows ? (uint32_t)(flat + lane - bro) : bfl;
+        cs = 0;
+        io = q;
+        rr = bro;
+        while (io >= nb) {
+            io -= nb;
+            ++rr;
+        }
+    };
+    auto replay = [&]() {  // the batch's rows: lane r <-> batch row r, records in superblock order
+        wave_lds_fence();
+        if (lane < bro) {
+            float v = 0.f;
+            const Rec *rc = recs + lane;
+#pragma unroll 4
+            for (int i = 0; i < nb; ++i) v = chain_step(TYPE, rc[i * bR], v);
+            outs[bfl] = v;
+        }
+        wave_lds_fence();
+        bro = 0;
+    };
+    int consumed = 0;
+    if (issued > 0) consume_unit(0);
+    const uint8_t *cslot = ring;
+#pragma unroll 1
+    while (consumed < issued) {
+        vm_wait_k<NI>(issued - consumed - 1);
+        if (ROWS_SB * cs + q < cG) {
+            const uint8_t *blk = cslot + cmis + q * BSZ;
+            const uint8_t *ab = actq + io * Q8L_STRIDE;
+            QuadOut r = TYPE == Q4_K ? quad_q4K(blk, ab, s) : TYPE == Q5_K ? quad_q5K(blk, ab, s) : quad_q6K(blk, ab, s);
+            const int isum = quad_sum(r.isum);
+            const int imin = quad_sum(r.imin);
+            if (s == 0) {
+                const float yd = *(const float *)ab;
+                Rec rec;
+                if (TYPE == Q6_K) {
+                    rec.a = isum - 32 * imin;
+                    rec.b = 0;
+                    rec.c = h2f(r.dh) * yd;  // d_all * y.d
+                    rec.e = 0.f;
+                } else {
+                    rec.a = isum;
+                    rec.b = imin;
+                    rec.c = yd * h2f(r.dh & 0xffffu);  // y.d * fp16(x.d)
+                    rec.e = yd * h2f(r.dh >> 16);      // y.d * fp16(x.dmin)
+                }
+                recs[io * bR + rr] = rec;
+            }
+        }
+        cslot = cslot + SLOT == ring_end ? ring : cslot + SLOT;
+        ++consumed;
+        ++cs;
+        if (!idone) issue(true);
+        if (RSTAMPS(a) && consumed == 1) sf = __builtin_amdgcn_s_memrealtime();
+        if (cs == cT) {  // the unit's last step: into the batch; replay when the next unit may not fit
+            bro += crows;
+            if (bro + U > bR || consumed == issued) replay();
+            ++kc;
+            if (consumed < issued) consume_unit(kc);
+        } else {
+            io += ROWS_SB;
+            while (io >= nb) {
+                io -= nb;
+                ++rr;
+            }
+        }
+    }
+
+    const uint64_t st2 = RSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
+    // ---- flush: the workgroup's rows, coalesced, with the residual ADD / SWIGLU epilogue
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(rv));
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    for (int f = f0; f < nflat; f += 64 * nwv) {
+        const int m = (f >= nr ? 1 : 0) + (f >= 2 * nr ? 1 : 0) + (f >= 3 * nr ? 1 : 0);
+        const int row = f == f0 ? frow : row_of(f - m * nr);
+        if (row >= N) continue;  // the short last unit's unused slots
+        const float *res = m == 0 ? a.res[0] : m == 1 ? a.res[1] : m == 2 ? a.res[2] : a.res[3];
+        float *y = m == 0 ? a.y[0] : m == 1 ? a.y[1] : m == 2 ? a.y[2] : a.y[3];
+        float v = outs[f];
+        if (res) v = v + (f == f0 ? __uint_as_float(rv) : res[row]);  // ggml_add(mul_mat, residual)
+        store_y(y + row, v);
+    }
+    if (a.epi) {  // y[0] = gate, y[1] = up: the same rows of both in this workgroup
+        const int n4 = a.epi_n & ~3;
+        for (int f = f0; f < nr; f += 64 * nwv) {
+            const int r = row_of(f);
+            if (r >= N) continue;
+            const float gv = outs[f], uv = outs[nr + f];
+            store_y(a.epi_y + r, r < n4 ? v_silu(gv) * uv : (gv / (1.0f + expf(-gv))) * uv);
+        }
+    }
+    if (RSTAMPS(a)) {  // the kq_rows stamp layout (tools/stamps.py); slot 7: units this wave took
+        const int64_t o = ((int64_t)blockIdx.x * ROWS_WAVES + wave) * 8;
+        if (lane == 0 && o + 7 < a.stamps_cap) {
+            RSTAMPS(a)[o] = st0;
+            RSTAMPS(a)[o + 1] = st1;
+            RSTAMPS(a)[o + 2] = st2;
+            RSTAMPS(a)[o + 3] = __builtin_amdgcn_s_memrealtime();
+            RSTAMPS(a)[o + 4] = sx;
+            RSTAMPS(a)[o + 5] = sq;
+            RSTAMPS(a)[o + 6] = sf;
+            RSTAMPS(a)[o + 7] = (uint64_t)(ki + 1);
+        }
+    }
+}
+template <int TMASK, bool FUSEDQ, int PRO>
+__global__ void __launch_bounds__(ROWS_WAVES * 64) kq_rows_dyn(const RowsArgs a) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    const uint64_t st0 = RSTAMPS(a) ? __builtin_amdgcn_s_memrealtime() : 0;
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const RowsDynLayout L =
+        rows_dyn_layout(a.nb, TMASK, a.bR, a.rpw, __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6)));
+    constexpr int TYPE = TMASK == 1 ? Q4_K : TMASK == 2 ? Q5_K : Q6_K;
+    rows_dyn_body<TYPE, FUSEDQ, PRO>(a, smem, L, wave, lane, st0);
+}
+
+#define KQ_ROWS_DYN_INST(TM, FQ, PR) template __global__ void kq_rows_dyn<TM, FQ, PR>(const RowsArgs a);
+#define KQ_ROWS_DYN_INST_T(TM)        \
+    KQ_ROWS_DYN_INST(TM, true, 0)     \
+    KQ_ROWS_DYN_INST(TM, true, 1)     \
+    KQ_ROWS_DYN_INST(TM, true, 2)     \
+    KQ_ROWS_DYN_INST(TM, false, 0)
+KQ_ROWS_DYN_INST_T(1)
+KQ_ROWS_DYN_INST_T(2)
+KQ_ROWS_DYN_INST_T(4)
+
 }  // namespace kq

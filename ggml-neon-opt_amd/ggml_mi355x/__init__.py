@@ -249,12 +249,13 @@ def lib():
     return L
 
 
-GEMV_AUTO, GEMV_TASKS, GEMV_ROWS = 0, 1, 2
+GEMV_AUTO, GEMV_TASKS, GEMV_ROWS, GEMV_DYN = 0, 1, 2, 3
 
 
 def gemv_impl(impl):
     """Select the decode GEMV kernel (GEMV_AUTO / GEMV_ROWS: row-stream kq_rows, one
-    launch per stage; GEMV_TASKS: kq_gemv). Returns the previous selection."""
+    launch per stage, the claimed-row kq_rows_dyn where enough rows per wave; GEMV_TASKS:
+    kq_gemv; GEMV_DYN: kq_rows_dyn for every one-type launch). Returns the previous selection."""
     prev = lib().mi355x_gemv_impl(impl)
     if prev < 0:
         raise Mi355xError(f"mi355x_gemv_impl failed with status {prev}")
@@ -414,7 +415,7 @@ def gemv_waves(waves):
 
 DEBUG_KNOBS = ("GEMV_DIAG", "GEMV_RING", "GEMV_PRE0", "GEMV_PF", "GEMV_XMODE", "GEMV_SMALL_MB", "GEMV_WPC",
                "GEMV_SMALL_WG", "GEMV_FQMAX", "MMF_WAVES", "MMF_ORDER", "ATTN_DIAG", "LOOPBACK_NOCOPY",
-               "ATTN_OPROJ", "AO_NRB")
+               "ATTN_OPROJ", "AO_NRB", "GEMV_DYN", "GEMV_DYN_P")
 
 
 def debug_knob(name, value=float("nan")):

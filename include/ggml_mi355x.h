@@ -237,13 +237,16 @@ int mi355x_timing_read(mi355x_launch_timing *out, int max);
  * 8 x uint64 per wave, [(blockIdx.x * 4 + wave) * 8 + i]. NULL disables. */
 int mi355x_diag_stamps(void *buf, size_t bytes);
 /* Decode-GEMV implementation selector (A/B runs, parity of every path):
- * MI355X_GEMV_AUTO (row-stream kq_rows when rows are contiguous, else kq_gemv),
- * MI355X_GEMV_TASKS (always the 8-row-task kq_gemv) or MI355X_GEMV_ROWS (kq_rows,
- * one launch per stage; what AUTO does today). Returns the previous value, or
- * MI355X_E_INVAL. */
+ * MI355X_GEMV_AUTO (row-stream kq_rows when rows are contiguous, else kq_gemv; the
+ * claimed-row form kq_rows_dyn for one-type launches with enough rows per wave),
+ * MI355X_GEMV_TASKS (always the 8-row-task kq_gemv), MI355X_GEMV_ROWS (kq_rows, one
+ * launch per stage; as AUTO) or MI355X_GEMV_DYN (kq_rows_dyn for every one-type
+ * launch: rows claimed per workgroup from an LDS counter). Same numerics in all.
+ * Returns the previous value, or MI355X_E_INVAL. */
 #define MI355X_GEMV_AUTO 0
 #define MI355X_GEMV_TASKS 1
 #define MI355X_GEMV_ROWS 2
+#define MI355X_GEMV_DYN 3
 int mi355x_gemv_impl(int impl);
 /* Prefill (ne11 >= 16) GEMM selector for the int8-MFMA tile kernel: MI355X_MMQ_TILE64
  * (64 weight rows x 64 activation columns per workgroup), MI355X_MMQ_TILE128 (128 rows x

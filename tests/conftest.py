@@ -36,10 +36,12 @@ def dev():
     return torch.device("cuda:0")
 
 
-@pytest.fixture(params=[(0, 0), (1, 0), (0, 12), (0, 6)], ids=["rows", "tasks", "rows12", "rows6"])
+@pytest.fixture(params=[(0, 0), (1, 0), (0, 12), (0, 6), (3, 0), (3, 6)],
+                ids=["rows", "tasks", "rows12", "rows6", "dyn", "dyn6"])
 def impl(request):
-    """Runs a decode-GEMV test on both kernels, kq_rows (default) and kq_gemv, and kq_rows
-    at both launch shapes: waves per workgroup by launch size (default), 12 and 6."""
+    """Runs a decode-GEMV test on every kernel: kq_rows (default), kq_gemv, kq_rows at both
+    launch shapes (waves per workgroup by launch size, 12 and 6), and the claimed-row
+    kq_rows_dyn forced on every one-type launch (by size, and at 6 waves)."""
     import ggml_mi355x as g
     which, waves = request.param
     prev = g.gemv_impl(which)

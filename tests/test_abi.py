@@ -89,7 +89,9 @@ def test_argument_validation_without_device():
     assert L.mi355x_gemv_impl(7) == -1
     prev = L.mi355x_gemv_impl(2)  # GEMV_ROWS
     assert L.mi355x_gemv_impl(prev) == 2
-    assert L.mi355x_gemv_impl(3) == -1
+    prev = L.mi355x_gemv_impl(3)  # GEMV_DYN (claimed rows)
+    assert L.mi355x_gemv_impl(prev) == 3
+    assert L.mi355x_gemv_impl(4) == -1
     # no device here -> the HIP path reports it instead of falling back
     descs = (g.GemvDesc * 1)(g.GemvDesc(12, 0x1000, 4, 144, 0x3000))
     rc = L.mi355x_gemv_fused(descs, 1, 0x2000, 256, None, 0, None)

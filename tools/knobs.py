@@ -20,7 +20,8 @@ def apply_env(environ=None):
             g.debug_knob(k, float(v))
             done[k] = float(v)
     sel = {
-        "MI355X_GEMV_IMPL": (g.gemv_impl, {"tasks": g.GEMV_TASKS, "rows": g.GEMV_ROWS, "auto": g.GEMV_AUTO}),
+        "MI355X_GEMV_IMPL": (g.gemv_impl, {"tasks": g.GEMV_TASKS, "rows": g.GEMV_ROWS, "auto": g.GEMV_AUTO,
+                                           "dyn": g.GEMV_DYN}),
         "MI355X_MMQ_IMPL": (g.mmq_impl, {"tile64": g.MMQ_TILE64, "tile128": g.MMQ_TILE128,
                                          "tile128w": g.MMQ_TILE128W, "tile64w": g.MMQ_TILE64W, "tile128x": g.MMQ_TILE128X, "tile192": g.MMQ_TILE192,
                                          "auto": g.MMQ_AUTO}),
