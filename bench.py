@@ -1206,7 +1206,7 @@ def main():
         if prefill is not None:
             prefill["roofline"] = {"bound": "mfma", "achieved": prefill["int_TOPS"], "peak": I8_PEAK_TOPS,
                                    "unit": "TOPS (int8 dense)", "frac": round(prefill["int_TOPS"] / I8_PEAK_TOPS, 4),
-                                   "mfma_pmc": "profiles/r03_prefill_mfma.md"}
+                                   "mfma_pmc": "profiles/r05_prefill_mfma.md", "stall_pmc": "profiles/r06_prefill_stall.md"}
         cpu = None
         if world == 1 and not args.no_cpu_baseline:
             cpu = cpu_baseline_token(chain, args.cpu_seconds) if isinstance(chain, Token) else \
