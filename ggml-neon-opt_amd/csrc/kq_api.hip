@@ -671,7 +671,7 @@ const void *mmq_fn(int type, bool mixed, MmqShape sh) {
     KQ_MMQ_PICK(64, 1)
 #undef KQ_MMQ_PICK
 }
-// two superblock buffers: mmq_cols(cw) Q8L columns + rt weight rows (Q6_K: 224-B granule span),
+// two superblock buffers: mmq_cols(cw) Q8L columns + rt weight rows (Q6_K: KQ_MMQ_Q6_STRIDE, the 224-B granule span + padding),
 // +16 B for the Q6_K realign reads past the last row
 size_t mmq_lds(int type, MmqShape sh) {
     return (size_t)mmq_nbuf(type, sh.rt, sh.cw) * (size_t)mmq_buf_bytes(type, sh.rt, sh.cw) + 16 + MMQ_PF_LDS;

@@ -169,8 +169,16 @@ constexpr int Q8L_STRIDE = 304; // LDS/workspace Q8_K block: d @0, qs @16, bsums
 __host__ __device__ constexpr int mmq_cgroups(int cw) { return cw == 4 ? 1 : 2; }
 __host__ __device__ constexpr int mmq_cols(int cw) { return 32 * cw * mmq_cgroups(cw); }
 __host__ __device__ constexpr int mmq_waves(int rt, int cw) { return rt / 32 * mmq_cgroups(cw); }
+// Q6_K rows staged at KQ_MMQ_Q6_STRIDE bytes: the 14 granules of a 210-B block (fetched from
+// the 16-B boundary below it, 224 B) plus one padding granule at 240, so consecutive rows start
+// 60 dwords apart (16 bank offsets) instead of 56 (8): the tile's realigned row reads
+// conflicted for 71 % of the LDS's active cycles at 224 (profiles/r06_prefill_stall.md).
+#ifndef KQ_MMQ_Q6_STRIDE
+#define KQ_MMQ_Q6_STRIDE 240
+#endif
+static_assert(KQ_MMQ_Q6_STRIDE % 16 == 0 && KQ_MMQ_Q6_STRIDE >= 224, "whole granules");
 __host__ __device__ constexpr int mmq_buf_bytes(int type, int rt, int cw) {
-    return mmq_cols(cw) * Q8L_STRIDE + rt * (type == Q6_K ? 224 : block_bytes(type));
+    return mmq_cols(cw) * Q8L_STRIDE + rt * (type == Q6_K ? KQ_MMQ_Q6_STRIDE : block_bytes(type));
 }
 __host__ __device__ constexpr int mmq_nbuf(int type, int rt, int cw) {
     return KQ_MMQ_NBUF == 1 ? 1 : KQ_MMQ_NBUF >= 3 && ((rt == 128 && cw == 1) || (rt == 64 && cw == 2)) &&

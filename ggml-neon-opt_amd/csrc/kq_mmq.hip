@@ -101,8 +101,9 @@ __device__ __forceinline__ uint32_t as_u32(u16x2 v) {
 // Weight bytes per row in the LDS tile: the superblock itself (Q4_K 144, Q5_K 176,
 // 16-B aligned rows), or for Q6_K (210 B, any alignment) the 14 granules from the
 // 16-B boundary below it.
-__host__ __device__ constexpr int mmq_row_bytes(int type) { return type == Q6_K ? 224 : block_bytes(type); }
-__host__ __device__ constexpr int mmq_b_instr(int type, int rt) { return rt * mmq_row_bytes(type) / 1024; }  // 9 / 11 / 14 per 64 rows
+__host__ __device__ constexpr int mmq_row_bytes(int type) { return type == Q6_K ? KQ_MMQ_Q6_STRIDE : block_bytes(type); }
+__host__ __device__ constexpr int mmq_b_instr(int type, int rt) { return rt * mmq_row_bytes(type) / 1024; }  // 9 / 11 / 15 per 64 rows
+static_assert(64 * KQ_MMQ_Q6_STRIDE % 1024 == 0, "whole DMA instructions per 64 rows");
 
 
 // Scale-split multipliers of sub-blocks 2jp (lo nibbles) and 2jp+1 (hi nibbles) as 16-bit
@@ -297,7 +298,8 @@ __device__ __forceinline__ void mmq_tile(const MmqArgs &a, int tx, int ty) {
             } else {
                 constexpr int RG = mmq_row_bytes(TYPE) / 16;
                 int rw = g / RG;
-                const int piece = g - rw * RG;
+                int piece = g - rw * RG;
+                if (TYPE == Q6_K && piece > 13) piece = 13;  // padding granules: the row's last one again
                 rw = row0 + rw < a.n_rows ? row0 + rw : a.n_rows - 1;
                 const uintptr_t blk = (uintptr_t)(a.w + (int64_t)rw * a.row_stride + (int64_t)b * BSZ);
                 src = (const uint8_t *)(blk & ~(uintptr_t)15) + 16 * piece;
