@@ -549,12 +549,11 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                 }
                 const float mx = fmaxf(fmaxf(scal[0], scal[1]), fmaxf(scal[2], scal[3]));
                 // the group sums' double sum: each wave sums its own groups and publishes one
-                // double with a flag; where every group sum meets softmax_group_sum's exactness
-                // bound (every partial sum exact: any order gives ggml's in-order bits) the four
-                // wave sums are the sum, else the in-order sum over gsum
-                const int thr = (31 - __builtin_clz((unsigned)n_kv)) - 29;  // floor(log2(4 n_groups)) - 29
-                double part = 0.0;
-                bool ok = true;
+                // double with its min last-bit exponent and a non-finite flag; where the total
+                // meets softmax_group_sum's exactness bound (every partial sum exact: any order
+                // gives ggml's in-order bits) the four wave sums are the sum, else the in-order
+                // sum over gsum
+                SumExact se;
                 for (int c = 0; c < n_ch; ++c) {  // (uniform trip count: every lane in the quad sums)
                     const int cell = 256 * c + t;
                     const float sv = cell < n_kv ? w[cell] : -INFINITY;
@@ -566,27 +565,33 @@ __device__ __forceinline__ void attn_head(const AttnArgs &a, int h, int t, uint8
                         w[cell] = ec;
                         if ((t & 3) == 0) {
                             gsum[cell >> 2] = (double)g4;
-                            const int ef = (__float_as_int(g4) >> 23) & 0xff;
-                            ok = ok && (g4 == 0.0f || (ef != 0 && ef != 255 && ef - 127 >= thr));
-                            part += (double)g4;
+                            se.add(g4);
                         }
                     }
                 }
-                const bool wok = __all(ok);
-                const double wsum = wave_sum_exact_f64(part);  // (meaningful only where wok)
+                const bool wbad = __any(se.bad);
+                const int wgmin = wave_imin(se.gmin);
+                const double wsum = wave_sum_exact_f64(se.part);  // (meaningful only where exact)
                 if ((t & 63) == 0) {
                     *(double *)(kring + 16 * wv) = wsum;  // (the K ring is free: every chunk consumed)
-                    *(int *)(kring + 16 * wv + 8) = wok;
+                    *(int *)(kring + 16 * wv + 8) = wgmin;
+                    *(int *)(kring + 16 * wv + 12) = wbad;
                 }
                 __syncthreads();
-                bool allok = true;
+                bool anybad = false;
+                int gmin = 1 << 20;
                 double s4[4];
 #pragma unroll
                 for (int q = 0; q < 4; ++q) {
                     s4[q] = *(const double *)(kring + 16 * q);
-                    allok = allok && *(const int *)(kring + 16 * q + 8) != 0;
+                    const int gq = *(const int *)(kring + 16 * q + 8);
+                    gmin = gq < gmin ? gq : gmin;
+                    anybad = anybad || *(const int *)(kring + 16 * q + 12) != 0;
                 }
-                const double sum = allok ? (s4[0] + s4[1]) + (s4[2] + s4[3]) : seq_sum_lds(gsum, n_kv / 4);
+                const double s4t = (s4[0] + s4[1]) + (s4[2] + s4[3]);
+                const double sum = sum_exact_ok(s4t, gmin, anybad)
+                                       ? s4t
+                                       : (KQ_SEQ_SUM_WAVE ? seq_sum_wave(gsum, n_kv / 4, t & 63) : seq_sum_lds(gsum, n_kv / 4));
                 const float inv = (float)(1.0 / sum);
                 for (int c = 0; c < n_ch; ++c) {
                     const int cell = 256 * c + t;

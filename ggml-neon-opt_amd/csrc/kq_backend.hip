@@ -1520,6 +1520,14 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
             b->ly_tabs.push_back(std::move(tb));
         }
     }
+    for (const Launch &l : launches) {  // long-cache decode attention: its score workspace, outside any capture
+        const mi355x_tensor *t = nodes[l.first];
+        if (l.kind != 0 || t->op != MI355X_OP_ATTN_DECODE || t->src[0]->ne[1] != 1) continue;
+        mi355x_attn_desc d = {};
+        attn_desc_of(t, d);
+        kq::AttnArgs a = {};
+        if (kq::attn_args_from(&d, a) == MI355X_OK && kq::attn_cells_reserve(a) != MI355X_OK) return MI355X_E_WORKSPACE;
+    }
     if (!use_graph) return enqueue(b, nodes, launches);
     std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);
     mi355x_backend::Captured *c = find_graph(b, key);

@@ -230,6 +230,313 @@ __global__ void __launch_bounds__(TPH) kq_attn_decode(const AttnArgs a) {
                                                                      true, ds);
 }
 
+// ------------------------------------------------------------ long caches: KQ split over cells
+// Past what the output split's LDS holds (kq_attn_decode<HD, true, DS> keeps the head's scores
+// and its V slice in one workgroup: ~3000 cells at head_dim 64), the one-workgroup-per-head
+// kernel streams every K and V row of a head through one CU (tg4096: ~21 us per layer). There
+// the head's KQ splits over cells instead, in two launches:
+//  A kq_attn_cells: workgroup (chunk, g) scores ATTN_CHUNK cells of kv group g for EVERY query
+//    head of the group (each K row read once for the gsz heads) into a score workspace
+//    [n_head][n_ctx]; the workgroup whose chunk holds the position writes the new cell to both
+//    caches (rope'd k, f16 v) and scores that cell from its own copy;
+//  B kq_attn_cells_kqv: workgroup (h, ds): soft_max over the head's scores and KQV for its
+//    HD / DS outputs from the V cache (the new cell included: A wrote it, a kernel boundary
+//    before).
+// Every score is the same NEON-FP16 vec_dot as the one-launch kernels', soft_max's max, exps,
+// group sums and in-order double sum and the KQV accumulator chains are theirs: bit-exact.
+constexpr int ATTN_CHUNK = 64;
+#ifndef KQ_ATTN_CELLS_OVER_SPLIT
+#define KQ_ATTN_CELLS_OVER_SPLIT 0  // experiment builds: the two launches also where the output split fits
+#endif
+#ifndef KQ_ATTN_CELLS_MIN
+#define KQ_ATTN_CELLS_MIN 1024  // caches of more cells than this take the two launches when the output split does not fit
+#endif
+#ifndef KQ_ATTN_CELLS_OVERLAP
+#define KQ_ATTN_CELLS_OVERLAP 1  // B's soft_max waits for the scores only, the V rows land meanwhile
+#endif
+#ifndef KQ_ATTN_CELLS_RS64
+#define KQ_ATTN_CELLS_RS64 8  // B's outputs per workgroup at head_dim 64 (8: 256 workgroups for 32 heads)
+#endif
+#ifndef KQ_ATTN_CELLS_RS128
+#define KQ_ATTN_CELLS_RS128 16  // at head_dim 128 (16: 256 workgroups for 32 heads, one round)
+#endif
+#ifndef KQ_ATTN_CELLS_STOP
+#define KQ_ATTN_CELLS_STOP 0  // diagnostic builds: B stops after its loads (1) or soft_max (2)
+#endif
+#ifndef KQ_ATTN_CELLS_VPAD
+#define KQ_ATTN_CELLS_VPAD 64  // bytes past 2 n_ctx per V row in B's LDS (a multiple of 16)
+#endif
+constexpr int ATTN_CELLS_VPAD = KQ_ATTN_CELLS_VPAD;
+constexpr int ATTN_CELLS_GMAX = 8;  // B's soft_max: 4-cell groups per thread in registers (n_ctx <= 8192)
+
+template <int HD>
+__global__ void __launch_bounds__(256) kq_attn_cells(const AttnArgs a, float *scores) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int KV4 = HD / 8;                        // 16-B pieces of a K row
+    constexpr int KPT = ATTN_CHUNK * KV4 / 256;        // pieces per thread
+    const int g = blockIdx.y, c0 = blockIdx.x * ATTN_CHUNK, t = threadIdx.x;
+    const int gsz = a.n_head / a.n_head_kv;
+    const int kvw = a.n_head_kv * HD;
+    // every load that does not depend on the position goes out with it: the chunk's K rows
+    // (cells < n_ctx: valid memory whatever the position; cell pos's row is stale and unused)
+    uint4 kr[KPT];
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+        const int i = t + 256 * u, r = i / KV4, k = i % KV4;
+        kr[u] = *(const uint4 *)(a.k_cache + (int64_t)(c0 + r) * kvw + (int64_t)g * HD + 8 * k);
+    }
+    const int pos_in = *a.pos;
+    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;  // no cache cell: caches untouched, B outputs NaN
+    const int pos = bad ? 0 : pos_in;
+    int n_kv = (pos + 1 + 31) / 32 * 32;
+    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
+    if (c0 >= n_kv) return;  // (uniform)
+    // LDS: q16 [gsz][HD] | k16 [HD] | K rows [ATTN_CHUNK][KV4] (piece k of row r at k ^ (r % KV4))
+    uint16_t *q16 = (uint16_t *)smem;
+    uint16_t *k16 = q16 + gsz * HD;
+    uint4 *krow = (uint4 *)(k16 + HD);
+    const bool holds = pos >= c0 && pos < c0 + ATTN_CHUNK;
+#pragma unroll
+    for (int u = 0; u < KPT; ++u) {
+        const int i = t + 256 * u, r = i / KV4, k = i % KV4;
+        krow[r * KV4 + (k ^ (r % KV4))] = kr[u];
+    }
+    // rope(q) of the group's heads at pos (kq_attn_head.h step 1), and the new cell where held
+    const float *tc = a.rope_table + (a.rope_row ? 0 : (int64_t)pos * (HD / 2) * 2);
+    for (int i = t; i < gsz * (HD / 2); i += 256) {
+        const int hh = i / (HD / 2), p2 = i % (HD / 2);
+        const float *qp = a.q + (int64_t)(g * gsz + hh) * HD + 2 * p2;
+        const float2 rq = rope_pair(qp[0], qp[1], tc[2 * p2], tc[2 * p2 + 1]);
+        q16[hh * HD + 2 * p2] = h2u(f2h_rne(rq.x));
+        q16[hh * HD + 2 * p2 + 1] = h2u(f2h_rne(rq.y));
+    }
+    if (holds) {
+        for (int p2 = t; p2 < HD / 2; p2 += 256) {
+            const float *kp = a.k + (int64_t)g * HD + 2 * p2;
+            const float2 rk = rope_pair(kp[0], kp[1], tc[2 * p2], tc[2 * p2 + 1]);
+            const uint16_t k0 = h2u(f2h_rne(rk.x)), k1 = h2u(f2h_rne(rk.y));
+            k16[2 * p2] = k0;
+            k16[2 * p2 + 1] = k1;
+            if (!bad) *(uint32_t *)(a.k_cache + (int64_t)pos * kvw + (int64_t)g * HD + 2 * p2) = k0 | ((uint32_t)k1 << 16);
+        }
+        for (int d = t; d < HD && !bad; d += 256)
+            a.v_cache[(int64_t)(g * HD + d) * a.n_ctx + pos] = h2u(f2h_rne(a.v[(int64_t)g * HD + d]));
+    }
+    __syncthreads();
+    for (int i = t; i < ATTN_CHUNK * gsz; i += 256) {  // lane <-> cell, waves <-> heads
+        const int r = i % ATTN_CHUNK, hh = i / ATTN_CHUNK, c = c0 + r;
+        if (c >= n_kv) continue;
+        float sc = -INFINITY;  // cells past pos: masked
+        if (c <= pos) {
+            uint4 kv[KV4];
+            if (c == pos) {
+#pragma unroll
+                for (int k = 0; k < KV4; ++k) kv[k] = ((const uint4 *)k16)[k];
+            } else {
+#pragma unroll
+                for (int k = 0; k < KV4; ++k) kv[k] = krow[r * KV4 + (k ^ (r % KV4))];
+            }
+            sc = vec_dot_f16_rows<HD>(kv, (const uint4 *)(q16 + hh * HD)) * a.scale;
+        }
+        scores[(int64_t)(g * gsz + hh) * a.n_ctx + c] = sc;
+    }
+}
+
+// B: every input of the workgroup — the head's n_kv scores and its RS = HD / DS V rows over
+// cells [0, n_kv) — arrives by LDS-DMA issued at entry, all in flight at once (a thread's KQV
+// chain runs over n_kv / 32 iterations in order: loading them from global memory as it goes
+// paid one memory latency per batch). soft_max waits for the scores only (a counted vmcnt: the
+// V rows were issued after them), so the V rows land while it runs; KQV reads LDS only.
+// LDS: the scores (n_ctx f32; once in registers the region holds the group sums, then p16) |
+// red (KQV words, RS x 16 u32) | scal (24 f32: wave maxima, wave ok flags, wave sums as f64) |
+// the V rows (RS x VSTR).
+template <int VM>
+__device__ __forceinline__ void waitcnt_vm_le() {  // s_waitcnt vmcnt(VM) (expcnt, lgkmcnt free)
+    static_assert(VM >= 0 && VM < 64, "vmcnt is 6 bits");
+    __builtin_amdgcn_s_waitcnt((VM & 15) | ((VM >> 4) << 14) | 0x0F70);
+}
+__device__ __forceinline__ void waitcnt_vm_floor8(int n) {  // vmcnt(8 floor(min(n, 63) / 8)) <= n
+    switch ((n > 63 ? 63 : n) >> 3) {
+    case 0: waitcnt_vm_le<0>(); break;
+    case 1: waitcnt_vm_le<8>(); break;
+    case 2: waitcnt_vm_le<16>(); break;
+    case 3: waitcnt_vm_le<24>(); break;
+    case 4: waitcnt_vm_le<32>(); break;
+    case 5: waitcnt_vm_le<40>(); break;
+    case 6: waitcnt_vm_le<48>(); break;
+    default: waitcnt_vm_le<56>(); break;
+    }
+}
+template <int HD, int DS>
+__global__ void __launch_bounds__(256) kq_attn_cells_kqv(const AttnArgs a, const float *scores) {
+    extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+    constexpr int RS = HD / DS;  // outputs of this workgroup
+    static_assert(RS * 16 <= 256 && (RS & (RS - 1)) == 0 && RS >= 4, "16 threads per output, whole rows per wave");
+    int h = blockIdx.x / DS, ds = blockIdx.x % DS;
+    if ((a.n_head & 7) == 0) {  // XCD-aware order, as kq_attn_decode (speed only)
+        const int x = blockIdx.x & 7, i = blockIdx.x >> 3;
+        h = x * (a.n_head >> 3) + i / DS;
+        ds = i % DS;
+    }
+    const int t = threadIdx.x, ln = t & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int g = h / (a.n_head / a.n_head_kv);
+    const int pos_in = *a.pos;
+    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;
+    const int pos = bad ? 0 : pos_in;
+    int n_kv = (pos + 1 + 31) / 32 * 32;
+    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
+    const int n_it = (pos + 32) / 32;  // 32-cell iterations holding a cell <= pos
+    float *w = (float *)smem;
+    double *gsum = (double *)smem;
+    uint16_t *p16 = (uint16_t *)smem;
+    uint32_t *red = (uint32_t *)(w + a.n_ctx);
+    float *scal = (float *)(red + RS * 16);
+    uint8_t *vlds = (uint8_t *)(scal + 24);
+    const int VSTR = 2 * a.n_ctx + ATTN_CELLS_VPAD;  // rows 16 words apart in the banks
+    int nv = 0;  // this wave's V-row DMAs (issued after its score DMAs)
+    {
+        const uint8_t *src = (const uint8_t *)(scores + (int64_t)h * a.n_ctx);
+        const int sg = n_kv / 4;
+        for (int i = wv; 64 * i < sg; i += 4) {
+            const int n = sg - 64 * i < 64 ? sg - 64 * i : 64;
+            attn_dma16_lanes(src + 1024 * i + 16 * ln,
+                             __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS void *)((uint8_t *)w + 1024 * i)), ln, n);
+        }
+        const int vg = n_kv / 8;
+        for (int r = wv; r < RS; r += 4) {
+            const uint8_t *vsrc = (const uint8_t *)(a.v_cache + (int64_t)(g * HD + ds * RS + r) * a.n_ctx);
+            for (int i = 0; 64 * i < vg; ++i, ++nv) {
+                const int n = vg - 64 * i < 64 ? vg - 64 * i : 64;
+                attn_dma16_lanes(vsrc + 1024 * i + 16 * ln,
+                                 __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(LDS void *)(vlds + r * VSTR + 1024 * i)),
+                                 ln, n);
+            }
+        }
+    }
+#if KQ_ATTN_CELLS_OVERLAP
+    waitcnt_vm_floor8(nv);  // this wave's score granules have landed (loads complete in order)
+#else
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+#endif
+    __syncthreads();
+#if KQ_ATTN_CELLS_STOP == 1
+    __builtin_amdgcn_s_waitcnt(0x0F70);
+    __syncthreads();
+    if (t < RS) a.out[(int64_t)h * HD + ds * RS + t] = w[t] + (float)vlds[t * VSTR];
+    return;
+#endif
+    // soft_max (kq_attn_head.h, the general path): max (order-free), exps and the vaddvq group
+    // sums, ggml's in-order double sum, p = e * (float)(1 / sum) -> f16. Thread t holds the
+    // 4-cell groups t + 256 k in registers (one LDS read each, all issued together); the double
+    // sum is a tree over the block where that is exact (softmax_group_sum's condition: every
+    // group sum a float >= 2^(floor(log2(4 ng)) - 29), or zero), else the in-order sum of gsum.
+    const int ng = n_kv >> 2;
+    float4 ev[ATTN_CELLS_GMAX];
+    float m = -INFINITY;
+#pragma unroll
+    for (int k = 0; k < ATTN_CELLS_GMAX; ++k) {
+        const int gi = t + 256 * k;
+        ev[k] = gi < ng ? ((const float4 *)w)[gi] : make_float4(-INFINITY, -INFINITY, -INFINITY, -INFINITY);
+        m = fmaxf(m, fmaxf(fmaxf(ev[k].x, ev[k].y), fmaxf(ev[k].z, ev[k].w)));
+    }
+    const float wmx = wave_fmax(m);
+    if (ln == 0) scal[wv] = wmx;
+    __syncthreads();  // (also: every score is in registers, the region is free)
+    const float mx = fmaxf(fmaxf(scal[0], scal[1]), fmaxf(scal[2], scal[3]));
+    SumExact se;
+#pragma unroll
+    for (int k = 0; k < ATTN_CELLS_GMAX; ++k) {
+        const int gi = t + 256 * k;
+        if (gi < ng) {
+            float4 e = ev[k];
+            e.x = e.x == -INFINITY ? 0.0f : v_expf(e.x - mx);
+            e.y = e.y == -INFINITY ? 0.0f : v_expf(e.y - mx);
+            e.z = e.z == -INFINITY ? 0.0f : v_expf(e.z - mx);
+            e.w = e.w == -INFINITY ? 0.0f : v_expf(e.w - mx);
+            ev[k] = e;
+            const float gs = (e.x + e.y) + (e.z + e.w);
+            gsum[gi] = (double)gs;
+            se.add(gs);  // (exact when the total passes the bound: a subset's sum)
+        }
+    }
+    const bool wbad = __any(se.bad);
+    const int wgmin = wave_imin(se.gmin);
+    double part = se.part;
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    double *scald = (double *)(scal + 8);
+    if (ln == 0) {
+        scald[wv] = part;
+        ((int *)scal)[4 + wv] = wgmin;
+        ((int *)scal)[20 + wv] = wbad;
+    }
+    __syncthreads();
+    const int *sgm = (const int *)scal + 4, *sbad = (const int *)scal + 20;
+    const int gmin = min(min(sgm[0], sgm[1]), min(sgm[2], sgm[3]));
+    const double st = (scald[0] + scald[1]) + (scald[2] + scald[3]);
+    double sum;
+    if (sum_exact_ok(st, gmin, (sbad[0] | sbad[1] | sbad[2] | sbad[3]) != 0)) {  // (uniform)
+        sum = st;
+    } else {
+        if (t < 64) {
+            const double s = KQ_SEQ_SUM_WAVE ? seq_sum_wave(gsum, ng, t) : seq_sum_lds(gsum, ng);
+            if (t == 0) scald[4] = s;
+        }
+        __syncthreads();
+        sum = scald[4];
+    }
+    __syncthreads();  // gsum's readers are done before p16 overwrites it
+    const float inv = (float)(1.0 / sum);
+#pragma unroll
+    for (int k = 0; k < ATTN_CELLS_GMAX; ++k) {
+        const int gi = t + 256 * k;
+        if (gi < ng) {
+            const uint32_t lo = (uint32_t)h2u(f2h_rne(ev[k].x * inv)) | ((uint32_t)h2u(f2h_rne(ev[k].y * inv)) << 16);
+            const uint32_t hi = (uint32_t)h2u(f2h_rne(ev[k].z * inv)) | ((uint32_t)h2u(f2h_rne(ev[k].w * inv)) << 16);
+            ((uint2 *)p16)[gi] = make_uint2(lo, hi);
+        }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0): this wave's V rows have landed
+    __syncthreads();
+#if KQ_ATTN_CELLS_STOP == 2
+    if (t < RS) a.out[(int64_t)h * HD + ds * RS + t] = (float)p16[t] + (float)vlds[t * VSTR];
+    return;
+#endif
+    // KQV: word q (f16 lanes 2q, 2q + 1) of accumulator j of output vr over cells 32 it + 8 j +
+    // 2 q + {0, 1}, in order: 16 threads per output, each one chain of pk_fmas
+    {
+        const int vr = t >> 4, jq = t & 15;
+        uint32_t acc1 = 0;
+        if (vr < RS) {
+            const uint32_t *vrow = (const uint32_t *)(vlds + vr * VSTR) + jq;
+            const uint32_t *prow = (const uint32_t *)p16 + jq;
+            int it = 0;
+            for (; it + 16 <= n_it; it += 16) {
+                uint32_t vb[16], pb[16];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) {
+                    vb[k] = vrow[16 * (it + k)];
+                    pb[k] = prow[16 * (it + k)];
+                }
+#pragma unroll
+                for (int k = 0; k < 16; ++k) acc1 = pk_fma_w(vb[k], pb[k], acc1);
+            }
+            for (; it < n_it; ++it) acc1 = pk_fma_w(vrow[16 * it], prow[16 * it], acc1);
+            red[t] = acc1;
+        }
+        __syncthreads();
+    }
+    // the GGML_F16_VEC_REDUCE of output vr_l's 4 accumulators: quad (vr_l, j = 0..3)
+    const int vr_l = (t >> 2) & (RS - 1), j = t & 3;
+    const bool kt = t < 4 * RS;
+    uint32_t acc[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc[k] = red[16 * vr_l + 4 * j + k];
+    const float o = f16x8_reduce_quad(acc);  // every lane active; quad (4 vr_l .. +3) holds output vr_l
+    if (kt && j == 0) a.out[(int64_t)h * HD + ds * RS + vr_l] = bad ? __builtin_nanf("") : o;
+}
+
 // One workgroup per kv group (kq_attn_device.h): the group's cells [0, n_kv) are read
 // once into LDS and serve its n_head/n_head_kv query heads, one wave each.
 template <int HD>
@@ -555,13 +862,16 @@ size_t attn_lds_v(int hd, int n_ctx, int ds = 1, bool ring = false) {
 // Every slice scores every cell, so the K reads grow with the slices: 16 slices at 4096 cells
 // (head_dim 64) measured slower than one workgroup per head (tg4096 894 against 925 tok/s,
 // profiles/r05_attn_split_ab.txt).
-// The split path LDS-DMAs K-cache rows and V rows and stages q / k / v and the rope row
-// with 16-B transfers (attn_dma16): every one of those operands must be 16-B aligned,
-// otherwise the per-head kernel runs.
+// The split path LDS-DMAs whole K-cache rows and V rows (16-B pieces at 16-B offsets from the
+// cache bases: both caches must be 16-B aligned, else the per-head kernel runs) and stages q / k
+// / v and the rope row with 16-B transfers from 4-B aligned f32 vectors: the global side of an
+// LDS-DMA need not be 16-B aligned on this device (the decode graph's staged rope row sits 8 B
+// into its input tensor: every decode-graph test past 256 cells runs that way).
 int attn_slices(const AttnArgs &a) {
-    const uintptr_t mis = (uintptr_t)a.v_cache | (uintptr_t)a.k_cache | (uintptr_t)a.q | (uintptr_t)a.k |
-                          (uintptr_t)a.v | (uintptr_t)a.rope_table;
-    if (attn_impl() != MI355X_ATTN_SPLIT || a.n_ctx <= KQ_ATTN_BATCH_CTX || a.n_ctx % 8 || (mis & 15u))
+    const uintptr_t mis16 = (uintptr_t)a.v_cache | (uintptr_t)a.k_cache;
+    const uintptr_t mis4 = (uintptr_t)a.q | (uintptr_t)a.k | (uintptr_t)a.v | (uintptr_t)a.rope_table;
+    if (attn_impl() != MI355X_ATTN_SPLIT || a.n_ctx <= KQ_ATTN_BATCH_CTX || a.n_ctx % 8 || (mis16 & 15u) ||
+        (mis4 & 3u))
         return 1;
     for (int ds = KQ_ATTN_DSMIN; ds <= 8; ds *= 2)
         if (attn_lds_v(a.head_dim, a.n_ctx, ds) <= 160 * 1024) return ds;
@@ -637,6 +947,80 @@ bool attn_group_ok(const AttnArgs &a, int nwaves) {
 std::atomic<int> g_attn_impl{KQ_ATTN_DEFAULT_IMPL};
 int attn_impl() { return g_attn_impl.load(); }
 
+size_t attn_cells_lds_a(int hd, int gsz) { return (size_t)gsz * hd * 2 + (size_t)hd * 2 + (size_t)ATTN_CHUNK * hd * 2; }
+// B's LDS: the scores region (p16 and the group sums reuse it), red, 96 B of scalars, and RS V
+// rows of 2 n_ctx + VPAD bytes
+int attn_cells_rs(int hd) { return hd == 64 ? KQ_ATTN_CELLS_RS64 : KQ_ATTN_CELLS_RS128; }
+size_t attn_cells_lds_b(int n_ctx, int rs) {
+    return (size_t)n_ctx * 4 + (size_t)rs * 64 + 96 + (size_t)rs * (2 * (size_t)n_ctx + ATTN_CELLS_VPAD);
+}
+
+// The score workspace [n_head][n_ctx] f32: one grow-only buffer per device, allocated outside
+// any stream capture (mi355x_attn_cells_reserve; the backend reserves before it captures). An
+// older, smaller buffer stays allocated: a captured graph may still point at it.
+struct CellsScratch {
+    std::mutex mu;
+    std::vector<std::pair<int, std::pair<void *, size_t>>> cur;  // device -> (buffer, bytes)
+};
+CellsScratch &cells_scratch() {
+    static CellsScratch s;
+    return s;
+}
+void *attn_cells_buffer(size_t bytes, bool may_alloc) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+    CellsScratch &cs = cells_scratch();
+    std::lock_guard<std::mutex> lk(cs.mu);
+    for (auto &e : cs.cur)
+        if (e.first == dev) {
+            if (e.second.second >= bytes) return e.second.first;
+            if (!may_alloc) return nullptr;
+            void *p = nullptr;
+            if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+            e.second = {p, bytes};  // (the old one is kept: graphs may read it)
+            return p;
+        }
+    if (!may_alloc) return nullptr;
+    void *p = nullptr;
+    if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
+    cs.cur.push_back({dev, {p, bytes}});
+    return p;
+}
+
+bool attn_cells_applies(const AttnArgs &a) {
+    const int gsz = a.n_head_kv > 0 ? a.n_head / a.n_head_kv : 0;
+    return attn_impl() == MI355X_ATTN_SPLIT && a.n_ctx > KQ_ATTN_CELLS_MIN && a.n_ctx % ATTN_CHUNK == 0 &&
+           a.n_ctx <= 1024 * ATTN_CELLS_GMAX &&
+           (a.head_dim == 64 || a.head_dim == 128) && gsz >= 1 && gsz <= 16 &&
+           (KQ_ATTN_CELLS_OVER_SPLIT || attn_slices(a) == 1) &&
+           attn_cells_lds_b(a.n_ctx, attn_cells_rs(a.head_dim)) <= 160 * 1024 && ((uintptr_t)a.k_cache & 15u) == 0 &&
+           ((uintptr_t)a.v_cache & 15u) == 0;
+}
+
+// The workspace of a decode attention that will take the two launches, allocated now (callers
+// that capture graphs call this first; an eager launch allocates on its own)
+int attn_cells_reserve(const AttnArgs &a) {
+    if (!attn_cells_applies(a)) return MI355X_OK;
+    return attn_cells_buffer((size_t)a.n_head * a.n_ctx * 4, true) ? MI355X_OK : MI355X_E_WORKSPACE;
+}
+
+template <int HD, int RS>
+int launch_attn_cells_t(const AttnArgs &a, float *ws, hipStream_t s, const char *na, const char *nb) {
+    const int gsz = a.n_head / a.n_head_kv;
+    const size_t la = attn_cells_lds_a(HD, gsz), lb = attn_cells_lds_b(a.n_ctx, RS);
+    const dim3 ga((unsigned)(a.n_ctx / ATTN_CHUNK), (unsigned)a.n_head_kv);
+    const int rc = timed_launch(na, 0.0, kq_attn_cells<HD>, ga, dim3(256), la, s, a, ws);
+    if (rc) return rc;
+    allow_lds((const void *)kq_attn_cells_kqv<HD, HD / RS>, lb);
+    return timed_launch(nb, 0.0, kq_attn_cells_kqv<HD, HD / RS>, dim3((unsigned)(a.n_head * (HD / RS))), dim3(256), lb, s,
+                        a, (const float *)ws);
+}
+int launch_attn_cells(const AttnArgs &a, float *ws, hipStream_t s) {
+    if (a.head_dim == 64)
+        return launch_attn_cells_t<64, KQ_ATTN_CELLS_RS64>(a, ws, s, "kq::kq_attn_cells<64>", "kq::kq_attn_cells_kqv<64>");
+    return launch_attn_cells_t<128, KQ_ATTN_CELLS_RS128>(a, ws, s, "kq::kq_attn_cells<128>", "kq::kq_attn_cells_kqv<128>");
+}
+
 int launch_attn(const AttnArgs &a, hipStream_t s) {
     const double bytes = 0;  // context-dependent; not a roofline kernel
     const int nw = attn_group_waves(a);
@@ -671,6 +1055,13 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
         KQ_ATTN_SPLIT_LAUNCH(128, 8)
 #undef KQ_ATTN_SPLIT_LAUNCH
         return MI355X_E_INVAL;
+    }
+    if (attn_cells_applies(a)) {  // long caches past the output split: KQ split over cells, two launches
+        hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
+        const bool capturing = hipStreamIsCapturing(s, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
+        void *ws = attn_cells_buffer((size_t)a.n_head * a.n_ctx * 4, !capturing);
+        if (ws) return launch_attn_cells(a, (float *)ws, s);
+        // (captured without a reserved workspace: the one-launch kernel below)
     }
     if (KQ_ATTN_KDMA1 && a.n_ctx <= KQ_ATTN_BATCH_CTX && a.n_ctx % 8 == 0 && ((uintptr_t)a.v_cache & 15u) == 0 &&
         ((uintptr_t)a.k_cache & 15u) == 0) {

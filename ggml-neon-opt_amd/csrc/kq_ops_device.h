@@ -291,33 +291,123 @@ __device__ __forceinline__ double seq_sum_lds(const double *p, int n) {
     return sum;
 }
 
+#ifndef KQ_SEQ_SUM_WAVE
+#define KQ_SEQ_SUM_WAVE 0  // soft_max's in-order fallback: seq_sum_wave (0: seq_sum_lds, one dependent add per term)
+#endif
+// ggml's in-order `sum += g[i]` over n LDS doubles g[i] >= 0 (or non-finite), bit for bit, by
+// one whole wave, 64 terms a round instead of one dependent add per term (soft_max's group
+// sums; not for signed terms). While the running sum s stays in one binade [2^E, 2^(E+1)), s
+// is a multiple of u = 2^(E-52) and s + g rounds to s + RN(g / u) u whatever s's other bits
+// are, unless g / u is an exact tie (the even neighbour then depends on s). Lane l takes term
+// i0 + l: RN(g / u) as an integer, an inclusive scan over the lanes (DPP; exact below 2^53,
+// >= 2^53 when it is not), and the first lane whose s would reach 2^(E+1), or that holds a tie
+// or a non-finite term, is added as is after the exact sum of the lanes before it; the next
+// round starts after it. A sum that changes binade too often finishes in order.
+// (tests/test_ops_oracle.py mirrors this in numpy against the plain loop.)
+template <int CTRL, int ROWS>
+__device__ __forceinline__ double dpp_f64_or0(double v) {  // lanes without a source: +0
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)b, CTRL, ROWS, 0xF, false);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_update_dpp(0, (int)(uint32_t)(b >> 32), CTRL, ROWS, 0xF, false);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+__device__ __forceinline__ double seq_sum_wave(const double *g, int n, int lane) {
+    double s = 0.0;
+    int i0 = 0;
+    const int max_rounds = (n >> 6) + 48;
+    for (int round = 0; i0 < n && round < max_rounds; ++round) {
+        if (!(s < INFINITY)) break;  // inf / NaN: the rest in order
+        const int len = n - i0 < 64 ? n - i0 : 64;
+        const double v = lane < len ? g[i0 + lane] : 0.0;
+        int k;  // the lane added as is
+        if (s == 0.0) {  // no binade yet: zeros add nothing, the first nonzero term as is
+            const uint64_t bl = __ballot(v != 0.0);
+            if (bl == 0) {
+                i0 += len;
+                continue;
+            }
+            k = __builtin_ctzll(bl);
+        } else {
+            const int ex = (int)((__double_as_longlong(s) >> 52) & 0x7ff);  // s normal: >= 2^-149
+            const double sc = __longlong_as_double((long long)(2098 - ex) << 52);  // 1 / u
+            const double uu = __longlong_as_double((long long)(ex - 52) << 52);    // u
+            const double su = s * sc;                                              // in [2^52, 2^53)
+            const double x = v * sc;  // exact (a power of two)
+            const bool fin = x < INFINITY;
+            const double xf = fin ? x : 0.0;
+            bool fl = !fin || xf - __builtin_floor(xf) == 0.5;
+            double q = __builtin_rint(xf);
+            q += dpp_f64_or0<0x111, 0xF>(q);  // row_shr:1
+            q += dpp_f64_or0<0x112, 0xF>(q);  // row_shr:2
+            q += dpp_f64_or0<0x114, 0xF>(q);  // row_shr:4
+            q += dpp_f64_or0<0x118, 0xF>(q);  // row_shr:8
+            q += dpp_f64_or0<0x142, 0xA>(q);  // row_bcast:15 (rows 1, 3)
+            q += dpp_f64_or0<0x143, 0xC>(q);  // row_bcast:31 (rows 2, 3)
+            fl = lane < len && (fl || su + q >= 0x1p53);
+            const uint64_t bl = __ballot(fl);
+            if (bl == 0) {
+                s = (su + readlane_f64(q, 63)) * uu;  // (lanes >= len add 0)
+                i0 += len;
+                continue;
+            }
+            k = __builtin_ctzll(bl);
+            s = (su + (k > 0 ? readlane_f64(q, k - 1) : 0.0)) * uu;
+        }
+        s += readlane_f64(v, k);
+        i0 += k + 1;
+    }
+    for (; i0 < n; ++i0) s += g[i0];
+    return s;
+}
+
 // soft_max's double sum of the n vaddvq group sums g[0..n) (LDS doubles, each a float
 // (e0 + e1) + (e2 + e3) >= 0, e <= 1: every g <= 4), with the bits of ggml's in-order
 // `sum += (ggml_float)g` (ggml_vec_soft_max_f32), computed by one whole wave.
-// Every nonzero float g is a multiple of 2^(e(g) - 23) (e: its unbiased exponent), so
-// every partial sum of such terms, in ANY order, is a multiple of 2^(e_min - 23) no
-// larger than 4n: exactly representable in double while 4n < 2^(e_min + 30), i.e.
-// e_min >= floor(log2(4n)) - 29 (n_kv 128: g >= 2^-22). Then the in-order sum never
-// rounds and equals the exact sum, which a tree over the wave computes in 6 steps
-// instead of n dependent f64 adds; any smaller, subnormal or non-finite g (a very
-// peaked soft_max) takes the in-order sum itself.
+// Every nonzero float g is a multiple of 2^G(g) (G: the exponent of its last mantissa bit,
+// max(biased exponent, 1) - 150), so every partial sum of such terms, in ANY order, is a
+// multiple of 2^Gmin no larger than the total T: exactly representable in double while
+// T < 2^(Gmin + 53). Then the in-order sum never rounds and equals the exact sum, which a tree
+// over the wave computes in 6 steps instead of n dependent f64 adds. The test uses the tree's
+// own total S (within 2^-48 of T, so S <= (1 - 2^-40) 2^(Gmin + 53) proves T < 2^(Gmin + 53)):
+// exact whenever the smallest group sum is within ~2^-30 of the total (round 6; rounds 1-5
+// bounded T by 4n, 2^-29 of it, up to 9 binades stricter at 1024 groups). A more peaked
+// soft_max, or a non-finite g, takes the in-order sum itself.
+struct SumExact {
+    double part = 0.0;  // this lane's terms, any order
+    int gmin = 1 << 20; // min G over its nonzero terms (none: 2^20)
+    bool bad = false;   // a non-finite term
+    __device__ __forceinline__ void add(float gf) {
+        const int ef = (__float_as_int(gf) >> 23) & 0xff;
+        bad = bad || ef == 255;
+        const int G = (ef > 1 ? ef : 1) - 150;
+        gmin = gf != 0.0f && G < gmin ? G : gmin;
+        part += (double)gf;
+    }
+};
+// the bound test for a total s of terms with min G gmin: true = every partial sum is exact
+__device__ __forceinline__ bool sum_exact_ok(double s, int gmin, bool bad) {
+    if (bad) return false;
+    if (gmin >= (1 << 20)) return true;  // every term zero
+    return s <= __longlong_as_double((long long)(gmin + 53 + 1023) << 52) * (1.0 - 0x1p-40);
+}
+__device__ __forceinline__ int wave_imin(int v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const int y = __shfl_xor(v, o, 64);
+        v = y < v ? y : v;
+    }
+    return v;
+}
 __device__ __forceinline__ double softmax_group_sum(const double *g, int n, int lane) {
     if (n <= 0) return 0.0;
-    const int thr = (31 - __builtin_clz((unsigned)(4 * n))) - 29;
-    double part = 0.0;
-    bool ok = true;
-    for (int i = lane; i < n; i += 64) {
-        const double v = g[i];
-        const int ef = (__float_as_int((float)v) >> 23) & 0xff;  // (float)v is exact: v holds a float
-        ok = ok && (v == 0.0 || (ef != 0 && ef != 255 && ef - 127 >= thr));
-        part += v;  // exact when ok (a subset's sum)
-    }
-    if (__all(ok)) {
+    SumExact se;
+    for (int i = lane; i < n; i += 64) se.add((float)g[i]);  // (float)g is exact: g holds a float
+    double part = se.part;
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
-        return part;
-    }
-    return seq_sum_lds(g, n);
+    for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
+    const double p0 = readlane_f64(part, 0);  // (one value for the whole wave's decision)
+    if (sum_exact_ok(p0, wave_imin(se.gmin), __any(se.bad))) return p0;
+    return KQ_SEQ_SUM_WAVE ? seq_sum_wave(g, n, lane) : seq_sum_lds(g, n);
 }
 
 }  // namespace kq

@@ -690,7 +690,7 @@ __device__ __forceinline__ void rows_dyn_body(const RowsArgs &a, uint8_t *smem, 
     static_assert(D >= 2 && D <= 4, "vm_wait_k covers 3 steps in flight");
     const int nb = a.nb, U = a.dyn_u, P = a.dyn_p, bR = a.bR;
     const int nwv = __builtin_amdgcn_readfirstlane((int)(blockDim.x >> 6));
-    const int G = (int)gridDim.x, b = (int)blockIdx.x;
+    const int b = (int)blockIdx.x;
     const int q = lane >> 2, s = lane & 3;
     uint8_t *const ring = smem + L.ring + wave * L.ring_stride;
     uint8_t *const ring_end = ring + D * SLOT;

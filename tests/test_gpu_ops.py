@@ -179,6 +179,59 @@ def test_attn_decode_long_random_cache(dev, O, attn_impl, hd, nh, nkv, n_ctx):
     assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
 
 
+@pytest.mark.parametrize("hd,nh,nkv,n_ctx,qs", [(64, 32, 4, 4096, 2.0), (128, 32, 8, 4096, 2.0), (64, 8, 2, 6144, 2.0),
+                                                 (128, 16, 2, 3072, 2.0), (64, 32, 4, 4096, 40.0), (128, 32, 8, 4096, 40.0)])
+def test_attn_decode_cells_split(dev, O, hd, nh, nkv, n_ctx, qs):
+    """Caches past what the output split's LDS holds (round 6): the head's KQ split over cells in
+    two launches (kq_attn_cells scores 64-cell chunks of a kv group for all its heads into a
+    workspace and stores the new cell; kq_attn_cells_kqv runs soft_max and KQV per output
+    slice). Every cell random, positions across the whole cache: bit-exact with the oracle,
+    both caches too, and the launch names show the two kernels ran. q scaled by 2 (group sums
+    on both sides of the exact-tree bound) and by 40 (very peaked: soft_max's in-order sum,
+    seq_sum_wave, with many binade changes and exact zeros)."""
+    import torch
+    import ggml_mi355x as g
+    prev = g.attn_impl(2)  # split (the default)
+    try:
+        rng = np.random.default_rng(n_ctx + 3 * hd)
+        kvw = nkv * hd
+        tab = g.rope_table(n_ctx, hd, 10000.0, 1.0, device=dev)
+        tref = O.rope_table(n_ctx, hd, 10000.0)
+        kc_ref = rng.standard_normal((n_ctx, kvw)).astype(np.float16).view(np.uint16)
+        vc_ref = rng.standard_normal((kvw, n_ctx)).astype(np.float16).view(np.uint16)
+        kc = torch.from_numpy(kc_ref.view(np.int16).copy()).to(dev)
+        vc = torch.from_numpy(vc_ref.view(np.int16).copy()).to(dev)
+        scale = float(np.float32(1.0) / np.sqrt(np.float32(hd)))
+        positions = [0, 1, 31, 32, 63, 64, 65, 1000, n_ctx // 2 + 7, n_ctx - 65, n_ctx - 64, n_ctx - 9, n_ctx - 1]
+        for i, p in enumerate(positions):
+            q = (rng.standard_normal(nh * hd) * qs).astype(np.float32)
+            k = (rng.standard_normal(kvw) * 2).astype(np.float32)
+            v = rng.standard_normal(kvw).astype(np.float32)
+            pos = torch.tensor([p], dtype=torch.int32, device=dev)
+            if i == 0:
+                g.timing_enable(True)
+            got = g.attn_decode(t(q, dev), t(k, dev), t(v, dev), pos, tab[p].contiguous(), kc, vc, nh, nkv, hd, scale,
+                                rope_row=True).cpu().numpy()
+            if i == 0:
+                names = [r[0] for r in g.timing_read()]
+                g.timing_enable(False)
+                assert any("kq_attn_cells<" in n for n in names) and any("kq_attn_cells_kqv" in n for n in names), names
+            ref = O.attn_decode(O.rope(q, hd, hd, p, tref), O.rope(k, hd, hd, p, tref), v, kc_ref, vc_ref, p, nh, nkv,
+                                hd, scale)
+            assert bits_equal(got, ref), (p, first_mismatch(got, ref))
+        assert (kc.cpu().numpy().view(np.uint16) == kc_ref).all()
+        assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
+        # a position outside the cache: NaN, caches untouched
+        x = torch.ones(nh * hd, device=dev)
+        out = g.attn_decode(x, x[:kvw], x[:kvw], torch.tensor([n_ctx], dtype=torch.int32, device=dev), tab, kc, vc,
+                            nh, nkv, hd, scale)
+        assert torch.isnan(out).all()
+        assert (kc.cpu().numpy().view(np.uint16) == kc_ref).all()
+        assert (vc.cpu().numpy().view(np.uint16) == vc_ref).all()
+    finally:
+        g.attn_impl(prev)
+
+
 @pytest.mark.parametrize("qscale", [0.05, 2.0, 40.0], ids=["flat", "normal", "peaked"])
 def test_attn_softmax_sum_tree_and_fallback(dev, O, attn_impl, qscale):
     """soft_max's double sum runs as a wave tree where every partial sum is exact (then it

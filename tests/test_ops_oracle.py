@@ -311,3 +311,125 @@ def test_get_rows_q5K_matches_numpy_restatement(O):
                     ref.append(N.fma_f32(np.full(32, d1, np.float32), q.astype(np.float32), np.full(32, -m1, np.float32)))
         ref = np.concatenate(ref)
         assert (got[r].view(np.uint32) == ref.view(np.uint32)).all(), r
+
+
+def _seq_sum_wave_mirror(g):
+    """numpy mirror of seq_sum_wave (csrc/kq_ops_device.h): 64 terms a round, one per lane, each
+    RN(g / u) in ulp units u of the running sum's binade, an in-order scan over the lanes, the
+    first lane that reaches the next binade or holds a tie or a non-finite term added as is."""
+    import math
+    n = len(g)
+    s, i0, rounds = 0.0, 0, 0
+    while i0 < n and rounds < (n >> 6) + 48:
+        rounds += 1
+        if not s < math.inf:
+            break
+        ln = min(64, n - i0)
+        v = np.array(g[i0:i0 + ln], np.float64)
+        if s == 0.0:
+            nz = np.nonzero(v != 0.0)[0]
+            if len(nz) == 0:
+                i0 += ln
+                continue
+            k = int(nz[0])
+        else:
+            ex = int((np.float64(s).view(np.int64) >> 52) & 0x7FF)
+            sc = np.int64((2098 - ex) << 52).view(np.float64)
+            uu = np.int64((ex - 52) << 52).view(np.float64)
+            su = s * sc
+            with np.errstate(invalid="ignore", over="ignore"):
+                x = v * sc
+                fin = x < np.inf
+                xf = np.where(fin, x, 0.0)
+                fl = ~fin | (xf - np.floor(xf) == 0.5)
+                q = np.cumsum(np.where(fin, np.rint(xf), x))
+                fl |= su + q >= 2.0 ** 53
+            if not fl.any():
+                s = float((su + q[-1]) * uu)
+                i0 += ln
+                continue
+            k = int(np.argmax(fl))
+            s = float((su + (q[k - 1] if k > 0 else 0.0)) * uu)
+        s += v[k]
+        i0 += k + 1
+    for i in range(i0, n):
+        s += g[i]
+    return s
+
+
+def test_seq_sum_wave_mirror_matches_in_order():
+    """The wave-parallel in-order double sum (seq_sum_wave) gives the plain loop's bits on
+    soft_max-like group sums from flat to very peaked, leading zeros, exact ties against the
+    running sum's ulp, and non-finite terms (mirror of the device algorithm; the GPU side is
+    tests/test_gpu_ops.py's peaked soft_max cases)."""
+    rng = np.random.default_rng(11)
+    cases = []
+    for n in (1, 2, 7, 63, 64, 65, 200, 1000, 1024, 1537):
+        for spread in (1.0, 8.0, 30.0, 90.0):
+            w = rng.standard_normal(4 * n).astype(np.float32) * np.float32(spread)
+            e = np.exp((w - w.max()).astype(np.float64)).astype(np.float32).reshape(n, 4)
+            gs = ((e[:, 0] + e[:, 1]) + (e[:, 2] + e[:, 3])).astype(np.float32)
+            cases.append(gs.astype(np.float64))
+    z = np.zeros(300)
+    z[150:] = rng.random(150) * 1e-30
+    cases.append(z)
+    t = np.zeros(130)
+    t[0] = 1.0
+    t[1:] = 2.0 ** -53  # every add an exact tie against s = 1 (ulp 2^-52)
+    cases.append(t)
+    t2 = np.full(129, 3.0 * 2.0 ** -53)
+    t2[0] = 1.0
+    cases.append(t2)
+    inf = np.ones(100)
+    inf[70] = np.inf
+    cases.append(inf)
+    nan = np.ones(100)
+    nan[3] = np.nan
+    cases.append(nan)
+    cases.append(np.zeros(0))
+    for g in cases:
+        ref = 0.0
+        for v in g:
+            ref += v
+        got = _seq_sum_wave_mirror(list(g))
+        assert np.float64(got).tobytes() == np.float64(ref).tobytes() or (np.isnan(got) and np.isnan(ref)), (len(g), got, ref)
+
+
+def test_softmax_sum_bound_by_total():
+    """Round 6's exactness test (sum_exact_ok, kq_ops_device.h): with G the exponent of a float
+    term's last mantissa bit (max(biased exponent, 1) - 150) and S any-order total, S <= (1 -
+    2^-40) 2^(Gmin + 53) proves every partial sum exact, so the wave tree equals ggml's in-order
+    sum; the test admits far more peaked soft_max rows than rounds 1-5's 4n bound."""
+    import math
+    rng = np.random.default_rng(5)
+    admitted_new = admitted_old = 0
+    for trial in range(400):
+        n = int(rng.integers(16, 1500))
+        spread = float(rng.choice([2.0, 4.0, 6.0, 9.0]))
+        w = (rng.standard_normal(4 * n) * spread).astype(np.float32)
+        e = np.exp((w - w.max()).astype(np.float64)).astype(np.float32).reshape(n, 4)
+        g = ((e[:, 0] + e[:, 1]) + (e[:, 2] + e[:, 3])).astype(np.float32)
+        nz = g[g != 0]
+        ef = (nz.view(np.uint32) >> 23) & 0xFF
+        gmin = int((np.maximum(ef, 1).astype(np.int64) - 150).min()) if len(nz) else 1 << 20
+        d = g.astype(np.float64)
+        perm = rng.permutation(n)
+        tree = d[perm].copy()
+        while len(tree) > 1:
+            if len(tree) % 2:
+                tree = np.append(tree, 0.0)
+            tree = tree[0::2] + tree[1::2]
+        st = float(tree[0])
+        ok_new = gmin >= (1 << 20) or st <= math.ldexp(1.0 - 2.0 ** -40, gmin + 53)
+        thr = int(math.floor(math.log2(4 * n))) - 29
+        ok_old = all(v == 0 or (((int(np.float32(v).view(np.uint32)) >> 23) & 0xFF) - 127 >= thr and
+                                ((int(np.float32(v).view(np.uint32)) >> 23) & 0xFF) != 0) for v in g)
+        assert not ok_old or ok_new  # the new test admits everything the old one did
+        seq = 0.0
+        for v in d:
+            seq += v
+        if ok_new:
+            admitted_new += 1
+            assert st == seq == math.fsum(d)
+        admitted_old += ok_old
+    assert admitted_new > admitted_old
