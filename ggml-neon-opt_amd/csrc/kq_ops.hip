@@ -248,6 +248,9 @@ constexpr int ATTN_CHUNK = 64;
 #ifndef KQ_ATTN_CELLS_OVER_SPLIT
 #define KQ_ATTN_CELLS_OVER_SPLIT 0  // experiment builds: the two launches also where the output split fits
 #endif
+#ifndef KQ_ATTN_CELLS_SLICES
+#define KQ_ATTN_CELLS_SLICES 8  // ... and where it needs this many slices (tg3072 +5 %, 8B tg2048 +5.5 %; 4: equal)
+#endif
 #ifndef KQ_ATTN_CELLS_MIN
 #define KQ_ATTN_CELLS_MIN 1024  // caches of more cells than this take the two launches when the output split does not fit
 #endif
@@ -992,7 +995,7 @@ bool attn_cells_applies(const AttnArgs &a) {
     return attn_impl() == MI355X_ATTN_SPLIT && a.n_ctx > KQ_ATTN_CELLS_MIN && a.n_ctx % ATTN_CHUNK == 0 &&
            a.n_ctx <= 1024 * ATTN_CELLS_GMAX &&
            (a.head_dim == 64 || a.head_dim == 128) && gsz >= 1 && gsz <= 16 &&
-           (KQ_ATTN_CELLS_OVER_SPLIT || attn_slices(a) == 1) &&
+           (KQ_ATTN_CELLS_OVER_SPLIT || attn_slices(a) == 1 || attn_slices(a) >= KQ_ATTN_CELLS_SLICES) &&
            attn_cells_lds_b(a.n_ctx, attn_cells_rs(a.head_dim)) <= 160 * 1024 && ((uintptr_t)a.k_cache & 15u) == 0 &&
            ((uintptr_t)a.v_cache & 15u) == 0;
 }
@@ -1040,7 +1043,7 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     // the register prefetch, which issues V with the position itself.
     AttnArgs b = a;
     const int ds = attn_slices(a);
-    if (ds > 1) {
+    if (ds > 1 && !attn_cells_applies(a)) {  // (the two launches where the split would need its widest form)
         const size_t lds = attn_lds_v(a.head_dim, a.n_ctx, ds);
         const dim3 grid((unsigned)(a.n_head * ds));
 #define KQ_ATTN_SPLIT_LAUNCH(HD, DS)                                                                        \
