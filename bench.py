@@ -1170,14 +1170,14 @@ def main():
             # the same launch kind from the committed rocprofv3 passes of this bench command:
             # graph-replayed duration (kernel trace) and HBM read (FETCH_SIZE x2, the gfx950
             # correction), per launch; frac_rocprof = the roofline at the replayed duration
-            prof = os.path.join(ROOT, "profiles", "r05f_token_summary.json")
+            prof = os.path.join(ROOT, "profiles", "r06f_token_summary.json")
             if os.path.exists(prof):
                 with open(prof) as f:
                     pk = json.load(f).get("by_kind", {}).get(roof["launch_kind"])
                 if pk:
                     roof["traffic"] = round(pk["hbm_read_per_launch"], 0) if pk.get("hbm_read_per_launch") else None
                     roof["traffic_unit"] = "bytes/launch (HBM read, rocprofv3 FETCH_SIZE x2)"
-                    roof["rocprof_source"] = "profiles/r05f_token_summary.json"
+                    roof["rocprof_source"] = "profiles/r06f_token_summary.json"
                     roof["rocprof_us_per_launch"] = round(pk["us_per_launch"], 3)
                     ach_r = roof["bytes_per_launch"] / (pk["us_per_launch"] * 1e-6) / 1e9
                     roof["frac_rocprof"] = round(ach_r / HBM_PEAK_GBS, 4)
