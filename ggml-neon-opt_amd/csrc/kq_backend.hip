@@ -1526,7 +1526,7 @@ int mi355x_backend_graph_compute(mi355x_backend_t b, mi355x_tensor *const *nodes
         mi355x_attn_desc d = {};
         attn_desc_of(t, d);
         kq::AttnArgs a = {};
-        if (kq::attn_args_from(&d, a) == MI355X_OK && kq::attn_cells_reserve(a) != MI355X_OK) return MI355X_E_WORKSPACE;
+        if (kq::attn_args_from(&d, a) == MI355X_OK && kq::attn_cells_reserve(a, b->stream) != MI355X_OK) return MI355X_E_WORKSPACE;
     }
     if (!use_graph) return enqueue(b, nodes, launches);
     std::vector<uint64_t> key = graph_key_of(nodes, n_nodes);

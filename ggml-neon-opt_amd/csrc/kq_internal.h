@@ -53,7 +53,7 @@ int launch_rms_norm(const float *x, const float *w, float *y, int64_t n, int64_t
 int launch_binary(int op, const float *a, const float *b, float *y, int64_t n, hipStream_t s,
                   int64_t nb = 0);  // 0 add, 1 mul; b of nb elements repeated (0: nb = n)
 int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s);
-int attn_cells_reserve(const AttnArgs &a);  // long-cache attention workspace, before any capture
+int attn_cells_reserve(const AttnArgs &a, hipStream_t stream);  // long-cache attention workspace (per stream), before any capture
 bool attn_prompt_q8_ok(const AttnArgs &a);  // the group kernel can write a.q8_out
 // prefill (ne11 >= 16) pieces, for the backend's shared-activation runs
 bool mmq_applies(int type, const void *w, int64_t N, size_t row_stride, int64_t M);

@@ -958,35 +958,42 @@ size_t attn_cells_lds_b(int n_ctx, int rs) {
     return (size_t)n_ctx * 4 + (size_t)rs * 64 + 96 + (size_t)rs * (2 * (size_t)n_ctx + ATTN_CELLS_VPAD);
 }
 
-// The score workspace [n_head][n_ctx] f32: one grow-only buffer per device, allocated outside
-// any stream capture (mi355x_attn_cells_reserve; the backend reserves before it captures). An
-// older, smaller buffer stays allocated: a captured graph may still point at it.
+// The score workspace [n_head][n_ctx] f32: one grow-only buffer per (device, stream), so two
+// streams' attentions never share one, allocated outside any stream capture (the backend
+// reserves before it captures: attn_cells_reserve). An older, smaller buffer stays allocated:
+// a captured graph may still point at it.
 struct CellsScratch {
+    struct Entry {
+        int dev;
+        hipStream_t stream;
+        void *p;
+        size_t bytes;
+    };
     std::mutex mu;
-    std::vector<std::pair<int, std::pair<void *, size_t>>> cur;  // device -> (buffer, bytes)
+    std::vector<Entry> cur;
 };
 CellsScratch &cells_scratch() {
     static CellsScratch s;
     return s;
 }
-void *attn_cells_buffer(size_t bytes, bool may_alloc) {
+void *attn_cells_buffer(size_t bytes, hipStream_t stream, bool may_alloc) {
     int dev = 0;
     if (hipGetDevice(&dev) != hipSuccess) return nullptr;
     CellsScratch &cs = cells_scratch();
     std::lock_guard<std::mutex> lk(cs.mu);
     for (auto &e : cs.cur)
-        if (e.first == dev) {
-            if (e.second.second >= bytes) return e.second.first;
+        if (e.dev == dev && e.stream == stream) {
+            if (e.bytes >= bytes) return e.p;
             if (!may_alloc) return nullptr;
             void *p = nullptr;
             if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-            e.second = {p, bytes};  // (the old one is kept: graphs may read it)
+            e.p = p, e.bytes = bytes;  // (the old one is kept: graphs may read it)
             return p;
         }
     if (!may_alloc) return nullptr;
     void *p = nullptr;
     if (hipMalloc(&p, bytes) != hipSuccess) return nullptr;
-    cs.cur.push_back({dev, {p, bytes}});
+    cs.cur.push_back({dev, stream, p, bytes});
     return p;
 }
 
@@ -1002,9 +1009,9 @@ bool attn_cells_applies(const AttnArgs &a) {
 
 // The workspace of a decode attention that will take the two launches, allocated now (callers
 // that capture graphs call this first; an eager launch allocates on its own)
-int attn_cells_reserve(const AttnArgs &a) {
+int attn_cells_reserve(const AttnArgs &a, hipStream_t stream) {
     if (!attn_cells_applies(a)) return MI355X_OK;
-    return attn_cells_buffer((size_t)a.n_head * a.n_ctx * 4, true) ? MI355X_OK : MI355X_E_WORKSPACE;
+    return attn_cells_buffer((size_t)a.n_head * a.n_ctx * 4, stream, true) ? MI355X_OK : MI355X_E_WORKSPACE;
 }
 
 template <int HD, int RS>
@@ -1062,7 +1069,7 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     if (attn_cells_applies(a)) {  // long caches past the output split: KQ split over cells, two launches
         hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
         const bool capturing = hipStreamIsCapturing(s, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
-        void *ws = attn_cells_buffer((size_t)a.n_head * a.n_ctx * 4, !capturing);
+        void *ws = attn_cells_buffer((size_t)a.n_head * a.n_ctx * 4, s, !capturing);
         if (ws) return launch_attn_cells(a, (float *)ws, s);
         // (captured without a reserved workspace: the one-launch kernel below)
     }

@@ -232,6 +232,53 @@ def test_attn_decode_cells_split(dev, O, hd, nh, nkv, n_ctx, qs):
         g.attn_impl(prev)
 
 
+def test_attn_decode_cells_two_streams(dev, O):
+    """The split over cells keeps its score workspace per (device, stream): two decoders'
+    long-cache attentions enqueued on two streams at once, interleaved and unsynchronized,
+    each bit-exact with the oracle (one shared workspace would mix their scores)."""
+    import torch
+    import ggml_mi355x as g
+    prev = g.attn_impl(2)
+    try:
+        hd, nh, nkv, n_ctx = 64, 32, 4, 4096
+        kvw = nkv * hd
+        tab = g.rope_table(n_ctx, hd, 10000.0, 1.0, device=dev)
+        tref = O.rope_table(n_ctx, hd, 10000.0)
+        scale = float(np.float32(1.0) / np.sqrt(np.float32(hd)))
+        streams = [torch.cuda.Stream(device=dev), torch.cuda.Stream(device=dev)]
+        state = []
+        for si in range(2):
+            rng = np.random.default_rng(77 + si)
+            kc_ref = rng.standard_normal((n_ctx, kvw)).astype(np.float16).view(np.uint16)
+            vc_ref = rng.standard_normal((kvw, n_ctx)).astype(np.float16).view(np.uint16)
+            state.append(dict(rng=rng, kc_ref=kc_ref, vc_ref=vc_ref,
+                              kc=torch.from_numpy(kc_ref.view(np.int16).copy()).to(dev),
+                              vc=torch.from_numpy(vc_ref.view(np.int16).copy()).to(dev), outs=[]))
+        torch.cuda.synchronize()
+        positions = [4095, 2000, 3000, 17, 4094, 1500]
+        for p in positions:
+            for si, st in enumerate(state):
+                q = (st["rng"].standard_normal(nh * hd) * 2).astype(np.float32)
+                k = (st["rng"].standard_normal(kvw) * 2).astype(np.float32)
+                v = st["rng"].standard_normal(kvw).astype(np.float32)
+                with torch.cuda.stream(streams[si]):
+                    pos = torch.tensor([p], dtype=torch.int32, device=dev)
+                    got = g.attn_decode(t(q, dev), t(k, dev), t(v, dev), pos, tab[p].contiguous(), st["kc"], st["vc"], nh,
+                                        nkv, hd, scale, rope_row=True, stream=streams[si].cuda_stream)
+                st["outs"].append((p, q, k, v, got))
+        torch.cuda.synchronize()
+        for st in state:
+            for p, q, k, v, got in st["outs"]:
+                ref = O.attn_decode(O.rope(q, hd, hd, p, tref), O.rope(k, hd, hd, p, tref), v, st["kc_ref"], st["vc_ref"],
+                                    p, nh, nkv, hd, scale)
+                gn = got.cpu().numpy()
+                assert bits_equal(gn, ref), (p, first_mismatch(gn, ref))
+            assert (st["kc"].cpu().numpy().view(np.uint16) == st["kc_ref"]).all()
+            assert (st["vc"].cpu().numpy().view(np.uint16) == st["vc_ref"]).all()
+    finally:
+        g.attn_impl(prev)
+
+
 @pytest.mark.parametrize("qscale", [0.05, 2.0, 40.0], ids=["flat", "normal", "peaked"])
 def test_attn_softmax_sum_tree_and_fallback(dev, O, attn_impl, qscale):
     """soft_max's double sum runs as a wave tree where every partial sum is exact (then it
