@@ -264,6 +264,7 @@ struct AttnArgs {
                       // for the next GEMM (row i's superblock b at (i*nb + b)*304), or null
     int v_lds;        // kq_attn_decode only, set by launch_attn: the head's V rows are staged in
                       // LDS by LDS-DMA as soon as the position is known (attn_lds_v bytes)
+    int n_tok;        // prompt batch (kq_attn_prompt_group), set by launch_attn_prompt: its tokens
 };
 
 // Decode attention fused with the o-proj GEMV (kq_attn_oproj.hip): workgroup (s, rb) runs the

@@ -681,159 +681,242 @@ __global__ void __launch_bounds__(256) kq_attn_prompt(const AttnArgs a) {
     }
 }
 
-// The same per-query arithmetic with one workgroup per (kv group, token): the group's gsz
-// query heads share every K row and V chunk the workgroup loads (1/gsz of the cache reads
-// of kq_attn_prompt), each head keeping its own scores, soft_max and accumulators.
+// The same per-query arithmetic with one workgroup per (kv group, TPW tokens): the group's gsz
+// query heads of TPW tokens share every K row and V chunk the workgroup loads (1/(gsz TPW) of
+// the cache reads of kq_attn_prompt) and every barrier; each (token, head) row keeps its own
+// scores, soft_max and accumulators.
 constexpr int PROMPT_GMAX = 8;  // query heads per kv group handled by kq_attn_prompt_group
+#ifndef KQ_PROMPT_SUMLANES
+#define KQ_PROMPT_SUMLANES 1  // soft_max's in-order fallback sums: one lane per row, all rows at once
+#endif
+#ifndef KQ_PROMPT_TPW
+#define KQ_PROMPT_TPW 1  // tokens per workgroup where the LDS holds them (2: measured 1.37x slower, profiles/r06_prompt_ab.txt)
+#endif
 #ifndef KQ_PROMPT_DIAG
 #define KQ_PROMPT_DIAG 0  // timing-only builds: 1 no KQ dots, 2 no soft_max sums, 4 no KQV
 #endif
 
-// LDS: q16 [gsz][HD] | w [gsz][n_ctx] f32 | p16 [gsz][n_ctx] | scal [gsz][4] f32, with
-//      gsum [gsz][n_ctx/4] f64 over p16 (same bytes; read before p16 is written); the KQV
+// LDS: q16 [R][HD] | w [R][n_ctx] f32 | p16 [R][n_ctx] | scal [R][4] f32 (R = rows = gsz TPW),
+//      with gsum [R][n_ctx/4] f64 over p16 (same bytes; read before p16 is written); the KQV
 //      accumulators are reduced across lanes, not in LDS
-size_t attn_prompt_group_lds(int hd, int n_ctx, int gsz) {
-    return (size_t)gsz * ((size_t)2 * hd + (size_t)n_ctx * 6 + 16);
+size_t attn_prompt_group_lds(int hd, int n_ctx, int rows) {
+    return (size_t)rows * ((size_t)2 * hd + (size_t)n_ctx * 6 + 16);
 }
 
 // GSZ: the group size fixed at compile time (4: Llama-3-8B, 8: TinyLlama / 70B), or 0 for
 // any gsz <= PROMPT_GMAX: with it fixed, the per-head loops have no exits and hipcc keeps
 // several LDS reads of KQV in flight (with the run-time exit it waited lgkmcnt(0) before
-// every probability read).
-template <int HD, int GSZ = 0>
+// every probability read). Every per-token loop runs over a compile-time TPW (unrolled: no
+// array indexed at run time).
+template <int HD, int GSZ = 0, int TPW = 1>
 __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
     constexpr int KV4 = HD / 8;
     constexpr int ITEMS = HD * 4 / 256;
     constexpr int GM = GSZ > 0 ? GSZ : PROMPT_GMAX;  // heads the unrolled loops cover
     extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-    // the latest tokens (the most cells) are dispatched first: a shorter tail
-    const int g = blockIdx.x, i = (int)gridDim.y - 1 - (int)blockIdx.y, t = threadIdx.x;
+    // tokens [i0, i0 + TPW), the latest first (the most cells: a shorter tail); i0 + tt < 0: none
+    const int g = blockIdx.x, t = threadIdx.x;
+    const int i0 = a.n_tok - TPW * (1 + (int)blockIdx.y);
     const int gsz = GSZ > 0 ? GSZ : a.n_head / a.n_head_kv;  // <= PROMPT_GMAX (host check)
     const int kvw = a.n_head_kv * HD;
-    const int64_t qrow = (int64_t)i * a.n_head * HD;
-    const int pos_in = a.pos[i];
-    const bool bad = pos_in < 0 || pos_in >= a.n_ctx;
-    const int pos = bad ? 0 : pos_in;
-    int n_kv = (pos + 1 + 31) / 32 * 32;
-    n_kv = n_kv < a.n_ctx ? n_kv : a.n_ctx;
     const int nc = a.n_ctx;
-    uint16_t *q16 = (uint16_t *)smem;                       // [gsz][HD]
-    float *w = (float *)(q16 + gsz * HD);                   // [gsz][nc]
-    uint16_t *p16 = (uint16_t *)(w + gsz * nc);             // [gsz][nc]
-    float *scal = (float *)(p16 + gsz * nc);                // [gsz][4]
-    double *gsum = (double *)p16;                           // [gsz][nc/4], before p16
+    int posv[TPW], nkv[TPW];
+    bool badv[TPW], live[TPW];
+    int nkv_max = 0, pos_max = -1;
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+        live[tt] = i0 + tt >= 0;
+        const int pos_in = live[tt] ? a.pos[i0 + tt] : 0;
+        badv[tt] = pos_in < 0 || pos_in >= nc;
+        posv[tt] = badv[tt] ? 0 : pos_in;
+        int n = (posv[tt] + 1 + 31) / 32 * 32;
+        nkv[tt] = !live[tt] ? 0 : n < nc ? n : nc;
+        nkv_max = nkv[tt] > nkv_max ? nkv[tt] : nkv_max;
+        pos_max = live[tt] && posv[tt] > pos_max ? posv[tt] : pos_max;
+    }
+    const int R = TPW * gsz;                                // rows r = tt gsz + hh
+    uint16_t *q16 = (uint16_t *)smem;                       // [R][HD]
+    float *w = (float *)(q16 + R * HD);                     // [R][nc]
+    uint16_t *p16 = (uint16_t *)(w + R * nc);               // [R][nc]
+    float *scal = (float *)(p16 + R * nc);                  // [R][4]: max, 1 / sum, tree exact
+    double *gsum = (double *)p16;                           // [R][nc/4], before p16
 
-    for (int u = t; u < gsz * (HD / 2); u += 256) {  // rope(q) of the group's heads -> f16
-        const int hh = u / (HD / 2), pr = u - hh * (HD / 2);
-        const float *qp = a.q + qrow + (int64_t)(g * gsz + hh) * HD + 2 * pr;
-        const float *tc = a.rope_table + (int64_t)pos * (HD / 2) * 2;
-        const float2 rq = rope_pair(qp[0], qp[1], tc[2 * pr], tc[2 * pr + 1]);
-        q16[hh * HD + 2 * pr] = h2u(f2h_rne(rq.x));
-        q16[hh * HD + 2 * pr + 1] = h2u(f2h_rne(rq.y));
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {  // rope(q) of the group's heads -> f16
+        if (!live[tt]) continue;
+        const int64_t qrow = (int64_t)(i0 + tt) * a.n_head * HD;
+        const float *tc = a.rope_table + (int64_t)posv[tt] * (HD / 2) * 2;
+        for (int u = t; u < gsz * (HD / 2); u += 256) {
+            const int hh = u / (HD / 2), pr = u - hh * (HD / 2);
+            const float *qp = a.q + qrow + (int64_t)(g * gsz + hh) * HD + 2 * pr;
+            const float2 rq = rope_pair(qp[0], qp[1], tc[2 * pr], tc[2 * pr + 1]);
+            q16[(tt * gsz + hh) * HD + 2 * pr] = h2u(f2h_rne(rq.x));
+            q16[(tt * gsz + hh) * HD + 2 * pr + 1] = h2u(f2h_rne(rq.y));
+        }
     }
     __syncthreads();
-    // KQ: thread t owns cells t, t + 256, ...: one K row load serves every head of the group
-    for (int c = t; c < n_kv; c += 256) {
-        if (c <= pos) {
+    // KQ: thread t owns cells t, t + 256, ...: one K row load serves every row of the workgroup
+    for (int c = t; c < nkv_max; c += 256) {
+        if (c <= pos_max) {
             uint4 kv[KV4];
             const uint4 *kr = (const uint4 *)(a.k_cache + (int64_t)c * kvw + (int64_t)g * HD);
 #pragma unroll
             for (int k = 0; k < KV4; ++k) kv[k] = kr[k];
 #pragma unroll
-            for (int hh = 0; hh < GM; ++hh)
-                if (GSZ > 0 || hh < gsz)
-                    w[hh * nc + c] = (KQ_PROMPT_DIAG & 1) ? __uint_as_float(kv[0].x ^ kv[KV4 - 1].w) * 1e-30f
-                                                          : vec_dot_f16_rows<HD>(kv, (const uint4 *)(q16 + hh * HD)) * a.scale;
+            for (int tt = 0; tt < TPW; ++tt) {
+                const bool on = c <= posv[tt] && live[tt];
+#pragma unroll
+                for (int hh = 0; hh < GM; ++hh)
+                    if (GSZ > 0 || hh < gsz)
+                        w[(tt * gsz + hh) * nc + c] =
+                            !on ? -INFINITY
+                                : (KQ_PROMPT_DIAG & 1) ? __uint_as_float(kv[0].x ^ kv[KV4 - 1].w) * 1e-30f
+                                                       : vec_dot_f16_rows<HD>(kv, (const uint4 *)(q16 + (tt * gsz + hh) * HD)) * a.scale;
+            }
         } else {
-            for (int hh = 0; hh < gsz; ++hh) w[hh * nc + c] = -INFINITY;
+            for (int r = 0; r < TPW * gsz; ++r) w[r * nc + c] = -INFINITY;
         }
     }
     __syncthreads();
-    // soft_max per head: max (one wave per head, order-free), exp + vaddvq group sums
-    for (int hh = t >> 6; hh < gsz; hh += 4) {
-        const int l = t & 63;
-        float m = -INFINITY;
-        for (int c = l; c < n_kv; c += 64) m = fmaxf(m, w[hh * nc + c]);
+    // soft_max per row: max (one wave per row, order-free), exp + vaddvq group sums
 #pragma unroll
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
-        if (l == 0) scal[4 * hh] = m;
-    }
-    __syncthreads();
-    const int ng = n_kv / 4;
-    for (int u = t; u < gsz * ng; u += 256) {
-        const int hh = u / ng, gi = u - hh * ng;
-        const float mx = scal[4 * hh];
-        float e[4];
+    for (int tt = 0; tt < TPW; ++tt)
+        for (int hh = t >> 6; hh < gsz; hh += 4) {
+            const int l = t & 63, r = tt * gsz + hh;
+            float m = -INFINITY;
+            for (int c = l; c < nkv[tt]; c += 64) m = fmaxf(m, w[r * nc + c]);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const float wv = w[hh * nc + 4 * gi + k];
-            e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o, 64));
+            if (l == 0) scal[4 * r] = m;
         }
+    __syncthreads();
 #pragma unroll
-        for (int k = 0; k < 4; ++k) w[hh * nc + 4 * gi + k] = e[k];
-        gsum[hh * (nc / 4) + gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));
+    for (int tt = 0; tt < TPW; ++tt) {
+        const int ng = nkv[tt] / 4;
+        for (int u = t; u < gsz * ng; u += 256) {
+            const int hh = u / ng, gi = u - hh * ng, r = tt * gsz + hh;
+            const float mx = scal[4 * r];
+            float e[4];
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float wv = w[r * nc + 4 * gi + k];
+                e[k] = wv == -INFINITY ? 0.0f : v_expf(wv - mx);
+            }
+#pragma unroll
+            for (int k = 0; k < 4; ++k) w[r * nc + 4 * gi + k] = e[k];
+            gsum[r * (nc / 4) + gi] = (double)((e[0] + e[1]) + (e[2] + e[3]));
+        }
     }
     __syncthreads();
     if (KQ_PROMPT_DIAG & 2) {
-        if (t < gsz) scal[4 * t + 1] = (float)gsum[t * (nc / 4)];
-    } else if (t < 64 * (gsz < 4 ? gsz : 4)) {  // ggml's in-order double sums (trees where exact), a wave per head
-        for (int hh = t >> 6; hh < gsz; hh += 4) {
-            const float inv = (float)(1.0 / softmax_group_sum(gsum + hh * (nc / 4), ng, t & 63));
-            if ((t & 63) == 0) scal[4 * hh + 1] = inv;
+        if (t < R) scal[4 * t + 1] = (float)gsum[t * (nc / 4)];
+    } else {
+        // ggml's in-order double sums: a wave tree per row where that is provably exact; the
+        // other rows' in-order chains then run one lane per row, all at once (a wave per row
+        // ran them one after another)
+#pragma unroll
+        for (int tt = 0; tt < TPW; ++tt)
+            for (int hh = t >> 6; hh < gsz; hh += 4) {
+                const int r = tt * gsz + hh, ng = nkv[tt] / 4;
+                bool ok = true;
+                const double s = ng > 0 ? softmax_group_tree(gsum + r * (nc / 4), ng, t & 63, ok) : 0.0;
+                if ((t & 63) == 0) {
+                    scal[4 * r + 1] = (float)(1.0 / s);
+                    ((int *)scal)[4 * r + 2] = ok;
+                }
+            }
+        __syncthreads();
+        int ngr = 0;  // row t's groups (t < R)
+#pragma unroll
+        for (int tt = 0; tt < TPW; ++tt) ngr = t / gsz == tt ? nkv[tt] / 4 : ngr;
+        if (KQ_PROMPT_SUMLANES) {
+            if (t < R && !((const int *)scal)[4 * t + 2]) scal[4 * t + 1] = (float)(1.0 / seq_sum_lds(gsum + t * (nc / 4), ngr));
+        } else {  // (A/B builds: a wave per row, in turn)
+#pragma unroll
+            for (int tt = 0; tt < TPW; ++tt)
+                for (int hh = t >> 6; hh < gsz; hh += 4) {
+                    const int r = tt * gsz + hh;
+                    if (!((const int *)scal)[4 * r + 2]) {
+                        const double s = seq_sum_lds(gsum + r * (nc / 4), nkv[tt] / 4);
+                        if ((t & 63) == 0) scal[4 * r + 1] = (float)(1.0 / s);
+                    }
+                }
         }
     }
     __syncthreads();
-    for (int u = t; u < gsz * n_kv; u += 256) {
-        const int hh = u / n_kv, c = u - hh * n_kv;
-        p16[hh * nc + c] = h2u(f2h_rne(w[hh * nc + c] * scal[4 * hh + 1]));
-    }
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt)
+        for (int u = t; u < gsz * nkv[tt]; u += 256) {
+            const int hh = u / nkv[tt], c = u - hh * nkv[tt], r = tt * gsz + hh;
+            p16[r * nc + c] = h2u(f2h_rne(w[r * nc + c] * scal[4 * r + 1]));
+        }
     __syncthreads();
-    // KQV: thread (d, j) -> accumulator j of output d of every head; one V chunk per (d, j, it)
-    const int n_it = (KQ_PROMPT_DIAG & 4) ? 1 : (pos + 32) / 32;
+    // KQV: thread (d, j) -> accumulator j of output d of every row; one V chunk per (d, j, it)
+    // serves them all. A token's iterations past its own cells are computed and discarded (a
+    // select: the V cells there need not be finite), so every accumulator sees exactly its
+    // token's iterations, in order.
+    int nit[TPW], nit_max = 0;
+#pragma unroll
+    for (int tt = 0; tt < TPW; ++tt) {
+        nit[tt] = !live[tt] ? 0 : (KQ_PROMPT_DIAG & 4) ? 1 : (posv[tt] + 32) / 32;
+        nit_max = nit[tt] > nit_max ? nit[tt] : nit_max;
+    }
 #pragma unroll
     for (int ii = 0; ii < ITEMS; ++ii) {
         const int item = t + 256 * ii;
         const int d = item >> 2, j = item & 3;
         const uint16_t *vr = a.v_cache + (int64_t)(g * HD + d) * nc;
-        uint32_t acc[GM][4] = {};  // lanes 2k, 2k+1 of head hh's accumulator j in word k
-        // one 32-cell iteration: its V chunk against every head's probabilities
+        uint32_t acc[TPW][GM][4] = {};  // lanes 2k, 2k+1 of row (tt, hh)'s accumulator j in word k
+        // one 32-cell iteration: its V chunk against every row's probabilities
         auto step = [&](const uint4 &vv, int it) {
             const int c0 = 32 * it + 8 * j;
             const uint32_t vw[4] = {vv.x, vv.y, vv.z, vv.w};
 #pragma unroll
-            for (int hh = 0; hh < GM; ++hh) {
-                if (GSZ == 0 && hh >= gsz) break;
-                const uint4 pp = *(const uint4 *)(p16 + hh * nc + c0);
-                acc[hh][0] = pk_fma_w(vw[0], pp.x, acc[hh][0]);
-                acc[hh][1] = pk_fma_w(vw[1], pp.y, acc[hh][1]);
-                acc[hh][2] = pk_fma_w(vw[2], pp.z, acc[hh][2]);
-                acc[hh][3] = pk_fma_w(vw[3], pp.w, acc[hh][3]);
+            for (int tt = 0; tt < TPW; ++tt) {
+                const bool on = TPW == 1 || it < nit[tt];
+#pragma unroll
+                for (int hh = 0; hh < GM; ++hh) {
+                    if (GSZ == 0 && hh >= gsz) break;
+                    const uint4 pp = *(const uint4 *)(p16 + (tt * gsz + hh) * nc + c0);
+                    const uint32_t n0 = pk_fma_w(vw[0], pp.x, acc[tt][hh][0]);
+                    const uint32_t n1 = pk_fma_w(vw[1], pp.y, acc[tt][hh][1]);
+                    const uint32_t n2 = pk_fma_w(vw[2], pp.z, acc[tt][hh][2]);
+                    const uint32_t n3 = pk_fma_w(vw[3], pp.w, acc[tt][hh][3]);
+                    acc[tt][hh][0] = on ? n0 : acc[tt][hh][0];
+                    acc[tt][hh][1] = on ? n1 : acc[tt][hh][1];
+                    acc[tt][hh][2] = on ? n2 : acc[tt][hh][2];
+                    acc[tt][hh][3] = on ? n3 : acc[tt][hh][3];
+                }
             }
         };
         int it = 0;
-        for (; it + 4 <= n_it; it += 4) {  // whole batches: 4 V chunks in flight, no guards
+        for (; it + 4 <= nit_max; it += 4) {  // whole batches: 4 V chunks in flight, no guards
             uint4 vq[4];
 #pragma unroll
             for (int k = 0; k < 4; ++k) vq[k] = *(const uint4 *)(vr + 32 * (it + k) + 8 * j);
 #pragma unroll
             for (int k = 0; k < 4; ++k) step(vq[k], it + k);
         }
-        for (; it < n_it; ++it) step(*(const uint4 *)(vr + 32 * it + 8 * j), it);
+        for (; it < nit_max; ++it) step(*(const uint4 *)(vr + 32 * it + 8 * j), it);
         // the 4 accumulators of output d sit in the 4 lanes of a quad (j = t & 3)
 #pragma unroll
-        for (int hh = 0; hh < GM; ++hh) {
-            if (GSZ == 0 && hh >= gsz) break;
-            const float o = bad ? __builtin_nanf("") : f16x8_reduce_quad(acc[hh]);
-            if (j == 0) {
-                a.out[qrow + (int64_t)(g * gsz + hh) * HD + d] = o;
-                if (a.q8_out) w[hh * HD + d] = o;  // staged for the Q8L blocks (w is free now)
+        for (int tt = 0; tt < TPW; ++tt)
+#pragma unroll
+            for (int hh = 0; hh < GM; ++hh) {
+                if (GSZ == 0 && hh >= gsz) break;
+                const float o = badv[tt] ? __builtin_nanf("") : f16x8_reduce_quad(acc[tt][hh]);
+                if (j == 0 && live[tt]) {
+                    a.out[(int64_t)(i0 + tt) * a.n_head * HD + (int64_t)(g * gsz + hh) * HD + d] = o;
+                    if (a.q8_out) w[(tt * gsz + hh) * HD + d] = o;  // staged for the Q8L blocks (w is free now)
+                }
             }
-        }
     }
-    if (a.q8_out) {  // the group's gsz*HD outputs (whole superblocks of the row) -> Q8L
+    if (a.q8_out) {  // each token's gsz*HD outputs (whole superblocks of its row) -> Q8L
         __syncthreads();
-        const int nsb = gsz * HD / QK, rid = t >> 4, l = t & 15;
-        if (rid < nsb) {  // uniform over each 16-lane row (quant16_store's DPP row)
+        const int nsb = gsz * HD / QK, l = t & 15;
+        for (int rid = t >> 4; rid < TPW * nsb; rid += 16) {  // uniform over each 16-lane row (quant16_store's DPP row)
+            const int tt = rid / nsb, sb = rid - tt * nsb;
+            if (i0 + tt < 0) continue;
             const float *src = w + rid * QK + 16 * l;
             u32x4 v[4];
 #pragma unroll
@@ -842,7 +925,7 @@ __global__ void __launch_bounds__(256) kq_attn_prompt_group(const AttnArgs a) {
                 v[k] = u32x4{__float_as_uint(f.x), __float_as_uint(f.y), __float_as_uint(f.z), __float_as_uint(f.w)};
             }
             const int64_t nbr = (int64_t)a.n_head * HD / QK;  // superblocks per row
-            quant16_store<true>(v, l, a.q8_out + ((int64_t)i * nbr + (int64_t)g * nsb + rid) * Q8L_STRIDE);
+            quant16_store<true>(v, l, a.q8_out + ((int64_t)(i0 + tt) * nbr + (int64_t)g * nsb + sb) * Q8L_STRIDE);
         }
     }
 }
@@ -1110,6 +1193,14 @@ bool attn_prompt_group_ok(const AttnArgs &a) {
     return gsz <= PROMPT_GMAX && attn_prompt_group_lds(a.head_dim, a.n_ctx, gsz) <= 160 * 1024 &&
            g_prompt_impl.load() == MI355X_ATTN_GROUP;
 }
+// tokens per workgroup: KQ_PROMPT_TPW where its rows fit the LDS (fixed group sizes), else 1
+int attn_prompt_tpw(const AttnArgs &a) {
+    const int gsz = a.n_head / a.n_head_kv;
+    return KQ_PROMPT_TPW > 1 && (gsz == 4 || gsz == 8) &&
+                   attn_prompt_group_lds(a.head_dim, a.n_ctx, gsz * KQ_PROMPT_TPW) <= 160 * 1024
+               ? KQ_PROMPT_TPW
+               : 1;
+}
 
 // Q8L rows written by the group kernel: its slice (gsz*head_dim) must be whole superblocks
 bool attn_prompt_q8_ok(const AttnArgs &a) {
@@ -1117,30 +1208,35 @@ bool attn_prompt_q8_ok(const AttnArgs &a) {
            a.n_ctx >= a.head_dim;  // staged in the score rows: gsz*head_dim floats
 }
 
-int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
+int launch_attn_prompt(const AttnArgs &a0, int n_tok, hipStream_t s) {
     if (n_tok <= 0) return MI355X_OK;
+    AttnArgs a = a0;
+    a.n_tok = n_tok;
     const size_t lds = attn_prompt_lds(a.head_dim, a.n_ctx);
     const int gsz = a.n_head / a.n_head_kv;
-    const size_t glds = attn_prompt_group_lds(a.head_dim, a.n_ctx, gsz);
-    // one workgroup per (kv group, token) where the group's heads fit: 1/gsz of the cache reads
+    // one workgroup per (kv group, TPW tokens) where the rows fit: 1/(gsz TPW) of the cache reads
     const bool group = attn_prompt_group_ok(a);
     if (a.q8_out && !group) return MI355X_E_INVAL;  // only the group kernel writes the Q8L rows
+    const int tpw = group ? attn_prompt_tpw(a) : 1;
+    const size_t glds = attn_prompt_group_lds(a.head_dim, a.n_ctx, gsz * tpw);
     const dim3 gs((unsigned)n_tok, (unsigned)a.n_head_kv), ga((unsigned)a.n_head, (unsigned)n_tok);
-    const dim3 gg((unsigned)a.n_head_kv, (unsigned)n_tok);
+    const dim3 gg((unsigned)a.n_head_kv, (unsigned)((n_tok + tpw - 1) / tpw));
     int rc;
+#define KQ_PROMPT_GROUP_LAUNCH(HD, G, T)                                                                  \
+    {                                                                                                   \
+        allow_lds((const void *)kq_attn_prompt_group<HD, G, T>, glds);                                  \
+        return timed_launch("kq::kq_attn_prompt_group<" #HD ">", 0.0, kq_attn_prompt_group<HD, G, T>, gg, \
+                            dim3(256), glds, s, a);                                                     \
+    }
     if (a.head_dim == 64) {
         rc = a.no_store ? 0 : timed_launch("kq::kq_kv_store<64>", 0.0, kq_kv_store<64>, gs, dim3(256), 0, s, a);
         if (rc) return rc;
         if (group) {
-#define KQ_PROMPT_GROUP_LAUNCH(HD, G)                                                                     \
-    {                                                                                                   \
-        allow_lds((const void *)kq_attn_prompt_group<HD, G>, glds);                                     \
-        return timed_launch("kq::kq_attn_prompt_group<" #HD ">", 0.0, kq_attn_prompt_group<HD, G>, gg, dim3(256), \
-                            glds, s, a);                                                                \
-    }
-            if (gsz == 8) KQ_PROMPT_GROUP_LAUNCH(64, 8)
-            if (gsz == 4) KQ_PROMPT_GROUP_LAUNCH(64, 4)
-            KQ_PROMPT_GROUP_LAUNCH(64, 0)
+            if (gsz == 8 && tpw > 1) KQ_PROMPT_GROUP_LAUNCH(64, 8, KQ_PROMPT_TPW)
+            if (gsz == 4 && tpw > 1) KQ_PROMPT_GROUP_LAUNCH(64, 4, KQ_PROMPT_TPW)
+            if (gsz == 8) KQ_PROMPT_GROUP_LAUNCH(64, 8, 1)
+            if (gsz == 4) KQ_PROMPT_GROUP_LAUNCH(64, 4, 1)
+            KQ_PROMPT_GROUP_LAUNCH(64, 0, 1)
         }
         allow_lds((const void *)kq_attn_prompt<64>, lds);
         return timed_launch("kq::kq_attn_prompt<64>", 0.0, kq_attn_prompt<64>, ga, dim3(256), lds, s, a);
@@ -1148,11 +1244,13 @@ int launch_attn_prompt(const AttnArgs &a, int n_tok, hipStream_t s) {
     rc = a.no_store ? 0 : timed_launch("kq::kq_kv_store<128>", 0.0, kq_kv_store<128>, gs, dim3(256), 0, s, a);
     if (rc) return rc;
     if (group) {
-        if (gsz == 8) KQ_PROMPT_GROUP_LAUNCH(128, 8)
-        if (gsz == 4) KQ_PROMPT_GROUP_LAUNCH(128, 4)
-        KQ_PROMPT_GROUP_LAUNCH(128, 0)
-#undef KQ_PROMPT_GROUP_LAUNCH
+        if (gsz == 8 && tpw > 1) KQ_PROMPT_GROUP_LAUNCH(128, 8, KQ_PROMPT_TPW)
+        if (gsz == 4 && tpw > 1) KQ_PROMPT_GROUP_LAUNCH(128, 4, KQ_PROMPT_TPW)
+        if (gsz == 8) KQ_PROMPT_GROUP_LAUNCH(128, 8, 1)
+        if (gsz == 4) KQ_PROMPT_GROUP_LAUNCH(128, 4, 1)
+        KQ_PROMPT_GROUP_LAUNCH(128, 0, 1)
     }
+#undef KQ_PROMPT_GROUP_LAUNCH
     allow_lds((const void *)kq_attn_prompt<128>, lds);
     return timed_launch("kq::kq_attn_prompt<128>", 0.0, kq_attn_prompt<128>, ga, dim3(256), lds, s, a);
 }

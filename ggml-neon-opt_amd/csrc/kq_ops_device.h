@@ -398,15 +398,22 @@ __device__ __forceinline__ int wave_imin(int v) {
     }
     return v;
 }
-__device__ __forceinline__ double softmax_group_sum(const double *g, int n, int lane) {
-    if (n <= 0) return 0.0;
+// The wave tree alone: the sum and whether it is provably ggml's in-order sum (ok; wave-uniform)
+__device__ __forceinline__ double softmax_group_tree(const double *g, int n, int lane, bool &ok) {
     SumExact se;
     for (int i = lane; i < n; i += 64) se.add((float)g[i]);  // (float)g is exact: g holds a float
     double part = se.part;
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) part += __shfl_xor(part, o, 64);
     const double p0 = readlane_f64(part, 0);  // (one value for the whole wave's decision)
-    if (sum_exact_ok(p0, wave_imin(se.gmin), __any(se.bad))) return p0;
+    ok = sum_exact_ok(p0, wave_imin(se.gmin), __any(se.bad));
+    return p0;
+}
+__device__ __forceinline__ double softmax_group_sum(const double *g, int n, int lane) {
+    if (n <= 0) return 0.0;
+    bool ok;
+    const double p0 = softmax_group_tree(g, n, lane, ok);
+    if (ok) return p0;
     return KQ_SEQ_SUM_WAVE ? seq_sum_wave(g, n, lane) : seq_sum_lds(g, n);
 }
 
