@@ -118,7 +118,7 @@ const KnobDef kKnobs[KNOB_COUNT] = {
     {"GEMV_XMODE", 0}, {"GEMV_SMALL_MB", kRowsSmallBytes / 1e6},      {"GEMV_WPC", 0},
     {"GEMV_SMALL_WG", 0}, {"GEMV_FQMAX", (double)kRowsFusedMaxNb},   {"MMF_WAVES", 0},
     {"MMF_ORDER", 0},  {"ATTN_DIAG", 0},     {"LOOPBACK_NOCOPY", 0}, {"ATTN_OPROJ", 1},
-    {"AO_NRB", 0},     {"GEMV_DYN", 8},    {"GEMV_DYN_P", 0},
+    {"AO_NRB", 0},     {"GEMV_DYN", 8},    {"GEMV_DYN_P", 0},      {"GEMV_DYN_STEPS", 16},
 };
 std::atomic<double> g_knob[KNOB_COUNT];
 std::atomic<bool> g_knob_set[KNOB_COUNT];
@@ -537,7 +537,7 @@ int plan_rows(const mi355x_gemv_desc *d, int n_desc, int64_t K, bool fusedq, Row
         // (8B ffn_up, 70B ffn_down: +5 to +10 %) the units' bookkeeping costs more than the
         // balance gains
         const double per_wave = (double)rows / (double)n_wg / U / pl.nwv;
-        const bool auto_ok = per_wave >= dyn_min && steps_per_wave >= 16;
+        const bool auto_ok = per_wave >= dyn_min && steps_per_wave >= knob(KNOB_GEMV_DYN_STEPS);
         const RowsDynLayout DL = rows_dyn_layout((int)nb, tmask, bRd, (int)flat, pl.nwv);
         if ((force || auto_ok) && rows > 0 && (size_t)DL.total <= kMaxLds && flat < 0x7fffffff / 64) {
             pl.dyn = true;

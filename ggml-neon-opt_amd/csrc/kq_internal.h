@@ -139,6 +139,7 @@ enum Knob {
     KNOB_AO_NRB,           // kq_attn_oproj row blocks (0: by shape)
     KNOB_GEMV_DYN,         // kq_rows_dyn when a wave gets at least this many units (and 16 steps) on average (0: never)
     KNOB_GEMV_DYN_P,       // kq_rows_dyn: static units per wave (0: a ring's worth; A/B only)
+    KNOB_GEMV_DYN_STEPS,   // kq_rows_dyn AUTO: 16-superblock steps per wave at least (with GEMV_DYN units)
     KNOB_COUNT
 };
 double knob(Knob k);

@@ -415,7 +415,7 @@ def gemv_waves(waves):
 
 DEBUG_KNOBS = ("GEMV_DIAG", "GEMV_RING", "GEMV_PRE0", "GEMV_PF", "GEMV_XMODE", "GEMV_SMALL_MB", "GEMV_WPC",
                "GEMV_SMALL_WG", "GEMV_FQMAX", "MMF_WAVES", "MMF_ORDER", "ATTN_DIAG", "LOOPBACK_NOCOPY",
-               "ATTN_OPROJ", "AO_NRB", "GEMV_DYN", "GEMV_DYN_P")
+               "ATTN_OPROJ", "AO_NRB", "GEMV_DYN", "GEMV_DYN_P", "GEMV_DYN_STEPS")
 
 
 def debug_knob(name, value=float("nan")):

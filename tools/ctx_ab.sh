@@ -8,7 +8,7 @@ OUT=gpurun_out/ctx_ab.txt
 : > $OUT
 run() {  # lib[:KNOB=V] model n
   local lib=${1%%:*} kn=""
-  [ "$lib" != "$1" ] && kn="--knob ${1#*:}"
+  [ "$lib" != "$1" ] && kn="--knob ${1#*:}" && kn=${kn//,/ --knob }  # lib:K1=V1,K2=V2
   MI355X_LIB=ggml-neon-opt_amd/$lib timeout -k 10 400 python -u bench.py --model $2 --steps 16 --warmup 4 --tg $3 --no-cpu-baseline --no-large \
       --no-prefill --no-chain --no-8b --no-70b --no-collectives $kn > gpurun_out/cc_tmp.json 2> gpurun_out/cc_tmp.err
   rc=$?; [ $rc -eq 0 ] || { echo "rc=$rc $1 $2 $3"; tail -5 gpurun_out/cc_tmp.err; exit $rc; }
