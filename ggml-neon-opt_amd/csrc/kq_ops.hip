@@ -1036,9 +1036,13 @@ int attn_impl() { return g_attn_impl.load(); }
 size_t attn_cells_lds_a(int hd, int gsz) { return (size_t)gsz * hd * 2 + (size_t)hd * 2 + (size_t)ATTN_CHUNK * hd * 2; }
 // B's LDS: the scores region (p16 and the group sums reuse it), red, 96 B of scalars, and RS V
 // rows of 2 n_ctx + VPAD bytes
-int attn_cells_rs(int hd) { return hd == 64 ? KQ_ATTN_CELLS_RS64 : KQ_ATTN_CELLS_RS128; }
 size_t attn_cells_lds_b(int n_ctx, int rs) {
     return (size_t)n_ctx * 4 + (size_t)rs * 64 + 96 + (size_t)rs * (2 * (size_t)n_ctx + ATTN_CELLS_VPAD);
+}
+// head_dim 128: RS 16 (one round of workgroups) where its V rows fit the LDS, else 8
+int attn_cells_rs(int hd, int n_ctx) {
+    if (hd == 64) return KQ_ATTN_CELLS_RS64;
+    return attn_cells_lds_b(n_ctx, KQ_ATTN_CELLS_RS128) <= 160 * 1024 ? KQ_ATTN_CELLS_RS128 : 8;
 }
 
 // The score workspace [n_head][n_ctx] f32: one grow-only buffer per (device, stream), so two
@@ -1086,7 +1090,7 @@ bool attn_cells_applies(const AttnArgs &a) {
            a.n_ctx <= 1024 * ATTN_CELLS_GMAX &&
            (a.head_dim == 64 || a.head_dim == 128) && gsz >= 1 && gsz <= 16 &&
            (KQ_ATTN_CELLS_OVER_SPLIT || attn_slices(a) == 1 || attn_slices(a) >= KQ_ATTN_CELLS_SLICES) &&
-           attn_cells_lds_b(a.n_ctx, attn_cells_rs(a.head_dim)) <= 160 * 1024 && ((uintptr_t)a.k_cache & 15u) == 0 &&
+           attn_cells_lds_b(a.n_ctx, attn_cells_rs(a.head_dim, a.n_ctx)) <= 160 * 1024 && ((uintptr_t)a.k_cache & 15u) == 0 &&
            ((uintptr_t)a.v_cache & 15u) == 0;
 }
 
@@ -1111,13 +1115,29 @@ int launch_attn_cells_t(const AttnArgs &a, float *ws, hipStream_t s, const char 
 int launch_attn_cells(const AttnArgs &a, float *ws, hipStream_t s) {
     if (a.head_dim == 64)
         return launch_attn_cells_t<64, KQ_ATTN_CELLS_RS64>(a, ws, s, "kq::kq_attn_cells<64>", "kq::kq_attn_cells_kqv<64>");
-    return launch_attn_cells_t<128, KQ_ATTN_CELLS_RS128>(a, ws, s, "kq::kq_attn_cells<128>", "kq::kq_attn_cells_kqv<128>");
+    if (attn_cells_rs(128, a.n_ctx) == KQ_ATTN_CELLS_RS128)
+        return launch_attn_cells_t<128, KQ_ATTN_CELLS_RS128>(a, ws, s, "kq::kq_attn_cells<128>", "kq::kq_attn_cells_kqv<128>");
+    return launch_attn_cells_t<128, 8>(a, ws, s, "kq::kq_attn_cells<128>", "kq::kq_attn_cells_kqv<128>");
+}
+
+// The kernel launch_attn runs for these arguments (mi355x_attn_path; a captured launch without
+// a reserved workspace takes MI355X_ATTN_PATH_HEAD_BATCH instead of the cells split).
+int attn_path(const AttnArgs &a) {
+    if (attn_impl() == MI355X_ATTN_GROUP && attn_group_ok(a, attn_group_waves(a))) return MI355X_ATTN_PATH_GROUP;
+    const int ds = attn_slices(a);
+    if (ds > 1 && !attn_cells_applies(a)) return ds == 4 ? MI355X_ATTN_PATH_SPLIT4 : MI355X_ATTN_PATH_SPLIT8;
+    if (attn_cells_applies(a)) return MI355X_ATTN_PATH_CELLS;
+    if (KQ_ATTN_KDMA1 && a.n_ctx <= KQ_ATTN_BATCH_CTX && a.n_ctx % 8 == 0 && ((uintptr_t)a.v_cache & 15u) == 0 &&
+        ((uintptr_t)a.k_cache & 15u) == 0)
+        return MI355X_ATTN_PATH_KD1;
+    return a.n_ctx > KQ_ATTN_BATCH_CTX ? MI355X_ATTN_PATH_HEAD_BATCH : MI355X_ATTN_PATH_HEAD;
 }
 
 int launch_attn(const AttnArgs &a, hipStream_t s) {
     const double bytes = 0;  // context-dependent; not a roofline kernel
-    const int nw = attn_group_waves(a);
-    if (attn_impl() == MI355X_ATTN_GROUP && attn_group_ok(a, nw)) {
+    const int path = attn_path(a);
+    if (path == MI355X_ATTN_PATH_GROUP) {
+        const int nw = attn_group_waves(a);
         const size_t glds = attn_group_bytes(a, nw);
         if (a.head_dim == 64) {
             allow_lds((const void *)kq_attn_group<64>, glds);
@@ -1133,7 +1153,7 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
     // the register prefetch, which issues V with the position itself.
     AttnArgs b = a;
     const int ds = attn_slices(a);
-    if (ds > 1 && !attn_cells_applies(a)) {  // (the two launches where the split would need its widest form)
+    if (path == MI355X_ATTN_PATH_SPLIT4 || path == MI355X_ATTN_PATH_SPLIT8) {
         const size_t lds = attn_lds_v(a.head_dim, a.n_ctx, ds);
         const dim3 grid((unsigned)(a.n_head * ds));
 #define KQ_ATTN_SPLIT_LAUNCH(HD, DS)                                                                        \
@@ -1149,15 +1169,14 @@ int launch_attn(const AttnArgs &a, hipStream_t s) {
 #undef KQ_ATTN_SPLIT_LAUNCH
         return MI355X_E_INVAL;
     }
-    if (attn_cells_applies(a)) {  // long caches past the output split: KQ split over cells, two launches
+    if (path == MI355X_ATTN_PATH_CELLS) {  // long caches past the output split: KQ split over cells, two launches
         hipStreamCaptureStatus cst = hipStreamCaptureStatusNone;
         const bool capturing = hipStreamIsCapturing(s, &cst) == hipSuccess && cst != hipStreamCaptureStatusNone;
         void *ws = attn_cells_buffer((size_t)a.n_head * a.n_ctx * 4, s, !capturing);
         if (ws) return launch_attn_cells(a, (float *)ws, s);
         // (captured without a reserved workspace: the one-launch kernel below)
     }
-    if (KQ_ATTN_KDMA1 && a.n_ctx <= KQ_ATTN_BATCH_CTX && a.n_ctx % 8 == 0 && ((uintptr_t)a.v_cache & 15u) == 0 &&
-        ((uintptr_t)a.k_cache & 15u) == 0) {
+    if (path == MI355X_ATTN_PATH_KD1) {
         const size_t lds = attn_lds_v(a.head_dim, a.n_ctx, 1, true);
         if (a.head_dim == 64) {
             allow_lds((const void *)kq_attn_decode<64, true, 1, 256, true>, lds);
@@ -1353,6 +1372,12 @@ int mi355x_rope(const float *x, float *y, int head_dim, int n_dims, int n_heads,
     const int64_t pairs = (int64_t)n_heads * (head_dim / 2);
     return timed_launch("kq::kq_rope", pairs * 16.0, kq_rope, dim3((unsigned)((pairs + 255) / 256)), dim3(256), 0,
                         (hipStream_t)stream, x, y, head_dim, n_dims, n_heads, pos, table, n_pos);
+}
+
+int mi355x_attn_path(const mi355x_attn_desc *d) {
+    AttnArgs a = {};
+    const int rc = attn_args_from(d, a);
+    return rc != MI355X_OK ? rc : attn_path(a);
 }
 
 int mi355x_attn_decode(const mi355x_attn_desc *d, void *stream) {

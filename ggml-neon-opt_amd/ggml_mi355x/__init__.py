@@ -30,6 +30,8 @@ E_OK, E_INVAL, E_UNSUPPORTED, E_WORKSPACE, E_NODEVICE, E_COMM, E_LAYER = 0, -1, 
 PRO_NONE, PRO_RMS_NORM, PRO_SWIGLU = 0, 1, 2
 EPI_NONE, EPI_SWIGLU = 0, 1
 ATTN_GROUP, ATTN_HEAD, ATTN_SPLIT = 0, 1, 2
+# mi355x_attn_path: the decode attention kernel a descriptor takes
+ATTN_PATH_HEAD, ATTN_PATH_HEAD_BATCH, ATTN_PATH_SPLIT4, ATTN_PATH_SPLIT8, ATTN_PATH_CELLS, ATTN_PATH_GROUP, ATTN_PATH_KD1 = range(7)
 MMQ_AUTO, MMQ_TILE64, MMQ_TILE128, MMQ_TILE128W, MMQ_TILE64W, MMQ_TILE128X, MMQ_TILE192 = 0, 1, 2, 3, 4, 5, 6
 PREFILL_EXACT, PREFILL_F16, PREFILL_F16_ALL = 0, 1, 2
 
@@ -51,7 +53,7 @@ EXPORTED_SYMBOLS = (
     "mi355x_gguf_get_str", "mi355x_gguf_arr_n",
     "mi355x_gemv_ext_workspace_size", "mi355x_gemv_fused_ext", "mi355x_backend_set_fusion",
     "mi355x_get_rows", "mi355x_rms_norm", "mi355x_add", "mi355x_mul", "mi355x_swiglu",
-    "mi355x_rope_table_size", "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode",
+    "mi355x_rope_table_size", "mi355x_rope_table", "mi355x_rope", "mi355x_attn_decode", "mi355x_attn_path",
     "mi355x_comm_id_size", "mi355x_comm_get_unique_id", "mi355x_backend_set_comm", "mi355x_backend_comm_world",
     "mi355x_backend_set_comm_loopback", "mi355x_lower_ggml_graph", "mi355x_attn_impl",
     "mi355x_mmq_impl",
@@ -213,6 +215,8 @@ def lib():
     L.mi355x_rope_table.argtypes = [vp, i32, i32, f32, f32, vp]
     L.mi355x_rope.argtypes = [vp, vp, i32, i32, i32, vp, vp, i32, vp]
     L.mi355x_attn_decode.argtypes = [ctypes.POINTER(AttnDesc), vp]
+    L.mi355x_attn_path.argtypes = [ctypes.POINTER(AttnDesc)]
+    L.mi355x_attn_path.restype = i32
     L.mi355x_attn_prompt.argtypes = [ctypes.POINTER(AttnDesc), i32, vp]
     L.mi355x_attn_prompt_impl.argtypes = [i32]
     L.mi355x_attn_prompt_impl.restype = i32
@@ -535,6 +539,18 @@ def attn_decode(q, k, v, pos, table, k_cache, v_cache, n_head, n_head_kv, head_d
                  1 if rope_row else 0)
     _check(lib().mi355x_attn_decode(ctypes.byref(a), _stream(stream)), "mi355x_attn_decode")
     return out
+
+
+def attn_path(n_ctx, n_head, n_head_kv, head_dim, cache_offset=0, f32_offset=0, rope_row=True):
+    """The decode attention kernel (ATTN_PATH_*) mi355x_attn_decode would run for this shape under
+    the current selectors: no launch, no device access (the descriptor's addresses are synthetic,
+    16-B aligned plus `cache_offset` for the caches and `f32_offset` for q / k / v / rope)."""
+    base = 1 << 20
+    f = base + f32_offset
+    a = AttnDesc(f, f + 4096, f + 8192, base, f + 12288, base + (1 << 12) + cache_offset,
+                 base + (1 << 13) + cache_offset, base + (1 << 14), n_ctx, n_head, n_head_kv, head_dim,
+                 1.0 / float(head_dim) ** 0.5, 1 if rope_row else 0)
+    return int(lib().mi355x_attn_path(ctypes.byref(a)))
 
 
 def attn_prompt(q, k, v, pos, table, k_cache, v_cache, n_head, n_head_kv, head_dim, scale, out=None, stream=None):

@@ -351,6 +351,19 @@ typedef struct {
                                   (staged by the caller with *pos), read without waiting for pos */
 } mi355x_attn_desc;
 int mi355x_attn_decode(const mi355x_attn_desc *a, void *stream);
+/* Which decode attention kernel mi355x_attn_decode (and the ATTN_DECODE graph node) runs for
+ * this descriptor under the current selectors: no launch, no device access (the pointers are
+ * only checked and their alignment read). Returns one of the paths below, or a negative
+ * MI355X_E_* for a descriptor attn_decode would reject. A captured launch whose workspace was
+ * not reserved runs MI355X_ATTN_PATH_HEAD_BATCH in place of MI355X_ATTN_PATH_CELLS. */
+#define MI355X_ATTN_PATH_HEAD 0       /* one workgroup per query head, register path (<= 256 cells) */
+#define MI355X_ATTN_PATH_HEAD_BATCH 1 /* one workgroup per query head, batched cache loads */
+#define MI355X_ATTN_PATH_SPLIT4 2     /* each head split by output over 4 workgroups */
+#define MI355X_ATTN_PATH_SPLIT8 3     /* ... over 8 */
+#define MI355X_ATTN_PATH_CELLS 4      /* KQ split over cells: kq_attn_cells + kq_attn_cells_kqv */
+#define MI355X_ATTN_PATH_GROUP 5      /* one workgroup per KV group (MI355X_ATTN_GROUP) */
+#define MI355X_ATTN_PATH_KD1 6        /* experiment builds (KQ_ATTN_KDMA1) */
+int mi355x_attn_path(const mi355x_attn_desc *a);
 /* The same block for a prompt of n_tokens tokens in one graph (llama-bench pp: ggml's
  * batched non-flash path — SET_ROWS of the batch's cells, then KQ / soft_max with the
  * causal mask / KQV per query): q [n_tokens][n_head*head_dim], k, v [n_tokens][kvw],

@@ -180,7 +180,8 @@ def test_attn_decode_long_random_cache(dev, O, attn_impl, hd, nh, nkv, n_ctx):
 
 
 @pytest.mark.parametrize("hd,nh,nkv,n_ctx,qs", [(64, 32, 4, 4096, 2.0), (128, 32, 8, 4096, 2.0), (64, 8, 2, 6144, 2.0),
-                                                 (128, 16, 2, 3072, 2.0), (64, 32, 4, 4096, 40.0), (128, 32, 8, 4096, 40.0)])
+                                                 (128, 16, 2, 3072, 2.0), (64, 32, 4, 4096, 40.0), (128, 32, 8, 4096, 40.0),
+                                                 (128, 8, 2, 6144, 2.0)])
 def test_attn_decode_cells_split(dev, O, hd, nh, nkv, n_ctx, qs):
     """Caches past what the output split's LDS holds (round 6): the head's KQ split over cells in
     two launches (kq_attn_cells scores 64-cell chunks of a kv group for all its heads into a
