@@ -17,5 +17,6 @@ run() {  # lib[:KNOB=V] model n
 for l in ${LIBS}; do
   for n in ${TINY_NS:-}; do run $l tinyllama-1.1b $n; done
   for n in ${B8_NS:-}; do run $l llama-3-8b $n; done
+  for n in ${B70_NS:-}; do run $l llama-3-70b $n; done
 done
 cat $OUT
