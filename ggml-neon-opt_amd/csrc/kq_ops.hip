@@ -231,17 +231,19 @@ __global__ void __launch_bounds__(TPH) kq_attn_decode(const AttnArgs a) {
 }
 
 // ------------------------------------------------------------ long caches: KQ split over cells
-// Past what the output split's LDS holds (kq_attn_decode<HD, true, DS> keeps the head's scores
-// and its V slice in one workgroup: ~3000 cells at head_dim 64), the one-workgroup-per-head
-// kernel streams every K and V row of a head through one CU (tg4096: ~21 us per layer). There
-// the head's KQ splits over cells instead, in two launches:
+// The output split (kq_attn_decode<HD, true, DS>) keeps the head's scores and its V slice in
+// one workgroup and scores every cell in every slice; past what its LDS holds (~3000 cells at
+// head_dim 64) the one-workgroup-per-head kernel streams every K and V row of a head through
+// one CU (tg4096: ~21 us per layer). For caches of more than KQ_ATTN_CELLS_MIN cells where the
+// split would need 8 slices or does not fit (attn_path), the head's KQ splits over cells
+// instead, in two launches (DESIGN.md §4 "KQ split over cells", profiles/r06_cells_ab.txt):
 //  A kq_attn_cells: workgroup (chunk, g) scores ATTN_CHUNK cells of kv group g for EVERY query
 //    head of the group (each K row read once for the gsz heads) into a score workspace
 //    [n_head][n_ctx]; the workgroup whose chunk holds the position writes the new cell to both
 //    caches (rope'd k, f16 v) and scores that cell from its own copy;
-//  B kq_attn_cells_kqv: workgroup (h, ds): soft_max over the head's scores and KQV for its
-//    HD / DS outputs from the V cache (the new cell included: A wrote it, a kernel boundary
-//    before).
+//  B kq_attn_cells_kqv: workgroup (h, ds): soft_max over the head's scores held in registers
+//    and KQV for its RS = HD / DS outputs (16 threads per output) from its V rows, LDS-DMA'd
+//    under soft_max (the new cell included: A wrote it, a kernel boundary before).
 // Every score is the same NEON-FP16 vec_dot as the one-launch kernels', soft_max's max, exps,
 // group sums and in-order double sum and the KQV accumulator chains are theirs: bit-exact.
 constexpr int ATTN_CHUNK = 64;
@@ -252,7 +254,7 @@ constexpr int ATTN_CHUNK = 64;
 #define KQ_ATTN_CELLS_SLICES 8  // ... and where it needs this many slices (tg3072 +5 %, 8B tg2048 +5.5 %; 4: equal)
 #endif
 #ifndef KQ_ATTN_CELLS_MIN
-#define KQ_ATTN_CELLS_MIN 1024  // caches of more cells than this take the two launches when the output split does not fit
+#define KQ_ATTN_CELLS_MIN 1024  // only caches of more cells than this take the two launches
 #endif
 #ifndef KQ_ATTN_CELLS_OVERLAP
 #define KQ_ATTN_CELLS_OVERLAP 1  // B's soft_max waits for the scores only, the V rows land meanwhile
