@@ -233,6 +233,51 @@ def test_attn_decode_cells_split(dev, O, hd, nh, nkv, n_ctx, qs):
         g.attn_impl(prev)
 
 
+@pytest.mark.parametrize("hd", [64, 128])
+def test_decode_graph_cells_equals_per_head(dev, hd):
+    """The split over cells inside the decode graph (the backend reserves its workspace before
+    capture; eager steps and graph replays interleaved) over every position of a 4096-cell
+    cache: each token's logits equal those of the per-head kernel (MI355X_ATTN_HEAD, bit-exact
+    with the oracle at every cache size), TinyLlama's and Llama-3-8B's head shapes, one layer."""
+    import ggml_mi355x as g
+    from tests import llama_model as LM
+    from ggml_mi355x.llama import LlamaDecoder, hparams
+    hp = hparams(32 * hd, 1, 32, 4 if hd == 64 else 8, 1024, 512)
+    n_ctx = 4096
+    assert g.attn_path(n_ctx, 32, hp["n_head_kv"], hd) == g.ATTN_PATH_CELLS
+    wdev = LM.to_device(LM.build(hp, 21 + hd), dev)
+    tokens = np.random.default_rng(hd).integers(0, hp["n_vocab"], size=n_ctx).tolist()
+    keep = set(range(0, n_ctx, 61)) | set(range(n_ctx - 40, n_ctx))
+
+    def run(impl):
+        prev = g.attn_impl(impl)
+        b = g.Backend()
+        try:
+            dec = LlamaDecoder(b, hp, wdev, n_ctx, fuse=True)
+            out = {}
+            for p, tok in enumerate(tokens):
+                dec.step(tok, p, use_graph=(p % 11 != 5))
+                if p in keep:
+                    b.synchronize()
+                    out[p] = dec.logits.cpu().numpy().copy()
+            b.synchronize()
+            g.timing_enable(True)  # the last token again, eager: which attention kernels ran
+            dec.step(tokens[-1], n_ctx - 1, use_graph=False)
+            b.synchronize()
+            names = [r[0] for r in g.timing_read()]
+            g.timing_enable(False)
+            assert any("kq_attn_cells_kqv" in n for n in names) == (impl == g.ATTN_SPLIT), names
+            return out
+        finally:
+            b.close()
+            g.attn_impl(prev)
+
+    cells = run(g.ATTN_SPLIT)
+    head = run(g.ATTN_HEAD)
+    for p in sorted(keep):
+        assert bits_equal(cells[p], head[p]), (p, first_mismatch(cells[p], head[p]))
+
+
 def test_attn_decode_cells_two_streams(dev, O):
     """The split over cells keeps its score workspace per (device, stream): two decoders'
     long-cache attentions enqueued on two streams at once, interleaved and unsynchronized,
