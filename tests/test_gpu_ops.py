@@ -147,13 +147,15 @@ def test_attn_decode_sequence(dev, O, attn_impl, hd, nh, nkv, n_ctx, rope_row):
 
 
 @pytest.mark.parametrize("hd,nh,nkv,n_ctx", [(64, 32, 4, 1024), (128, 16, 4, 512), (64, 8, 2, 256), (64, 8, 2, 288),
-                                             (128, 8, 2, 2048), (128, 8, 2, 288)])
+                                             (128, 8, 2, 2048), (128, 8, 2, 288), (128, 8, 2, 1312), (64, 8, 2, 2400)])
 def test_attn_decode_long_random_cache(dev, O, attn_impl, hd, nh, nkv, n_ctx):
     """Every cell of both caches random (not only the cells this test wrote), then positions
     across the whole cache: the batched loads of kq_attn_decode<HD, true> (caches past 256
     cells: two K rows per round at head_dim 64, eight V chunks per batch) and the boundary
     cache sizes on either side of that choice, bit-exact with the oracle. The split kernel
-    (past 256 cells) at both head sizes, with 4 slices and (head_dim 128 at 2048 cells) 8."""
+    (past 256 cells) at both head sizes, with 4 slices and with 8 (1312 / 2400 cells: sizes
+    that are not whole 64-cell chunks, so the split over cells does not take them; at 2048
+    cells head_dim 128 now takes the split over cells, mi355x_attn_path)."""
     import torch
     import ggml_mi355x as g
     rng = np.random.default_rng(n_ctx + hd)
